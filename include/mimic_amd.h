@@ -1,0 +1,185 @@
+/*
+ * mimic_amd.h -- C ABI of the MI355X batch-eBPF engine (the drop-in boundary).
+ *
+ * The reference (dylandreimerink/mimic, Go) exposes the hot path as
+ *   NewLinuxEmulator / NewVM              vm.go:54-76, emulator_linux_.go:67-94
+ *   MapSpecToLinuxMap + emu.AddMap        emulator_linux_map.go:57-113, emulator_linux_.go:97-116
+ *   LinuxMap Lookup/Update/Delete/Keys    emulator_linux_map.go:14-54
+ *   VM.AddProgram                         vm.go:98-139 (+ RewriteProgram, emulator_linux_.go:292-339)
+ *   VM.NewProcess + Process.SetCPUID + Process.Run + Process.Cleanup
+ *                                         vm.go:198-374 with LinuxContextXDP, context_xdp_md.go:47-133
+ *   MemoryController.GetEntry + VMMem.Load/Read (host inspection)  memory_controller.go:117-145
+ * Each entry point below names the reference interface it replaces.  A Go maintainer
+ * binds them with cgo; tests bind them with ctypes.
+ *
+ * Conventions: every function returns 0 on success, a negative MIMIC_E* on failure
+ * (text via mimic_last_error), or -- for map operations only -- a positive errno that
+ * the reference returns gracefully as a syscall.Errno (E2BIG = 7).
+ * Host pointers are host memory unless a field says DEVICE.  The engine owns all device
+ * memory it allocates; the caller owns batch/result buffers.  One mimic_vm is one HIP
+ * device + one command stream; calls on one vm must be serialised by the caller
+ * (like the reference's single Process), distinct vms may run concurrently.
+ */
+#ifndef MIMIC_AMD_H
+#define MIMIC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIMIC_ABI_VERSION 1
+
+/* errors */
+#define MIMIC_EINVAL (-1)
+#define MIMIC_ENOMEM (-2)
+#define MIMIC_EDEVICE (-3)
+#define MIMIC_ENOTSUP (-4)
+#define MIMIC_ENOENT (-5)
+#define MIMIC_EFAULT (-6)
+
+/* Per-process status classes (one byte per packet).  Same numbering as the oracle. */
+enum mimic_status {
+    MIMIC_OK = 0,                    /* exited via EXIT (inst.go:277-296) */
+    MIMIC_ERR_PC_OOB = 1,            /* errInvalidProgramCount (vm.go:285,297,328) */
+    MIMIC_ERR_UNSUPPORTED_OP = 2,    /* emulator_linux_.go:287 */
+    MIMIC_ERR_MEM_UNRESOLVED = 3,    /* inst.go:302-305 */
+    MIMIC_ERR_MEM_NOT_VMMEM = 4,     /* inst.go:307-310 */
+    MIMIC_ERR_MEM_BOUNDS = 5,        /* memory_plain.go:27,57 */
+    MIMIC_ERR_MEM_NOT_DATASEC = 6,   /* emulator_linux_map_array.go:136-138 */
+    MIMIC_ERR_R10_WRITE = 7,         /* vm.go:459-460 */
+    MIMIC_ERR_HELPER_MAP_PTR = 8,    /* emulator_linux_helpers.go:415-447 */
+    MIMIC_ERR_HELPER_KEY = 9,        /* :449-471 */
+    MIMIC_ERR_HELPER_VALUE = 10,     /* :525-541 */
+    MIMIC_ERR_HELPER_MAP_OP = 11,    /* non-errno LinuxMap errors */
+    MIMIC_ERR_HELPER_TAILCALL = 12,  /* :674-710 */
+    MIMIC_ERR_HELPER_UNIMPLEMENTED = 13, /* emulator_linux_.go:184-191 */
+    MIMIC_ERR_HELPER_CANT_EMULATE = 14,  /* emulator_linux_helpers.go:473-475 */
+    MIMIC_ERR_LDABS = 15,            /* emulator_linux_.go:200-285 on an xdp_md ctx */
+    MIMIC_PANIC_DIV0 = 16,           /* Go panic, inst_gen.go:73-92,183-202 */
+    MIMIC_PANIC_SHIFT = 17,          /* Go panic, inst.go:118,129 */
+    MIMIC_PANIC_BADREG = 18,         /* vm.go:431-432,461-462 */
+    MIMIC_PANIC_CALLX = 19,          /* inst.go:270-273 */
+    MIMIC_PANIC_PC = 20,             /* negative PC, vm.go:300 */
+    MIMIC_PANIC_HELPER_NEG = 21,     /* negative helper id, emulator_linux_.go:126 */
+    MIMIC_ERR_STEP_LIMIT = 22,       /* step budget (stands for Run's ctx deadline, vm.go:344-350) */
+    MIMIC_ERR_CALL_DEPTH = 23,       /* > MIMIC_MAX_FRAMES nested BPF-to-BPF calls */
+    MIMIC_ERR_ENGINE_HELPER = 24,    /* helper the reference emulates but this engine does not */
+    MIMIC_ERR_NO_CPU = 25
+};
+
+/* Linux map types (ebpf.MapType). */
+#define MIMIC_MAP_HASH 1
+#define MIMIC_MAP_ARRAY 2
+#define MIMIC_MAP_PROG_ARRAY 3
+#define MIMIC_MAP_PERCPU_HASH 5
+#define MIMIC_MAP_PERCPU_ARRAY 6
+
+#define MIMIC_MAP_F_DATASEC 1u  /* Spec.Value is a *btf.Datasec (.data/.bss/.rodata) */
+
+/* schedules: which vCPU runs packet i (the caller's SetCPUID, vm.go:268) */
+#define MIMIC_SCHED_CHUNKED 0      /* contiguous chunks of ceil(N/V) packets per vCPU */
+#define MIMIC_SCHED_INTERLEAVED 1  /* packet i on vCPU i % V */
+#define MIMIC_SCHED_EXPLICIT 2     /* cpu[i] given; each vCPU runs its packets in index order */
+
+typedef struct mimic_vm mimic_vm;
+
+typedef struct {
+    int32_t vcpus;              /* VMSettings.VirtualCPUs (vm.go:21-22, VMOptSetvCPUs) */
+    int32_t stack_frame_size;   /* VMSettings.StackFrameSize, default 256 (vm.go:60) */
+    int32_t stack_frame_count;  /* VMSettings.StackFrameCount, default 8 (vm.go:62) */
+    int32_t max_tail_calls;     /* LinuxEmulatorSettings.MaxTailCalls, default 33 (emulator_linux_.go:78) */
+    int32_t device;             /* HIP device ordinal */
+    int32_t vcpu_begin;         /* this engine executes vCPUs [vcpu_begin, vcpu_begin+vcpu_count) */
+    int32_t vcpu_count;         /* 0 = all */
+    int32_t reserved;
+} mimic_vm_settings;
+
+typedef struct {
+    const char *name;
+    uint32_t type, key_size, value_size, max_entries, flags;
+} mimic_map_spec;
+
+typedef struct {
+    uint32_t slot;    /* raw slot of an LD_IMM64 with src PseudoMapFD(1)/PseudoMapValue(2) */
+    uint32_t map_id;
+} mimic_reloc;
+
+/* One batch of xdp_md processes.  All pointers are DEVICE pointers; NULL arrays fall
+ * back to the scalar next to them.  Packet memory i is pkt_data[pkt_off[i] ..
+ * pkt_off[i]+H+L+T) with the packet at +H (context_xdp_md.go:52-64); the engine zeroes the
+ * headroom/tailroom bytes, then runs the program on that memory IN PLACE, so the caller
+ * sees every packet write afterwards. */
+typedef struct {
+    uint32_t n;
+    uint32_t schedule;          /* MIMIC_SCHED_* */
+    uint8_t *pkt_data;
+    const uint64_t *pkt_off;
+    const uint32_t *pkt_len;
+    const uint32_t *headroom;  uint32_t headroom_all;
+    const uint32_t *tailroom;  uint32_t tailroom_all;
+    const int32_t *ingress_ifindex; int32_t ingress_all;
+    const int32_t *rx_queue_index;  int32_t rxq_all;
+    const int32_t *egress_ifindex;  int32_t egress_all;
+    const int32_t *cpu;         /* HOST array for MIMIC_SCHED_EXPLICIT (the engine builds the per-vCPU lists) */
+    uint64_t step_budget;       /* 0 = MIMIC default; Run's ctx deadline stand-in */
+} mimic_xdp_batch;
+
+typedef struct {                /* DEVICE arrays of n entries, any may be NULL */
+    uint64_t *r0;               /* p.Registers.R0 after Run */
+    uint8_t *status;            /* enum mimic_status */
+    uint32_t *steps;            /* number of Step() calls Run made */
+    int32_t *err_pc;            /* PC of the failing instruction, -1 on MIMIC_OK */
+} mimic_xdp_results;
+
+int mimic_abi_version(void);
+const char *mimic_last_error(const mimic_vm *vm);
+
+/* NewLinuxEmulator(OptMaxTailCalls) + NewVM(VMOptEmulator, VMOptSetvCPUs). vm.go:54-76 */
+int mimic_vm_create(const mimic_vm_settings *settings, mimic_vm **out);
+void mimic_vm_destroy(mimic_vm *vm);
+
+/* MapSpecToLinuxMap + LinuxEmulator.AddMap. emulator_linux_map.go:57, emulator_linux_.go:97 */
+int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id);
+/* LinuxMapUpdater.Update(key, value, flags, cpuid). emulator_linux_map.go:31-36 */
+int mimic_map_update(mimic_vm *vm, uint32_t map_id, const void *key, const void *value, uint32_t flags, int32_t cpu);
+/* LinuxMap.Lookup(key, cpuid) -> virtual address of the value (0 = not found). emulator_linux_map.go:25-27 */
+int mimic_map_lookup(mimic_vm *vm, uint32_t map_id, const void *key, int32_t cpu, uint32_t *addr_out);
+/* LinuxMapDeleter.Delete(key). emulator_linux_map.go:38-42 */
+int mimic_map_delete(mimic_vm *vm, uint32_t map_id, const void *key);
+/* Raw value backing of (map, cpu): E*S bytes, slot order (D2H copy). */
+int mimic_map_read_values(mimic_vm *vm, uint32_t map_id, int32_t cpu, void *out, size_t cap);
+/* Sum over vCPUs [cpu_begin, cpu_end) of a per-CPU map's u64 values -> out[E] (device reduction). */
+int mimic_map_sum_u64(mimic_vm *vm, uint32_t map_id, int32_t cpu_begin, int32_t cpu_end, uint64_t *out, size_t cap);
+/* MemoryController.GetEntryByObject(map).Addr */
+int mimic_map_addr(mimic_vm *vm, uint32_t map_id, uint32_t *addr_out);
+
+/* VM.AddProgram(spec) with the LinuxEmulator map rewrite. vm.go:98-139, emulator_linux_.go:292-339.
+ * insns = n_slots raw little-endian 8-byte instruction slots (ELF .text bytes). */
+int mimic_program_load(mimic_vm *vm, const char *name, const void *insns, uint32_t n_slots,
+                       const mimic_reloc *relocs, uint32_t n_relocs, uint32_t *prog_id);
+/* MemoryController.GetEntryByObject(prog).Addr -- the value a prog array stores. */
+int mimic_program_addr(mimic_vm *vm, uint32_t prog_id, uint32_t *addr_out);
+
+/* MemoryController.GetEntry(addr) + VMMem.Read / Load on static entries (maps). */
+int mimic_mem_read(mimic_vm *vm, uint32_t addr, void *buf, uint32_t len);
+int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out);
+/* Address the per-process stack entry gets (first free address after the static entries). */
+int mimic_stack_addr(mimic_vm *vm, uint32_t *addr_out);
+
+/* Batch form of: for each packet i { p := vm.NewProcess(prog, &LinuxContextXDP{...});
+ * p.SetCPUID(cpu(i)); p.Run(ctx); r0[i] = p.Registers.R0; p.Cleanup() }  (vm.go:198-374).
+ * Enqueued on `hip_stream` (a hipStream_t, NULL = the vm's own stream); returns when enqueued. */
+int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch,
+                  const mimic_xdp_results *results, void *hip_stream);
+/* Wait for all work the vm enqueued on `hip_stream` (NULL = own stream). */
+int mimic_sync(mimic_vm *vm, void *hip_stream);
+/* Executed Step() count of the last completed mimic_run_xdp (sum over packets). */
+int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,102 @@
+"""ctypes binding of the engine's C ABI (include/mimic_amd.h) -> mimic_amd/libmimic_amd.so.
+
+The shared library is built in-tree by ``__graft_entry__.build()``.  There is no fallback:
+if the library is missing the import fails loudly (the product path never runs on CPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmimic_amd.so")
+
+ABI_VERSION = 1
+
+# status codes (enum mimic_status)
+STATUS_NAMES = [
+    "OK", "ERR_PC_OOB", "ERR_UNSUPPORTED_OP", "ERR_MEM_UNRESOLVED", "ERR_MEM_NOT_VMMEM",
+    "ERR_MEM_BOUNDS", "ERR_MEM_NOT_DATASEC", "ERR_R10_WRITE", "ERR_HELPER_MAP_PTR",
+    "ERR_HELPER_KEY", "ERR_HELPER_VALUE", "ERR_HELPER_MAP_OP", "ERR_HELPER_TAILCALL",
+    "ERR_HELPER_UNIMPLEMENTED", "ERR_HELPER_CANT_EMULATE", "ERR_LDABS", "PANIC_DIV0",
+    "PANIC_SHIFT", "PANIC_BADREG", "PANIC_CALLX", "PANIC_PC", "PANIC_HELPER_NEG",
+    "ERR_STEP_LIMIT", "ERR_CALL_DEPTH", "ERR_ENGINE_HELPER", "ERR_NO_CPU",
+]
+STATUS = {n: i for i, n in enumerate(STATUS_NAMES)}
+
+SCHED_CHUNKED, SCHED_INTERLEAVED, SCHED_EXPLICIT = 0, 1, 2
+MAP_F_DATASEC = 1
+
+
+class VMSettings(C.Structure):
+    _fields_ = [("vcpus", C.c_int32), ("stack_frame_size", C.c_int32), ("stack_frame_count", C.c_int32),
+                ("max_tail_calls", C.c_int32), ("device", C.c_int32), ("vcpu_begin", C.c_int32),
+                ("vcpu_count", C.c_int32), ("reserved", C.c_int32)]
+
+
+class MapSpecC(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("type", C.c_uint32), ("key_size", C.c_uint32),
+                ("value_size", C.c_uint32), ("max_entries", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class Reloc(C.Structure):
+    _fields_ = [("slot", C.c_uint32), ("map_id", C.c_uint32)]
+
+
+class XDPBatch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("schedule", C.c_uint32), ("pkt_data", C.c_void_p),
+                ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p),
+                ("headroom", C.c_void_p), ("headroom_all", C.c_uint32),
+                ("tailroom", C.c_void_p), ("tailroom_all", C.c_uint32),
+                ("ingress_ifindex", C.c_void_p), ("ingress_all", C.c_int32),
+                ("rx_queue_index", C.c_void_p), ("rxq_all", C.c_int32),
+                ("egress_ifindex", C.c_void_p), ("egress_all", C.c_int32),
+                ("cpu", C.c_void_p), ("step_budget", C.c_uint64)]
+
+
+class XDPResults(C.Structure):
+    _fields_ = [("r0", C.c_void_p), ("status", C.c_void_p), ("steps", C.c_void_p), ("err_pc", C.c_void_p)]
+
+
+EXPORTS = {
+    "mimic_abi_version": (C.c_int, []),
+    "mimic_last_error": (C.c_char_p, [C.c_void_p]),
+    "mimic_vm_create": (C.c_int, [C.POINTER(VMSettings), C.POINTER(C.c_void_p)]),
+    "mimic_vm_destroy": (None, [C.c_void_p]),
+    "mimic_map_create": (C.c_int, [C.c_void_p, C.POINTER(MapSpecC), C.POINTER(C.c_uint32)]),
+    "mimic_map_update": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32]),
+    "mimic_map_lookup": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.POINTER(C.c_uint32)]),
+    "mimic_map_delete": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "mimic_map_read_values": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_size_t]),
+    "mimic_map_sum_u64": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_void_p, C.c_size_t]),
+    "mimic_map_addr": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "mimic_program_load": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.POINTER(Reloc),
+                                     C.c_uint32, C.POINTER(C.c_uint32)]),
+    "mimic_program_addr": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "mimic_mem_read": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
+    "mimic_mem_load": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(C.c_uint64)]),
+    "mimic_stack_addr": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "mimic_run_xdp": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPBatch), C.POINTER(XDPResults), C.c_void_p]),
+    "mimic_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mimic_last_steps": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libmimic_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mimic_abi_version() != ABI_VERSION:
+        raise ImportError("libmimic_amd.so ABI version mismatch")
+    _lib = lib
+    return lib

@@ -1,0 +1,703 @@
+// engine.cpp -- host side of the MI355X batch-eBPF engine: the C ABI of include/mimic_amd.h.
+//
+// Mirrors the reference's setup-time objects (NewVM / LinuxEmulator.AddMap / VM.AddProgram,
+// vm.go:54-139, emulator_linux_.go:67-116, emulator_linux_map_*.go Init) on the host and
+// keeps their state on the device:
+//  * the static part of the reference MemoryController (maps, programs) as a short segment
+//    table -- entries are appended exactly as AddEntry would place them (first fit from
+//    0x10000 with a one-byte gap; with no deletions that is "previous end + 1");
+//  * every map backing in one device arena;
+//  * the loaded programs as one decoded instruction array (DInsn, 16 B per slot).
+// The per-packet part (NewProcess/Load/Run/Cleanup) is the kernel in interp.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mimic_amd.h"
+#include "layout.h"
+
+extern "C" int mimic_launch_xdp(const KParams *kp, hipStream_t st);
+extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
+                                    hipStream_t st);
+
+namespace {
+
+struct HostMap {
+    std::string name;
+    uint32_t type, family, key_size, value_size, max_entries, datasec;
+    uint32_t obj_addr;      // map object entry
+    uint32_t backing_addr;  // cpu-0 backing entry
+    uint32_t addr_period;   // per-CPU
+    uint32_t ncpu;
+    uint64_t dev_off;       // arena offset of the cpu-0 backing
+    uint64_t dev_stride;    // arena distance between cpu backings
+};
+
+struct HostProg {
+    std::string name;
+    std::vector<DInsn> ins;
+    uint32_t addr;
+};
+
+}  // namespace
+
+struct mimic_vm {
+    mimic_vm_settings s;
+    std::string err;
+    hipStream_t stream = nullptr;
+    uint32_t next_addr = MIMIC_MEM_START;   // first-fit position after the static entries
+    std::vector<HostMap> maps;
+    std::vector<HostProg> progs;
+    std::vector<Seg> segs;
+    // device state
+    uint8_t *arena = nullptr;
+    uint64_t arena_size = 0, arena_cap = 0;
+    DInsn *d_insns = nullptr;
+    DProg *d_progs = nullptr;
+    Seg *d_segs = nullptr;
+    DMap *d_maps = nullptr;
+    bool tables_dirty = true;
+    uint8_t *priv = nullptr;
+    uint64_t priv_bytes = 0;
+    uint32_t priv_lanes = 0;
+    uint32_t *d_sched_start = nullptr, *d_sched_pkts = nullptr;
+    uint64_t sched_cap_start = 0, sched_cap_pkts = 0;
+    uint64_t *d_lane_steps = nullptr;
+    uint32_t lane_steps_cap = 0;
+    uint32_t last_lanes = 0;
+    hipStream_t last_stream = nullptr;
+};
+
+static int fail(mimic_vm *vm, int code, const char *fmt, ...) {
+    if (vm) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        vm->err = buf;
+    }
+    return code;
+}
+
+#define HIP_OK(vm, call)                                                                        \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess) return fail((vm), MIMIC_EDEVICE, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+static uint32_t stack_size(const mimic_vm *vm) {
+    return (uint32_t)(vm->s.stack_frame_size * vm->s.stack_frame_count);
+}
+
+// AddEntry for the static part: with no deletions the first fit is "after the last entry"
+static uint32_t add_entry(mimic_vm *vm, uint32_t size) {
+    uint32_t a = vm->next_addr;
+    vm->next_addr = a + size + 1;
+    return a;
+}
+
+static int arena_reserve(mimic_vm *vm, uint64_t bytes, uint64_t *off) {
+    uint64_t need = (vm->arena_size + 255) & ~255ull;
+    uint64_t end = need + bytes;
+    if (end > vm->arena_cap) {
+        uint64_t cap = std::max<uint64_t>(end, vm->arena_cap * 2);
+        cap = std::max<uint64_t>(cap, 1 << 20);
+        uint8_t *n = nullptr;
+        HIP_OK(vm, hipMalloc(&n, cap));
+        HIP_OK(vm, hipMemset(n, 0, cap));
+        if (vm->arena) {
+            HIP_OK(vm, hipMemcpy(n, vm->arena, vm->arena_size, hipMemcpyDeviceToDevice));
+            HIP_OK(vm, hipFree(vm->arena));
+        }
+        vm->arena = n;
+        vm->arena_cap = cap;
+    }
+    *off = need;
+    vm->arena_size = end;
+    return 0;
+}
+
+static int upload_tables(mimic_vm *vm) {
+    if (!vm->tables_dirty) return 0;
+    std::vector<DInsn> all;
+    std::vector<DProg> dp;
+    for (auto &p : vm->progs) {
+        DProg d{};
+        d.base = (uint32_t)all.size();
+        d.n = (uint32_t)p.ins.size();
+        d.addr = p.addr;
+        dp.push_back(d);
+        all.insert(all.end(), p.ins.begin(), p.ins.end());
+    }
+    all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
+    std::vector<DMap> dm;
+    for (auto &m : vm->maps) {
+        DMap d{};
+        d.family = m.family;
+        d.type = m.type;
+        d.key_size = m.key_size;
+        d.value_size = m.value_size;
+        d.max_entries = m.max_entries;
+        d.datasec = m.datasec;
+        d.obj_addr = m.obj_addr;
+        d.backing_addr = m.backing_addr;
+        d.addr_period = m.addr_period;
+        d.ncpu = m.ncpu;
+        d.dev_off = m.dev_off;
+        d.dev_stride = m.dev_stride;
+        dm.push_back(d);
+    }
+    if (dm.empty()) dm.push_back(DMap{});
+    if (dp.empty()) dp.push_back(DProg{});
+    std::vector<Seg> sg = vm->segs;
+    if (sg.empty()) sg.push_back(Seg{});
+    hipFree(vm->d_insns);
+    hipFree(vm->d_progs);
+    hipFree(vm->d_segs);
+    hipFree(vm->d_maps);
+    vm->d_insns = nullptr;
+    vm->d_progs = nullptr;
+    vm->d_segs = nullptr;
+    vm->d_maps = nullptr;
+    HIP_OK(vm, hipMalloc(&vm->d_insns, all.size() * sizeof(DInsn)));
+    HIP_OK(vm, hipMalloc(&vm->d_progs, dp.size() * sizeof(DProg)));
+    HIP_OK(vm, hipMalloc(&vm->d_segs, sg.size() * sizeof(Seg)));
+    HIP_OK(vm, hipMalloc(&vm->d_maps, dm.size() * sizeof(DMap)));
+    HIP_OK(vm, hipMemcpy(vm->d_insns, all.data(), all.size() * sizeof(DInsn), hipMemcpyHostToDevice));
+    HIP_OK(vm, hipMemcpy(vm->d_progs, dp.data(), dp.size() * sizeof(DProg), hipMemcpyHostToDevice));
+    HIP_OK(vm, hipMemcpy(vm->d_segs, sg.data(), sg.size() * sizeof(Seg), hipMemcpyHostToDevice));
+    HIP_OK(vm, hipMemcpy(vm->d_maps, dm.data(), dm.size() * sizeof(DMap), hipMemcpyHostToDevice));
+    vm->tables_dirty = false;
+    return 0;
+}
+
+// host-side MemoryController.GetEntry over the static entries
+struct HostRef {
+    int kind;          // 0 unresolved, 1 plain (arena), 2 not vmmem, 3 not datasec
+    uint64_t dev_off;  // arena offset of region start
+    uint32_t off, limit;
+};
+
+static HostRef host_resolve(const mimic_vm *vm, uint32_t a) {
+    HostRef R{0, 0, 0, 0};
+    for (const Seg &g : vm->segs) {
+        if (a < g.lo || a > g.hi) continue;
+        uint32_t off = a - g.lo;
+        switch (g.kind) {
+        case SEG_PLAIN: R = {1, g.dev_off, off, g.size}; break;
+        case SEG_ARRAY_OBJ: R = {g.datasec ? 1 : 3, g.dev_off, off, g.size}; break;
+        case SEG_MAP_OBJ: case SEG_PROG: R = {2, 0, 0, 0}; break;
+        case SEG_PERCPU_ARRAY: {
+            uint32_t c = off / g.period, r = off - c * g.period;
+            uint64_t base = g.dev_off + (uint64_t)c * g.dev_stride;
+            if (r <= 8) R = {g.datasec ? 1 : 3, base, r, g.size};
+            else R = {1, base, r - 9, g.size};
+            break;
+        }
+        case SEG_PERCPU_VALUES: {
+            uint32_t c = off / g.period, r = off - c * g.period;
+            R = {1, g.dev_off + (uint64_t)c * g.dev_stride, r, g.size};
+            break;
+        }
+        }
+        return R;
+    }
+    return R;
+}
+
+extern "C" {
+
+int mimic_abi_version(void) { return MIMIC_ABI_VERSION; }
+
+const char *mimic_last_error(const mimic_vm *vm) { return vm ? vm->err.c_str() : "null vm"; }
+
+int mimic_vm_create(const mimic_vm_settings *settings, mimic_vm **out) {
+    if (!settings || !out) return MIMIC_EINVAL;
+    if (settings->vcpus <= 0) return MIMIC_EINVAL;
+    mimic_vm *vm = new mimic_vm();
+    vm->s = *settings;
+    if (vm->s.stack_frame_size <= 0) vm->s.stack_frame_size = 256;
+    if (vm->s.stack_frame_count <= 0) vm->s.stack_frame_count = 8;
+    if (vm->s.vcpu_count <= 0) {
+        vm->s.vcpu_begin = 0;
+        vm->s.vcpu_count = vm->s.vcpus;
+    }
+    if (vm->s.vcpu_begin < 0 || vm->s.vcpu_begin + vm->s.vcpu_count > vm->s.vcpus) {
+        delete vm;
+        return MIMIC_EINVAL;
+    }
+    if (stack_size(vm) % 8 != 0 || stack_size(vm) > (1u << 20)) {
+        delete vm;
+        return MIMIC_EINVAL;
+    }
+    if (hipSetDevice(vm->s.device) != hipSuccess || hipStreamCreateWithFlags(&vm->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete vm;
+        return MIMIC_EDEVICE;
+    }
+    *out = vm;
+    return 0;
+}
+
+void mimic_vm_destroy(mimic_vm *vm) {
+    if (!vm) return;
+    hipSetDevice(vm->s.device);
+    if (vm->stream) hipStreamSynchronize(vm->stream);
+    hipFree(vm->arena);
+    hipFree(vm->d_insns);
+    hipFree(vm->d_progs);
+    hipFree(vm->d_segs);
+    hipFree(vm->d_maps);
+    hipFree(vm->priv);
+    hipFree(vm->d_sched_start);
+    hipFree(vm->d_sched_pkts);
+    hipFree(vm->d_lane_steps);
+    if (vm->stream) hipStreamDestroy(vm->stream);
+    delete vm;
+}
+
+// MapSpecToLinuxMap (emulator_linux_map.go:57-113) + Init + AddMap
+int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id) {
+    if (!vm || !spec || !map_id) return MIMIC_EINVAL;
+    hipSetDevice(vm->s.device);
+    std::string name = spec->name ? spec->name : "";
+    for (auto &m : vm->maps)
+        if (m.name == name) return fail(vm, MIMIC_EINVAL, "map with name '%s' already exists in emulator", name.c_str());
+    HostMap m{};
+    m.name = name;
+    m.type = spec->type;
+    m.key_size = spec->key_size;
+    m.value_size = spec->value_size;
+    m.max_entries = spec->max_entries;
+    m.datasec = (spec->flags & MIMIC_MAP_F_DATASEC) ? 1 : 0;
+    const uint32_t id = (uint32_t)vm->maps.size();
+    const uint64_t vbytes = (uint64_t)spec->max_entries * spec->value_size;
+    if (vbytes > 0xffffffffull) return fail(vm, MIMIC_EINVAL, "map too large");
+    const uint32_t ES = (uint32_t)vbytes;
+    switch (spec->type) {
+    case 2: case 3: case 12: case 14: case 15: case 16: case 17: case 8: case 20: {
+        // LinuxArrayMap.Init, emulator_linux_map_array.go:30-54
+        m.family = FAM_ARRAY;
+        int rc = arena_reserve(vm, ES, &m.dev_off);
+        if (rc) return rc;
+        m.obj_addr = add_entry(vm, 8);
+        m.backing_addr = add_entry(vm, ES);
+        m.ncpu = 1;
+        Seg o{};
+        o.lo = m.obj_addr;
+        o.hi = m.obj_addr + 8;
+        o.kind = SEG_ARRAY_OBJ;
+        o.id = id;
+        o.dev_off = m.dev_off;
+        o.size = ES;
+        o.datasec = m.datasec;
+        vm->segs.push_back(o);
+        Seg b{};
+        b.lo = m.backing_addr;
+        b.hi = m.backing_addr + ES;
+        b.kind = SEG_PLAIN;
+        b.id = id;
+        b.dev_off = m.dev_off;
+        b.size = ES;
+        vm->segs.push_back(b);
+        break;
+    }
+    case 6: {
+        // LinuxPerCPUArrayMap.Init, emulator_linux_map_array.go:185-215
+        m.family = FAM_PERCPU_ARRAY;
+        const uint32_t V = (uint32_t)vm->s.vcpus;
+        int rc = arena_reserve(vm, (uint64_t)ES * V, &m.dev_off);
+        if (rc) return rc;
+        m.dev_stride = ES;
+        m.obj_addr = add_entry(vm, 8);
+        Seg o{};
+        o.lo = m.obj_addr;
+        o.hi = m.obj_addr + 8;
+        o.kind = SEG_MAP_OBJ;
+        o.id = id;
+        vm->segs.push_back(o);
+        const uint32_t first = vm->next_addr;
+        const uint64_t period = (uint64_t)ES + 10;
+        if ((uint64_t)first + period * V > 0xffffffffull) return fail(vm, MIMIC_ENOMEM, "out of memory (32-bit address space)");
+        vm->next_addr = (uint32_t)(first + period * V);
+        m.backing_addr = first + 9;
+        m.addr_period = (uint32_t)period;
+        m.ncpu = V;
+        Seg g{};
+        g.lo = first;
+        g.hi = (uint32_t)(first + period * (V - 1) + 9 + ES);
+        g.kind = SEG_PERCPU_ARRAY;
+        g.id = id;
+        g.dev_off = m.dev_off;
+        g.size = ES;
+        g.period = (uint32_t)period;
+        g.count = V;
+        g.datasec = m.datasec;
+        g.dev_stride = ES;
+        vm->segs.push_back(g);
+        break;
+    }
+    case 1: case 5: case 13: case 18: case 19: case 21: case 24: case 25: case 26: case 28: case 29:
+        return fail(vm, MIMIC_ENOTSUP, "hash-family maps are not supported by this engine build yet");
+    default:
+        return fail(vm, MIMIC_ENOTSUP, "unsupported map type '%u'", spec->type);
+    }
+    vm->maps.push_back(m);
+    vm->tables_dirty = true;
+    *map_id = id;
+    return 0;
+}
+
+static int map_check(mimic_vm *vm, uint32_t id) {
+    if (!vm) return MIMIC_EINVAL;
+    if (id >= vm->maps.size()) return fail(vm, MIMIC_ENOENT, "no map %u", id);
+    hipSetDevice(vm->s.device);
+    return 0;
+}
+
+// cpu-resolved array backing offset; returns <0 on error (fatal in the reference)
+static int array_cpu(mimic_vm *vm, const HostMap &m, int32_t cpu, uint64_t *base) {
+    if (m.family == FAM_PERCPU_ARRAY) {
+        if (cpu < 0 || (uint32_t)cpu >= m.ncpu) return fail(vm, MIMIC_EINVAL, "invalid cpuid");
+        *base = m.dev_off + (uint64_t)cpu * m.dev_stride;
+    } else {
+        *base = m.dev_off;
+    }
+    return 0;
+}
+
+// LinuxArrayMap.Update / LinuxPerCPUArrayMap.Update (emulator_linux_map_array.go:97-113, 244-250)
+int mimic_map_update(mimic_vm *vm, uint32_t id, const void *key, const void *value, uint32_t flags, int32_t cpu) {
+    (void)flags;  // Q10: flags are ignored
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    uint64_t base;
+    if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
+    if (m.key_size != 4) return fail(vm, MIMIC_EINVAL, "invalid key length, must be 4 bytes for array maps");
+    uint32_t k;
+    memcpy(&k, key, 4);
+    if (k >= m.max_entries) return 7;  // syscall.E2BIG
+    HIP_OK(vm, hipMemcpy(vm->arena + base + (uint64_t)k * m.value_size, value, m.value_size, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int mimic_map_lookup(mimic_vm *vm, uint32_t id, const void *key, int32_t cpu, uint32_t *addr_out) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    uint64_t base;
+    if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
+    if (m.key_size != 4) return fail(vm, MIMIC_EINVAL, "invalid key length, must be 4 bytes for array maps");
+    uint32_t k;
+    memcpy(&k, key, 4);
+    uint32_t b = m.backing_addr + (m.family == FAM_PERCPU_ARRAY ? (uint32_t)cpu * m.addr_period : 0u);
+    *addr_out = k >= m.max_entries ? 0 : b + k * m.value_size;
+    return 0;
+}
+
+int mimic_map_delete(mimic_vm *vm, uint32_t id, const void *key) {
+    (void)key;
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    return fail(vm, MIMIC_EINVAL, "can't delete from given LinuxMap");
+}
+
+int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, size_t cap) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    uint64_t base;
+    if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
+    uint64_t n = (uint64_t)m.max_entries * m.value_size;
+    if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
+    if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
+    HIP_OK(vm, hipMemcpy(out, vm->arena + base, n, hipMemcpyDeviceToHost));
+    return (int)n;
+}
+
+int mimic_map_sum_u64(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_end, uint64_t *out, size_t cap) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    if (m.value_size != 8) return fail(vm, MIMIC_EINVAL, "value size must be 8");
+    if (cap < m.max_entries) return fail(vm, MIMIC_EINVAL, "buffer too small");
+    uint32_t c0 = 0, c1 = 1;
+    if (m.family == FAM_PERCPU_ARRAY) {
+        if (cpu_begin < 0 || cpu_end > (int32_t)m.ncpu || cpu_begin >= cpu_end) return fail(vm, MIMIC_EINVAL, "bad cpu range");
+        c0 = (uint32_t)cpu_begin;
+        c1 = (uint32_t)cpu_end;
+    }
+    uint64_t *d = nullptr;
+    HIP_OK(vm, hipMalloc(&d, m.max_entries * sizeof(uint64_t)));
+    hipStream_t st = vm->last_stream ? vm->last_stream : vm->stream;
+    hipError_t e = hipSuccess;
+    if (mimic_launch_sum_u64(vm->arena + m.dev_off + (uint64_t)c0 * m.dev_stride, m.dev_stride, m.max_entries, c1 - c0,
+                             d, st))
+        e = hipErrorLaunchFailure;
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, m.max_entries * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipFree(d);
+    if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "sum: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int mimic_map_addr(mimic_vm *vm, uint32_t id, uint32_t *addr_out) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    *addr_out = vm->maps[id].obj_addr;
+    return 0;
+}
+
+// VM.AddProgram (vm.go:98-139) + LinuxEmulator.RewriteProgram (emulator_linux_.go:292-339)
+int mimic_program_load(mimic_vm *vm, const char *name, const void *insns, uint32_t n_slots,
+                       const mimic_reloc *relocs, uint32_t n_relocs, uint32_t *prog_id) {
+    if (!vm || (!insns && n_slots) || !prog_id) return MIMIC_EINVAL;
+    if (n_slots >= (1u << MIMIC_PC_BITS)) return fail(vm, MIMIC_EINVAL, "program too long");
+    if (vm->progs.size() >= (1u << (32 - MIMIC_PC_BITS)) - 1) return fail(vm, MIMIC_EINVAL, "too many programs");
+    hipSetDevice(vm->s.device);
+    const uint8_t *raw = (const uint8_t *)insns;
+    HostProg p;
+    p.name = name ? name : "";
+    p.ins.resize(n_slots);
+    // cilium/ebpf v0.9.0 asm.Instruction.Unmarshal + the Nop after LD_IMM64 (vm.go:102-112)
+    for (uint32_t i = 0; i < n_slots; i++) {
+        const uint8_t *b = raw + 8ull * i;
+        uint32_t op = b[0], dst = b[1] & 0xf, src = b[1] >> 4;
+        uint16_t off = (uint16_t)(b[2] | (b[3] << 8));
+        int32_t imm;
+        memcpy(&imm, b + 4, 4);
+        DInsn d{};
+        d.w = op | (dst << 8) | (src << 12) | ((uint32_t)off << 16);
+        d.k = (uint64_t)(int64_t)imm;
+        if (op == 0x18) {
+            if (i + 1 >= n_slots) return fail(vm, MIMIC_EINVAL, "64bit immediate is missing second half");
+            const uint8_t *c = b + 8;
+            if (c[0] | c[1] | c[2] | c[3]) return fail(vm, MIMIC_EINVAL, "64bit immediate has non-zero fields");
+            uint32_t hi;
+            memcpy(&hi, c + 4, 4);
+            d.k = ((uint64_t)hi << 32) | (uint32_t)imm;
+            p.ins[i] = d;
+            p.ins[++i] = DInsn{0, 0, 0};
+            continue;
+        }
+        p.ins[i] = d;
+    }
+    for (uint32_t r = 0; r < n_relocs; r++) {
+        uint32_t s = relocs[r].slot;
+        if (s >= n_slots) return fail(vm, MIMIC_EINVAL, "relocation slot %u out of range", s);
+        DInsn &d = p.ins[s];
+        uint32_t op = d.w & 0xff, src = (d.w >> 12) & 0xf;
+        if (!(op == 0x18 && (src == 1 || src == 2))) continue;  // !IsLoadFromMap
+        if (relocs[r].map_id >= vm->maps.size())
+            return fail(vm, MIMIC_EINVAL, "program references a map that does not exist in the emulator");
+        uint32_t a = vm->maps[relocs[r].map_id].obj_addr;
+        if (src == 1) d.k = a;                                        // PseudoMapFD
+        else d.k = (uint64_t)((int64_t)a + (int64_t)(int16_t)(d.w >> 16));  // PseudoMapValue (Q16)
+    }
+    p.addr = add_entry(vm, 8);
+    Seg g{};
+    g.lo = p.addr;
+    g.hi = p.addr + 8;
+    g.kind = SEG_PROG;
+    g.id = (uint32_t)vm->progs.size();
+    vm->segs.push_back(g);
+    vm->progs.push_back(std::move(p));
+    vm->tables_dirty = true;
+    *prog_id = g.id;
+    return 0;
+}
+
+int mimic_program_addr(mimic_vm *vm, uint32_t prog_id, uint32_t *addr_out) {
+    if (!vm || prog_id >= vm->progs.size()) return MIMIC_EINVAL;
+    *addr_out = vm->progs[prog_id].addr;
+    return 0;
+}
+
+int mimic_stack_addr(mimic_vm *vm, uint32_t *addr_out) {
+    if (!vm) return MIMIC_EINVAL;
+    *addr_out = vm->next_addr;
+    return 0;
+}
+
+int mimic_mem_read(mimic_vm *vm, uint32_t addr, void *buf, uint32_t len) {
+    if (!vm) return MIMIC_EINVAL;
+    hipSetDevice(vm->s.device);
+    HostRef R = host_resolve(vm, addr);
+    if (R.kind == 0) return fail(vm, MIMIC_EFAULT, "memory controller can't resolve address 0x%x", addr);
+    if (R.kind == 2) return fail(vm, MIMIC_EFAULT, "not vm memory 0x%x", addr);
+    if (R.kind == 3) return fail(vm, MIMIC_EFAULT, "Can't access non-data-section array map directly");
+    if ((uint64_t)R.off + len > R.limit) return fail(vm, MIMIC_EFAULT, "out of bounds");
+    if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
+    HIP_OK(vm, hipMemcpy(buf, vm->arena + R.dev_off + R.off, len, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out) {
+    if (size != 1 && size != 2 && size != 4 && size != 8) return MIMIC_EINVAL;
+    uint64_t v = 0;
+    int rc = mimic_mem_read(vm, addr, &v, (uint32_t)size);
+    if (rc) return rc;
+    *out = v;
+    return 0;
+}
+
+// the batch form of NewProcess / SetCPUID / Run / Cleanup
+int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
+                  void *hip_stream) {
+    if (!vm || !b || !res) return MIMIC_EINVAL;
+    if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
+    if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
+    hipSetDevice(vm->s.device);
+    int rc = upload_tables(vm);
+    if (rc) return rc;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
+    const uint32_t lanes = (uint32_t)vm->s.vcpu_count;
+    const uint32_t S = stack_size(vm);
+    // private memory: stack | xdp_md overlay | saved frames, qword-interleaved over lanes
+    const uint32_t stack_q = S / 8;
+    const uint32_t xdp_q = stack_q;
+    const uint32_t frame_q = xdp_q + 3;
+    const uint32_t q_per_lane = frame_q + MIMIC_MAX_FRAMES * MIMIC_FRAME_QWORDS;
+    const uint32_t plan = (lanes + 255) & ~255u;
+    const uint64_t need = (uint64_t)q_per_lane * plan * 8;
+    if (need > vm->priv_bytes || plan != vm->priv_lanes) {
+        hipStreamSynchronize(st);
+        hipFree(vm->priv);
+        vm->priv = nullptr;
+        HIP_OK(vm, hipMalloc(&vm->priv, need));
+        vm->priv_bytes = need;
+        vm->priv_lanes = plan;
+    }
+    if (lanes > vm->lane_steps_cap) {
+        hipStreamSynchronize(st);
+        hipFree(vm->d_lane_steps);
+        vm->d_lane_steps = nullptr;
+        HIP_OK(vm, hipMalloc(&vm->d_lane_steps, (uint64_t)plan * sizeof(uint64_t)));
+        vm->lane_steps_cap = plan;
+    }
+    KParams kp{};
+    kp.insns = vm->d_insns;
+    kp.progs = vm->d_progs;
+    kp.segs = vm->d_segs;
+    kp.maps = vm->d_maps;
+    kp.arena = vm->arena;
+    kp.nprogs = (uint32_t)vm->progs.size();
+    kp.nsegs = (uint32_t)vm->segs.size();
+    kp.nmaps = (uint32_t)vm->maps.size();
+    kp.entry_prog = prog_id;
+    kp.static_next = vm->next_addr;
+    kp.stack_size = S;
+    kp.frame_size = (uint32_t)vm->s.stack_frame_size;
+    uint32_t shift = 3;
+    while ((S >> shift) > 64) shift++;
+    kp.chunk_shift = shift;
+    kp.max_tail_calls = (uint32_t)std::max(0, vm->s.max_tail_calls);
+    kp.total_vcpus = (uint32_t)vm->s.vcpus;
+    kp.vcpu_begin = (uint32_t)vm->s.vcpu_begin;
+    kp.lanes = lanes;
+    kp.priv_lanes = vm->priv_lanes;
+    kp.priv = vm->priv;
+    kp.priv_xdp_q = xdp_q;
+    kp.priv_frame_q = frame_q;
+    kp.budget = b->step_budget ? b->step_budget : MIMIC_DEFAULT_BUDGET;
+    kp.n = b->n;
+    kp.sched = b->schedule;
+    kp.pkt_data = b->pkt_data;
+    kp.pkt_off = b->pkt_off;
+    kp.pkt_len = b->pkt_len;
+    kp.headroom_arr = b->headroom;
+    kp.tailroom_arr = b->tailroom;
+    kp.ingress_arr = b->ingress_ifindex;
+    kp.rxq_arr = b->rx_queue_index;
+    kp.egress_arr = b->egress_ifindex;
+    kp.headroom = b->headroom_all;
+    kp.tailroom = b->tailroom_all;
+    kp.ingress = b->ingress_all;
+    kp.rxq = b->rxq_all;
+    kp.egress = b->egress_all;
+    kp.r0 = res->r0;
+    kp.status = res->status;
+    kp.steps = res->steps;
+    kp.err_pc = res->err_pc;
+    kp.lane_steps = vm->d_lane_steps;
+    switch (b->schedule) {
+    case MIMIC_SCHED_CHUNKED:
+        kp.per_lane = lanes ? (uint32_t)(((uint64_t)b->n + lanes - 1) / lanes) : 0;
+        break;
+    case MIMIC_SCHED_INTERLEAVED:
+        kp.per_lane = lanes ? (uint32_t)(((uint64_t)b->n + lanes - 1) / lanes) : 0;
+        break;
+    case MIMIC_SCHED_EXPLICIT: {
+        if (!b->cpu && b->n) return fail(vm, MIMIC_EINVAL, "explicit schedule needs cpu[]");
+        // stable counting sort of packets by vCPU (each vCPU runs its packets in order)
+        std::vector<uint32_t> start(lanes + 1, 0), pk(b->n);
+        for (uint32_t i = 0; i < b->n; i++) {
+            int64_t c = (int64_t)b->cpu[i] - vm->s.vcpu_begin;
+            if (c < 0 || c >= (int64_t)lanes) return fail(vm, MIMIC_EINVAL, "packet %u: cpu %d not on this engine", i, b->cpu[i]);
+            start[c + 1]++;
+        }
+        uint32_t mx = 0;
+        for (uint32_t c = 0; c < lanes; c++) {
+            mx = std::max(mx, start[c + 1]);
+            start[c + 1] += start[c];
+        }
+        std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+        for (uint32_t i = 0; i < b->n; i++) pk[fill[b->cpu[i] - vm->s.vcpu_begin]++] = i;
+        hipStreamSynchronize(st);
+        if (start.size() > vm->sched_cap_start) {
+            hipFree(vm->d_sched_start);
+            vm->d_sched_start = nullptr;
+            HIP_OK(vm, hipMalloc(&vm->d_sched_start, start.size() * 4));
+            vm->sched_cap_start = start.size();
+        }
+        if (pk.size() > vm->sched_cap_pkts || !vm->d_sched_pkts) {
+            hipFree(vm->d_sched_pkts);
+            vm->d_sched_pkts = nullptr;
+            HIP_OK(vm, hipMalloc(&vm->d_sched_pkts, std::max<size_t>(pk.size(), 1) * 4));
+            vm->sched_cap_pkts = std::max<size_t>(pk.size(), 1);
+        }
+        HIP_OK(vm, hipMemcpy(vm->d_sched_start, start.data(), start.size() * 4, hipMemcpyHostToDevice));
+        if (!pk.empty()) HIP_OK(vm, hipMemcpy(vm->d_sched_pkts, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+        kp.sched_start = vm->d_sched_start;
+        kp.sched_pkts = vm->d_sched_pkts;
+        kp.per_lane = mx;
+        break;
+    }
+    default:
+        return fail(vm, MIMIC_EINVAL, "unknown schedule %u", b->schedule);
+    }
+    if (mimic_launch_xdp(&kp, st)) return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    vm->last_lanes = lanes;
+    vm->last_stream = st;
+    return 0;
+}
+
+int mimic_sync(mimic_vm *vm, void *hip_stream) {
+    if (!vm) return MIMIC_EINVAL;
+    hipSetDevice(vm->s.device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
+    HIP_OK(vm, hipStreamSynchronize(st));
+    return 0;
+}
+
+int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out) {
+    if (!vm || !steps_out) return MIMIC_EINVAL;
+    hipSetDevice(vm->s.device);
+    *steps_out = 0;
+    if (!vm->last_lanes) return 0;
+    if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
+    std::vector<uint64_t> h(vm->last_lanes);
+    HIP_OK(vm, hipMemcpy(h.data(), vm->d_lane_steps, h.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t t = 0;
+    for (uint64_t v : h) t += v;
+    *steps_out = t;
+    return 0;
+}
+
+}  // extern "C"

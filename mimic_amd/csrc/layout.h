@@ -1,0 +1,126 @@
+// layout.h -- data layout shared by the host engine (engine.cpp) and the gfx950 batch
+// interpreter (interp.hip).  Plain structs only; no torch, no STL.
+//
+// The virtual 32-bit address space reproduces the reference's MemoryController layout
+// (memory_controller.go:58-112: first fit from 0x10000, one unused byte between entries).
+// Static entries (maps, programs) are created once on the host; every process of a batch
+// then gets the SAME three per-process entries appended after them (stack, packet,
+// xdp_md -- vm.go:218, context_xdp_md.go:66,107), because Cleanup removes them again
+// (vm.go:363-374).  So each lane can compute its addresses in O(1):
+//   St = static_next            stack  [St, St+S]            (S = frame_size*frame_count)
+//   P  = St + S + 1             packet [P, P+M]              (M = headroom+len+tailroom)
+//   X  = P + M + 1              xdp_md [X, X+24]
+// Static entries are summarised as a short sorted segment table (one segment per
+// entry, except the V per-CPU sub-arrays of a per-CPU array map, which are one strided
+// group segment, emulator_linux_map_array.go:185-215).
+#pragma once
+#include <stdint.h>
+
+#define MIMIC_MAX_FRAMES 32u          // engine bound on BPF-to-BPF call depth (oracle: ORC_MAX_FRAMES)
+#define MIMIC_DEFAULT_BUDGET (1ull << 22)
+#define MIMIC_MEM_START 0x10000u      // memStart + 1, memory_controller.go:55,70
+#define MIMIC_PC_BITS 20u             // wave-min key = prog << 20 | pc
+#define MIMIC_XDP_MD_SIZE 24u         // context_xdp_md.go:57
+#define MIMIC_FRAME_QWORDS 5u         // saved PC + R6..R9 (inst.go:277-296)
+
+enum SegKind : uint32_t {
+    SEG_PLAIN = 1,            // PlainMemory backing in the arena
+    SEG_ARRAY_OBJ = 2,        // LinuxArrayMap object (8 B): LinuxMap; VMMem only if datasec
+    SEG_MAP_OBJ = 3,          // per-CPU array / hash / per-CPU hash object: LinuxMap, not VMMem
+    SEG_PROG = 4,             // *ebpf.ProgramSpec: neither
+    SEG_PERCPU_ARRAY = 5,     // V x [sub-array object (8 B) | gap | backing (E*S) | gap]
+    SEG_PERCPU_VALUES = 6,    // V x [values backing (E*S) | gap]   (per-CPU hash values)
+};
+
+enum MapFamily : uint32_t { FAM_ARRAY = 1, FAM_PERCPU_ARRAY = 2, FAM_HASH = 3, FAM_PERCPU_HASH = 4 };
+
+struct Seg {
+    uint32_t lo, hi;        // [lo, hi] inclusive address range covered
+    uint32_t kind;          // SegKind
+    uint32_t id;            // map index (objects, groups, plain backings of maps) or prog index
+    uint64_t dev_off;       // arena offset: PLAIN backing / group cpu-0 backing
+    uint32_t size;          // PLAIN: backing size; groups: per-cpu backing size (E*S)
+    uint32_t period;        // groups: address distance between consecutive cpus
+    uint32_t count;         // groups: number of cpus
+    uint32_t datasec;       // ARRAY_OBJ / SEG_PERCPU_ARRAY sub-objects: Spec.Value is *btf.Datasec
+    uint64_t dev_stride;    // groups: arena distance between consecutive cpu backings
+};
+
+struct DMap {
+    uint32_t family, type, key_size, value_size, max_entries, datasec;
+    uint32_t obj_addr;       // map object address
+    uint32_t backing_addr;   // ARRAY: values backing; PERCPU_ARRAY: cpu-0 backing; HASH: values; PERCPU_HASH: cpu-0 values
+    uint32_t addr_period;    // per-CPU: address distance between cpu backings
+    uint32_t ncpu;           // per-CPU: number of cpus (len(arrayMaps) / len(values))
+    uint64_t dev_off;        // arena offset of cpu-0 backing
+    uint64_t dev_stride;     // arena distance between cpu backings
+    // hash maps (device open-addressing index, see hashmap notes in engine.cpp)
+    uint64_t keys_dev_off;   // arena offset of the keys backing
+    uint32_t keys_addr;
+    uint32_t ht_cap;         // power of two
+    uint64_t ht_dev_off;     // arena offset of int32 slot table [ht_cap]
+    uint64_t fl_dev_off;     // arena offset of the freelist ring (int32 [E+1]) + head/len words
+};
+
+struct DProg {
+    uint32_t base;   // first instruction in the concatenated instruction array
+    uint32_t n;      // len(Program.Instructions)
+    uint32_t addr;   // program object address
+    uint32_t pad;
+};
+
+// A decoded instruction slot: w = op | dst<<8 | src<<12 | (uint16)off<<16, k = asm.Instruction.Constant
+struct DInsn {
+    uint32_t w;
+    uint32_t aux;
+    uint64_t k;
+};
+
+enum Sched : uint32_t { SCHED_CHUNKED = 0, SCHED_INTERLEAVED = 1, SCHED_EXPLICIT = 2 };
+
+struct KParams {
+    // program / static memory
+    const DInsn *insns;
+    const DProg *progs;
+    const Seg *segs;
+    const DMap *maps;
+    uint8_t *arena;
+    uint32_t nprogs, nsegs, nmaps, entry_prog;
+    uint32_t static_next;       // St
+    uint32_t stack_size;        // S
+    uint32_t frame_size;
+    uint32_t chunk_shift;       // lazy-zero granule of the stack (bytes = 1 << shift)
+    uint32_t max_tail_calls;
+    uint32_t total_vcpus;       // V (VMSettings.VirtualCPUs)
+    uint32_t vcpu_begin;        // first vCPU executed by this launch
+    uint32_t lanes;             // vCPUs executed by this launch (= lanes used)
+    uint32_t priv_lanes;        // interleave stride of private memory (>= lanes)
+    uint8_t *priv;              // per-lane private memory, qword-interleaved
+    uint32_t priv_xdp_q;        // qword index of the xdp_md overlay
+    uint32_t priv_frame_q;      // qword index of the saved-frame area
+    uint64_t budget;
+    // batch
+    uint32_t n;
+    uint32_t sched;
+    uint32_t per_lane;          // CHUNKED: chunk; INTERLEAVED/EXPLICIT: max packets per lane
+    uint32_t pad0;
+    uint8_t *pkt_data;
+    const uint64_t *pkt_off;
+    const uint32_t *pkt_len;
+    const uint32_t *headroom_arr;
+    const uint32_t *tailroom_arr;
+    const int32_t *ingress_arr;
+    const int32_t *rxq_arr;
+    const int32_t *egress_arr;
+    uint32_t headroom, tailroom;
+    int32_t ingress, rxq, egress;
+    uint32_t pad1;
+    const uint32_t *sched_start;   // EXPLICIT: CSR over local lanes [lanes+1]
+    const uint32_t *sched_pkts;
+    // results
+    uint64_t *r0;
+    uint8_t *status;
+    uint32_t *steps;
+    int32_t *err_pc;
+    uint64_t *lane_steps;          // optional: per-lane executed steps (insns/s accounting)
+};

@@ -1,0 +1,574 @@
+"""Python mirror of mimic's Go surface for the Process.Run hot path, backed by the C ABI.
+
+Reference names are kept so parity tests read like the reference's own tests
+(emulator_linux_helpers_test.go, emulator_linux_map_array_test.go):
+
+    emu = NewLinuxEmulator()                                 # emulator_linux_.go:67
+    vm = NewVM(VMOptEmulator(emu), VMOptSetvCPUs(2))         # vm.go:54
+    m = LinuxPerCPUArrayMap(Spec=MapSpec(...))               # emulator_linux_map_array.go:177
+    emu.AddMap("per-cpu-array", m)                           # emulator_linux_.go:97
+    m.Update(key, value, 0, CPU0); addr = m.Lookup(key, CPU0)
+    vm.MemoryController.GetEntry(addr) / .Load(addr, 4)     # memory_controller.go:117
+    prog_id = vm.AddProgram(ProgramSpec(...))                # vm.go:98
+    p = vm.NewProcess(prog_id, LinuxContextXDP(Packet=...)) # vm.go:198 + context_xdp_md.go:47
+    p.SetCPUID(0); p.Run(); p.Registers.R0; p.Cleanup()      # vm.go:268,343,363
+
+plus the batch entry point the GPU exists for:
+
+    res = vm.RunXDPBatch(prog_id, XDPBatch.from_packets([...]))   # N processes at once
+
+Errors follow the reference: a graceful map error is a ``syscall.Errno``-like positive int
+(E2BIG = 7) returned by Update; fatal errors raise ``MimicError``.
+"""
+from __future__ import annotations
+
+import base64
+import ctypes as C
+import json
+import os
+from dataclasses import dataclass, field
+from enum import IntEnum
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+from . import _lib as L
+
+
+class MimicError(RuntimeError):
+    pass
+
+
+class MapType(IntEnum):  # ebpf.MapType (cilium/ebpf v0.9.0; kernel numbering)
+    Hash = 1
+    Array = 2
+    ProgramArray = 3
+    PerfEventArray = 4
+    PerCPUHash = 5
+    PerCPUArray = 6
+
+
+E2BIG = 7
+
+
+@dataclass
+class MapSpec:  # ebpf.MapSpec (the fields the emulator reads)
+    Name: str
+    Type: int
+    KeySize: int
+    ValueSize: int
+    MaxEntries: int
+    Datasec: bool = False  # Spec.Value is a *btf.Datasec
+
+
+@dataclass
+class ProgramSpec:  # ebpf.ProgramSpec: raw instruction slots + map references
+    Name: str
+    Instructions: bytes
+    References: List[Tuple[int, str]] = field(default_factory=list)  # (slot, map name)
+
+
+def _check(vm_handle, rc: int, what: str) -> int:
+    if rc < 0:
+        lib = L.load()
+        msg = lib.mimic_last_error(vm_handle) if vm_handle else b""
+        raise MimicError(f"{what}: {msg.decode(errors='replace') if msg else rc}")
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------
+# emulator + maps
+# ---------------------------------------------------------------------------------------------
+
+def OptMaxTailCalls(n: int):
+    return ("max_tail_calls", n)
+
+
+class LinuxEmulator:
+    """emulator_linux_.go:55-64.  Maps are created on the device when the emulator is attached
+    to a VM (the reference's Init needs the VM's memory controller too, vm.go:73)."""
+
+    def __init__(self, MaxTailCalls: int = 33):
+        self.MaxTailCalls = MaxTailCalls
+        self.Maps: Dict[str, "LinuxMap"] = {}
+        self.vm: Optional["VM"] = None
+
+    def SetVM(self, vm: "VM") -> None:  # emulator_linux_.go:120-122
+        self.vm = vm
+
+    def AddMap(self, name: str, m: "LinuxMap") -> None:  # emulator_linux_.go:97-116
+        if self.vm is None:
+            raise MimicError("emulator is not attached to a VM")
+        if name in self.Maps:
+            raise MimicError(f"map with name '{name}' already exists in emulator")
+        m.Init(self)
+        self.Maps[name] = m
+
+
+def NewLinuxEmulator(*opts) -> LinuxEmulator:
+    emu = LinuxEmulator()
+    for k, v in opts:
+        setattr(emu, {"max_tail_calls": "MaxTailCalls"}[k], v)
+    return emu
+
+
+class LinuxMap:
+    """Common LinuxMap surface (emulator_linux_map.go:14-54) over a device-resident map."""
+
+    def __init__(self, Spec: MapSpec):
+        self.Spec = Spec
+        self.id: Optional[int] = None
+        self.emulator: Optional[LinuxEmulator] = None
+
+    # LinuxMap.Init
+    def Init(self, emulator: LinuxEmulator) -> None:
+        vm = emulator.vm
+        spec = L.MapSpecC(self.Spec.Name.encode(), int(self.Spec.Type), self.Spec.KeySize, self.Spec.ValueSize,
+                          self.Spec.MaxEntries, L.MAP_F_DATASEC if self.Spec.Datasec else 0)
+        mid = C.c_uint32()
+        _check(vm.h, vm.lib.mimic_map_create(vm.h, C.byref(spec), C.byref(mid)), "map init")
+        self.id = mid.value
+        self.emulator = emulator
+
+    @property
+    def _vm(self) -> "VM":
+        return self.emulator.vm
+
+    def GetSpec(self) -> MapSpec:
+        return self.Spec
+
+    def Indices(self) -> int:
+        return 1
+
+    def Lookup(self, key: bytes, cpuid: int = 0) -> int:
+        """Virtual address of the value, 0 if absent (LinuxMap.Lookup)."""
+        vm = self._vm
+        addr = C.c_uint32()
+        kb = C.create_string_buffer(bytes(key), max(len(key), 1))
+        _check(vm.h, vm.lib.mimic_map_lookup(vm.h, self.id, kb, cpuid, C.byref(addr)), "lookup")
+        return addr.value
+
+    def Update(self, key: bytes, value: bytes, flags: int = 0, cpuid: int = 0) -> int:
+        """0 on success or a positive errno (graceful, e.g. E2BIG); raises on fatal errors."""
+        vm = self._vm
+        if len(value) != self.Spec.ValueSize:
+            raise MimicError(f"invalid value length, must be {self.Spec.ValueSize} bytes")
+        kb = C.create_string_buffer(bytes(key), max(len(key), 1))
+        vb = C.create_string_buffer(bytes(value), max(len(value), 1))
+        return _check(vm.h, vm.lib.mimic_map_update(vm.h, self.id, kb, vb, flags, cpuid), "update")
+
+    def Delete(self, key: bytes) -> int:
+        vm = self._vm
+        kb = C.create_string_buffer(bytes(key), max(len(key), 1))
+        return _check(vm.h, vm.lib.mimic_map_delete(vm.h, self.id, kb), "delete")
+
+    def Values(self, cpuid: int = 0) -> bytes:
+        """Raw value backing (MaxEntries * ValueSize bytes) of one cpu."""
+        vm = self._vm
+        n = self.Spec.MaxEntries * self.Spec.ValueSize
+        buf = C.create_string_buffer(max(n, 1))
+        _check(vm.h, vm.lib.mimic_map_read_values(vm.h, self.id, cpuid, buf, max(n, 1)), "read values")
+        return buf.raw[:n]
+
+    def SumU64(self, cpu_begin: int = 0, cpu_end: Optional[int] = None) -> List[int]:
+        """Per-key sum over vCPUs of a u64-valued map (device reduction)."""
+        vm = self._vm
+        if cpu_end is None:
+            cpu_end = vm.settings.vcpus if isinstance(self, LinuxPerCPUArrayMap) else 1
+        out = (C.c_uint64 * self.Spec.MaxEntries)()
+        _check(vm.h, vm.lib.mimic_map_sum_u64(vm.h, self.id, cpu_begin, cpu_end, out, self.Spec.MaxEntries),
+               "sum")
+        return list(out)
+
+    def Address(self) -> int:
+        vm = self._vm
+        a = C.c_uint32()
+        _check(vm.h, vm.lib.mimic_map_addr(vm.h, self.id, C.byref(a)), "map addr")
+        return a.value
+
+
+class LinuxArrayMap(LinuxMap):  # emulator_linux_map_array.go:21-168
+    def Keys(self, cpuid: int = 0) -> bytes:
+        return b"".join(i.to_bytes(4, "little") for i in range(self.Spec.MaxEntries))
+
+    def UpdateProgram(self, key: bytes, prog_id: int, flags: int = 0) -> int:
+        """Store a program's address (what a ProgramArray value holds, read at
+        emulator_linux_helpers.go:707)."""
+        vm = self._vm
+        return self.Update(key, vm.ProgramAddress(prog_id).to_bytes(4, "little"), flags, 0)
+
+
+class LinuxPerCPUArrayMap(LinuxMap):  # emulator_linux_map_array.go:177-250
+    def Indices(self) -> int:
+        return self._vm.settings.vcpus
+
+    def Keys(self, cpuid: int = 0) -> bytes:
+        return b"".join(i.to_bytes(4, "little") for i in range(self.Spec.MaxEntries))
+
+
+def MapSpecToLinuxMap(spec: MapSpec) -> LinuxMap:  # emulator_linux_map.go:57-113
+    t = int(spec.Type)
+    if t in (2, 3, 8, 12, 14, 15, 16, 17, 20):
+        return LinuxArrayMap(spec)
+    if t == 6:
+        return LinuxPerCPUArrayMap(spec)
+    raise MimicError(f"unsupported map type '{t}' in this engine build")
+
+
+# ---------------------------------------------------------------------------------------------
+# contexts
+# ---------------------------------------------------------------------------------------------
+
+@dataclass
+class LinuxContextXDP:  # context_xdp_md.go:22-34
+    Headroom: int = 0
+    Tailroom: int = 0
+    Packet: bytes = b""
+    IngessIfIndex: int = 0
+    RxQueueIndex: int = 0
+    EgressIfIndex: int = 0
+    Name: str = ""
+
+
+def UnmarshalContextJSON(text: str):
+    """context.go:57-71 + context_xdp_md.go:10-19 (xdp_md only)."""
+    obj = json.loads(text)
+    if obj.get("type") != "xdp_md":
+        raise MimicError(f"no context unmarshaller registered for type '{obj.get('type')}'")
+    c = obj.get("ctx") or {}
+    pkt = c.get("packet")
+    return LinuxContextXDP(Headroom=int(c.get("headroom", 0)), Tailroom=int(c.get("tailroom", 0)),
+                           Packet=base64.b64decode(pkt) if pkt else b"",
+                           IngessIfIndex=int(c.get("ingress_ifidx", 0)), RxQueueIndex=int(c.get("rx_queue_idx", 0)),
+                           EgressIfIndex=int(c.get("egress_ifidx", 0)), Name=obj.get("name", ""))
+
+
+# ---------------------------------------------------------------------------------------------
+# VM
+# ---------------------------------------------------------------------------------------------
+
+def VMOptEmulator(e: LinuxEmulator):
+    return ("emulator", e)
+
+
+def VMOptSetvCPUs(n: int):
+    return ("vcpus", n)
+
+
+def VMOptDevice(d: int):
+    return ("device", d)
+
+
+def VMOptShard(begin: int, count: int):
+    """Execute only vCPUs [begin, begin+count) on this engine (multi-GPU sharding)."""
+    return ("shard", (begin, count))
+
+
+@dataclass
+class VMSettings:
+    vcpus: int
+    stack_frame_size: int = 256
+    stack_frame_count: int = 8
+    device: int = 0
+    vcpu_begin: int = 0
+    vcpu_count: int = 0
+
+
+class MemoryControllerView:
+    """Host inspection of device-resident static memory (memory_controller.go:117-145 + VMMem)."""
+
+    def __init__(self, vm: "VM"):
+        self.vm = vm
+
+    def Read(self, addr: int, n: int) -> bytes:
+        buf = C.create_string_buffer(max(n, 1))
+        _check(self.vm.h, self.vm.lib.mimic_mem_read(self.vm.h, addr, buf, n), "mem read")
+        return buf.raw[:n]
+
+    def Load(self, addr: int, size: int) -> int:
+        v = C.c_uint64()
+        _check(self.vm.h, self.vm.lib.mimic_mem_load(self.vm.h, addr, size, C.byref(v)), "mem load")
+        return v.value
+
+
+class VM:
+    def __init__(self, emulator: LinuxEmulator, settings: VMSettings):
+        if emulator is None:  # vm.go:73 calls SetVM on a nil emulator
+            raise MimicError("NewVM requires an emulator (the reference panics without one)")
+        self.lib = L.load()
+        self.settings = settings
+        s = L.VMSettings(settings.vcpus, settings.stack_frame_size, settings.stack_frame_count,
+                         emulator.MaxTailCalls, settings.device, settings.vcpu_begin, settings.vcpu_count, 0)
+        h = C.c_void_p()
+        rc = self.lib.mimic_vm_create(C.byref(s), C.byref(h))
+        if rc != 0:
+            raise MimicError(f"mimic_vm_create failed ({rc})")
+        self.h = h
+        self.emulator = emulator
+        self.MemoryController = MemoryControllerView(self)
+        self.programs: List[ProgramSpec] = []
+        emulator.SetVM(self)
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.mimic_vm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # vm.go:98-139
+    def AddProgram(self, prog: ProgramSpec) -> int:
+        raw = bytes(prog.Instructions)
+        if len(raw) % 8:
+            raise MimicError("instruction stream is not a multiple of 8 bytes")
+        relocs = []
+        for slot, name in prog.References:
+            m = self.emulator.Maps.get(name)
+            if m is None:
+                raise MimicError(f"program references a map named '{name}', no map with that name exists in the emulator")
+            relocs.append(L.Reloc(slot, m.id))
+        arr = (L.Reloc * max(len(relocs), 1))(*relocs)
+        pid = C.c_uint32()
+        buf = C.create_string_buffer(raw, max(len(raw), 1))
+        _check(self.h, self.lib.mimic_program_load(self.h, prog.Name.encode(), buf, len(raw) // 8, arr, len(relocs),
+                                                   C.byref(pid)), "AddProgram")
+        self.programs.append(prog)
+        return pid.value
+
+    def GetPrograms(self) -> List[ProgramSpec]:
+        return list(self.programs)
+
+    def ProgramAddress(self, prog_id: int) -> int:
+        a = C.c_uint32()
+        _check(self.h, self.lib.mimic_program_addr(self.h, prog_id, C.byref(a)), "program addr")
+        return a.value
+
+    def StackAddress(self) -> int:
+        a = C.c_uint32()
+        _check(self.h, self.lib.mimic_stack_addr(self.h, C.byref(a)), "stack addr")
+        return a.value
+
+    def NewProcess(self, entrypoint: int, ctx: Optional[LinuxContextXDP]) -> "Process":  # vm.go:198-235
+        if entrypoint >= len(self.programs):
+            raise MimicError(f"no program with id '{entrypoint}' is loaded")
+        return Process(self, entrypoint, ctx)
+
+    # ---- batch entry point ------------------------------------------------------------------
+    def RunXDPBatch(self, prog_id: int, batch: "XDPBatch", results: Optional["XDPResults"] = None,
+                    stream=None, sync: bool = True) -> "XDPResults":
+        """N x {NewProcess, SetCPUID, Run, read R0, Cleanup} on the GPU."""
+        import torch
+
+        dev = batch.pkt_data.device
+        if results is None:
+            results = XDPResults.empty(batch.n, dev)
+        b = L.XDPBatch()
+        b.n = batch.n
+        b.schedule = batch.schedule
+        b.pkt_data = batch.pkt_data.data_ptr()
+        b.pkt_off = batch.pkt_off.data_ptr()
+        b.pkt_len = batch.pkt_len.data_ptr()
+        b.headroom = batch.headroom.data_ptr() if isinstance(batch.headroom, torch.Tensor) else None
+        b.headroom_all = 0 if isinstance(batch.headroom, torch.Tensor) else int(batch.headroom)
+        b.tailroom = batch.tailroom.data_ptr() if isinstance(batch.tailroom, torch.Tensor) else None
+        b.tailroom_all = 0 if isinstance(batch.tailroom, torch.Tensor) else int(batch.tailroom)
+        for fld, val in (("ingress_ifindex", batch.ingress), ("rx_queue_index", batch.rxq),
+                         ("egress_ifindex", batch.egress)):
+            allname = {"ingress_ifindex": "ingress_all", "rx_queue_index": "rxq_all",
+                       "egress_ifindex": "egress_all"}[fld]
+            if isinstance(val, torch.Tensor):
+                setattr(b, fld, val.data_ptr())
+                setattr(b, allname, 0)
+            else:
+                setattr(b, fld, None)
+                setattr(b, allname, int(val))
+        cpu_host = None
+        if batch.schedule == L.SCHED_EXPLICIT:
+            import numpy as np
+            cpu_host = np.ascontiguousarray(np.asarray(batch.cpu, dtype=np.int32))
+            b.cpu = cpu_host.ctypes.data
+        else:
+            b.cpu = None
+        b.step_budget = batch.step_budget
+        r = L.XDPResults(results.r0.data_ptr(), results.status.data_ptr(), results.steps.data_ptr(),
+                         results.err_pc.data_ptr())
+        st = stream.cuda_stream if stream is not None else None
+        _check(self.h, self.lib.mimic_run_xdp(self.h, prog_id, C.byref(b), C.byref(r), st), "RunXDPBatch")
+        if sync:
+            _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
+        return results
+
+    def LastSteps(self) -> int:
+        v = C.c_uint64()
+        _check(self.h, self.lib.mimic_last_steps(self.h, C.byref(v)), "last steps")
+        return v.value
+
+
+def NewVM(*opts) -> VM:  # vm.go:54-76
+    emu = None
+    s = VMSettings(vcpus=os.cpu_count() or 1)  # VirtualCPUs defaults to runtime.NumCPU()
+    for k, v in opts:
+        if k == "emulator":
+            emu = v
+        elif k == "vcpus":
+            s.vcpus = v
+        elif k == "device":
+            s.device = v
+        elif k == "shard":
+            s.vcpu_begin, s.vcpu_count = v
+    return VM(emu, s)
+
+
+class Registers:
+    def __init__(self):
+        self.PC = 0
+        self.R0 = 0
+
+
+class Process:
+    """Single process = a one-packet batch on the GPU (the Process.Run drop-in)."""
+
+    def __init__(self, vm: VM, prog_id: int, ctx: Optional[LinuxContextXDP]):
+        self.VM = vm
+        self.prog_id = prog_id
+        self.Context = ctx
+        self.Registers = Registers()
+        self.cpuID = -1
+        self.Steps = 0
+        self.Status = None
+        self.ErrPC = -1
+        self.PacketAfter: Optional[bytes] = None
+
+    def CPUID(self) -> int:
+        return self.cpuID
+
+    def SetCPUID(self, i: int) -> None:  # vm.go:268-283
+        if i < 0:
+            raise MimicError("not a valid CPU ID")
+        if i > self.VM.settings.vcpus:
+            raise MimicError(f"vm only has {self.VM.settings.vcpus} vCPUs")
+        self.cpuID = i
+
+    def Run(self, step_budget: int = 0) -> None:  # vm.go:343-360
+        import torch
+
+        ctx = self.Context or LinuxContextXDP()
+        if self.cpuID < 0 or self.cpuID >= self.VM.settings.vcpus:
+            raise MimicError("process has no valid CPU ID (SetCPUID first)")
+        batch = XDPBatch.from_packets([ctx.Packet], device=f"cuda:{self.VM.settings.device}",
+                                      headroom=ctx.Headroom, tailroom=ctx.Tailroom, ingress=ctx.IngessIfIndex,
+                                      rxq=ctx.RxQueueIndex, egress=ctx.EgressIfIndex,
+                                      schedule=L.SCHED_EXPLICIT, cpu=[self.cpuID], step_budget=step_budget)
+        res = self.VM.RunXDPBatch(self.prog_id, batch)
+        self.Registers.R0 = int(res.r0[0].item()) & 0xFFFFFFFFFFFFFFFF
+        self.Steps = int(res.steps[0].item())
+        self.Status = int(res.status[0].item())
+        self.ErrPC = int(res.err_pc[0].item())
+        self.PacketAfter = batch.packet_bytes(0)
+        if self.Status != 0:
+            raise MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[self.Status]} at PC({self.ErrPC})")
+
+    def Cleanup(self) -> None:
+        pass
+
+
+# ---------------------------------------------------------------------------------------------
+# batch containers (device tensors)
+# ---------------------------------------------------------------------------------------------
+
+class XDPBatch:
+    """A batch of xdp_md contexts resident on the GPU (see mimic_xdp_batch)."""
+
+    def __init__(self, pkt_data, pkt_off, pkt_len, headroom=0, tailroom=0, ingress=0, rxq=0, egress=0,
+                 schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+        self.pkt_data, self.pkt_off, self.pkt_len = pkt_data, pkt_off, pkt_len
+        self.headroom, self.tailroom = headroom, tailroom
+        self.ingress, self.rxq, self.egress = ingress, rxq, egress
+        self.schedule, self.cpu, self.step_budget = schedule, cpu, step_budget
+
+    @property
+    def n(self) -> int:
+        return int(self.pkt_len.numel())
+
+    @staticmethod
+    def layout(lengths: Sequence[int], headroom=0, tailroom=0, align: int = 64):
+        """Offsets of each packet memory (H+L+T) in one buffer, each aligned to `align`."""
+        import numpy as np
+
+        lens = np.asarray(lengths, dtype=np.int64)
+        H = np.asarray(headroom, dtype=np.int64) if not np.isscalar(headroom) else np.full(lens.shape, headroom)
+        T = np.asarray(tailroom, dtype=np.int64) if not np.isscalar(tailroom) else np.full(lens.shape, tailroom)
+        sizes = (H + lens + T + align - 1) // align * align
+        off = np.zeros(lens.shape, dtype=np.int64)
+        if len(lens) > 1:
+            off[1:] = np.cumsum(sizes)[:-1]
+        total = int(sizes.sum()) if len(lens) else 0
+        return off.astype(np.uint64), total
+
+    @classmethod
+    def from_packets(cls, packets: Sequence[bytes], device="cuda", headroom=0, tailroom=0, ingress=0, rxq=0,
+                     egress=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+        import numpy as np
+        import torch
+
+        lens = [len(p) for p in packets]
+        H_arr = None if np.isscalar(headroom) else np.asarray(headroom, dtype=np.uint32)
+        T_arr = None if np.isscalar(tailroom) else np.asarray(tailroom, dtype=np.uint32)
+        off, total = cls.layout(lens, headroom, tailroom)
+        buf = np.zeros(max(total, 1), dtype=np.uint8)
+        for i, p in enumerate(packets):
+            h = int(H_arr[i]) if H_arr is not None else int(headroom)
+            buf[int(off[i]) + h:int(off[i]) + h + len(p)] = np.frombuffer(bytes(p), dtype=np.uint8)
+        return cls.from_numpy(buf, off, np.asarray(lens, dtype=np.uint32), device, H_arr if H_arr is not None
+                              else headroom, T_arr if T_arr is not None else tailroom, ingress, rxq, egress,
+                              schedule, cpu, step_budget)
+
+    @classmethod
+    def from_numpy(cls, buf, off, lens, device="cuda", headroom=0, tailroom=0, ingress=0, rxq=0, egress=0,
+                   schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+        import numpy as np
+        import torch
+
+        def t(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=dt))).to(device)
+
+        def opt(v, dt):
+            return v if np.isscalar(v) else t(v, dt)
+
+        return cls(t(buf, np.uint8), t(np.asarray(off, dtype=np.uint64).view(np.int64), np.int64),
+                   t(np.asarray(lens, dtype=np.uint32).view(np.int32), np.int32),
+                   opt(headroom, np.int32), opt(tailroom, np.int32), opt(ingress, np.int32), opt(rxq, np.int32),
+                   opt(egress, np.int32), schedule, cpu, step_budget)
+
+    def packet_bytes(self, i: int) -> bytes:
+        """Packet memory i (H+L+T bytes) as it is now on the device."""
+        import numpy as np
+
+        o = int(self.pkt_off[i].item())
+        h = int(self.headroom[i].item()) if not np.isscalar(self.headroom) else int(self.headroom)
+        t_ = int(self.tailroom[i].item()) if not np.isscalar(self.tailroom) else int(self.tailroom)
+        n = h + int(self.pkt_len[i].item()) + t_
+        return bytes(self.pkt_data[o:o + n].cpu().numpy().tobytes())
+
+
+class XDPResults:
+    def __init__(self, r0, status, steps, err_pc):
+        self.r0, self.status, self.steps, self.err_pc = r0, status, steps, err_pc
+
+    @classmethod
+    def empty(cls, n: int, device):
+        import torch
+
+        return cls(torch.zeros(max(n, 1), dtype=torch.int64, device=device),
+                   torch.zeros(max(n, 1), dtype=torch.uint8, device=device),
+                   torch.zeros(max(n, 1), dtype=torch.int32, device=device),
+                   torch.zeros(max(n, 1), dtype=torch.int32, device=device))
+
+    def numpy(self, n: Optional[int] = None):
+        import numpy as np
+
+        n = self.r0.numel() if n is None else n
+        return {"r0": self.r0[:n].cpu().numpy().view(np.uint64), "status": self.status[:n].cpu().numpy(),
+                "steps": self.steps[:n].cpu().numpy().view(np.uint32), "err_pc": self.err_pc[:n].cpu().numpy()}

@@ -1,0 +1,1416 @@
+/*
+ * mimic_oracle.c -- CPU restatement of dylandreimerink/mimic's Process.Run hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see mimic_oracle.h).  This file restates, as plain C,
+ * the *effective* behaviour of the Go reference at /root/reference, including its
+ * quirks.  It is deliberately literal -- a sorted entry
+ * list with first-fit allocation, a binary search per memory access, per-process
+ * heap allocations -- because it doubles as the CPU baseline ("port") that bench.py
+ * times beside the GPU engine.
+ *
+ * Third-party algorithms restated here (not present in /root/reference, pinned by
+ * the reference's go.mod): cilium/ebpf v0.9.0 asm.Instruction.Unmarshal (LD_IMM64
+ * fusing, imm sign extension), OpCode.SetALUOp/SetJumpOp (InvalidOpCode=0xff for a
+ * wrong class), Size.Sizeof.  Go language semantics restated: integer conversion
+ * sign/zero extension, unmasked shifts, panics on divide-by-zero / negative signed
+ * shift counts / out-of-range slice index.
+ */
+#include "mimic_oracle.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MEM_START 0xFFFFu            /* memory_controller.go:55 */
+#define ORC_MAX_FRAMES 32            /* engine bound, mirrored by the product (MIMIC_MAX_FRAMES) */
+#define DEFAULT_BUDGET (1ull << 22)
+#define EXIT_SIGNAL (-1)
+
+#define E2BIG_ERRNO 7u
+#define EINVAL_ERRNO 22u
+#define EPERM_ERRNO 1u
+
+/* ------------------------------------------------------------------------- */
+/* objects registered in the memory controller                               */
+/* ------------------------------------------------------------------------- */
+
+typedef enum { K_PLAIN, K_ARRAY, K_PERCPU_ARRAY, K_HASH, K_PERCPU_HASH, K_PROG } objkind;
+
+typedef struct {
+    uint8_t *b;
+    uint32_t len;
+    int big_endian;
+} plain_mem; /* memory_plain.go:15-18 */
+
+typedef struct {
+    char name[64];
+    uint32_t type, key_size, value_size, max_entries;
+    int datasec; /* Spec.Value is *btf.Datasec, emulator_linux_map_array.go:136 */
+} map_spec;
+
+enum { FAM_ARRAY = 1, FAM_PERCPU_ARRAY, FAM_HASH, FAM_PERCPU_HASH };
+
+typedef struct orc_map {
+    int family;
+    map_spec *spec;
+    /* array: emulator_linux_map_array.go:21-27 */
+    plain_mem backing;
+    uint32_t addr;
+    /* per-CPU array: :177-182 */
+    struct orc_map **subs;
+    int nsubs;
+    /* hash: emulator_linux_map_hash.go:21-40 (+ per-CPU :417-436) */
+    uint32_t tcap;      /* open-addressing table standing in for KeyToIndex (exact key, sha256 collisions ignored) */
+    uint8_t *tkeys;
+    int32_t *tidx;      /* -1 empty, -2 deleted, else slot index */
+    uint32_t tcount, ntomb;
+    int32_t *fl;        /* freelist channel, capacity E+1, FIFO */
+    uint32_t fl_cap, fl_head, fl_len;
+    plain_mem keys;
+    uint32_t keys_addr;
+    plain_mem *values;  /* 1 (hash) or V (per-CPU hash) */
+    uint32_t *values_addr;
+    int nvalues;
+} orc_map;
+
+typedef struct {
+    uint8_t op, dst, src;
+    int16_t off;
+    int64_t k; /* asm.Instruction.Constant */
+} insn;
+
+typedef struct {
+    char name[64];
+    insn *ins;
+    uint32_t n;
+} program;
+
+typedef struct {
+    uint32_t addr, size;
+    objkind kind;
+    void *obj;
+} entry;
+
+struct orc_vm {
+    int vcpus, frame_size, frame_count, max_tail_calls;
+    entry *e;
+    size_t n, cap;
+    size_t tight; /* entries [0,tight) form a gap-free chain from MEM_START (first-fit can never use them) */
+    orc_map **maps;
+    int nmaps;
+    program **progs;
+    int nprogs;
+    plain_mem **scratch;
+    int nscratch;
+    char err[256];
+};
+
+typedef struct {
+    int64_t pc;
+    uint64_t r[11];
+} regs;
+
+struct orc_proc {
+    orc_vm *vm;
+    program *prog;
+    plain_mem stack;
+    regs R;
+    int cpu;
+    regs *frames;
+    int nframes, frames_cap;
+    int tailcalls;
+    /* xdp_md context (context_xdp_md.go:22-34) */
+    int has_ctx;
+    plain_mem *pkt, *xdpmd;
+};
+
+static void set_err(orc_vm *vm, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(vm->err, sizeof vm->err, fmt, ap);
+    va_end(ap);
+}
+
+const char *orc_last_error(orc_vm *vm) { return vm->err; }
+
+/* ------------------------------------------------------------------------- */
+/* MemoryController, memory_controller.go                                     */
+/* ------------------------------------------------------------------------- */
+
+/* AddEntry, memory_controller.go:58-112 (first fit from memStart+1, one-byte gaps). */
+static int mc_add(orc_vm *vm, void *obj, objkind kind, uint32_t size, uint32_t *addr_out) {
+    size_t i = 0;
+    uint32_t addr = MEM_START + 1;
+    if (vm->n > 0) {
+        /* entries before vm->tight are a contiguous chain; the reference loop would
+         * only step through them, so start the literal loop at the last one of them. */
+        size_t s = vm->tight < vm->n ? vm->tight : vm->n - 1;
+        addr = s == 0 ? MEM_START + 1 : vm->e[s - 1].addr + vm->e[s - 1].size + 1;
+        for (size_t j = s; j < vm->n; j++) {
+            entry *cur = &vm->e[j];
+            if ((uint32_t)(addr + size) < cur->addr) {
+                i = j;
+                break;
+            }
+            addr = cur->addr + cur->size + 1;
+            if (j == vm->n - 1) {
+                uint32_t avail = 0xFFFFFFFFu - addr;
+                if (avail < size) {
+                    set_err(vm, "out of memory");
+                    return -1;
+                }
+                i = j + 1;
+            }
+        }
+    }
+    if (vm->n == vm->cap) {
+        vm->cap = vm->cap ? vm->cap * 2 : 64;
+        vm->e = (entry *)realloc(vm->e, vm->cap * sizeof(entry));
+    }
+    memmove(&vm->e[i + 1], &vm->e[i], (vm->n - i) * sizeof(entry));
+    vm->e[i].addr = addr;
+    vm->e[i].size = size;
+    vm->e[i].kind = kind;
+    vm->e[i].obj = obj;
+    vm->n++;
+    /* maintain the gap-free prefix: [0,i) is unchanged, re-extend from i */
+    if (vm->tight > i) vm->tight = i;
+    while (vm->tight < vm->n) {
+        uint32_t expect = vm->tight == 0 ? MEM_START + 1 : vm->e[vm->tight - 1].addr + vm->e[vm->tight - 1].size + 1;
+        if (vm->e[vm->tight].addr != expect) break;
+        vm->tight++;
+    }
+    if (addr_out) *addr_out = addr;
+    return 0;
+}
+
+/* GetEntry, memory_controller.go:117-145 (inclusive upper bound at :137). */
+static entry *mc_get(orc_vm *vm, uint32_t addr, uint32_t *off) {
+    size_t lo = 0, hi = vm->n;
+    while (lo < hi) { /* sort.Search: first entry with Addr >= addr */
+        size_t mid = (lo + hi) / 2;
+        if (vm->e[mid].addr >= addr) hi = mid; else lo = mid + 1;
+    }
+    if (lo < vm->n && vm->e[lo].addr == addr) {
+        *off = 0;
+        return &vm->e[lo];
+    }
+    if (lo != 0) {
+        entry *prev = &vm->e[lo - 1];
+        if (addr >= prev->addr && (uint64_t)addr <= (uint64_t)prev->addr + prev->size) {
+            *off = addr - prev->addr;
+            return prev;
+        }
+    }
+    return NULL;
+}
+
+/* DelEntryByObj, memory_controller.go:202-232. */
+static void mc_del_obj(orc_vm *vm, void *obj) {
+    for (size_t j = vm->n; j-- > 0;) {
+        if (vm->e[j].obj == obj) {
+            memmove(&vm->e[j], &vm->e[j + 1], (vm->n - j - 1) * sizeof(entry));
+            vm->n--;
+            if (vm->tight > j) vm->tight = j;
+            return;
+        }
+    }
+}
+
+static entry *mc_by_obj(orc_vm *vm, void *obj) {
+    for (size_t j = vm->n; j-- > 0;)
+        if (vm->e[j].obj == obj) return &vm->e[j];
+    return NULL;
+}
+
+uint32_t orc_mem_next_free(orc_vm *vm) {
+    if (vm->n == 0) return MEM_START + 1;
+    return vm->e[vm->n - 1].addr + vm->e[vm->n - 1].size + 1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* PlainMemory, memory_plain.go                                               */
+/* ------------------------------------------------------------------------- */
+
+static int size_bytes(uint8_t op) { /* asm.Size.Sizeof on op&0x18 */
+    switch (op & 0x18) {
+    case 0x00: return 4;
+    case 0x08: return 2;
+    case 0x10: return 1;
+    default: return 8;
+    }
+}
+
+/* Load, memory_plain.go:25-52 */
+static int pm_load(plain_mem *m, uint32_t off, int n, uint64_t *v) {
+    if ((uint64_t)off + (uint64_t)n > m->len) return ORC_ERR_MEM_BOUNDS;
+    uint64_t x = 0;
+    if (m->big_endian) {
+        for (int k = 0; k < n; k++) x = (x << 8) | m->b[off + k];
+    } else {
+        for (int k = n - 1; k >= 0; k--) x = (x << 8) | m->b[off + k];
+    }
+    *v = x;
+    return 0;
+}
+
+/* Store, memory_plain.go:55-87 */
+static int pm_store(plain_mem *m, uint32_t off, uint64_t v, int n) {
+    if ((uint64_t)off + (uint64_t)n > m->len) return ORC_ERR_MEM_BOUNDS;
+    for (int k = 0; k < n; k++) {
+        int sh = m->big_endian ? (n - 1 - k) * 8 : k * 8;
+        m->b[off + k] = (uint8_t)(v >> sh);
+    }
+    return 0;
+}
+
+/* Read / Write, memory_plain.go:90-119 */
+static int pm_read(plain_mem *m, uint32_t off, uint8_t *out, uint32_t n) {
+    if ((uint64_t)off + n > m->len) return ORC_ERR_MEM_BOUNDS;
+    memcpy(out, m->b + off, n);
+    return 0;
+}
+static int pm_write(plain_mem *m, uint32_t off, const uint8_t *in, uint32_t n) {
+    if ((uint64_t)off + n > m->len) return ORC_ERR_MEM_BOUNDS;
+    memcpy(m->b + off, in, n);
+    return 0;
+}
+
+static plain_mem *pm_new(uint32_t len) {
+    plain_mem *m = (plain_mem *)calloc(1, sizeof *m);
+    m->b = (uint8_t *)calloc(len ? len : 1, 1);
+    m->len = len;
+    return m;
+}
+static void pm_free(plain_mem *m) {
+    if (!m) return;
+    free(m->b);
+    free(m);
+}
+
+/* VMMem dispatch for an entry: PlainMemory or LinuxArrayMap (emulator_linux_map_array.go:134-168).
+ * Returns ORC_ERR_MEM_NOT_VMMEM for objects that do not implement VMMem. */
+static int vm_load(entry *e, uint32_t off, int n, uint64_t *v) {
+    if (e->kind == K_PLAIN) return pm_load((plain_mem *)e->obj, off, n, v);
+    if (e->kind == K_ARRAY) {
+        orc_map *m = (orc_map *)e->obj;
+        if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
+        return pm_load(&m->backing, off, n, v);
+    }
+    return ORC_ERR_MEM_NOT_VMMEM;
+}
+static int vm_store(entry *e, uint32_t off, uint64_t v, int n) {
+    if (e->kind == K_PLAIN) return pm_store((plain_mem *)e->obj, off, v, n);
+    if (e->kind == K_ARRAY) {
+        orc_map *m = (orc_map *)e->obj;
+        if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
+        return pm_store(&m->backing, off, v, n);
+    }
+    return ORC_ERR_MEM_NOT_VMMEM;
+}
+static int vm_read(entry *e, uint32_t off, uint8_t *out, uint32_t n) {
+    if (e->kind == K_PLAIN) return pm_read((plain_mem *)e->obj, off, out, n);
+    if (e->kind == K_ARRAY) {
+        orc_map *m = (orc_map *)e->obj;
+        if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
+        return pm_read(&m->backing, off, out, n);
+    }
+    return ORC_ERR_MEM_NOT_VMMEM;
+}
+static int vm_write(entry *e, uint32_t off, const uint8_t *in, uint32_t n) {
+    if (e->kind == K_PLAIN) return pm_write((plain_mem *)e->obj, off, in, n);
+    if (e->kind == K_ARRAY) {
+        orc_map *m = (orc_map *)e->obj;
+        if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
+        return pm_write(&m->backing, off, in, n);
+    }
+    return ORC_ERR_MEM_NOT_VMMEM;
+}
+static int is_vmmem(objkind k) { return k == K_PLAIN || k == K_ARRAY; }
+static int is_linuxmap(objkind k) { return k == K_ARRAY || k == K_PERCPU_ARRAY || k == K_HASH || k == K_PERCPU_HASH; }
+
+/* ------------------------------------------------------------------------- */
+/* VM                                                                          */
+/* ------------------------------------------------------------------------- */
+
+orc_vm *orc_vm_new(int vcpus, int frame_size, int frame_count, int max_tail_calls) {
+    orc_vm *vm = (orc_vm *)calloc(1, sizeof *vm);
+    vm->vcpus = vcpus;                     /* VMOptSetvCPUs, vm.go:36-40 */
+    vm->frame_size = frame_size > 0 ? frame_size : 256;  /* vm.go:60 */
+    vm->frame_count = frame_count > 0 ? frame_count : 8; /* vm.go:62 */
+    vm->max_tail_calls = max_tail_calls;   /* emulator_linux_.go:78 default 33 */
+    return vm;
+}
+
+static void map_free(orc_map *m) {
+    if (!m) return;
+    free(m->backing.b);
+    if (m->subs) {
+        for (int i = 0; i < m->nsubs; i++) {
+            free(m->subs[i]->backing.b);
+            free(m->subs[i]);
+        }
+        free(m->subs);
+    }
+    free(m->tkeys);
+    free(m->tidx);
+    free(m->fl);
+    free(m->keys.b);
+    if (m->values) {
+        for (int i = 0; i < m->nvalues; i++) free(m->values[i].b);
+        free(m->values);
+    }
+    free(m->values_addr);
+    free(m->spec);
+    free(m);
+}
+
+void orc_vm_free(orc_vm *vm) {
+    if (!vm) return;
+    for (int i = 0; i < vm->nmaps; i++) map_free(vm->maps[i]);
+    for (int i = 0; i < vm->nprogs; i++) {
+        free(vm->progs[i]->ins);
+        free(vm->progs[i]);
+    }
+    for (int i = 0; i < vm->nscratch; i++) pm_free(vm->scratch[i]);
+    free(vm->scratch);
+    free(vm->maps);
+    free(vm->progs);
+    free(vm->e);
+    free(vm);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Maps                                                                        */
+/* ------------------------------------------------------------------------- */
+
+/* LinuxArrayMap.Init, emulator_linux_map_array.go:30-54 */
+static int array_init(orc_vm *vm, orc_map *m) {
+    uint32_t size = m->spec->max_entries * m->spec->value_size;
+    m->backing.b = (uint8_t *)calloc(size ? size : 1, 1);
+    m->backing.len = size;
+    if (mc_add(vm, m, K_ARRAY, 8, NULL)) return -1;
+    if (mc_add(vm, &m->backing, K_PLAIN, size, &m->addr)) return -1;
+    return 0;
+}
+
+static uint32_t fnv(const uint8_t *k, uint32_t n) {
+    uint32_t h = 2166136261u;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ k[i]) * 16777619u;
+    return h;
+}
+
+/* LinuxHashMap.Init, emulator_linux_map_hash.go:43-97; LinuxPerCPUHashMap.Init :439-500 */
+static int hash_init(orc_vm *vm, orc_map *m, int percpu) {
+    map_spec *s = m->spec;
+    uint32_t E = s->max_entries;
+    m->tcap = 16;
+    while (m->tcap < 2 * E + 2) m->tcap <<= 1;
+    m->tkeys = (uint8_t *)calloc((size_t)m->tcap * (s->key_size ? s->key_size : 1), 1);
+    m->tidx = (int32_t *)malloc(sizeof(int32_t) * m->tcap);
+    for (uint32_t i = 0; i < m->tcap; i++) m->tidx[i] = -1;
+    m->fl_cap = E + 1;
+    m->fl = (int32_t *)malloc(sizeof(int32_t) * m->fl_cap);
+    for (uint32_t i = 0; i < E; i++) m->fl[i] = (int32_t)i;
+    m->fl_head = 0;
+    m->fl_len = E;
+    m->keys.b = (uint8_t *)calloc((size_t)E * s->key_size + 1, 1);
+    m->keys.len = E * s->key_size;
+    m->nvalues = percpu ? vm->vcpus : 1;
+    m->values = (plain_mem *)calloc((size_t)m->nvalues, sizeof(plain_mem));
+    m->values_addr = (uint32_t *)calloc((size_t)m->nvalues, sizeof(uint32_t));
+    for (int i = 0; i < m->nvalues; i++) {
+        m->values[i].b = (uint8_t *)calloc((size_t)E * s->value_size + 1, 1);
+        m->values[i].len = E * s->value_size;
+    }
+    if (percpu) {
+        for (int i = 0; i < m->nvalues; i++)
+            if (mc_add(vm, &m->values[i], K_PLAIN, m->values[i].len, &m->values_addr[i])) return -1;
+        if (mc_add(vm, m, K_PERCPU_HASH, 8, NULL)) return -1;
+        if (mc_add(vm, &m->keys, K_PLAIN, m->keys.len, &m->keys_addr)) return -1;
+    } else {
+        if (mc_add(vm, m, K_HASH, 8, NULL)) return -1;
+        if (mc_add(vm, &m->keys, K_PLAIN, m->keys.len, &m->keys_addr)) return -1;
+        if (mc_add(vm, &m->values[0], K_PLAIN, m->values[0].len, &m->values_addr[0])) return -1;
+    }
+    return 0;
+}
+
+static int32_t ht_find(orc_map *m, const uint8_t *key, uint32_t *pos_out) {
+    uint32_t K = m->spec->key_size;
+    uint32_t p = fnv(key, K) & (m->tcap - 1);
+    for (;;) {
+        int32_t t = m->tidx[p];
+        if (t == -1) {
+            if (pos_out) *pos_out = p;
+            return -1;
+        }
+        if (t >= 0 && memcmp(m->tkeys + (size_t)p * K, key, K) == 0) {
+            if (pos_out) *pos_out = p;
+            return t;
+        }
+        p = (p + 1) & (m->tcap - 1);
+    }
+}
+
+static void ht_place(orc_map *m, const uint8_t *key, int32_t idx) {
+    uint32_t K = m->spec->key_size;
+    uint32_t p = fnv(key, K) & (m->tcap - 1);
+    while (m->tidx[p] >= 0) p = (p + 1) & (m->tcap - 1);
+    if (m->tidx[p] == -2) m->ntomb--;
+    m->tidx[p] = idx;
+    memcpy(m->tkeys + (size_t)p * K, key, K);
+    m->tcount++;
+}
+
+/* rebuild the probe table when deletions have left too many tombstones */
+static void ht_rehash(orc_map *m) {
+    uint32_t K = m->spec->key_size, cap = m->tcap;
+    uint8_t *ok = m->tkeys;
+    int32_t *oi = m->tidx;
+    m->tkeys = (uint8_t *)calloc((size_t)cap * (K ? K : 1), 1);
+    m->tidx = (int32_t *)malloc(sizeof(int32_t) * cap);
+    for (uint32_t i = 0; i < cap; i++) m->tidx[i] = -1;
+    m->tcount = 0;
+    m->ntomb = 0;
+    for (uint32_t i = 0; i < cap; i++)
+        if (oi[i] >= 0) ht_place(m, ok + (size_t)i * K, oi[i]);
+    free(ok);
+    free(oi);
+}
+
+static void ht_insert(orc_map *m, const uint8_t *key, int32_t idx) {
+    if ((m->tcount + m->ntomb + 1) * 4 > m->tcap * 3) ht_rehash(m);
+    ht_place(m, key, idx);
+}
+
+/* MapSpecToLinuxMap, emulator_linux_map.go:57-113 + LinuxEmulator.AddMap, emulator_linux_.go:97-116 */
+int orc_map_create(orc_vm *vm, const char *name, uint32_t type, uint32_t key_size, uint32_t value_size,
+                   uint32_t max_entries, int datasec) {
+    for (int i = 0; i < vm->nmaps; i++) {
+        if (strcmp(vm->maps[i]->spec->name, name) == 0) {
+            set_err(vm, "map with name '%s' already exists in emulator", name);
+            return -1;
+        }
+    }
+    orc_map *m = (orc_map *)calloc(1, sizeof *m);
+    m->spec = (map_spec *)calloc(1, sizeof *m->spec);
+    snprintf(m->spec->name, sizeof m->spec->name, "%s", name);
+    m->spec->type = type;
+    m->spec->key_size = key_size;
+    m->spec->value_size = value_size;
+    m->spec->max_entries = max_entries;
+    m->spec->datasec = datasec;
+    int rc;
+    switch (type) {
+    case ORC_MAP_ARRAY: case ORC_MAP_PROG_ARRAY: case ORC_MAP_ARRAY_OF_MAPS: case ORC_MAP_DEVMAP:
+    case ORC_MAP_SOCKMAP: case ORC_MAP_CPUMAP: case ORC_MAP_XSKMAP: case ORC_MAP_CGROUP_ARRAY:
+    case ORC_MAP_REUSEPORT_SOCKARRAY:
+        m->family = FAM_ARRAY;
+        rc = array_init(vm, m);
+        break;
+    case ORC_MAP_PERCPU_ARRAY:
+        /* LinuxPerCPUArrayMap.Init, emulator_linux_map_array.go:185-215 */
+        m->family = FAM_PERCPU_ARRAY;
+        rc = mc_add(vm, m, K_PERCPU_ARRAY, 8, NULL);
+        m->subs = (orc_map **)calloc((size_t)(vm->vcpus > 0 ? vm->vcpus : 1), sizeof(orc_map *));
+        for (int i = 0; rc == 0 && i < vm->vcpus; i++) {
+            orc_map *sub = (orc_map *)calloc(1, sizeof *sub);
+            sub->family = FAM_ARRAY;
+            sub->spec = m->spec; /* Spec: m.Spec (shared, parent's type) */
+            rc = array_init(vm, sub);
+            m->subs[m->nsubs++] = sub;
+        }
+        break;
+    case ORC_MAP_HASH: case ORC_MAP_HASH_OF_MAPS: case ORC_MAP_SOCKHASH: case ORC_MAP_CGROUP_STORAGE:
+    case ORC_MAP_SK_STORAGE: case ORC_MAP_DEVMAP_HASH: case ORC_MAP_STRUCT_OPS: case ORC_MAP_INODE_STORAGE:
+    case ORC_MAP_TASK_STORAGE:
+        m->family = FAM_HASH;
+        rc = hash_init(vm, m, 0);
+        break;
+    case ORC_MAP_PERCPU_HASH: case ORC_MAP_PERCPU_CGROUP_STORAGE:
+        m->family = FAM_PERCPU_HASH;
+        rc = hash_init(vm, m, 1);
+        break;
+    default:
+        set_err(vm, "unsupported map type '%u'", type);
+        free(m->spec);
+        free(m);
+        return -1;
+    }
+    if (rc) {
+        set_err(vm, "map init: out of memory");
+        return -1;
+    }
+    vm->maps = (orc_map **)realloc(vm->maps, sizeof(orc_map *) * (size_t)(vm->nmaps + 1));
+    vm->maps[vm->nmaps] = m;
+    return vm->nmaps++;
+}
+
+/* status codes for map ops: 0 ok, >0 errno (graceful), <0 fatal */
+#define MAPOP_FATAL (-1)
+
+/* LinuxArrayMap.Lookup :78-94 / LinuxPerCPUArrayMap.Lookup :235-241 / LinuxHashMap.Lookup
+ * emulator_linux_map_hash.go:134-155 / LinuxPerCPUHashMap.Lookup :537-561 */
+static int map_lookup(orc_vm *vm, orc_map *m, const uint8_t *key, uint32_t klen, int cpu, uint32_t *addr) {
+    (void)vm;
+    switch (m->family) {
+    case FAM_ARRAY: {
+        if (klen != 4) return MAPOP_FATAL;
+        uint32_t k;
+        memcpy(&k, key, 4);
+        *addr = k >= m->spec->max_entries ? 0 : m->addr + k * m->spec->value_size;
+        return 0;
+    }
+    case FAM_PERCPU_ARRAY:
+        if (cpu < 0 || cpu >= m->nsubs) return MAPOP_FATAL;
+        return map_lookup(vm, m->subs[cpu], key, klen, cpu, addr);
+    case FAM_HASH: {
+        if (klen != m->spec->key_size) return MAPOP_FATAL;
+        int32_t idx = ht_find(m, key, NULL);
+        *addr = idx < 0 ? 0 : m->values_addr[0] + (uint32_t)idx * m->spec->value_size;
+        return 0;
+    }
+    case FAM_PERCPU_HASH: {
+        if (klen != m->spec->key_size) return MAPOP_FATAL;
+        if (cpu < 0 || cpu >= m->nvalues) return MAPOP_FATAL;
+        int32_t idx = ht_find(m, key, NULL);
+        *addr = idx < 0 ? 0 : m->values_addr[cpu] + (uint32_t)idx * m->spec->value_size;
+        return 0;
+    }
+    }
+    return MAPOP_FATAL;
+}
+
+/* Update: emulator_linux_map_array.go:97-113, :244-250; emulator_linux_map_hash.go:158-203, :564-612 */
+static int map_update(orc_vm *vm, orc_map *m, const uint8_t *key, uint32_t klen, const uint8_t *val,
+                      uint32_t vlen, uint32_t flags, int cpu) {
+    (void)flags; /* Q10: flags are ignored by every map */
+    switch (m->family) {
+    case FAM_ARRAY: {
+        if (klen != 4) return MAPOP_FATAL;
+        if (vlen != m->spec->value_size) return MAPOP_FATAL;
+        uint32_t k;
+        memcpy(&k, key, 4);
+        if (k >= m->spec->max_entries) return (int)E2BIG_ERRNO;
+        if (pm_write(&m->backing, k * m->spec->value_size, val, vlen)) return MAPOP_FATAL;
+        return 0;
+    }
+    case FAM_PERCPU_ARRAY:
+        if (cpu < 0 || cpu >= m->nsubs) return MAPOP_FATAL;
+        return map_update(vm, m->subs[cpu], key, klen, val, vlen, flags, cpu);
+    case FAM_HASH:
+    case FAM_PERCPU_HASH: {
+        int percpu = m->family == FAM_PERCPU_HASH;
+        if (klen != m->spec->key_size) return MAPOP_FATAL;
+        if (vlen != m->spec->value_size) return MAPOP_FATAL;
+        if (percpu && (cpu < 0 || cpu >= m->nvalues)) return MAPOP_FATAL;
+        int32_t idx = ht_find(m, key, NULL);
+        if (idx < 0) {
+            if (m->fl_len == 0) return (int)E2BIG_ERRNO;
+            idx = m->fl[m->fl_head];
+            m->fl_head = (m->fl_head + 1) % m->fl_cap;
+            m->fl_len--;
+            ht_insert(m, key, idx);
+        }
+        if (pm_write(&m->keys, (uint32_t)idx * m->spec->key_size, key, klen)) return MAPOP_FATAL;
+        if (pm_write(&m->values[percpu ? cpu : 0], (uint32_t)idx * m->spec->value_size, val, vlen)) return MAPOP_FATAL;
+        return 0;
+    }
+    }
+    return MAPOP_FATAL;
+}
+
+/* Delete: emulator_linux_map_hash.go:225-255, :634-664 (arrays are not LinuxMapDeleter) */
+static int map_delete(orc_map *m, const uint8_t *key, uint32_t klen) {
+    if (m->family != FAM_HASH && m->family != FAM_PERCPU_HASH) return MAPOP_FATAL;
+    if (klen != m->spec->key_size) return MAPOP_FATAL;
+    uint32_t pos;
+    int32_t idx = ht_find(m, key, &pos);
+    if (idx < 0) return 0;
+    m->tidx[pos] = -2;
+    m->tcount--;
+    m->ntomb++;
+    if (m->fl_len == m->fl_cap) abort(); /* panic("freelist is full") -- unreachable */
+    m->fl[(m->fl_head + m->fl_len) % m->fl_cap] = idx;
+    m->fl_len++;
+    return 0;
+}
+
+int orc_map_update(orc_vm *vm, int id, const void *key, const void *value, uint32_t flags, int cpu) {
+    orc_map *m = vm->maps[id];
+    return map_update(vm, m, (const uint8_t *)key, m->spec->key_size, (const uint8_t *)value, m->spec->value_size, flags, cpu);
+}
+int orc_map_lookup(orc_vm *vm, int id, const void *key, int cpu, uint32_t *addr_out) {
+    orc_map *m = vm->maps[id];
+    return map_lookup(vm, m, (const uint8_t *)key, m->spec->key_size, cpu, addr_out);
+}
+int orc_map_delete(orc_vm *vm, int id, const void *key) {
+    orc_map *m = vm->maps[id];
+    return map_delete(m, (const uint8_t *)key, m->spec->key_size);
+}
+uint32_t orc_map_addr(orc_vm *vm, int id) {
+    entry *e = mc_by_obj(vm, vm->maps[id]);
+    return e ? e->addr : 0;
+}
+int orc_map_values(orc_vm *vm, int id, int cpu, void *out, size_t cap) {
+    orc_map *m = vm->maps[id];
+    plain_mem *b;
+    switch (m->family) {
+    case FAM_ARRAY: b = &m->backing; break;
+    case FAM_PERCPU_ARRAY:
+        if (cpu < 0 || cpu >= m->nsubs) return -1;
+        b = &m->subs[cpu]->backing;
+        break;
+    case FAM_HASH: b = &m->values[0]; break;
+    case FAM_PERCPU_HASH:
+        if (cpu < 0 || cpu >= m->nvalues) return -1;
+        b = &m->values[cpu];
+        break;
+    default: return -1;
+    }
+    if (cap < b->len) return -1;
+    memcpy(out, b->b, b->len);
+    return (int)b->len;
+}
+int orc_map_slots(orc_vm *vm, int id, int32_t *slot_out, uint8_t *keys_out, size_t cap_keys) {
+    orc_map *m = vm->maps[id];
+    if (m->family != FAM_HASH && m->family != FAM_PERCPU_HASH) return -1;
+    uint32_t K = m->spec->key_size;
+    int n = 0;
+    for (uint32_t p = 0; p < m->tcap; p++) {
+        if (m->tidx[p] < 0) continue;
+        if ((size_t)n >= cap_keys) return -1;
+        slot_out[n] = m->tidx[p];
+        memcpy(keys_out + (size_t)n * K, m->tkeys + (size_t)p * K, K);
+        n++;
+    }
+    return n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Programs: VM.AddProgram, vm.go:98-139; RewriteProgram, emulator_linux_.go:292-339 */
+/* ------------------------------------------------------------------------- */
+
+int orc_prog_load(orc_vm *vm, const char *name, const uint8_t *raw, uint32_t n_slots,
+                  const orc_reloc *relocs, uint32_t n_relocs) {
+    program *p = (program *)calloc(1, sizeof *p);
+    snprintf(p->name, sizeof p->name, "%s", name ? name : "");
+    p->ins = (insn *)calloc(n_slots ? n_slots : 1, sizeof(insn));
+    p->n = n_slots;
+    /* cilium/ebpf v0.9.0 asm.Instruction.Unmarshal (little endian), then the Nop
+     * re-inserted after every LD_IMM64 by AddProgram (vm.go:102-112). */
+    for (uint32_t i = 0; i < n_slots; i++) {
+        const uint8_t *b = raw + 8 * (size_t)i;
+        insn *x = &p->ins[i];
+        x->op = b[0];
+        x->dst = b[1] & 0xf;
+        x->src = b[1] >> 4;
+        x->off = (int16_t)(uint16_t)(b[2] | (b[3] << 8));
+        int32_t imm = (int32_t)((uint32_t)b[4] | ((uint32_t)b[5] << 8) | ((uint32_t)b[6] << 16) | ((uint32_t)b[7] << 24));
+        x->k = (int64_t)imm;
+        if (x->op == 0x18) {
+            if (i + 1 >= n_slots) {
+                set_err(vm, "64bit immediate is missing second half");
+                free(p->ins);
+                free(p);
+                return -1;
+            }
+            const uint8_t *c = raw + 8 * (size_t)(i + 1);
+            if (c[0] | c[1] | c[2] | c[3]) {
+                set_err(vm, "64bit immediate has non-zero fields");
+                free(p->ins);
+                free(p);
+                return -1;
+            }
+            uint32_t hi = (uint32_t)c[4] | ((uint32_t)c[5] << 8) | ((uint32_t)c[6] << 16) | ((uint32_t)c[7] << 24);
+            x->k = (int64_t)(((uint64_t)hi << 32) | (uint32_t)imm);
+            i++;
+            memset(&p->ins[i], 0, sizeof(insn)); /* asm.Instruction{OpCode: 0} */
+        }
+    }
+    /* RewriteProgram: map references -> map object address */
+    for (uint32_t r = 0; r < n_relocs; r++) {
+        uint32_t s = relocs[r].slot;
+        if (s >= p->n) {
+            set_err(vm, "relocation slot %u out of range", s);
+            free(p->ins);
+            free(p);
+            return -1;
+        }
+        insn *x = &p->ins[s];
+        if (!(x->op == 0x18 && (x->src == 1 || x->src == 2))) continue; /* !IsLoadFromMap */
+        if (relocs[r].map_id >= (uint32_t)vm->nmaps) {
+            set_err(vm, "program references a map that does not exist in the emulator");
+            free(p->ins);
+            free(p);
+            return -1;
+        }
+        entry *e = mc_by_obj(vm, vm->maps[relocs[r].map_id]);
+        if (x->src == 1) x->k = (int64_t)e->addr;               /* PseudoMapFD */
+        else x->k = (int64_t)e->addr + (int64_t)x->off;         /* PseudoMapValue (Q16) */
+    }
+    /* fixupJumpsAndCalls (vm.go:142-194) is the identity on raw bytecode whose call/jump
+     * immediates are already relative; AddEntry(prog, 8) (vm.go:131). */
+    if (mc_add(vm, p, K_PROG, 8, NULL)) {
+        free(p->ins);
+        free(p);
+        return -1;
+    }
+    vm->progs = (program **)realloc(vm->progs, sizeof(program *) * (size_t)(vm->nprogs + 1));
+    vm->progs[vm->nprogs] = p;
+    return vm->nprogs++;
+}
+
+uint32_t orc_prog_addr(orc_vm *vm, int id) {
+    entry *e = mc_by_obj(vm, vm->progs[id]);
+    return e ? e->addr : 0;
+}
+
+uint32_t orc_mem_add_scratch(orc_vm *vm, uint32_t size) {
+    plain_mem *m = pm_new(size);
+    uint32_t a = 0;
+    if (mc_add(vm, m, K_PLAIN, size, &a)) {
+        pm_free(m);
+        return 0;
+    }
+    vm->scratch = (plain_mem **)realloc(vm->scratch, sizeof(plain_mem *) * (size_t)(vm->nscratch + 1));
+    vm->scratch[vm->nscratch++] = m;
+    return a;
+}
+int orc_mem_read(orc_vm *vm, uint32_t addr, void *buf, uint32_t len) {
+    uint32_t off;
+    entry *e = mc_get(vm, addr, &off);
+    if (!e) return ORC_ERR_MEM_UNRESOLVED;
+    return vm_read(e, off, (uint8_t *)buf, len);
+}
+int orc_mem_write(orc_vm *vm, uint32_t addr, const void *buf, uint32_t len) {
+    uint32_t off;
+    entry *e = mc_get(vm, addr, &off);
+    if (!e) return ORC_ERR_MEM_UNRESOLVED;
+    return vm_write(e, off, (const uint8_t *)buf, len);
+}
+int orc_mem_load(orc_vm *vm, uint32_t addr, int size, uint64_t *out) {
+    uint32_t off;
+    entry *e = mc_get(vm, addr, &off);
+    if (!e) return ORC_ERR_MEM_UNRESOLVED;
+    return vm_load(e, off, size, out);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Registers, vm.go:407-466                                                    */
+/* ------------------------------------------------------------------------- */
+
+#define GET(reg, out)                                              \
+    do {                                                           \
+        if ((reg) > 10) return ORC_PANIC_BADREG;                   \
+        (out) = p->R.r[(reg)];                                     \
+    } while (0)
+#define SET(reg, val)                                              \
+    do {                                                           \
+        if ((reg) == 10) return ORC_ERR_R10_WRITE;                 \
+        if ((reg) > 10) return ORC_PANIC_BADREG;                   \
+        p->R.r[(reg)] = (val);                                     \
+    } while (0)
+
+/* ------------------------------------------------------------------------- */
+/* Instruction handlers                                                        */
+/* ------------------------------------------------------------------------- */
+
+/* Generated ALU handlers, inst_gen.go:7-225 (ADD..XOR, x{32,64}x{IMM,Reg}).
+ * ALU32: uint64(uint32(dst) op uint32(x)); ALU64: dst op x with x = uint64(Constant). */
+static int h_alu_gen(orc_proc *p, const insn *i) {
+    int is64 = (i->op & 7) == 7;
+    int reg = (i->op & 0x08) != 0;
+    int aop = i->op & 0xf0;
+    uint64_t d, s;
+    GET(i->dst, d);
+    if (reg) GET(i->src, s);
+    else s = (uint64_t)i->k;
+    uint64_t r;
+    if (is64) {
+        switch (aop) {
+        case 0x00: r = d + s; break;
+        case 0x10: r = d - s; break;
+        case 0x20: r = d * s; break;
+        case 0x30: if (s == 0) return ORC_PANIC_DIV0; r = d / s; break;
+        case 0x40: r = d | s; break;
+        case 0x50: r = d & s; break;
+        case 0x60: r = s >= 64 ? 0 : d << s; break;   /* Go: shifts >= width yield 0 */
+        case 0x70: r = s >= 64 ? 0 : d >> s; break;
+        case 0x90: if (s == 0) return ORC_PANIC_DIV0; r = d % s; break;
+        default: r = d ^ s; break; /* 0xa0 */
+        }
+    } else {
+        uint32_t a = (uint32_t)d, b = (uint32_t)s, x;
+        switch (aop) {
+        case 0x00: x = a + b; break;
+        case 0x10: x = a - b; break;
+        case 0x20: x = a * b; break;
+        case 0x30: if (b == 0) return ORC_PANIC_DIV0; x = a / b; break;
+        case 0x40: x = a | b; break;
+        case 0x50: x = a & b; break;
+        case 0x60: x = b >= 32 ? 0 : a << b; break;   /* uint32(dst) << uint32(x) */
+        case 0x70: x = b >= 32 ? 0 : a >> b; break;
+        case 0x90: if (b == 0) return ORC_PANIC_DIV0; x = a % b; break;
+        default: x = a ^ b; break;
+        }
+        r = (uint64_t)x;
+    }
+    SET(i->dst, r);
+    return 0;
+}
+
+/* inst.go:86-94 (Q6: ALU32 NEG sign-extends) */
+static int h_neg(orc_proc *p, const insn *i) {
+    uint64_t d;
+    GET(i->dst, d);
+    uint64_t r;
+    if ((i->op & 7) == 7) r = (uint64_t)(-(int64_t)d);
+    else r = (uint64_t)(int64_t)(int32_t)(0u - (uint32_t)d);
+    SET(i->dst, r);
+    return 0;
+}
+
+/* inst.go:96-114 */
+static int h_mov(orc_proc *p, const insn *i) {
+    int is64 = (i->op & 7) == 7;
+    uint64_t v;
+    if (i->op & 0x08) {
+        GET(i->src, v);
+        if (!is64) v = (uint32_t)v;
+    } else {
+        v = is64 ? (uint64_t)i->k : (uint64_t)(uint32_t)i->k;
+    }
+    SET(i->dst, v);
+    return 0;
+}
+
+/* inst.go:116-136 (Q5/Q6: Go signed shift; negative IMM count panics; ALU32 result sign-extends) */
+static int h_arsh(orc_proc *p, const insn *i) {
+    int is64 = (i->op & 7) == 7;
+    uint64_t d, s;
+    int reg = (i->op & 0x08) != 0;
+    if (reg) {
+        GET(i->src, s);
+        GET(i->dst, d);
+    } else {
+        GET(i->dst, d);
+        if (i->k < 0) return ORC_PANIC_SHIFT;
+        s = (uint64_t)i->k;
+    }
+    uint64_t r;
+    if (is64) {
+        int64_t x = (int64_t)d;
+        r = (uint64_t)(s >= 64 ? (x < 0 ? -1 : 0) : (x >> s));
+    } else {
+        int32_t x = (int32_t)(uint32_t)d;
+        int32_t y = s >= 32 ? (x < 0 ? -1 : 0) : (x >> s);
+        r = (uint64_t)(int64_t)y;
+    }
+    SET(i->dst, r);
+    return 0;
+}
+
+static uint64_t bswap16(uint64_t x) { return ((x >> 8) & 0xff) | ((x & 0xff) << 8); }
+static uint64_t bswap32(uint64_t x) {
+    return ((x >> 24) & 0xff) | ((x >> 8) & 0xff00) | ((x << 8) & 0xff0000) | ((x << 24) & 0xff000000u);
+}
+
+/* inst.go:138-198 (Q4) */
+static int h_end(orc_proc *p, const insn *i) {
+    uint64_t d;
+    GET(i->dst, d);
+    int to_be = (i->op & 0x08) != 0;
+    switch (i->k) {
+    case 16: d = to_be ? (d & 0xffff) : bswap16(d & 0xffff); break;
+    case 32: d = to_be ? (d & 0xffffffffu) : bswap32(d & 0xffffffffu); break;
+    case 64: d = to_be ? (d >> 32) : bswap32(d >> 32); break;
+    default: break;
+    }
+    SET(i->dst, d);
+    return 0;
+}
+
+/* Conditional jumps, inst_gen.go:227-605 and inst.go:205-241.
+ * width32: compare uint32/int32 views.  Taken => PC += Offset. */
+static int jump_cond(int jop, uint64_t d, uint64_t s, int width32) {
+    if (width32) {
+        uint32_t a = (uint32_t)d, b = (uint32_t)s;
+        int32_t sa = (int32_t)a, sb = (int32_t)b;
+        switch (jop) {
+        case 0x10: return a == b;
+        case 0x20: return a > b;
+        case 0x30: return a >= b;
+        case 0x40: return (a & b) == 0; /* Q3: inverted JSET */
+        case 0x50: return a != b;
+        case 0x60: return sa > sb;
+        case 0x70: return sa >= sb;
+        case 0xa0: return a < b;
+        case 0xb0: return a <= b;
+        case 0xc0: return sa < sb;
+        case 0xd0: return sa <= sb;
+        }
+    } else {
+        int64_t sa = (int64_t)d, sb = (int64_t)s;
+        switch (jop) {
+        case 0x10: return d == s;
+        case 0x20: return d > s;
+        case 0x30: return d >= s;
+        case 0x40: return (d & s) == 0;
+        case 0x50: return d != s;
+        case 0x60: return sa > sb;
+        case 0x70: return sa >= sb;
+        case 0xa0: return d < s;
+        case 0xb0: return d <= s;
+        case 0xc0: return sa < sb;
+        case 0xd0: return sa <= sb;
+        }
+    }
+    return 0;
+}
+
+/* width: 32 or 64.  Register-source handlers read Src first (inst_gen.go:246-247). */
+static int h_jcond(orc_proc *p, const insn *i, int width32, int jop) {
+    uint64_t d, s;
+    if (i->op & 0x08) {
+        GET(i->src, s);
+        GET(i->dst, d);
+    } else {
+        GET(i->dst, d);
+        s = (uint64_t)i->k;
+    }
+    if (jump_cond(jop, d, s, width32)) p->R.pc += i->off;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Helpers, emulator_linux_helpers.go                                          */
+/* ------------------------------------------------------------------------- */
+
+/* regToMap, emulator_linux_helpers.go:415-447 */
+static orc_map *reg_to_map(orc_proc *p, uint64_t regval) {
+    uint32_t off;
+    entry *e = mc_get(p->vm, (uint32_t)regval, &off);
+    if (!e) return NULL;
+    if (is_linuxmap(e->kind)) return (orc_map *)e->obj;
+    if (is_vmmem(e->kind)) {
+        uint64_t a;
+        if (vm_load(e, off, 4, &a)) return NULL;
+        e = mc_get(p->vm, (uint32_t)a, &off);
+        if (!e) return NULL;
+        if (is_linuxmap(e->kind)) return (orc_map *)e->obj;
+    }
+    return NULL;
+}
+
+/* derefMapKey, :449-471 (also the value deref of :525-541) */
+static int deref_bytes(orc_proc *p, uint64_t regval, uint32_t n, uint8_t *out) {
+    uint32_t off;
+    entry *e = mc_get(p->vm, (uint32_t)regval, &off);
+    if (!e) return -1;
+    if (!is_vmmem(e->kind)) return -1;
+    if (vm_read(e, off, out, n)) return -1;
+    return 0;
+}
+
+static int helper_lookup(orc_proc *p) { /* :477-504 */
+    orc_map *m = reg_to_map(p, p->R.r[1]);
+    if (!m) return ORC_ERR_HELPER_MAP_PTR;
+    uint8_t kb[512];
+    uint8_t *key = m->spec->key_size <= sizeof kb ? kb : (uint8_t *)malloc(m->spec->key_size);
+    int rc = 0;
+    if (deref_bytes(p, p->R.r[2], m->spec->key_size, key)) {
+        rc = ORC_ERR_HELPER_KEY;
+    } else {
+        uint32_t a = 0;
+        int r = map_lookup(p->vm, m, key, m->spec->key_size, p->cpu, &a);
+        if (r < 0) rc = ORC_ERR_HELPER_MAP_OP;
+        else if (r > 0) p->R.r[0] = (uint64_t)r; /* Q9 (lookups never return an errno) */
+        else p->R.r[0] = a;
+    }
+    if (key != kb) free(key);
+    return rc;
+}
+
+static int helper_update(orc_proc *p) { /* :506-555 */
+    orc_map *m = reg_to_map(p, p->R.r[1]);
+    if (!m) return ORC_ERR_HELPER_MAP_PTR;
+    uint32_t K = m->spec->key_size, S = m->spec->value_size;
+    uint8_t *key = (uint8_t *)malloc(K + 1), *val = (uint8_t *)malloc(S + 1);
+    int rc = 0;
+    if (deref_bytes(p, p->R.r[2], K, key)) rc = ORC_ERR_HELPER_KEY;
+    else if (deref_bytes(p, p->R.r[3], S, val)) rc = ORC_ERR_HELPER_VALUE;
+    else {
+        int r = map_update(p->vm, m, key, K, val, S, (uint32_t)p->R.r[4], p->cpu);
+        if (r < 0) rc = ORC_ERR_HELPER_MAP_OP;
+        else p->R.r[0] = (uint64_t)(uint32_t)r; /* Q9: R0 = uint64(errno), positive */
+    }
+    free(key);
+    free(val);
+    return rc;
+}
+
+static int helper_delete(orc_proc *p) { /* :557-586 */
+    orc_map *m = reg_to_map(p, p->R.r[1]);
+    if (!m) return ORC_ERR_HELPER_MAP_PTR;
+    if (m->family != FAM_HASH && m->family != FAM_PERCPU_HASH) return ORC_ERR_HELPER_MAP_OP;
+    uint32_t K = m->spec->key_size;
+    uint8_t *key = (uint8_t *)malloc(K + 1);
+    int rc = 0;
+    if (deref_bytes(p, p->R.r[2], K, key)) rc = ORC_ERR_HELPER_KEY;
+    else {
+        int r = map_delete(m, key, K);
+        if (r < 0) rc = ORC_ERR_HELPER_MAP_OP;
+        else p->R.r[0] = (uint64_t)(uint32_t)r;
+    }
+    free(key);
+    return rc;
+}
+
+static int helper_tailcall(orc_proc *p) { /* :649-738 */
+    if (p->tailcalls >= p->vm->max_tail_calls) {
+        p->R.r[0] = (uint64_t)(0 - (uint64_t)EPERM_ERRNO);
+        return 0;
+    }
+    orc_map *m = reg_to_map(p, p->R.r[2]);
+    if (!m) return ORC_ERR_HELPER_MAP_PTR;
+    if (m->spec->type != ORC_MAP_PROG_ARRAY || m->spec->key_size != 4) return ORC_ERR_HELPER_TAILCALL;
+    if (m->family != FAM_ARRAY) return ORC_ERR_HELPER_TAILCALL;
+    uint32_t k = (uint32_t)p->R.r[3];
+    uint32_t ptr = 0;
+    if (map_lookup(p->vm, m, (uint8_t *)&k, 4, p->cpu, &ptr) < 0) return ORC_ERR_HELPER_TAILCALL;
+    uint32_t off;
+    entry *e = mc_get(p->vm, ptr, &off);
+    if (!e) {
+        p->R.r[0] = (uint64_t)(0 - (uint64_t)EINVAL_ERRNO);
+        return 0;
+    }
+    if (!is_vmmem(e->kind)) return ORC_ERR_HELPER_TAILCALL;
+    uint64_t pa = 0;
+    if (vm_load(e, off, 4, &pa)) pa = 0; /* error ignored (checks `ok` instead of err, :708) */
+    e = mc_get(p->vm, (uint32_t)pa, &off);
+    if (!e || e->kind != K_PROG) {
+        p->R.r[0] = (uint64_t)(0 - (uint64_t)EINVAL_ERRNO);
+        return 0;
+    }
+    p->prog = (program *)e->obj;
+    p->R.pc = -1;
+    p->tailcalls++;
+    return 0;
+}
+
+/* bpf_xdp_adjust_tail, :842-861 (only the always-EINVAL prefix; a 20-byte PlainMemory ctx
+ * is outside the engine's supported set) */
+static int helper_xdp_adjust_tail(orc_proc *p) {
+    uint32_t off;
+    entry *e = mc_get(p->vm, (uint32_t)p->R.r[1], &off);
+    if (!e || e->kind != K_PLAIN || ((plain_mem *)e->obj)->len != 20) {
+        p->R.r[0] = (uint64_t)(0 - (uint64_t)EINVAL_ERRNO);
+        return 0;
+    }
+    return ORC_ERR_ENGINE_HELPER;
+}
+
+static int helper_class(int32_t n) {
+    /* emulatedLinuxHelpers table, emulator_linux_helpers.go:28-204: 0 nil, 1 emulated, 2 CantEmulate */
+    static const int ce[] = {4, 14, 15, 16, 17, 22, 24, 27, 35, 36, 42, 45, 46, 47, 55, 56, 67, 69, 80,
+                             112, 113, 114, 115, 119, 120, 122, 123, 128, 129, 141, 148, 151};
+    static const int em[] = {1, 2, 3, 5, 7, 8, 9, 12, 25, 38, 65, 87, 88, 89, 125, 160};
+    for (size_t k = 0; k < sizeof ce / sizeof ce[0]; k++) if (ce[k] == n) return 2;
+    for (size_t k = 0; k < sizeof em / sizeof em[0]; k++) if (em[k] == n) return 1;
+    return 0;
+}
+
+/* LinuxEmulator.CallHelperFunction, emulator_linux_.go:125-194 */
+static int call_helper(orc_proc *p, int32_t n) {
+    if (n < 0) return ORC_PANIC_HELPER_NEG;             /* replayableHelpers[n] index panic */
+    if (n >= 176) return ORC_ERR_HELPER_UNIMPLEMENTED;  /* len(emulatedLinuxHelpers) == 176 */
+    int c = helper_class(n);
+    if (c == 0) return ORC_ERR_HELPER_UNIMPLEMENTED;
+    if (c == 2) return ORC_ERR_HELPER_CANT_EMULATE;
+    switch (n) {
+    case 1: return helper_lookup(p);
+    case 2: return helper_update(p);
+    case 3: return helper_delete(p);
+    case 8: p->R.r[0] = (uint64_t)(int64_t)p->cpu; return 0; /* :603-606 */
+    case 12: return helper_tailcall(p);
+    case 65: return helper_xdp_adjust_tail(p);
+    default: return ORC_ERR_ENGINE_HELPER; /* ktime, prandom, skb_store_bytes, perf output, ... */
+    }
+}
+
+/* inst.go:243-266 */
+static int h_call(orc_proc *p, const insn *i) {
+    if (i->src == 1) { /* PseudoCall: BPF-to-BPF */
+        if (p->nframes >= ORC_MAX_FRAMES) return ORC_ERR_CALL_DEPTH;
+        if (p->nframes == p->frames_cap) {
+            p->frames_cap = p->frames_cap ? p->frames_cap * 2 : 4;
+            p->frames = (regs *)realloc(p->frames, sizeof(regs) * (size_t)p->frames_cap);
+        }
+        p->frames[p->nframes++] = p->R;
+        p->R.pc += (int64_t)i->k - 1;
+        p->R.r[10] += (uint64_t)p->vm->frame_size;
+        return 0;
+    }
+    return call_helper(p, (int32_t)i->k);
+}
+
+/* inst.go:277-296 */
+static int h_exit(orc_proc *p) {
+    if (p->nframes > 0) {
+        regs *s = &p->frames[p->nframes - 1];
+        p->R.pc = s->pc;
+        p->R.r[6] = s->r[6];
+        p->R.r[7] = s->r[7];
+        p->R.r[8] = s->r[8];
+        p->R.r[9] = s->r[9];
+        p->nframes--;
+        p->R.r[10] -= (uint64_t)p->vm->frame_size;
+        return 0;
+    }
+    return EXIT_SIGNAL;
+}
+
+/* inst.go:298-363 */
+static int h_ldx(orc_proc *p, const insn *i) {
+    uint64_t s;
+    GET(i->src, s);
+    uint32_t addr = (uint32_t)(s + (uint64_t)(int64_t)i->off);
+    uint32_t off;
+    entry *e = mc_get(p->vm, addr, &off);
+    if (!e) return ORC_ERR_MEM_UNRESOLVED;
+    if (!is_vmmem(e->kind)) return ORC_ERR_MEM_NOT_VMMEM;
+    uint64_t v;
+    int rc = vm_load(e, off, size_bytes(i->op), &v);
+    if (rc) return rc;
+    SET(i->dst, v);
+    return 0;
+}
+
+static int h_st(orc_proc *p, const insn *i, int reg) {
+    uint64_t s = 0, d;
+    if (reg) GET(i->src, s);
+    GET(i->dst, d);
+    if (!reg) s = (uint64_t)i->k;
+    uint32_t addr = (uint32_t)(d + (uint64_t)(int64_t)i->off);
+    uint32_t off;
+    entry *e = mc_get(p->vm, addr, &off);
+    if (!e) return ORC_ERR_MEM_UNRESOLVED;
+    if (!is_vmmem(e->kind)) return ORC_ERR_MEM_NOT_VMMEM;
+    return vm_store(e, off, s, size_bytes(i->op));
+}
+
+/* LinuxEmulator.CustomInstruction, emulator_linux_.go:198-288 (XDP path: R6 is never a *SKBuff) */
+static int h_custom(orc_proc *p, const insn *i) {
+    switch (i->op) {
+    case 0x20: case 0x28: case 0x30: case 0x38:
+    case 0x40: case 0x48: case 0x50: case 0x58:
+        return ORC_ERR_LDABS;
+    }
+    return ORC_ERR_UNSUPPORTED_OP;
+}
+
+/* Effective dispatch table (inst.go:15-78 after inst_gen.go:607-688), SURVEY Appendix A. */
+static int exec_insn(orc_proc *p, const insn *i) {
+    uint8_t op = i->op;
+    switch (op) {
+    case 0x00: return 0; /* instNop */
+    case 0x18: SET(i->dst, (uint64_t)i->k); return 0; /* instLoad64Imm */
+    case 0x61: case 0x69: case 0x71: case 0x79: return h_ldx(p, i);
+    case 0x62: case 0x6a: case 0x72: case 0x7a: return h_st(p, i, 0);
+    case 0x63: case 0x6b: case 0x73: case 0x7b: return h_st(p, i, 1);
+    case 0x84: case 0x8c: case 0x87: case 0x8f: return h_neg(p, i);
+    case 0xb4: case 0xbc: case 0xb7: case 0xbf: return h_mov(p, i);
+    case 0xc4: case 0xcc: case 0xc7: case 0xcf: return h_arsh(p, i);
+    case 0xd4: case 0xdc: return h_end(p, i);
+    case 0x05: p->R.pc += i->off; return 0; /* instJump */
+    case 0x85: return h_call(p, i);
+    case 0x8d: return ORC_PANIC_CALLX;
+    case 0x95: return h_exit(p);
+    case 0xff: return h_jcond(p, i, 0, 0xd0); /* Q: 0xff = instJump64JSLEReg (last write wins) */
+    default: break;
+    }
+    uint8_t cls = op & 7, hi = op & 0xf0;
+    if (cls == 4 || cls == 7) { /* ALU / ALU64 generated ops */
+        switch (hi) {
+        case 0x00: case 0x10: case 0x20: case 0x30: case 0x40: case 0x50:
+        case 0x60: case 0x70: case 0x90: case 0xa0:
+            return h_alu_gen(p, i);
+        }
+        return h_custom(p, i);
+    }
+    if (cls == 5) { /* JMP: K = 64-bit; X = 32-bit (Q1) except JSET X (64-bit) */
+        switch (hi) {
+        case 0x10: case 0x20: case 0x30: case 0x50: case 0x60: case 0x70:
+        case 0xa0: case 0xb0: case 0xc0: case 0xd0:
+            return h_jcond(p, i, (op & 0x08) != 0, hi);
+        case 0x40:
+            return h_jcond(p, i, 0, hi);
+        }
+        return h_custom(p, i);
+    }
+    if (cls == 6) { /* JMP32: K = 32-bit; X = nil except JSET X (Q2) */
+        switch (hi) {
+        case 0x10: case 0x20: case 0x30: case 0x50: case 0x60: case 0x70:
+        case 0xa0: case 0xb0: case 0xc0: case 0xd0:
+            if (op & 0x08) return h_custom(p, i);
+            return h_jcond(p, i, 1, hi);
+        case 0x40:
+            return h_jcond(p, i, 1, hi);
+        }
+        return h_custom(p, i);
+    }
+    return h_custom(p, i);
+}
+
+/* Process.Step, vm.go:291-340.  Returns 0 = continue, EXIT_SIGNAL = exited, >0 status. */
+static int step(orc_proc *p, int32_t *err_pc) {
+    program *prog = p->prog;
+    if ((int64_t)prog->n <= p->R.pc) {
+        *err_pc = (int32_t)p->R.pc;
+        return ORC_ERR_PC_OOB;
+    }
+    if (p->R.pc < 0) {
+        *err_pc = (int32_t)p->R.pc;
+        return ORC_PANIC_PC;
+    }
+    int64_t pc = p->R.pc;
+    int rc = exec_insn(p, &prog->ins[pc]);
+    if (rc == EXIT_SIGNAL) return EXIT_SIGNAL;
+    if (rc) {
+        *err_pc = (int32_t)pc;
+        return rc;
+    }
+    if ((int64_t)p->prog->n <= p->R.pc + 1) {
+        p->R.pc = pc;
+        *err_pc = (int32_t)pc;
+        return ORC_ERR_PC_OOB;
+    }
+    p->R.pc++;
+    return 0;
+}
+
+/* Process.Run, vm.go:343-360 (the ctx deadline is the step budget) */
+static int run(orc_proc *p, uint64_t budget, uint32_t *steps, int32_t *err_pc) {
+    uint64_t n = 0;
+    int st;
+    *err_pc = -1;
+    for (;;) {
+        if (n == budget) {
+            st = ORC_ERR_STEP_LIMIT;
+            *err_pc = (int32_t)p->R.pc;
+            break;
+        }
+        n++;
+        int rc = step(p, err_pc);
+        if (rc == 0) continue;
+        st = rc == EXIT_SIGNAL ? ORC_OK : rc;
+        break;
+    }
+    *steps = (uint32_t)n;
+    return st;
+}
+
+/* VM.NewProcess, vm.go:198-235 (without a context) */
+static orc_proc *proc_new(orc_vm *vm, int prog_id) {
+    orc_proc *p = (orc_proc *)calloc(1, sizeof *p);
+    p->vm = vm;
+    p->prog = vm->progs[prog_id];
+    uint32_t sz = (uint32_t)(vm->frame_count * vm->frame_size);
+    p->stack.b = (uint8_t *)calloc(sz ? sz : 1, 1);
+    p->stack.len = sz;
+    p->cpu = -1;
+    uint32_t a;
+    mc_add(vm, &p->stack, K_PLAIN, sz, &a);
+    p->R.r[10] = (uint64_t)(a + (uint32_t)vm->frame_size);
+    return p;
+}
+
+orc_proc *orc_proc_new(orc_vm *vm, int prog_id) {
+    if (prog_id < 0 || prog_id >= vm->nprogs) return NULL;
+    return proc_new(vm, prog_id);
+}
+
+/* Process.Cleanup, vm.go:363-374 + LinuxContextXDP.Cleanup, context_xdp_md.go:118-133 */
+static void proc_cleanup(orc_proc *p) {
+    mc_del_obj(p->vm, &p->stack);
+    if (p->has_ctx) {
+        mc_del_obj(p->vm, p->pkt);
+        mc_del_obj(p->vm, p->xdpmd);
+        pm_free(p->pkt);
+        pm_free(p->xdpmd);
+    }
+    free(p->stack.b);
+    free(p->frames);
+}
+
+void orc_proc_free(orc_proc *p) {
+    if (!p) return;
+    proc_cleanup(p);
+    free(p);
+}
+
+int orc_proc_set_cpu(orc_proc *p, int id) { /* vm.go:268-283 (Q18: id == V accepted) */
+    if (id < 0) return -1;
+    if (id > p->vm->vcpus) return -1;
+    p->cpu = id;
+    return 0;
+}
+uint64_t orc_proc_get_reg(orc_proc *p, int r) { return p->R.r[r]; }
+void orc_proc_set_reg(orc_proc *p, int r, uint64_t v) { p->R.r[r] = v; }
+int orc_proc_call_helper(orc_proc *p, int32_t helper) { return call_helper(p, helper); }
+
+/* LinuxContextXDP.Load, context_xdp_md.go:47-115 */
+static void xdp_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t H, uint32_t T, int32_t ingress,
+                     int32_t rxq, int32_t egress) {
+    p->has_ctx = 1;
+    p->pkt = pm_new(H + L + T);
+    p->xdpmd = pm_new(24);
+    memcpy(p->pkt->b + H, pkt, L);
+    uint32_t pa;
+    mc_add(p->vm, p->pkt, K_PLAIN, H + L + T, &pa);
+    pm_store(p->xdpmd, 0, (uint64_t)pa + H, 4);
+    pm_store(p->xdpmd, 4, (uint64_t)pa + H + L, 4);
+    pm_store(p->xdpmd, 8, (uint64_t)pa + H, 4);
+    pm_store(p->xdpmd, 12, (uint64_t)(int64_t)ingress, 4);
+    pm_store(p->xdpmd, 16, (uint64_t)(int64_t)rxq, 4);
+    pm_store(p->xdpmd, 20, (uint64_t)(int64_t)egress, 4);
+    uint32_t xa;
+    mc_add(p->vm, p->xdpmd, K_PLAIN, 24, &xa);
+    p->R.r[1] = xa;
+}
+
+int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_results *out) {
+    if (prog_id < 0 || prog_id >= vm->nprogs) {
+        set_err(vm, "no program with id '%d' is loaded", prog_id);
+        return -1;
+    }
+    uint64_t budget = b->step_budget ? b->step_budget : DEFAULT_BUDGET;
+    for (uint32_t i = 0; i < b->n; i++) {
+        uint32_t H = b->headroom_arr ? b->headroom_arr[i] : b->headroom;
+        uint32_t T = b->tailroom_arr ? b->tailroom_arr[i] : b->tailroom;
+        uint32_t L = b->pkt_len[i];
+        uint8_t *mem = b->pkt_data + b->pkt_off[i];
+        orc_proc *p = proc_new(vm, prog_id);
+        xdp_load(p, mem + H, L, H, T, b->ingress_ifindex ? b->ingress_ifindex[i] : 0,
+                 b->rx_queue_index ? b->rx_queue_index[i] : 0, b->egress_ifindex ? b->egress_ifindex[i] : 0);
+        int cpu = b->cpu ? b->cpu[i] : 0;
+        uint32_t steps = 0;
+        int32_t epc = -1;
+        int st;
+        if (orc_proc_set_cpu(p, cpu)) {
+            st = ORC_ERR_NO_CPU;
+        } else {
+            st = run(p, budget, &steps, &epc);
+        }
+        if (out->r0) out->r0[i] = p->R.r[0];
+        if (out->status) out->status[i] = (uint8_t)st;
+        if (out->steps) out->steps[i] = steps;
+        if (out->err_pc) out->err_pc[i] = st == ORC_OK ? -1 : epc;
+        if (b->write_back) memcpy(mem, p->pkt->b, H + L + T);
+        orc_proc_free(p);
+    }
+    return 0;
+}

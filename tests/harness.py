@@ -1,0 +1,136 @@
+"""Shared test harness: build the same VM (maps, programs, prog-array entries) on the CPU
+oracle and on the GPU engine, run one xdp_md batch on both, compare everything."""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from mimic_amd import asm as A  # noqa: E402
+
+
+@dataclass
+class Scenario:
+    vcpus: int = 4
+    maps: List[dict] = field(default_factory=list)          # name,type,key_size,value_size,max_entries[,datasec]
+    progs: List[Tuple[str, bytes, List[Tuple[int, str]]]] = field(default_factory=list)
+    prog_array: List[Tuple[str, int, int]] = field(default_factory=list)  # (map, key, prog index)
+    map_init: List[Tuple[str, bytes, bytes, int]] = field(default_factory=list)  # (map, key, value, cpu)
+    max_tail_calls: int = 33
+
+
+def build_oracle(sc: Scenario):
+    import oracle
+
+    vm = oracle.OracleVM(sc.vcpus, 256, 8, sc.max_tail_calls)
+    mids = {}
+    for m in sc.maps:
+        mids[m["name"]] = vm.map_create(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"],
+                                        m.get("datasec", False))
+    pids = []
+    for name, raw, rel in sc.progs:
+        pids.append(vm.prog_load(name, raw, [(s, mids[n]) for s, n in rel]))
+    for mname, key, pi in sc.prog_array:
+        rc = vm.map_update(mids[mname], key.to_bytes(4, "little"), vm.prog_addr(pids[pi]).to_bytes(4, "little"))
+        assert rc == 0
+    for mname, key, val, cpu in sc.map_init:
+        assert vm.map_update(mids[mname], key, val, 0, cpu) == 0
+    return vm, mids, pids
+
+
+def build_engine(sc: Scenario, device: int = 0, shard=None):
+    import mimic_amd as M
+
+    emu = M.NewLinuxEmulator(M.OptMaxTailCalls(sc.max_tail_calls))
+    opts = [M.VMOptEmulator(emu), M.VMOptSetvCPUs(sc.vcpus), M.VMOptDevice(device)]
+    if shard is not None:
+        opts.append(M.VMOptShard(*shard))
+    vm = M.NewVM(*opts)
+    maps = {}
+    for m in sc.maps:
+        mm = M.MapSpecToLinuxMap(M.MapSpec(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"],
+                                           m.get("datasec", False)))
+        emu.AddMap(m["name"], mm)
+        maps[m["name"]] = mm
+    pids = [vm.AddProgram(M.ProgramSpec(name, raw, list(rel))) for name, raw, rel in sc.progs]
+    for mname, key, pi in sc.prog_array:
+        assert maps[mname].UpdateProgram(key.to_bytes(4, "little"), pids[pi]) == 0
+    for mname, key, val, cpu in sc.map_init:
+        assert maps[mname].Update(key, val, 0, cpu) == 0
+    return vm, maps, pids
+
+
+def packets_to_buffer(packets: Sequence[bytes], headroom=0, tailroom=0, align: int = 64):
+    import mimic_amd as M
+
+    lens = np.array([len(p) for p in packets], dtype=np.uint32)
+    off, total = M.XDPBatch.layout(lens, headroom, tailroom, align)
+    buf = np.zeros(max(total, 1), dtype=np.uint8)
+    for i, p in enumerate(packets):
+        h = headroom if np.isscalar(headroom) else int(headroom[i])
+        buf[int(off[i]) + h:int(off[i]) + h + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    return buf, off, lens
+
+
+def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, tailroom=0, ingress=None,
+               rxq=None, egress=None, step_budget=0):
+    vm, mids, pids = build_oracle(sc)
+    out = vm.run_xdp_batch(pids[entry], buf.copy(), off, lens, cpu, headroom, tailroom, ingress, rxq, egress,
+                           step_budget)
+    out["maps"] = {}
+    for m in sc.maps:
+        ncpu = sc.vcpus if m["type"] in (5, 6) else 1
+        out["maps"][m["name"]] = [vm.map_values(mids[m["name"]], c) for c in range(ncpu)]
+    vm.close()
+    return out
+
+
+def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=0, tailroom=0, ingress=0, rxq=0,
+               egress=0, step_budget=0, schedule=None, device: int = 0):
+    import mimic_amd as M
+
+    vm, maps, pids = build_engine(sc, device)
+    if schedule is None:
+        schedule = M.SCHED_EXPLICIT
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device=f"cuda:{device}", headroom=headroom, tailroom=tailroom,
+                                  ingress=ingress, rxq=rxq, egress=egress, schedule=schedule, cpu=cpu,
+                                  step_budget=step_budget)
+    res = vm.RunXDPBatch(pids[entry], batch)
+    out = res.numpy(len(lens))
+    out["pkt"] = batch.pkt_data.cpu().numpy()
+    out["maps"] = {}
+    for m in sc.maps:
+        ncpu = sc.vcpus if m["type"] in (5, 6) else 1
+        out["maps"][m["name"]] = [maps[m["name"]].Values(c) for c in range(ncpu)]
+    out["steps_total"] = vm.LastSteps()
+    vm.close()
+    return out
+
+
+def assert_same(o, e, check_pkt: bool = True, n: Optional[int] = None):
+    for k in ("r0", "status", "steps", "err_pc"):
+        a = np.asarray(o[k])
+        b = np.asarray(e[k])
+        if n is not None:
+            a, b = a[:n], b[:n]
+        a = a.astype(np.uint64) if k == "r0" else a.astype(np.int64)
+        b = b.astype(np.uint64) if k == "r0" else b.astype(np.int64)
+        bad = np.nonzero(a != b)[0]
+        assert len(bad) == 0, f"{k} differs at {bad[:8]}: oracle={a[bad[:8]]} engine={b[bad[:8]]}"
+    if check_pkt:
+        assert np.array_equal(o["pkt"][:len(e["pkt"])], e["pkt"][:len(o["pkt"])]), "packet memory differs"
+    for name, vals in o["maps"].items():
+        for c, v in enumerate(vals):
+            assert v == e["maps"][name][c], f"map {name} cpu {c} differs"
+
+
+def single(sc: Scenario, packet: bytes = b"\x00" * 64, cpu: int = 0, **kw):
+    buf, off, lens = packets_to_buffer([packet], kw.pop("headroom", 0), kw.pop("tailroom", 0))
+    return buf, off, lens, np.array([cpu], dtype=np.int32)
