@@ -47,7 +47,8 @@ def dist_env():
 
 
 def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps) -> int:
-    """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU map state."""
+    """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU map state.
+    (The engine's actual descriptor is 12 B and it also writes a 1-B status; not counted.)"""
     b = int(lens.astype(np.int64).sum()) + 16 * len(lens)
     for m in maps:
         ncpu = vcpus if m["type"] in (5, 6) else 1
@@ -155,7 +156,7 @@ def main():
     buf, off, lens = W.make_packets(n, cfg["sizes"], cfg["weights"], seed=W.SEED + rank)
     sched = M.SCHED_INTERLEAVED if args.sched == "interleaved" else M.SCHED_CHUNKED
     batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, ingress=1, schedule=sched)
-    res = M.XDPResults.empty(n, dev)
+    res = M.XDPResults.empty(n, dev, full=False)  # R0 + status per packet; steps via per-lane counters
     stream = torch.cuda.Stream(device=dev)
 
     def step():

@@ -123,17 +123,142 @@ static int arena_reserve(mimic_vm *vm, uint64_t bytes, uint64_t *off) {
     return 0;
 }
 
+// Host predecode of one slot into a handler id + uniform facts (see layout.h).  Mirrors the
+// effective dispatch table (inst.go:15-78 after inst_gen.go:607-688) and the
+// order in which each handler reports errors; anything whose outcome can differ per lane goes
+// to H_SLOW or to a fast handler that checks per lane.
+static int helper_class(int32_t n) {  // emulator_linux_helpers.go:28-204
+    static const int ce[] = {4, 14, 15, 16, 17, 22, 24, 27, 35, 36, 42, 45, 46, 47, 55, 56, 67, 69, 80,
+                             112, 113, 114, 115, 119, 120, 122, 123, 128, 129, 141, 148, 151};
+    static const int em[] = {1, 2, 3, 5, 7, 8, 9, 12, 25, 38, 65, 87, 88, 89, 125, 160};
+    for (int v : ce) if (v == n) return 2;
+    for (int v : em) if (v == n) return 1;
+    return 0;
+}
+
+static uint32_t predecode(const DInsn &x, int64_t i, int64_t n) {
+    const uint32_t op = x.w & 0xff, dst = (x.w >> 8) & 0xf, src = (x.w >> 12) & 0xf;
+    const int64_t off = (int16_t)(x.w >> 16);
+    const int32_t imm32 = (int32_t)(uint32_t)x.k;
+    const uint32_t cls = op & 7, hi = op & 0xf0;
+    const bool xs = (op & 8) != 0;
+    const int64_t tgt = op == 0x85 ? i + (int64_t)imm32 : i + off + 1;  // after Step's PC++
+    uint32_t a = 0;
+    if (i + 1 < n) a |= AUX_FALL_OK;
+    if (tgt >= 0 && tgt < n) a |= AUX_JT_OK;
+    if (tgt < 0) a |= AUX_JT_NEG;
+    auto err = [&](uint32_t st) { return a | H_ERR | (st << 16); };
+    auto sz = [&](uint32_t o) -> uint32_t {
+        switch (o & 0x18) { case 0x00: return 4; case 0x08: return 2; case 0x10: return 1; default: return 8; }
+    };
+    auto jcc_ok = [&](uint32_t jop) {
+        switch (jop) {
+        case 0x10: case 0x20: case 0x30: case 0x40: case 0x50: case 0x60: case 0x70:
+        case 0xa0: case 0xb0: case 0xc0: case 0xd0: return true;
+        default: return false;
+        }
+    };
+    if (op == 0x00) return a | H_NOP;
+    if (op == 0xff) {  // instJump64JSLEReg (Appendix A)
+        if (src > 10 || dst > 10) return err(MIMIC_PANIC_BADREG);
+        return a | H_JCC | AUX_X | (0xd0u << 16);
+    }
+    if (cls == 4 || cls == 7) {
+        const bool is64 = cls == 7;
+        const uint32_t H = is64 ? H_ALU64 : H_ALU32;
+        switch (hi) {
+        case 0x00: case 0x10: case 0x20: case 0x40: case 0x50: case 0x60: case 0x70: case 0xa0:
+        case 0x30: case 0x90: {
+            if (dst > 10 || (xs && src > 10)) return err(MIMIC_PANIC_BADREG);
+            const bool div = hi == 0x30 || hi == 0x90;
+            if (div && xs) return a | H_SLOW;                                   // per-lane div-by-zero
+            if (div && (is64 ? x.k == 0 : (uint32_t)x.k == 0)) return err(MIMIC_PANIC_DIV0);
+            if (dst == 10) return err(MIMIC_ERR_R10_WRITE);
+            return a | H | (xs ? AUX_X : 0);
+        }
+        case 0x80:  // NEG
+            if (dst > 10) return err(MIMIC_PANIC_BADREG);
+            if (dst == 10) return err(MIMIC_ERR_R10_WRITE);
+            return a | H;
+        case 0xb0:  // MOV
+            if ((xs && src > 10) || dst > 10) return err(MIMIC_PANIC_BADREG);
+            if (dst == 10) return err(MIMIC_ERR_R10_WRITE);
+            return a | H | (xs ? AUX_X : 0);
+        case 0xc0:  // ARSH
+            if (dst > 10 || (xs && src > 10)) return err(MIMIC_PANIC_BADREG);
+            if (!xs && (int64_t)x.k < 0) return err(MIMIC_PANIC_SHIFT);
+            if (dst == 10) return err(MIMIC_ERR_R10_WRITE);
+            return a | H | (xs ? AUX_X : 0);
+        case 0xd0:
+            if (is64) return err(MIMIC_ERR_UNSUPPORTED_OP);
+            return a | H_SLOW;  // END
+        default:
+            return err(MIMIC_ERR_UNSUPPORTED_OP);
+        }
+    }
+    if (cls == 5 || cls == 6) {
+        const bool j32 = cls == 6;
+        if (!j32 && hi == 0x00) return xs ? err(MIMIC_ERR_UNSUPPORTED_OP) : (a | H_JA);
+        if (!j32 && hi == 0x90) return xs ? err(MIMIC_ERR_UNSUPPORTED_OP) : (a | H_EXIT);
+        if (!j32 && hi == 0x80) {
+            if (xs) return err(MIMIC_PANIC_CALLX);
+            if (src == 1) return a | H_CALL_LOCAL;
+            if (imm32 < 0) return err(MIMIC_PANIC_HELPER_NEG);
+            if (imm32 >= 176) return err(MIMIC_ERR_HELPER_UNIMPLEMENTED);
+            const int hc = helper_class(imm32);
+            if (hc == 0) return err(MIMIC_ERR_HELPER_UNIMPLEMENTED);
+            if (hc == 2) return err(MIMIC_ERR_HELPER_CANT_EMULATE);
+            switch (imm32) {
+            case 1: case 2: case 3: case 8: case 12: case 65: return a | H_CALL;
+            default: return err(MIMIC_ERR_ENGINE_HELPER);
+            }
+        }
+        if (jcc_ok(hi)) {
+            if (j32 && xs && hi != 0x40) return err(MIMIC_ERR_UNSUPPORTED_OP);  // Q2
+            if (dst > 10 || (xs && src > 10)) return err(MIMIC_PANIC_BADREG);
+            const bool w32 = j32 || (xs && hi != 0x40);                          // Q1
+            return a | H_JCC | (w32 ? AUX_W32 : 0) | (xs ? AUX_X : 0) | (hi << 16);
+        }
+        return err(MIMIC_ERR_UNSUPPORTED_OP);
+    }
+    if (cls == 1) {
+        if ((op & 0xe0) != 0x60) return err(MIMIC_ERR_UNSUPPORTED_OP);
+        if (src > 10) return err(MIMIC_PANIC_BADREG);
+        if (dst >= 10) return a | H_SLOW;  // memory errors come before the register error
+        return a | H_LDX | (sz(op) << 24);
+    }
+    if (cls == 2 || cls == 3) {
+        if ((op & 0xe0) != 0x60) return err(MIMIC_ERR_UNSUPPORTED_OP);
+        if (dst > 10 || (cls == 3 && src > 10)) return err(MIMIC_PANIC_BADREG);
+        return a | (cls == 2 ? H_ST : H_STX) | (sz(op) << 24);
+    }
+    // LD class
+    if (op == 0x18) {
+        if (dst > 10) return err(MIMIC_PANIC_BADREG);
+        if (dst == 10) return err(MIMIC_ERR_R10_WRITE);
+        return a | H_LDIMM;
+    }
+    if ((op & 0xe0) == 0x20 || (op & 0xe0) == 0x40) return err(MIMIC_ERR_LDABS);
+    return err(MIMIC_ERR_UNSUPPORTED_OP);
+}
+
 static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     std::vector<DInsn> all;
     std::vector<DProg> dp;
-    for (auto &p : vm->progs) {
+    for (size_t pi = 0; pi < vm->progs.size(); pi++) {
+        auto &p = vm->progs[pi];
         DProg d{};
         d.base = (uint32_t)all.size();
         d.n = (uint32_t)p.ins.size();
         d.addr = p.addr;
         dp.push_back(d);
-        all.insert(all.end(), p.ins.begin(), p.ins.end());
+        const int64_t n = (int64_t)p.ins.size();
+        for (int64_t i = 0; i < n; i++) {
+            DInsn x = p.ins[i];
+            x.aux = predecode(x, i, n);
+            all.push_back(x);
+        }
     }
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
     std::vector<DMap> dm;
@@ -458,8 +583,10 @@ int mimic_map_addr(mimic_vm *vm, uint32_t id, uint32_t *addr_out) {
 int mimic_program_load(mimic_vm *vm, const char *name, const void *insns, uint32_t n_slots,
                        const mimic_reloc *relocs, uint32_t n_relocs, uint32_t *prog_id) {
     if (!vm || (!insns && n_slots) || !prog_id) return MIMIC_EINVAL;
-    if (n_slots >= (1u << MIMIC_PC_BITS)) return fail(vm, MIMIC_EINVAL, "program too long");
-    if (vm->progs.size() >= (1u << (32 - MIMIC_PC_BITS)) - 1) return fail(vm, MIMIC_EINVAL, "too many programs");
+    uint64_t total = n_slots;
+    for (auto &q : vm->progs) total += q.ins.size();
+    if (n_slots >= (1u << MIMIC_PC_BITS) || total >= 0x7fffffffull) return fail(vm, MIMIC_EINVAL, "program too long");
+    if (vm->progs.size() >= 65535) return fail(vm, MIMIC_EINVAL, "too many programs");
     hipSetDevice(vm->s.device);
     const uint8_t *raw = (const uint8_t *)insns;
     HostProg p;
@@ -594,8 +721,8 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
     kp.static_next = vm->next_addr;
     kp.stack_size = S;
     kp.frame_size = (uint32_t)vm->s.stack_frame_size;
-    uint32_t shift = 3;
-    while ((S >> shift) > 64) shift++;
+    uint32_t shift = 3;  // lazy-zero granule above the first 512 stack bytes
+    while (S > 512 && ((S - 512 + (1u << shift) - 1) >> shift) > 64) shift++;
     kp.chunk_shift = shift;
     kp.max_tail_calls = (uint32_t)std::max(0, vm->s.max_tail_calls);
     kp.total_vcpus = (uint32_t)vm->s.vcpus;

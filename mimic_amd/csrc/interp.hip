@@ -38,6 +38,25 @@ typedef uint64_t __attribute__((aligned(1))) u64u;
 
 #define DEV static __device__ __forceinline__
 
+// Read-only tables are read through the constant address space so that wave-uniform
+// indices become scalar (s_load) fetches through the scalar cache.
+#define CONST_AS __attribute__((address_space(4)))
+template <typename T>
+DEV T cget(const T *p, uint32_t i) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized tables only");
+    uint32_t w[sizeof(T) / 4];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const CONST_AS uint32_t *q = (const CONST_AS uint32_t *)(p + i);
+#else
+    const uint32_t *q = (const uint32_t *)(p + i);  // host pass: never executed
+#endif
+#pragma unroll
+    for (unsigned k = 0; k < sizeof(T) / 4; k++) w[k] = q[k];
+    T out;
+    __builtin_memcpy(&out, w, sizeof(T));
+    return out;
+}
+
 enum RegionKind : uint32_t { RK_UNRES = 0, RK_STACK = 1, RK_XDP = 2, RK_GLOBAL = 3, RK_NOTVMMEM = 4, RK_NOTDATASEC = 5 };
 
 struct Ref {
@@ -53,7 +72,7 @@ struct Lane {
     uint8_t *pkt;         // packet memory (device)
     uint32_t data, data_end, ingress, rxq, egress;
     uint32_t xdp_dirty;
-    uint64_t smask;       // stack granules already zeroed in this process
+    uint64_t sm0, sm1;    // stack words / granules already written in this process
     uint32_t nframes, tailcalls;
 };
 
@@ -106,35 +125,61 @@ DEV void priv_store(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n, ui
 
 // ---------------------------------------------------------------------------------------
 // stack (PlainMemory of StackFrameCount*StackFrameSize zero bytes, vm.go:208-210)
+//
+// The reference gives every process a fresh zeroed stack.  Instead of zeroing 2 KiB per
+// packet, validity is tracked per lane: sm0 has one bit per 8-byte word of the first 512
+// bytes (frames 0 and 1, where programs live), sm1 one bit per (1<<chunk_shift)-byte
+// granule of the rest.  Reads of never-written bytes return 0 without touching memory; the
+// first write to a word stores the whole zero-extended word.
 // ---------------------------------------------------------------------------------------
-DEV void stack_touch(const KParams &kp, Lane &L, uint32_t c) {
-    if (!((L.smask >> c) & 1)) {
-        uint32_t q0 = (c << kp.chunk_shift) >> 3, nq = (1u << kp.chunk_shift) >> 3;
-        for (uint32_t q = 0; q < nq; q++) *(uint64_t *)priv_b(kp, L.lane, (q0 + q) << 3) = 0;
-        L.smask |= 1ull << c;
+#define STK_FINE 512u
+DEV bool stk_valid(const KParams &kp, const Lane &L, uint32_t o) {
+    return o < STK_FINE ? ((L.sm0 >> (o >> 3)) & 1) : ((L.sm1 >> ((o - STK_FINE) >> kp.chunk_shift)) & 1);
+}
+DEV void stk_touch(const KParams &kp, Lane &L, uint32_t o) {
+    if (o < STK_FINE) {
+        const uint32_t q = o >> 3;
+        if (!((L.sm0 >> q) & 1)) {
+            *(uint64_t *)priv_b(kp, L.lane, q << 3) = 0;
+            L.sm0 |= 1ull << q;
+        }
+    } else {
+        const uint32_t c = (o - STK_FINE) >> kp.chunk_shift;
+        if (!((L.sm1 >> c) & 1)) {
+            const uint32_t q0 = (STK_FINE + (c << kp.chunk_shift)) >> 3, nq = (1u << kp.chunk_shift) >> 3;
+            for (uint32_t q = 0; q < nq; q++) *(uint64_t *)priv_b(kp, L.lane, (q0 + q) << 3) = 0;
+            L.sm1 |= 1ull << c;
+        }
     }
 }
 DEV uint64_t stack_load(const KParams &kp, const Lane &L, uint32_t o, uint32_t n) {
     if ((o & 7) + n <= 8) {
-        if (!((L.smask >> (o >> kp.chunk_shift)) & 1)) return 0;
+        if (!stk_valid(kp, L, o)) return 0;
         return ld_n(priv_b(kp, L.lane, o), n);
     }
     uint64_t v = 0;
     for (uint32_t i = 0; i < n; i++) {
-        uint32_t oo = o + i;
-        if ((L.smask >> (oo >> kp.chunk_shift)) & 1) v |= (uint64_t)*priv_b(kp, L.lane, oo) << (8 * i);
+        const uint32_t oo = o + i;
+        if (stk_valid(kp, L, oo)) v |= (uint64_t)*priv_b(kp, L.lane, oo) << (8 * i);
     }
     return v;
 }
 DEV void stack_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t v) {
     if ((o & 7) + n <= 8) {
-        stack_touch(kp, L, o >> kp.chunk_shift);
+        if (o < STK_FINE && !((L.sm0 >> (o >> 3)) & 1)) {
+            // first write to this word: store the whole word, zero-extended around the value
+            const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+            *(uint64_t *)priv_b(kp, L.lane, o & ~7u) = (v & m) << (8 * (o & 7));
+            L.sm0 |= 1ull << (o >> 3);
+            return;
+        }
+        stk_touch(kp, L, o);
         st_n(priv_b(kp, L.lane, o), n, v);
         return;
     }
     for (uint32_t i = 0; i < n; i++) {
-        uint32_t oo = o + i;
-        stack_touch(kp, L, oo >> kp.chunk_shift);
+        const uint32_t oo = o + i;
+        stk_touch(kp, L, oo);
         *priv_b(kp, L.lane, oo) = (uint8_t)(v >> (8 * i));
     }
 }
@@ -209,7 +254,7 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
     }
     bool found = false;
     for (uint32_t s = 0; s < kp.nsegs; s++) {
-        const Seg g = kp.segs[s];
+        const Seg g = cget(kp.segs, s);
         if (!found && a >= g.lo && a <= g.hi) {
             found = true;
             uint32_t off = a - g.lo;
@@ -506,7 +551,7 @@ DEV uint32_t wave_min(uint32_t v) {
     uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
     a = a < b ? a : b;
     c = c < d ? c : d;
-    return a < c ? a : c;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(a < c ? a : c));  // provably wave-uniform
 }
 
 // ---------------------------------------------------------------------------------------
@@ -566,9 +611,65 @@ DEV uint32_t size_bytes(uint32_t op) {
 }
 
 // ---------------------------------------------------------------------------------------
+// fast ALU ops (inst_gen.go:7-225, inst.go:86-136); the host only routes valid forms here
+// ---------------------------------------------------------------------------------------
+DEV uint64_t alu64(uint32_t hi, uint64_t d, uint64_t x) {
+    switch (hi) {
+    case 0x00: return d + x;
+    case 0x10: return d - x;
+    case 0x20: return d * x;
+    case 0x30: return d / x;   // K form, x != 0 (predecoded)
+    case 0x40: return d | x;
+    case 0x50: return d & x;
+    case 0x60: return x >= 64 ? 0 : d << x;
+    case 0x70: return x >= 64 ? 0 : d >> x;
+    case 0x80: return (uint64_t)(-(int64_t)d);
+    case 0x90: return d % x;
+    case 0xa0: return d ^ x;
+    case 0xb0: return x;
+    default: { // 0xc0 ARSH (x >= 0)
+        const int64_t a = (int64_t)d;
+        return (uint64_t)(x >= 64 ? (a < 0 ? -1 : 0) : (a >> x));
+    }
+    }
+}
+DEV uint64_t alu32(uint32_t hi, uint64_t d, uint64_t x) {
+    const uint32_t a = (uint32_t)d, b = (uint32_t)x;
+    switch (hi) {
+    case 0x00: return (uint32_t)(a + b);
+    case 0x10: return (uint32_t)(a - b);
+    case 0x20: return (uint32_t)(a * b);
+    case 0x30: return a / b;
+    case 0x40: return a | b;
+    case 0x50: return a & b;
+    case 0x60: return b >= 32 ? 0 : (uint32_t)(a << b);
+    case 0x70: return b >= 32 ? 0 : a >> b;
+    case 0x80: return (uint64_t)(int64_t)(int32_t)(0u - a);          // Q6: sign-extends
+    case 0x90: return a % b;
+    case 0xa0: return a ^ b;
+    case 0xb0: return b;
+    default: { // ARSH: the 64-bit shift count is not truncated; result sign-extends (Q5/Q6)
+        const int32_t sa = (int32_t)a;
+        return (uint64_t)(int64_t)(x >= 32 ? (sa < 0 ? -1 : 0) : (sa >> x));
+    }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
+#define WAVES_PER_BLOCK 4
+#define NREGS 11
+#define KEY_DONE 0xffffffffu
+
 extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(KParams kp) {
+    // eBPF registers r0..r10 of every lane live in LDS, [wave][reg][lane] (8-byte words): a
+    // wave-uniform register number addresses 64 consecutive words (conflict-free ds_read_b64),
+    // and multi-register updates (exit, helpers) need no register-array copies.
+    __shared__ uint64_t sreg[WAVES_PER_BLOCK][NREGS][64];
+    uint64_t *const RB = &sreg[threadIdx.x >> 6][0][threadIdx.x & 63];
+#define REG(r) RB[(r) * 64]
+
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const bool lane_valid = g < kp.lanes;
     Lane L;
@@ -581,7 +682,8 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(KParams kp) {
         ex_count = kp.sched_start[g + 1] - ex_begin;
     }
     uint64_t lane_steps = 0;
-    const DProg entry = kp.progs[kp.entry_prog];
+    const DProg entry = cget(kp.progs, kp.entry_prog);
+    const uint32_t P = kp.static_next + kp.stack_size + 1;
 
     for (uint32_t j = 0; j < kp.per_lane; j++) {
         // ---- which packet does this lane run in iteration j -----------------------------
@@ -597,335 +699,248 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(KParams kp) {
                 i = kp.sched_pkts[ex_begin + j];
             }
         }
-        bool running = i != 0xffffffffu;
 
         // ---- NewProcess + LinuxContextXDP.Load --------------------------------------------
-        uint64_t r[12];
 #pragma unroll
-        for (int q = 0; q < 12; q++) r[q] = 0;
-        uint32_t prog = kp.entry_prog, pn = entry.n;
-        int32_t pc = 0, err_pc = -1;
-        uint32_t steps = 0, status = MIMIC_OK;
-        L.smask = 0;
+        for (int q = 0; q < NREGS; q++) REG(q) = 0;
+        uint32_t pn = entry.n, pbase = entry.base;
+        uint32_t key = KEY_DONE;   // global instruction index = pbase + PC; KEY_DONE = not running
+        uint32_t steps = 0;
+        L.sm0 = 0;
+        L.sm1 = 0;
         L.xdp_dirty = 0;
         L.nframes = 0;
         L.tailcalls = 0;
         L.M = 0;
         L.pkt = nullptr;
-        if (running) {
-            uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;
-            uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;
-            uint32_t len = kp.pkt_len[i];
+        // a process ends here: results straight to HBM (Run's return + p.Registers.R0)
+#define TERM(st_, epc_)                                                \
+        do {                                                           \
+            if (kp.r0) kp.r0[i] = REG(0);                              \
+            if (kp.status) kp.status[i] = (uint8_t)(st_);              \
+            if (kp.steps) kp.steps[i] = steps;                         \
+            if (kp.err_pc) kp.err_pc[i] = (int32_t)(epc_);             \
+            lane_steps += steps;                                       \
+            key = KEY_DONE;                                            \
+        } while (0)
+        if (i != 0xffffffffu) {
+            const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;
+            const uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;
+            const uint32_t len = kp.pkt_len[i];
             L.pkt = kp.pkt_data + kp.pkt_off[i];
             L.M = H + len + T;
             for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;
             for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;
-            const uint32_t P = kp.static_next + kp.stack_size + 1;
             L.data = P + H;
             L.data_end = P + H + len;
             L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);
             L.rxq = (uint32_t)(kp.rxq_arr ? kp.rxq_arr[i] : kp.rxq);
             L.egress = (uint32_t)(kp.egress_arr ? kp.egress_arr[i] : kp.egress);
-            r[1] = P + L.M + 1;                       // R1 = xdp_md address
-            r[10] = kp.static_next + kp.frame_size;   // R10 = stack + StackFrameSize
-            if (pn == 0) {                            // Step on an empty program (vm.go:297-299)
+            REG(1) = P + L.M + 1;                        // R1 = xdp_md address
+            REG(10) = kp.static_next + kp.frame_size;    // R10 = stack + StackFrameSize (vm.go:224)
+            key = pbase;
+            if (pn == 0) {                               // Step on an empty program (vm.go:297-299)
                 steps = 1;
-                status = MIMIC_ERR_PC_OOB;
-                err_pc = 0;
-                running = false;
+                TERM(MIMIC_ERR_PC_OOB, 0);
             }
         }
 
         // ---- Process.Run ------------------------------------------------------------------
+        uint64_t wsteps = 0;          // wave-steps since the packets started: bounds every lane's steps
+        uint32_t cand = KEY_DONE;     // speculated next key (where the first executing lane went)
         for (;;) {
-            const uint32_t key = running ? ((prog << MIMIC_PC_BITS) | (uint32_t)pc) : 0xffffffffu;
-            const uint32_t kw = wave_min(key);
-            if (kw == 0xffffffffu) break;
-            const uint32_t prog_w = kw >> MIMIC_PC_BITS, pc_w = kw & ((1u << MIMIC_PC_BITS) - 1);
-            const DInsn in = kp.insns[kp.progs[prog_w].base + pc_w];
-            if (key != kw) continue;
-
-            if ((uint64_t)steps == kp.budget) {
-                status = MIMIC_ERR_STEP_LIMIT;
-                err_pc = pc;
-                running = false;
-                continue;
-            }
-            steps++;
-
-            const uint32_t op = in.w & 0xff;
-            const uint32_t dst = (in.w >> 8) & 0xf, src = (in.w >> 12) & 0xf;
-            const int32_t off = (int16_t)(in.w >> 16);
-            const uint64_t k = in.k;
-            const uint32_t cls = op & 7, hi = op & 0xf0;
-            const bool xsrc = (op & 0x08) != 0;
-            const uint64_t d = r[dst < 11 ? dst : 11];
-            const uint64_t s = r[src < 11 ? src : 11];
-
-            int st = 0;
-            int64_t pcx = pc;        // PC after the handler, before Step's PC++
-            uint32_t wd = 11;        // destination register written (11 = none)
-            uint64_t wv = 0;
-
-            if (op == 0x00) {
-                // instNop
-            } else if (op == 0xff) { // Appendix A: slot 0xff = instJump64JSLEReg
-                if (src > 10 || dst > 10) st = MIMIC_PANIC_BADREG;
-                else if ((int64_t)d <= (int64_t)s) pcx += off;
-            } else if (cls == 4 || cls == 7) {
-                const bool is64 = cls == 7;
-                switch (hi) {
-                case 0x00: case 0x10: case 0x20: case 0x30: case 0x40: case 0x50:
-                case 0x60: case 0x70: case 0x90: case 0xa0: { // inst_gen.go:7-225
-                    if (dst > 10 || (xsrc && src > 10)) { st = MIMIC_PANIC_BADREG; break; }
-                    const uint64_t x = xsrc ? s : k;
-                    uint64_t res = 0;
-                    if (is64) {
-                        switch (hi) {
-                        case 0x00: res = d + x; break;
-                        case 0x10: res = d - x; break;
-                        case 0x20: res = d * x; break;
-                        case 0x30: if (x == 0) st = MIMIC_PANIC_DIV0; else res = d / x; break;
-                        case 0x40: res = d | x; break;
-                        case 0x50: res = d & x; break;
-                        case 0x60: res = x >= 64 ? 0 : d << x; break;
-                        case 0x70: res = x >= 64 ? 0 : d >> x; break;
-                        case 0x90: if (x == 0) st = MIMIC_PANIC_DIV0; else res = d % x; break;
-                        default: res = d ^ x; break;
+            const uint64_t live = __ballot(key != KEY_DONE);
+            if (live == 0) break;
+            uint32_t kw;
+            if (cand != KEY_DONE && (__ballot(key != cand) & live) == 0) kw = cand;  // converged
+            else kw = wave_min(key);                                                 // min-PC
+            kw = (uint32_t)__builtin_amdgcn_readfirstlane((int)kw);
+            const DInsn in = cget(kp.insns, kw);    // scalar loads
+            const uint64_t act = __ballot(key == kw);
+            const uint64_t wbefore = wsteps++;
+            if (key == kw) {
+                const uint32_t pc = kw - pbase;     // PC of this instruction
+                if (wbefore >= kp.budget && (uint64_t)steps == kp.budget) {   // Run's deadline
+                    TERM(MIMIC_ERR_STEP_LIMIT, pc);
+                } else {
+                    steps++;
+                    const uint32_t aux = in.aux;
+                    const uint32_t op = in.w & 0xff;
+                    const uint32_t dst = (in.w >> 8) & 0xf, src = (in.w >> 12) & 0xf;
+                    const int32_t off = (int16_t)(in.w >> 16);
+                    const uint64_t k = in.k;
+                    int st = 0;          // fatal status of this step (EXIT_SIG = clean exit)
+                    int jmp = 0;         // 0 fall through, 1 taken (pc+off+1 / call target), 2 explicit nk
+                    uint32_t nk = 0;
+                    switch (AUX_H(aux)) {
+                    case H_NOP:
+                        break;
+                    case H_ALU64: {
+                        const uint64_t d = REG(dst);
+                        const uint64_t x = (aux & AUX_X) ? REG(src) : k;
+                        REG(dst) = alu64(op & 0xf0, d, x);
+                        break;
+                    }
+                    case H_ALU32: {
+                        const uint64_t d = REG(dst);
+                        const uint64_t x = (aux & AUX_X) ? REG(src) : k;
+                        REG(dst) = alu32(op & 0xf0, d, x);
+                        break;
+                    }
+                    case H_LDIMM:
+                        REG(dst) = k;
+                        break;
+                    case H_JA:
+                        jmp = 1;
+                        break;
+                    case H_JCC: {
+                        const uint64_t d = REG(dst);
+                        const uint64_t x = (aux & AUX_X) ? REG(src) : k;
+                        jmp = jcond(AUX_ARG(aux), d, x, (aux & AUX_W32) != 0) ? 1 : 0;
+                        break;
+                    }
+                    case H_LDX: {
+                        const Ref R = resolve(kp, L, (uint32_t)(REG(src) + (uint64_t)(int64_t)off));
+                        uint64_t v = 0;
+                        st = mem_load(kp, L, R, AUX_SZ(aux), v);
+                        if (!st) REG(dst) = v;
+                        break;
+                    }
+                    case H_ST:
+                    case H_STX: {
+                        const uint64_t v = AUX_H(aux) == H_STX ? REG(src) : k;
+                        const Ref R = resolve(kp, L, (uint32_t)(REG(dst) + (uint64_t)(int64_t)off));
+                        st = mem_store(kp, L, R, AUX_SZ(aux), v);
+                        break;
+                    }
+                    case H_EXIT:  // inst.go:277-296
+                        if (L.nframes > 0) {
+                            L.nframes--;
+                            const uint32_t fq = kp.priv_frame_q + L.nframes * MIMIC_FRAME_QWORDS;
+                            const uint32_t spc = (uint32_t)priv_load(kp, L.lane, fq * 8, 8);
+                            REG(6) = priv_load(kp, L.lane, (fq + 1) * 8, 8);
+                            REG(7) = priv_load(kp, L.lane, (fq + 2) * 8, 8);
+                            REG(8) = priv_load(kp, L.lane, (fq + 3) * 8, 8);
+                            REG(9) = priv_load(kp, L.lane, (fq + 4) * 8, 8);
+                            REG(10) = REG(10) - kp.frame_size;
+                            if (pn <= spc + 1) st = MIMIC_ERR_PC_OOB;   // vm.go:328-334
+                            else { jmp = 2; nk = pbase + spc + 1; }
+                        } else {
+                            st = EXIT_SIG;
                         }
-                    } else {
-                        const uint32_t a = (uint32_t)d, b = (uint32_t)x;
-                        uint32_t rr = 0;
-                        switch (hi) {
-                        case 0x00: rr = a + b; break;
-                        case 0x10: rr = a - b; break;
-                        case 0x20: rr = a * b; break;
-                        case 0x30: if (b == 0) st = MIMIC_PANIC_DIV0; else rr = a / b; break;
-                        case 0x40: rr = a | b; break;
-                        case 0x50: rr = a & b; break;
-                        case 0x60: rr = b >= 32 ? 0 : a << b; break;
-                        case 0x70: rr = b >= 32 ? 0 : a >> b; break;
-                        case 0x90: if (b == 0) st = MIMIC_PANIC_DIV0; else rr = a % b; break;
-                        default: rr = a ^ b; break;
-                        }
-                        res = rr;
-                    }
-                    if (!st) {
-                        if (dst == 10) st = MIMIC_ERR_R10_WRITE;
-                        else { wd = dst; wv = res; }
-                    }
-                    break;
-                }
-                case 0x80: // NEG, inst.go:86-94 (Q6)
-                    if (dst > 10) { st = MIMIC_PANIC_BADREG; break; }
-                    if (dst == 10) { st = MIMIC_ERR_R10_WRITE; break; }
-                    wd = dst;
-                    wv = is64 ? (uint64_t)(-(int64_t)d) : (uint64_t)(int64_t)(int32_t)(0u - (uint32_t)d);
-                    break;
-                case 0xb0: { // MOV, inst.go:96-114
-                    if (xsrc && src > 10) { st = MIMIC_PANIC_BADREG; break; }
-                    if (dst > 10) { st = MIMIC_PANIC_BADREG; break; }
-                    if (dst == 10) { st = MIMIC_ERR_R10_WRITE; break; }
-                    uint64_t v = xsrc ? s : (is64 ? k : (uint64_t)(uint32_t)k);
-                    if (xsrc && !is64) v = (uint32_t)v;
-                    wd = dst;
-                    wv = v;
-                    break;
-                }
-                case 0xc0: { // ARSH, inst.go:116-136 (Q5/Q6)
-                    if (dst > 10 || (xsrc && src > 10)) { st = MIMIC_PANIC_BADREG; break; }
-                    if (!xsrc && (int64_t)k < 0) { st = MIMIC_PANIC_SHIFT; break; }
-                    const uint64_t x = xsrc ? s : k;
-                    uint64_t res;
-                    if (is64) {
-                        const int64_t a = (int64_t)d;
-                        res = (uint64_t)(x >= 64 ? (a < 0 ? -1 : 0) : (a >> x));
-                    } else {
-                        const int32_t a = (int32_t)(uint32_t)d;
-                        const int32_t y = x >= 32 ? (a < 0 ? -1 : 0) : (a >> x);
-                        res = (uint64_t)(int64_t)y;
-                    }
-                    if (dst == 10) { st = MIMIC_ERR_R10_WRITE; break; }
-                    wd = dst;
-                    wv = res;
-                    break;
-                }
-                case 0xd0: // END, inst.go:138-198 (Q4); only the ALU32 slots exist
-                    if (is64) { st = MIMIC_ERR_UNSUPPORTED_OP; break; }
-                    if (dst > 10) { st = MIMIC_PANIC_BADREG; break; }
-                    {
-                        uint64_t v = d;
-                        if (k == 16) {
-                            v = xsrc ? (d & 0xffff) : (((d >> 8) & 0xff) | ((d & 0xff) << 8));
-                        } else if (k == 32) {
-                            v = xsrc ? (d & 0xffffffffull) : (uint64_t)__builtin_bswap32((uint32_t)d);
-                        } else if (k == 64) {
-                            v = xsrc ? (d >> 32) : (uint64_t)__builtin_bswap32((uint32_t)(d >> 32));
-                        }
-                        if (dst == 10) { st = MIMIC_ERR_R10_WRITE; break; }
-                        wd = dst;
-                        wv = v;
-                    }
-                    break;
-                default:
-                    st = MIMIC_ERR_UNSUPPORTED_OP;
-                    break;
-                }
-            } else if (cls == 5 || cls == 6) {
-                const bool j32 = cls == 6;
-                if (!j32 && hi == 0x00 && !xsrc) {           // JA
-                    pcx += off;
-                } else if (!j32 && hi == 0x90 && !xsrc) {    // EXIT, inst.go:277-296
-                    if (L.nframes > 0) {
-                        L.nframes--;
-                        const uint32_t fq = kp.priv_frame_q + L.nframes * MIMIC_FRAME_QWORDS;
-                        pcx = (int64_t)(int32_t)(uint32_t)priv_load(kp, L.lane, fq * 8, 8);
-                        r[6] = priv_load(kp, L.lane, (fq + 1) * 8, 8);
-                        r[7] = priv_load(kp, L.lane, (fq + 2) * 8, 8);
-                        r[8] = priv_load(kp, L.lane, (fq + 3) * 8, 8);
-                        r[9] = priv_load(kp, L.lane, (fq + 4) * 8, 8);
-                        r[10] -= kp.frame_size;
-                    } else {
-                        st = EXIT_SIG;
-                    }
-                } else if (!j32 && hi == 0x80) {             // CALL / CALLX
-                    if (xsrc) {
-                        st = MIMIC_PANIC_CALLX;               // inst.go:270-273
-                    } else if (src == 1) {                    // BPF-to-BPF, inst.go:244-258
+                        break;
+                    case H_CALL_LOCAL:  // BPF-to-BPF, inst.go:244-258
                         if (L.nframes >= MIMIC_MAX_FRAMES) {
                             st = MIMIC_ERR_CALL_DEPTH;
                         } else {
                             const uint32_t fq = kp.priv_frame_q + L.nframes * MIMIC_FRAME_QWORDS;
-                            priv_store(kp, L.lane, fq * 8, 8, (uint64_t)(uint32_t)pc);
-                            priv_store(kp, L.lane, (fq + 1) * 8, 8, r[6]);
-                            priv_store(kp, L.lane, (fq + 2) * 8, 8, r[7]);
-                            priv_store(kp, L.lane, (fq + 3) * 8, 8, r[8]);
-                            priv_store(kp, L.lane, (fq + 4) * 8, 8, r[9]);
+                            priv_store(kp, L.lane, fq * 8, 8, (uint64_t)pc);
+                            priv_store(kp, L.lane, (fq + 1) * 8, 8, REG(6));
+                            priv_store(kp, L.lane, (fq + 2) * 8, 8, REG(7));
+                            priv_store(kp, L.lane, (fq + 3) * 8, 8, REG(8));
+                            priv_store(kp, L.lane, (fq + 4) * 8, 8, REG(9));
                             L.nframes++;
-                            pcx = (int64_t)pc + (int64_t)k - 1;
-                            r[10] += kp.frame_size;
+                            REG(10) = REG(10) + kp.frame_size;
+                            jmp = 1;
                         }
-                    } else {                                  // helper, emulator_linux_.go:125-194
+                        break;
+                    case H_CALL: {  // helpers, emulator_linux_.go:125-194
                         const int32_t hn = (int32_t)(uint32_t)k;
-                        if (hn < 0) st = MIMIC_PANIC_HELPER_NEG;
-                        else if (hn >= 176) st = MIMIC_ERR_HELPER_UNIMPLEMENTED;
-                        else {
-                            const int hc = helper_class(hn);
-                            if (hc == 0) st = MIMIC_ERR_HELPER_UNIMPLEMENTED;
-                            else if (hc == 2) st = MIMIC_ERR_HELPER_CANT_EMULATE;
-                            else {
-                                HelperOut ho = {0, 0, false, false, 0};
-                                if (hn == 1) ho = helper_lookup(kp, L, r[1], r[2]);
-                                else if (hn == 2) ho = helper_update(kp, L, r[1], r[2], r[3]);
-                                else if (hn == 3) ho = helper_delete(kp, L, r[1], r[2]);
-                                else if (hn == 8) { ho.r0 = (uint64_t)(int64_t)L.cpu; ho.set_r0 = true; }
-                                else if (hn == 12) ho = helper_tailcall(kp, L, r[2], r[3]);
-                                else if (hn == 65) { // bpf_xdp_adjust_tail, emulator_linux_helpers.go:842-864
-                                    Ref R = resolve(kp, L, (uint32_t)r[1]);
-                                    bool plain20 = (R.rk == RK_GLOBAL || R.rk == RK_STACK) && R.map < 0 && R.limit == 20; // a *PlainMemory of 20 bytes
-                                    if (plain20) ho.st = MIMIC_ERR_ENGINE_HELPER;
-                                    else { ho.r0 = (uint64_t)(int64_t)-22; ho.set_r0 = true; }
-                                } else ho.st = MIMIC_ERR_ENGINE_HELPER;
-                                st = ho.st;
-                                if (!st) {
-                                    if (ho.set_r0) r[0] = ho.r0;
-                                    if (ho.tail) {
-                                        prog = ho.new_prog;
-                                        pn = kp.progs[prog].n;
-                                        pcx = -1;
-                                        L.tailcalls++;
-                                    }
+                        HelperOut ho = {0, 0, false, false, 0};
+                        if (hn == 1) ho = helper_lookup(kp, L, REG(1), REG(2));
+                        else if (hn == 2) ho = helper_update(kp, L, REG(1), REG(2), REG(3));
+                        else if (hn == 3) ho = helper_delete(kp, L, REG(1), REG(2));
+                        else if (hn == 8) { ho.r0 = (uint64_t)(int64_t)L.cpu; ho.set_r0 = true; }
+                        else if (hn == 12) ho = helper_tailcall(kp, L, REG(2), REG(3));
+                        else {  // 65: bpf_xdp_adjust_tail, emulator_linux_helpers.go:842-864
+                            const Ref R = resolve(kp, L, (uint32_t)REG(1));
+                            const bool plain20 = (R.rk == RK_GLOBAL || R.rk == RK_STACK) && R.map < 0 && R.limit == 20;
+                            if (plain20) ho.st = MIMIC_ERR_ENGINE_HELPER;
+                            else { ho.r0 = (uint64_t)(int64_t)-22; ho.set_r0 = true; }
+                        }
+                        st = ho.st;
+                        if (!st) {
+                            if (ho.set_r0) REG(0) = ho.r0;
+                            if (ho.tail) {  // PC = -1, then Step's bounds check on the new program
+                                const DProg np = kp.progs[ho.new_prog];
+                                L.tailcalls++;
+                                if (np.n == 0) st = MIMIC_ERR_PC_OOB;
+                                else {
+                                    pn = np.n;
+                                    pbase = np.base;
+                                    jmp = 2;
+                                    nk = np.base;
                                 }
                             }
                         }
+                        break;
                     }
-                } else if (is_cond_jop(hi)) {
-                    if (j32 && xsrc && hi != 0x40) {
-                        st = MIMIC_ERR_UNSUPPORTED_OP;     // Q2: JMP32 register slots are nil
-                    } else {
-                        if (dst > 10 || (xsrc && src > 10)) st = MIMIC_PANIC_BADREG;
-                        else {
-                            // Q1: JMP register compares use 32-bit views, except JSET
-                            const bool w32 = j32 || (xsrc && hi != 0x40);
-                            if (jcond(hi, d, xsrc ? s : k, w32)) pcx += off;
+                    case H_ERR:
+                        st = (int)AUX_ARG(aux);
+                        break;
+                    default: {  // H_SLOW: rare forms whose error order is per lane, and END
+                        const uint32_t cls = op & 7, hi = op & 0xf0;
+                        const bool xsrc = (op & 0x08) != 0;
+                        const uint64_t d = REG(dst < NREGS ? dst : 10);
+                        const uint64_t s = REG(src < NREGS ? src : 10);
+                        uint64_t wv = 0;
+                        bool wr = false;
+                        if (cls == 1) {  // LDX with dst >= 10, inst.go:298-318
+                            const Ref R = resolve(kp, L, (uint32_t)(s + (uint64_t)(int64_t)off));
+                            st = mem_load(kp, L, R, size_bytes(op), wv);
+                            if (!st) st = dst > 10 ? MIMIC_PANIC_BADREG : MIMIC_ERR_R10_WRITE;
+                        } else if (hi == 0xd0) {  // END, inst.go:138-198 (Q4)
+                            if (dst > 10) st = MIMIC_PANIC_BADREG;
+                            else {
+                                wv = d;
+                                if (k == 16) wv = xsrc ? (d & 0xffff) : (((d >> 8) & 0xff) | ((d & 0xff) << 8));
+                                else if (k == 32) wv = xsrc ? (d & 0xffffffffull) : (uint64_t)__builtin_bswap32((uint32_t)d);
+                                else if (k == 64) wv = xsrc ? (d >> 32) : (uint64_t)__builtin_bswap32((uint32_t)(d >> 32));
+                                if (dst == 10) st = MIMIC_ERR_R10_WRITE;
+                                else wr = true;
+                            }
+                        } else {  // DIV / MOD with a register divisor (per-lane Go panic)
+                            const bool is64 = cls == 7;
+                            if (is64 ? s == 0 : (uint32_t)s == 0) st = MIMIC_PANIC_DIV0;
+                            else if (dst == 10) st = MIMIC_ERR_R10_WRITE;
+                            else {
+                                wv = is64 ? alu64(hi, d, s) : alu32(hi, d, s);
+                                wr = true;
+                            }
                         }
+                        if (wr) {
+                            const uint32_t wdu = (uint32_t)__builtin_amdgcn_readfirstlane((int)dst);
+                            REG(wdu) = wv;
+                        }
+                        break;
                     }
-                } else {
-                    st = MIMIC_ERR_UNSUPPORTED_OP;
-                }
-            } else if (cls == 1) { // LDX, inst.go:298-318
-                if ((op & 0xe0) != 0x60) st = MIMIC_ERR_UNSUPPORTED_OP;
-                else if (src > 10) st = MIMIC_PANIC_BADREG;
-                else {
-                    const Ref R = resolve(kp, L, (uint32_t)(s + (uint64_t)(int64_t)off));
-                    uint64_t v = 0;
-                    st = mem_load(kp, L, R, size_bytes(op), v);
-                    if (!st) {
-                        if (dst > 10) st = MIMIC_PANIC_BADREG;
-                        else if (dst == 10) st = MIMIC_ERR_R10_WRITE;
-                        else { wd = dst; wv = v; }
+                    }
+
+                    if (st == EXIT_SIG) {
+                        TERM(MIMIC_OK, -1);
+                    } else if (st) {
+                        TERM(st, pc);
+                    } else if (jmp == 0) {                 // PC+1 (vm.go:328-337)
+                        if (aux & AUX_FALL_OK) key = kw + 1;
+                        else TERM(MIMIC_ERR_PC_OOB, pc);
+                    } else if (jmp == 2) {
+                        key = nk;
+                    } else {                               // taken jump / BPF-to-BPF call
+                        const int32_t tgt = op == 0x85 ? (int32_t)pc + (int32_t)(uint32_t)k : (int32_t)pc + off + 1;
+                        if (aux & AUX_JT_OK) key = pbase + (uint32_t)tgt;
+                        else if (aux & AUX_JT_NEG) {       // next Step indexes Instructions[-x] (vm.go:300)
+                            if ((uint64_t)steps == kp.budget) TERM(MIMIC_ERR_STEP_LIMIT, tgt);
+                            else { steps++; TERM(MIMIC_PANIC_PC, tgt); }
+                        } else TERM(MIMIC_ERR_PC_OOB, pc);
                     }
                 }
-            } else if (cls == 2 || cls == 3) { // ST / STX, inst.go:320-363
-                if ((op & 0xe0) != 0x60) st = MIMIC_ERR_UNSUPPORTED_OP;
-                else if (dst > 10 || (cls == 3 && src > 10)) st = MIMIC_PANIC_BADREG;
-                else {
-                    const Ref R = resolve(kp, L, (uint32_t)(d + (uint64_t)(int64_t)off));
-                    st = mem_store(kp, L, R, size_bytes(op), cls == 3 ? s : k);
-                }
-            } else { // LD class
-                if (op == 0x18) { // instLoad64Imm
-                    if (dst > 10) st = MIMIC_PANIC_BADREG;
-                    else if (dst == 10) st = MIMIC_ERR_R10_WRITE;
-                    else { wd = dst; wv = k; }
-                } else if ((op & 0xe0) == 0x20 || (op & 0xe0) == 0x40) {
-                    st = MIMIC_ERR_LDABS; // R6 never names a *SKBuff in an xdp_md process
-                } else {
-                    st = MIMIC_ERR_UNSUPPORTED_OP;
-                }
             }
-
-            // single register write site (keeps r[] in VGPRs without copies)
-            {
-                const uint64_t old = r[wd];
-                r[wd] = st ? old : wv;
-            }
-
-            if (st == EXIT_SIG) {
-                status = MIMIC_OK;
-                err_pc = -1;
-                running = false;
-            } else if (st) {
-                status = (uint32_t)st;
-                err_pc = pc;
-                running = false;
-            } else if ((int64_t)pn <= pcx + 1) { // vm.go:328-334
-                status = MIMIC_ERR_PC_OOB;
-                err_pc = pc;
-                running = false;
-            } else {
-                const int64_t np = pcx + 1;
-                if (np < 0) { // the next Step indexes Instructions[-x] and panics (vm.go:300)
-                    if ((uint64_t)steps == kp.budget) status = MIMIC_ERR_STEP_LIMIT;
-                    else { steps++; status = MIMIC_PANIC_PC; }
-                    err_pc = (int32_t)np;
-                    running = false;
-                } else {
-                    pc = (int32_t)np;
-                }
-            }
+            cand = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(act));
         }
-
-        // ---- results + Cleanup -----------------------------------------------------------
-        if (i != 0xffffffffu) {
-            if (kp.r0) kp.r0[i] = r[0];
-            if (kp.status) kp.status[i] = (uint8_t)status;
-            if (kp.steps) kp.steps[i] = steps;
-            if (kp.err_pc) kp.err_pc[i] = err_pc;
-            lane_steps += steps;
-        }
+#undef TERM
     }
     if (lane_valid && kp.lane_steps) kp.lane_steps[g] = lane_steps;
+#undef REG
 }
 
 // Sum of a per-CPU u64 array over cpus: out[k] = sum_c base[c*stride + 8k] (the "sum over CPUs"

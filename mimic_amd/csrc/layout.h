@@ -19,7 +19,7 @@
 #define MIMIC_MAX_FRAMES 32u          // engine bound on BPF-to-BPF call depth (oracle: ORC_MAX_FRAMES)
 #define MIMIC_DEFAULT_BUDGET (1ull << 22)
 #define MIMIC_MEM_START 0x10000u      // memStart + 1, memory_controller.go:55,70
-#define MIMIC_PC_BITS 20u             // wave-min key = prog << 20 | pc
+#define MIMIC_PC_BITS 24u             // max program length = 2^24 slots
 #define MIMIC_XDP_MD_SIZE 24u         // context_xdp_md.go:57
 #define MIMIC_FRAME_QWORDS 5u         // saved PC + R6..R9 (inst.go:277-296)
 
@@ -69,7 +69,35 @@ struct DProg {
     uint32_t pad;
 };
 
-// A decoded instruction slot: w = op | dst<<8 | src<<12 | (uint16)off<<16, k = asm.Instruction.Constant
+// A decoded instruction slot: w = op | dst<<8 | src<<12 | (uint16)off<<16, k = asm.Instruction.Constant,
+// aux = handler id and facts the host predecodes at load time.  All lanes executing a slot
+// share its PC, so "is PC+1 / the jump target inside the program" and every error that
+// depends only on the instruction (bad register numbers, unsupported opcodes, helper ids,
+// constant divisors ...) are properties of the slot.
+enum Handler : uint32_t {
+    H_SLOW = 0,        // full generic decode (rare forms: END, per-lane-ordered errors ...)
+    H_ERR = 1,         // instruction-determined fatal status in AUX_ARG
+    H_NOP = 2,
+    H_ALU64 = 3,       // ADD SUB MUL DIV/MOD(K, k!=0) OR AND LSH RSH XOR MOV NEG ARSH, dst<=9
+    H_ALU32 = 4,
+    H_LDIMM = 5,
+    H_JA = 6,
+    H_JCC = 7,         // conditional jump; AUX_ARG = jump op, AUX_W32 / AUX_X flags
+    H_LDX = 8,         // dst<=9, src<=10; AUX_SZ = size
+    H_ST = 9,
+    H_STX = 10,
+    H_EXIT = 11,
+    H_CALL = 12,       // helper 1/2/3/8/12/65
+    H_CALL_LOCAL = 13, // BPF-to-BPF
+};
+#define AUX_H(a) ((a) & 0xffu)
+#define AUX_FALL_OK (1u << 8)    // PC+1 < len(Instructions)
+#define AUX_JT_OK (1u << 9)      // jump / BPF-to-BPF call target (after Step's PC++) in [0, len)
+#define AUX_JT_NEG (1u << 10)    // target < 0: the next Step panics
+#define AUX_W32 (1u << 11)       // 32-bit compare
+#define AUX_X (1u << 12)         // register source
+#define AUX_ARG(a) (((a) >> 16) & 0xffu)
+#define AUX_SZ(a) ((a) >> 24)
 struct DInsn {
     uint32_t w;
     uint32_t aux;
@@ -89,7 +117,7 @@ struct KParams {
     uint32_t static_next;       // St
     uint32_t stack_size;        // S
     uint32_t frame_size;
-    uint32_t chunk_shift;       // lazy-zero granule of the stack (bytes = 1 << shift)
+    uint32_t chunk_shift;       // lazy-zero granule of the stack above 512 B (bytes = 1 << shift)
     uint32_t max_tail_calls;
     uint32_t total_vcpus;       // V (VMSettings.VirtualCPUs)
     uint32_t vcpu_begin;        // first vCPU executed by this launch

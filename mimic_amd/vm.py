@@ -392,8 +392,10 @@ class VM:
         else:
             b.cpu = None
         b.step_budget = batch.step_budget
-        r = L.XDPResults(results.r0.data_ptr(), results.status.data_ptr(), results.steps.data_ptr(),
-                         results.err_pc.data_ptr())
+        def ptr(t):
+            return t.data_ptr() if t is not None else None
+
+        r = L.XDPResults(ptr(results.r0), ptr(results.status), ptr(results.steps), ptr(results.err_pc))
         st = stream.cuda_stream if stream is not None else None
         _check(self.h, self.lib.mimic_run_xdp(self.h, prog_id, C.byref(b), C.byref(r), st), "RunXDPBatch")
         if sync:
@@ -558,13 +560,14 @@ class XDPResults:
         self.r0, self.status, self.steps, self.err_pc = r0, status, steps, err_pc
 
     @classmethod
-    def empty(cls, n: int, device):
+    def empty(cls, n: int, device, full: bool = True):
+        """full=False allocates only r0 and status (the process's R0 and error)."""
         import torch
 
         return cls(torch.zeros(max(n, 1), dtype=torch.int64, device=device),
                    torch.zeros(max(n, 1), dtype=torch.uint8, device=device),
-                   torch.zeros(max(n, 1), dtype=torch.int32, device=device),
-                   torch.zeros(max(n, 1), dtype=torch.int32, device=device))
+                   torch.zeros(max(n, 1), dtype=torch.int32, device=device) if full else None,
+                   torch.zeros(max(n, 1), dtype=torch.int32, device=device) if full else None)
 
     def numpy(self, n: Optional[int] = None):
         import numpy as np
