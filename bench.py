@@ -128,6 +128,7 @@ def main():
     torch.cuda.set_device(dev)
 
     import mimic_amd as M
+    from mimic_amd import dist as D
     from mimic_amd import workloads as W
 
     cfg = CONFIGS[args.config]
@@ -137,15 +138,10 @@ def main():
 
     # program bytes: built on rank 0, broadcast over RCCL (the setup-time exchange)
     prog = getattr(W, cfg["prog"])()
-    raw = torch.zeros(len(prog.raw), dtype=torch.uint8, device=dev)
-    if rank == 0:
-        raw.copy_(torch.frombuffer(bytearray(prog.raw), dtype=torch.uint8))
-    if ws > 1:
-        dist.broadcast(raw, 0)
-    raw_bytes = bytes(raw.cpu().numpy().tobytes())
+    raw_bytes = D.broadcast_bytes(prog.raw if rank == 0 else None, dev) if ws > 1 else prog.raw
 
     emu = M.NewLinuxEmulator()
-    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(V), M.VMOptDevice(local), M.VMOptShard(rank * vpg, vpg))
+    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(V), M.VMOptDevice(local), M.VMOptShard(*D.shard(vpg, rank)))
     maps = {}
     for m in prog.maps:
         mm = M.MapSpecToLinuxMap(M.MapSpec(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"]))
@@ -183,12 +179,8 @@ def main():
     steps_per_batch = vm.LastSteps()
     st = res.status[:n].cpu().numpy()
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([steps_per_batch], dtype=torch.float64, device=dev)
-        dist.all_reduce(s)
-        steps_total_batch = float(s.item())
+        elapsed = D.allreduce_max_f64(elapsed, dev)
+        steps_total_batch = float(D.allreduce_sum_u64([steps_per_batch], dev)[0])
     else:
         steps_total_batch = float(steps_per_batch)
 
@@ -196,11 +188,9 @@ def main():
     counters = None
     if prog.maps:
         m0 = prog.maps[0]
-        local_sum = maps[m0["name"]].SumU64(rank * vpg, (rank + 1) * vpg)
-        cs = torch.tensor(np.asarray(local_sum, dtype=np.int64), device=dev)
-        if ws > 1:
-            dist.all_reduce(cs)
-        counters = cs.cpu().numpy().tolist()
+        b0, cnt = D.shard(vpg, rank)
+        local_sum = maps[m0["name"]].SumU64(b0, b0 + cnt)
+        counters = D.allreduce_sum_u64(local_sum, dev) if ws > 1 else local_sum
 
     if rank == 0:
         total_pkts = n * ws * args.steps

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 
 from harness import Scenario, assert_same, packets_to_buffer, run_engine, run_oracle, single
-from mimic_amd import asm as A
+from mimic_amd import asm as A  # noqa: F401
 from mimic_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
@@ -46,3 +46,103 @@ def test_fuzz_programs(gpu, seed):
     o = run_oracle(sc, buf, off, lens, cpu, step_budget=5000)
     e = run_engine(sc, buf, off, lens, cpu, step_budget=5000)
     assert_same(o, e)
+
+
+def test_classifier_full_size_exact(gpu):
+    """BASELINE configs[1] at full size: 1 048 576 x 64 B, V = 262 144 vCPUs, exact per-packet
+    parity with the oracle plus the size-independent property sum(counters) == packets."""
+    p = W.prog_classifier()
+    n, V = 1 << 20, 1 << 18
+    sc = _prog_scenario(p, V)
+    buf, off, lens = W.make_packets(n)
+    cpu = W.schedule_cpu(n, V, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    import mimic_amd as M
+    e = run_engine(sc, buf, off, lens, cpu, schedule=M.SCHED_INTERLEAVED)
+    assert_same(o, e)
+    tot = sum(int(np.frombuffer(v, np.uint64).sum()) for v in e["maps"]["verdicts"])
+    assert tot == n
+    assert e["steps_total"] == int(o["steps"].astype(np.int64).sum())
+
+
+def test_parse5_imix_exact(gpu):
+    p = W.prog_parse5()
+    n, V = 1 << 16, 4096
+    sc = _prog_scenario(p, V)
+    buf, off, lens = W.make_packets(n, **W.IMIX)
+    cpu = W.schedule_cpu(n, V, "chunked")
+    import mimic_amd as M
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu, schedule=M.SCHED_CHUNKED)
+    assert_same(o, e)
+    assert set(np.unique(o["r0"]).tolist()) <= {1, 2}
+
+
+@pytest.mark.parametrize("sched", ["chunked", "interleaved", "explicit"])
+def test_schedules(gpu, sched):
+    import mimic_amd as M
+    p = W.prog_classifier()
+    n, V = 5000, 96
+    sc = _prog_scenario(p, V)
+    buf, off, lens = W.make_packets(n, seed=7)
+    if sched == "explicit":
+        cpu = np.random.default_rng(3).integers(0, V, n).astype(np.int32)
+        mode = M.SCHED_EXPLICIT
+    else:
+        cpu = W.schedule_cpu(n, V, sched)
+        mode = M.SCHED_CHUNKED if sched == "chunked" else M.SCHED_INTERLEAVED
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu if mode == M.SCHED_EXPLICIT else None, schedule=mode)
+    assert_same(o, e)
+
+
+def test_tailcall_divergence(gpu):
+    """Lanes of one wave tail-call into different programs (and some do not) -- the wave
+    runs several programs at once (min-key scheduling over global instruction indices)."""
+    PA = dict(name="progs", type=3, key_size=4, value_size=4, max_entries=4)
+    CNT = dict(name="cnt", type=6, key_size=4, value_size=8, max_entries=4)
+    main = [A.mov64_reg(6, 1), A.ldx(4, 2, 6, 0), A.ldx(4, 3, 6, 4), A.mov64_reg(4, 2), A.alu64("add", 4, 1),
+            A.jmp("jgt", 4, 3, "out", reg=True), A.ldx(1, 3, 2, 0), A.alu64("and", 3, 3), A.mov64_reg(1, 6),
+            A.ld_map_fd(2, "progs"), A.call(A.FN_TAIL_CALL), "out", A.mov64_imm(0, 99), A.exit_()]
+
+    def leaf(v):
+        return [A.st(4, 10, -4, v), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, "cnt"),
+                A.call(1), A.jmp("jeq", 0, 0, 3), A.ldx(8, 1, 0, 0), A.alu64("add", 1, 1), A.stx(8, 0, 0, 1),
+                A.mov64_imm(0, v), A.exit_()]
+
+    progs = [("main", *A.assemble(main))] + [(f"l{v}", *A.assemble(leaf(v))) for v in range(3)]
+    sc = Scenario(vcpus=32, maps=[PA, CNT], progs=progs, prog_array=[("progs", 0, 1), ("progs", 1, 2),
+                                                                      ("progs", 2, 3)])
+    rng = np.random.default_rng(11)
+    pk = [bytes(rng.integers(0, 256, int(rng.choice([0, 8, 64])), dtype=np.uint8)) for _ in range(3000)]
+    buf, off, lens = packets_to_buffer(pk)
+    cpu = rng.integers(0, 32, len(pk)).astype(np.int32)
+    assert_same(run_oracle(sc, buf, off, lens, cpu), run_engine(sc, buf, off, lens, cpu))
+
+
+def test_packet_rewrite_and_room(gpu):
+    """XDP_TX-style MAC swap written in place, per-packet headroom/tailroom arrays."""
+    items = [A.ldx(4, 2, 1, 0), A.ldx(4, 3, 1, 4), A.mov64_reg(4, 2), A.alu64("add", 4, 12),
+             A.jmp("jgt", 4, 3, "out", reg=True),
+             A.ldx(4, 5, 2, 0), A.ldx(2, 6, 2, 4), A.ldx(4, 7, 2, 6), A.ldx(2, 8, 2, 10),
+             A.stx(4, 2, 0, 7), A.stx(2, 2, 4, 8), A.stx(4, 2, 6, 5), A.stx(2, 2, 10, 6),
+             A.ldx(1, 9, 2, -1), A.mov64_imm(0, A.XDP_TX), A.alu64("add", 0, 9, reg=True), A.exit_(),
+             "out", A.mov64_imm(0, A.XDP_DROP), A.exit_()]
+    raw, rel = A.assemble(items)
+    sc = Scenario(vcpus=8, progs=[("tx", raw, rel)])
+    rng = np.random.default_rng(5)
+    n = 700
+    pk = [bytes(rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8)) for _ in range(n)]
+    H = rng.integers(1, 40, n).astype(np.uint32)
+    T = rng.integers(0, 17, n).astype(np.uint32)
+    buf, off, lens = packets_to_buffer(pk, H, T)
+    buf[:] = rng.integers(0, 256, len(buf), dtype=np.uint8)   # dirty room bytes: the engine must zero them
+    for i, p_ in enumerate(pk):
+        buf[int(off[i]) + int(H[i]):int(off[i]) + int(H[i]) + len(p_)] = np.frombuffer(p_, np.uint8)
+    cpu = rng.integers(0, 8, n).astype(np.int32)
+    o = run_oracle(sc, buf, off, lens, cpu, headroom=H, tailroom=T)
+    e = run_engine(sc, buf, off, lens, cpu, headroom=H, tailroom=T)
+    for i in range(n):  # compare only packet memories (the gaps between them are not process memory)
+        a, m = int(off[i]), int(H[i] + lens[i] + T[i])
+        assert bytes(o["pkt"][a:a + m]) == bytes(e["pkt"][a:a + m]), i
+    assert_same(o, e, check_pkt=False)
