@@ -36,6 +36,9 @@ CONFIGS = {
     "parse5": dict(prog="prog_parse5", packets=1 << 24, sizes=(64, 576, 1500), weights=(7, 4, 1),
                    workload="cfg3: 16M IMIX 7:4:1 (64/576/1500B) xdp_md, L2/L3/L4 parse + 5-tuple hash, "
                             "per-CPU array E=256 S=8"),
+    "flowtrack": dict(prog="prog_flowtrack", packets=1 << 21, sizes=(64, 576, 1500), weights=(7, 4, 1),
+                      workload="cfg4 per-GPU shard: 2M IMIX xdp_md (16M over 8 GPUs), 5-tuple parse + "
+                               "insert-if-absent into a shared hash map K=16 S=8 E=131072"),
 }
 
 
@@ -47,12 +50,17 @@ def dist_env():
 
 
 def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps) -> int:
-    """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU map state.
+    """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU array
+    state, 2*E*(K+S) of hash-map state (K + V*S for a per-CPU hash).
     (The engine's actual descriptor is 12 B and it also writes a 1-B status; not counted.)"""
     b = int(lens.astype(np.int64).sum()) + 16 * len(lens)
     for m in maps:
-        ncpu = vcpus if m["type"] in (5, 6) else 1
-        b += 2 * ncpu * m["max_entries"] * m["value_size"]
+        if m["type"] in (1, 5):
+            ncpu = vcpus if m["type"] == 5 else 1
+            b += 2 * m["max_entries"] * (m["key_size"] + ncpu * m["value_size"])
+        else:
+            ncpu = vcpus if m["type"] == 6 else 1
+            b += 2 * ncpu * m["max_entries"] * m["value_size"]
     return b
 
 

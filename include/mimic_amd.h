@@ -149,6 +149,13 @@ int mimic_map_update(mimic_vm *vm, uint32_t map_id, const void *key, const void 
 int mimic_map_lookup(mimic_vm *vm, uint32_t map_id, const void *key, int32_t cpu, uint32_t *addr_out);
 /* LinuxMapDeleter.Delete(key). emulator_linux_map.go:38-42 */
 int mimic_map_delete(mimic_vm *vm, uint32_t map_id, const void *key);
+/* LinuxMap.Keys(cpuid): the live keys packed (key_size bytes each) into out, count in *n_out.
+ * emulator_linux_map_hash.go:113-131 (Go map order there, table order here), emulator_linux_map_array.go:64-75 */
+int mimic_map_keys(mimic_vm *vm, uint32_t map_id, void *out, size_t cap, uint32_t *n_out);
+/* Hash maps: live keys with their slot (LinuxHashMap.KeyToIndex, emulator_linux_map_hash.go:29-30);
+ * the value of key i on cpu c is values[c][slot_i * value_size]. */
+int mimic_map_entries(mimic_vm *vm, uint32_t map_id, void *keys_out, int32_t *slots_out, size_t cap_entries,
+                      uint32_t *n_out);
 /* Raw value backing of (map, cpu): E*S bytes, slot order (D2H copy). */
 int mimic_map_read_values(mimic_vm *vm, uint32_t map_id, int32_t cpu, void *out, size_t cap);
 /* Sum over vCPUs [cpu_begin, cpu_end) of a per-CPU map's u64 values -> out[E] (device reduction). */

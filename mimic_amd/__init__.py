@@ -3,8 +3,8 @@
 Product path: hand-written gfx950 HIP interpreter (csrc/interp.hip) + C++ host engine
 (csrc/engine.cpp) behind the C ABI in include/mimic_amd.h, bound here with ctypes.
 """
-from .vm import (E2BIG, LinuxArrayMap, LinuxContextXDP, LinuxEmulator, LinuxMap, LinuxPerCPUArrayMap, MapSpec,
-                 MapSpecToLinuxMap, MapType, MimicError, NewLinuxEmulator, NewVM, OptMaxTailCalls, Process,
+from .vm import (E2BIG, LinuxArrayMap, LinuxContextXDP, LinuxEmulator, LinuxHashMap, LinuxMap, LinuxPerCPUArrayMap,
+                 LinuxPerCPUHashMap, MapSpec, MapSpecToLinuxMap, MapType, MimicError, NewLinuxEmulator, NewVM, OptMaxTailCalls, Process,
                  ProgramSpec, UnmarshalContextJSON, VM, VMOptDevice, VMOptEmulator, VMOptSetvCPUs, VMOptShard,
                  XDPBatch, XDPResults)
 from ._lib import STATUS, STATUS_NAMES, SCHED_CHUNKED, SCHED_EXPLICIT, SCHED_INTERLEAVED

@@ -22,6 +22,9 @@
 #include "layout.h"
 
 extern "C" int mimic_launch_xdp(const KParams *kp, hipStream_t st);
+extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
+                                    int32_t cpu, int32_t *out, hipStream_t st);
+extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
 
@@ -36,6 +39,9 @@ struct HostMap {
     uint32_t ncpu;
     uint64_t dev_off;       // arena offset of the cpu-0 backing
     uint64_t dev_stride;    // arena distance between cpu backings
+    // hash families (hashmap.h)
+    uint64_t keys_dev_off, ht_dev_off;
+    uint32_t keys_addr, ht_cap, rec_q, nlocks, fl_cap;
 };
 
 struct HostProg {
@@ -242,6 +248,32 @@ static uint32_t predecode(const DInsn &x, int64_t i, int64_t n) {
     return err(MIMIC_ERR_UNSUPPORTED_OP);
 }
 
+static DMap to_dmap(const HostMap &m) {
+    DMap d{};
+    d.family = m.family;
+    d.type = m.type;
+    d.key_size = m.key_size;
+    d.value_size = m.value_size;
+    d.max_entries = m.max_entries;
+    d.datasec = m.datasec;
+    d.obj_addr = m.obj_addr;
+    d.backing_addr = m.backing_addr;
+    d.addr_period = m.addr_period;
+    d.ncpu = m.ncpu;
+    d.dev_off = m.dev_off;
+    d.dev_stride = m.dev_stride;
+    d.keys_dev_off = m.keys_dev_off;
+    d.keys_addr = m.keys_addr;
+    d.ht_cap = m.ht_cap;
+    d.ht_dev_off = m.ht_dev_off;
+    d.rec_q = m.rec_q;
+    d.nlocks = m.nlocks;
+    d.fl_cap = m.fl_cap;
+    return d;
+}
+
+static bool is_hash(const HostMap &m) { return m.family == FAM_HASH || m.family == FAM_PERCPU_HASH; }
+
 static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     std::vector<DInsn> all;
@@ -262,22 +294,7 @@ static int upload_tables(mimic_vm *vm) {
     }
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
     std::vector<DMap> dm;
-    for (auto &m : vm->maps) {
-        DMap d{};
-        d.family = m.family;
-        d.type = m.type;
-        d.key_size = m.key_size;
-        d.value_size = m.value_size;
-        d.max_entries = m.max_entries;
-        d.datasec = m.datasec;
-        d.obj_addr = m.obj_addr;
-        d.backing_addr = m.backing_addr;
-        d.addr_period = m.addr_period;
-        d.ncpu = m.ncpu;
-        d.dev_off = m.dev_off;
-        d.dev_stride = m.dev_stride;
-        dm.push_back(d);
-    }
+    for (auto &m : vm->maps) dm.push_back(to_dmap(m));
     if (dm.empty()) dm.push_back(DMap{});
     if (dp.empty()) dp.push_back(DProg{});
     std::vector<Seg> sg = vm->segs;
@@ -467,8 +484,90 @@ int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id)
         vm->segs.push_back(g);
         break;
     }
-    case 1: case 5: case 13: case 18: case 19: case 21: case 24: case 25: case 26: case 28: case 29:
-        return fail(vm, MIMIC_ENOTSUP, "hash-family maps are not supported by this engine build yet");
+    case 1: case 13: case 18: case 19: case 24: case 25: case 26: case 28: case 29:
+    case 5: case 21: {
+        // LinuxHashMap.Init (emulator_linux_map_hash.go:43-97) / LinuxPerCPUHashMap.Init (:439-500)
+        const bool percpu = spec->type == 5 || spec->type == 21;
+        m.family = percpu ? FAM_PERCPU_HASH : FAM_HASH;
+        const uint64_t kbytes = (uint64_t)spec->max_entries * spec->key_size;
+        if (kbytes > 0xffffffffull) return fail(vm, MIMIC_EINVAL, "map too large");
+        const uint32_t EK = (uint32_t)kbytes;
+        const uint32_t V = percpu ? (uint32_t)vm->s.vcpus : 1u;
+        m.ncpu = V;
+        m.dev_stride = ES;
+        int rc = arena_reserve(vm, (uint64_t)ES * V, &m.dev_off);
+        if (!rc) rc = arena_reserve(vm, EK, &m.keys_dev_off);
+        // device index: capacity for E live keys at load <= 1/2
+        m.ht_cap = 16;
+        while (m.ht_cap < 2ull * spec->max_entries + 2) m.ht_cap <<= 1;
+        m.rec_q = 1 + (spec->key_size + 7) / 8;
+        m.nlocks = std::min<uint32_t>(m.ht_cap, 1u << 16);
+        m.fl_cap = 16;
+        while (m.fl_cap < 2ull * spec->max_entries + 2) m.fl_cap <<= 1;
+        // index region (hashmap.h h_table): records | rebuild copy | locks | freelist ring | HashCtl
+        const uint64_t rec_bytes = (uint64_t)m.ht_cap * m.rec_q * 8;
+        const uint64_t lock_off = 2 * rec_bytes, fl_off = lock_off + (uint64_t)m.nlocks * 4,
+                       ctl_off = fl_off + (uint64_t)m.fl_cap * 4;
+        if (!rc) rc = arena_reserve(vm, ctl_off + sizeof(HashCtl), &m.ht_dev_off);
+        if (rc) return rc;
+        HIP_OK(vm, hipMemset(vm->arena + m.ht_dev_off, 0xff, rec_bytes));
+        std::vector<int32_t> fl(m.fl_cap, -1);
+        for (uint32_t i = 0; i < spec->max_entries; i++) fl[i] = (int32_t)i;  // freelist <- 0..E-1 (:61-64)
+        HIP_OK(vm, hipMemcpy(vm->arena + m.ht_dev_off + fl_off, fl.data(), fl.size() * 4, hipMemcpyHostToDevice));
+        HashCtl c{};
+        c.head = 0;
+        c.tail = spec->max_entries;
+        c.avail = (int32_t)spec->max_entries;
+        HIP_OK(vm, hipMemcpy(vm->arena + m.ht_dev_off + ctl_off, &c, sizeof c, hipMemcpyHostToDevice));
+        auto plain = [&](uint32_t lo, uint32_t size, uint64_t dev_off) {
+            Seg b{};
+            b.lo = lo;
+            b.hi = lo + size;
+            b.kind = SEG_PLAIN;
+            b.id = id;
+            b.dev_off = dev_off;
+            b.size = size;
+            vm->segs.push_back(b);
+        };
+        auto obj = [&]() {
+            m.obj_addr = add_entry(vm, 8);
+            Seg o{};
+            o.lo = m.obj_addr;
+            o.hi = m.obj_addr + 8;
+            o.kind = SEG_MAP_OBJ;
+            o.id = id;
+            vm->segs.push_back(o);
+        };
+        if (percpu) {  // values per cpu first, then the map object, then the keys
+            const uint32_t first = vm->next_addr;
+            const uint64_t period = (uint64_t)ES + 1;
+            if ((uint64_t)first + period * V > 0xffffffffull) return fail(vm, MIMIC_ENOMEM, "out of memory (32-bit address space)");
+            vm->next_addr = (uint32_t)(first + period * V);
+            m.backing_addr = first;
+            m.addr_period = (uint32_t)period;
+            Seg g{};
+            g.lo = first;
+            g.hi = (uint32_t)(first + period * (V - 1) + ES);
+            g.kind = SEG_PERCPU_VALUES;
+            g.id = id;
+            g.dev_off = m.dev_off;
+            g.size = ES;
+            g.period = (uint32_t)period;
+            g.count = V;
+            g.dev_stride = ES;
+            vm->segs.push_back(g);
+            obj();
+            m.keys_addr = add_entry(vm, EK);
+            plain(m.keys_addr, EK, m.keys_dev_off);
+        } else {       // map object, keys, values
+            obj();
+            m.keys_addr = add_entry(vm, EK);
+            plain(m.keys_addr, EK, m.keys_dev_off);
+            m.backing_addr = add_entry(vm, ES);
+            plain(m.backing_addr, ES, m.dev_off);
+        }
+        break;
+    }
     default:
         return fail(vm, MIMIC_ENOTSUP, "unsupported map type '%u'", spec->type);
     }
@@ -485,10 +584,11 @@ static int map_check(mimic_vm *vm, uint32_t id) {
     return 0;
 }
 
-// cpu-resolved array backing offset; returns <0 on error (fatal in the reference)
+// cpu-resolved backing offset (array / per-CPU array / hash values / per-CPU hash values);
+// returns <0 on error (fatal in the reference)
 static int array_cpu(mimic_vm *vm, const HostMap &m, int32_t cpu, uint64_t *base) {
-    if (m.family == FAM_PERCPU_ARRAY) {
-        if (cpu < 0 || (uint32_t)cpu >= m.ncpu) return fail(vm, MIMIC_EINVAL, "invalid cpuid");
+    if (m.family == FAM_PERCPU_ARRAY || m.family == FAM_PERCPU_HASH) {
+        if (cpu < 0 || (uint32_t)cpu >= m.ncpu) return fail(vm, MIMIC_EINVAL, "invalid CPU ID");
         *base = m.dev_off + (uint64_t)cpu * m.dev_stride;
     } else {
         *base = m.dev_off;
@@ -496,27 +596,77 @@ static int array_cpu(mimic_vm *vm, const HostMap &m, int32_t cpu, uint64_t *base
     return 0;
 }
 
-// LinuxArrayMap.Update / LinuxPerCPUArrayMap.Update (emulator_linux_map_array.go:97-113, 244-250)
+// wait for the last batch before touching map state from the host
+static int settle(mimic_vm *vm) {
+    if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
+    return 0;
+}
+
+// one hash-map operation on the device (the same code the kernel's helpers run):
+// op 0 lookup, 1 update, 2 delete; *slot = slot index or -1
+static int hash_op(mimic_vm *vm, const HostMap &m, uint32_t op, const void *key, const void *value, int32_t cpu,
+                   int32_t *slot) {
+    int rc = settle(vm);
+    if (rc) return rc;
+    const size_t kb = std::max<uint32_t>(m.key_size, 1), vb = std::max<uint32_t>(m.value_size, 1);
+    uint8_t *d = nullptr;
+    HIP_OK(vm, hipMalloc(&d, kb + vb + 16));
+    int32_t *dout = (int32_t *)(d + ((kb + vb + 7) & ~size_t(7)));
+    hipError_t e = hipMemcpy(d, key, m.key_size, hipMemcpyHostToDevice);
+    if (e == hipSuccess && value) e = hipMemcpy(d + kb, value, m.value_size, hipMemcpyHostToDevice);
+    const DMap dm = to_dmap(m);
+    if (e == hipSuccess && mimic_launch_hash_op(vm->arena, &dm, op, d, d + kb, cpu, dout, vm->stream))
+        e = hipErrorLaunchFailure;
+    if (e == hipSuccess) e = hipMemcpyAsync(slot, dout, 4, hipMemcpyDeviceToHost, vm->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(vm->stream);
+    hipFree(d);
+    if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "hash map op: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// LinuxArrayMap.Update / LinuxPerCPUArrayMap.Update (emulator_linux_map_array.go:97-113, 244-250),
+// LinuxHashMap.Update / LinuxPerCPUHashMap.Update (emulator_linux_map_hash.go:158-203, 564-612)
 int mimic_map_update(mimic_vm *vm, uint32_t id, const void *key, const void *value, uint32_t flags, int32_t cpu) {
     (void)flags;  // Q10: flags are ignored
     int rc = map_check(vm, id);
     if (rc) return rc;
     const HostMap &m = vm->maps[id];
     uint64_t base;
+    if (is_hash(m)) {
+        if (m.family == FAM_HASH) cpu = 0;  // LinuxHashMap ignores cpuid
+        else if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
+        int32_t slot = -1;
+        if ((rc = hash_op(vm, m, 1, key, value, cpu, &slot))) return rc;
+        return slot < 0 ? 7 : 0;  // full freelist: syscall.E2BIG
+    }
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     if (m.key_size != 4) return fail(vm, MIMIC_EINVAL, "invalid key length, must be 4 bytes for array maps");
     uint32_t k;
     memcpy(&k, key, 4);
     if (k >= m.max_entries) return 7;  // syscall.E2BIG
+    if ((rc = settle(vm))) return rc;
     HIP_OK(vm, hipMemcpy(vm->arena + base + (uint64_t)k * m.value_size, value, m.value_size, hipMemcpyHostToDevice));
     return 0;
 }
 
+// LinuxMap.Lookup: the value's virtual address, 0 when absent (emulator_linux_map_array.go:78-94,
+// 235-241; emulator_linux_map_hash.go:134-155, 537-561)
 int mimic_map_lookup(mimic_vm *vm, uint32_t id, const void *key, int32_t cpu, uint32_t *addr_out) {
     int rc = map_check(vm, id);
     if (rc) return rc;
     const HostMap &m = vm->maps[id];
     uint64_t base;
+    if (is_hash(m)) {
+        uint32_t b = m.backing_addr;
+        if (m.family == FAM_PERCPU_HASH) {
+            if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
+            b += (uint32_t)cpu * m.addr_period;
+        }
+        int32_t slot = -1;
+        if ((rc = hash_op(vm, m, 0, key, nullptr, 0, &slot))) return rc;
+        *addr_out = slot < 0 ? 0 : b + (uint32_t)slot * m.value_size;
+        return 0;
+    }
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     if (m.key_size != 4) return fail(vm, MIMIC_EINVAL, "invalid key length, must be 4 bytes for array maps");
     uint32_t k;
@@ -526,11 +676,61 @@ int mimic_map_lookup(mimic_vm *vm, uint32_t id, const void *key, int32_t cpu, ui
     return 0;
 }
 
+// LinuxMapDeleter.Delete (emulator_linux_map_hash.go:225-255, 634-664); arrays are not deleters
 int mimic_map_delete(mimic_vm *vm, uint32_t id, const void *key) {
-    (void)key;
     int rc = map_check(vm, id);
     if (rc) return rc;
-    return fail(vm, MIMIC_EINVAL, "can't delete from given LinuxMap");
+    const HostMap &m = vm->maps[id];
+    if (!is_hash(m)) return fail(vm, MIMIC_EINVAL, "can't delete from given LinuxMap");
+    int32_t slot = -1;
+    return hash_op(vm, m, 2, key, nullptr, 0, &slot);
+}
+
+// live (key, slot) pairs of a hash map in table order
+static int hash_entries(mimic_vm *vm, const HostMap &m, uint8_t *keys, int32_t *slots, size_t cap_entries,
+                        uint32_t *n_out) {
+    int rc = settle(vm);
+    if (rc) return rc;
+    std::vector<uint64_t> rec((size_t)m.ht_cap * m.rec_q);
+    HIP_OK(vm, hipMemcpy(rec.data(), vm->arena + m.ht_dev_off, rec.size() * 8, hipMemcpyDeviceToHost));
+    uint32_t n = 0;
+    for (uint32_t p = 0; p < m.ht_cap; p++) {
+        const uint64_t *r = &rec[(size_t)p * m.rec_q];
+        if ((uint32_t)r[0] >= m.max_entries) continue;
+        if (n >= cap_entries) return fail(vm, MIMIC_EINVAL, "buffer too small");
+        if (keys) memcpy(keys + (size_t)n * m.key_size, r + 1, m.key_size);
+        if (slots) slots[n] = (int32_t)(uint32_t)r[0];
+        n++;
+    }
+    *n_out = n;
+    return 0;
+}
+
+// LinuxMap.Keys (emulator_linux_map_hash.go:113-131): the live keys, packed, in table order
+// (the reference returns Go map order, which is unspecified)
+int mimic_map_keys(mimic_vm *vm, uint32_t id, void *out, size_t cap, uint32_t *n_out) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    if (!n_out) return MIMIC_EINVAL;
+    if (!is_hash(m)) {  // array family: keys 0..E-1 (emulator_linux_map_array.go:64-75)
+        if (cap < (uint64_t)m.max_entries * 4) return fail(vm, MIMIC_EINVAL, "buffer too small");
+        for (uint32_t k = 0; k < m.max_entries; k++) memcpy((uint8_t *)out + 4ull * k, &k, 4);
+        *n_out = m.max_entries;
+        return 0;
+    }
+    return hash_entries(vm, m, (uint8_t *)out, nullptr, m.key_size ? cap / m.key_size : m.max_entries, n_out);
+}
+
+// KeyToIndex as (key, slot) pairs: where each live key's value sits in the values backing(s)
+int mimic_map_entries(mimic_vm *vm, uint32_t id, void *keys_out, int32_t *slots_out, size_t cap_entries,
+                      uint32_t *n_out) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    if (!n_out) return MIMIC_EINVAL;
+    if (!is_hash(m)) return fail(vm, MIMIC_EINVAL, "not a hash map");
+    return hash_entries(vm, m, (uint8_t *)keys_out, slots_out, cap_entries, n_out);
 }
 
 int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, size_t cap) {
@@ -541,7 +741,7 @@ int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, siz
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     uint64_t n = (uint64_t)m.max_entries * m.value_size;
     if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
-    if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
+    if ((rc = settle(vm))) return rc;
     HIP_OK(vm, hipMemcpy(out, vm->arena + base, n, hipMemcpyDeviceToHost));
     return (int)n;
 }
@@ -553,11 +753,12 @@ int mimic_map_sum_u64(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_
     if (m.value_size != 8) return fail(vm, MIMIC_EINVAL, "value size must be 8");
     if (cap < m.max_entries) return fail(vm, MIMIC_EINVAL, "buffer too small");
     uint32_t c0 = 0, c1 = 1;
-    if (m.family == FAM_PERCPU_ARRAY) {
+    if (m.family == FAM_PERCPU_ARRAY || m.family == FAM_PERCPU_HASH) {
         if (cpu_begin < 0 || cpu_end > (int32_t)m.ncpu || cpu_begin >= cpu_end) return fail(vm, MIMIC_EINVAL, "bad cpu range");
         c0 = (uint32_t)cpu_begin;
         c1 = (uint32_t)cpu_end;
     }
+    if (m.max_entries == 0) return 0;
     uint64_t *d = nullptr;
     HIP_OK(vm, hipMalloc(&d, m.max_entries * sizeof(uint64_t)));
     hipStream_t st = vm->last_stream ? vm->last_stream : vm->stream;
@@ -690,7 +891,11 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
     const uint32_t stack_q = S / 8;
     const uint32_t xdp_q = stack_q;
     const uint32_t frame_q = xdp_q + 3;
-    const uint32_t q_per_lane = frame_q + MIMIC_MAX_FRAMES * MIMIC_FRAME_QWORDS;
+    const uint32_t key_q = frame_q + MIMIC_MAX_FRAMES * MIMIC_FRAME_QWORDS;
+    uint32_t key_words = 0;  // hash helpers copy the key here once (derefMapKey)
+    for (auto &m : vm->maps)
+        if (is_hash(m)) key_words = std::max(key_words, (m.key_size + 7) / 8);
+    const uint32_t q_per_lane = key_q + key_words;
     const uint32_t plan = (lanes + 255) & ~255u;
     const uint64_t need = (uint64_t)q_per_lane * plan * 8;
     if (need > vm->priv_bytes || plan != vm->priv_lanes) {
@@ -732,6 +937,7 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
     kp.priv = vm->priv;
     kp.priv_xdp_q = xdp_q;
     kp.priv_frame_q = frame_q;
+    kp.priv_key_q = key_q;
     kp.budget = b->step_budget ? b->step_budget : MIMIC_DEFAULT_BUDGET;
     kp.n = b->n;
     kp.sched = b->schedule;
@@ -798,6 +1004,13 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
     }
     default:
         return fail(vm, MIMIC_EINVAL, "unknown schedule %u", b->schedule);
+    }
+    // compact hash tables whose buckets are mostly tombstones (device-side check, no host sync)
+    for (auto &m : vm->maps) {
+        if (!is_hash(m)) continue;
+        const DMap dm = to_dmap(m);
+        if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
     if (mimic_launch_xdp(&kp, st)) return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     vm->last_lanes = lanes;

@@ -1,0 +1,230 @@
+// hashmap.h -- device side of LinuxHashMap / LinuxPerCPUHashMap (emulator_linux_map_hash.go).
+//
+// The reference keeps, per map: a keys backing and a values backing (E slots each, VM
+// memory), a Go map sha256(key) -> slot, and a FIFO freelist of slots (a buffered channel
+// holding 0..E-1 initially, :56-64).  A new key takes the slot at the head of the freelist
+// (:179-186); Delete returns the slot to the tail (:244-250); a full freelist is E2BIG.
+//
+// Here the Go map becomes an open-addressing table in HBM that every lane of every wave can
+// use concurrently:
+//   * bucket record = one u64 word (tag<<32 | state) + the key in ceil(K/8) u64 words;
+//     state is a slot index, HT_EMPTY, HT_TOMB (deleted) or HT_BUSY (being filled);
+//   * lookups are lock-free: probe from the home bucket until EMPTY, compare the tag, then the
+//     key words, then re-read the state word (a concurrent delete+reuse shows up there);
+//   * inserts and deletes take a stripe lock chosen by the key's home bucket, so two lanes can
+//     never insert the same key twice; a wave runs its inserting lanes one at a time;
+//   * the freelist is a ring of 2^k >= 2(E+1) entries with agent-scope head/tail/avail
+//     counters.  Popped positions are reset to -1, and a push waits for its position to be
+//     free again, so FIFO order is the reference's whenever operations are sequential;
+//   * everything shared between lanes of different XCDs (state words, key words, ring,
+//     counters) is accessed with agent-scope atomics or sc1 loads/stores.  Per-XCD L2s are not
+//     coherent, so plain accesses would be wrong here.
+// The map values themselves are plain VM memory.  Concurrent vCPUs writing one shared map race
+// on them exactly as the reference's processPool workers do.
+#pragma once
+#include "layout.h"
+
+#define HDEV static __device__ __forceinline__
+
+HDEV uint64_t h_ld(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+HDEV void h_st(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+HDEV bool h_cas(uint64_t *p, uint64_t expect, uint64_t want) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+HDEV void h_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// the index region of one map: [records | rebuild copy | locks | freelist ring | HashCtl]
+struct HT {
+    uint8_t *base;
+    uint32_t cap, rec_q, K, nlocks, fl_cap;
+};
+HDEV HT h_table(uint8_t *arena, const DMap &m) {
+    return HT{arena + m.ht_dev_off, m.ht_cap, m.rec_q, m.key_size, m.nlocks, m.fl_cap};
+}
+HDEV size_t h_rec_bytes(const HT &t) { return (size_t)t.cap * t.rec_q * 8; }
+HDEV uint64_t *h_rec(const HT &t, uint32_t p) { return (uint64_t *)t.base + (size_t)p * t.rec_q; }
+HDEV uint64_t *h_tmp(const HT &t) { return (uint64_t *)(t.base + h_rec_bytes(t)); }
+HDEV uint32_t *h_locks(const HT &t) { return (uint32_t *)(t.base + 2 * h_rec_bytes(t)); }
+HDEV int32_t *h_ring(const HT &t) { return (int32_t *)(h_locks(t) + t.nlocks); }
+HDEV HashCtl *h_ctl(const HT &t) { return (HashCtl *)(h_ring(t) + t.fl_cap); }
+
+// key hash over the zero-padded little-endian key words (any good 64-bit mix; the reference's
+// sha256 only names Go-map buckets, which no program can observe)
+template <class KS>
+HDEV uint64_t h_hash(const KS &ks, uint32_t K) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ K;
+    const uint32_t nq = (K + 7) >> 3;
+    for (uint32_t q = 0; q < nq; q++) {
+        h = (h ^ ks.word(q)) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
+    }
+    h ^= h >> 29;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 32;
+    return h;
+}
+
+template <class KS>
+HDEV bool h_key_eq(const uint64_t *r, const KS &ks, uint32_t K) {
+    const uint32_t nq = (K + 7) >> 3;
+    for (uint32_t q = 0; q < nq; q++)
+        if (h_ld(r + 1 + q) != ks.word(q)) return false;
+    return true;
+}
+
+// lock-free lookup: slot index or -1; *pos = bucket of the key
+template <class KS>
+HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos) {
+    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32);
+    uint32_t p = (uint32_t)h & mask;
+    for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+        const uint64_t *r = h_rec(t, p);
+        const uint64_t w = h_ld(r);
+        const uint32_t s = (uint32_t)w;
+        if (s == HT_EMPTY) return -1;
+        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K) && h_ld(r) == w) {
+            if (pos) *pos = p;
+            return (int32_t)s;
+        }
+    }
+    return -1;
+}
+
+// freelist (emulator_linux_map_hash.go:179-186 pop, :244-250 push)
+HDEV int32_t h_fl_pop(const HT &t) {
+    HashCtl *c = h_ctl(t);
+    const int32_t a = __hip_atomic_fetch_add(&c->avail, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a <= 0) {
+        __hip_atomic_fetch_add(&c->avail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return -1;
+    }
+    const unsigned long long at = __hip_atomic_fetch_add(&c->head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t *f = h_ring(t) + (at & (t.fl_cap - 1));
+    int32_t v;
+    // the push that fills this position has already reserved it (avail counted it)
+    while ((v = __hip_atomic_exchange(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0) __builtin_amdgcn_s_sleep(1);
+    return v;
+}
+HDEV void h_fl_push(const HT &t, int32_t idx) {
+    HashCtl *c = h_ctl(t);
+    const unsigned long long at = __hip_atomic_fetch_add(&c->tail, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t *f = h_ring(t) + (at & (t.fl_cap - 1));
+    for (;;) {
+        int32_t e = -1;
+        if (__hip_atomic_compare_exchange_strong(f, &e, idx, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_fetch_add(&c->avail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+HDEV uint32_t *h_lock(const HT &t, uint64_t h) {
+    return h_locks(t) + ((uint32_t)h & (t.nlocks - 1));
+}
+HDEV void h_acquire(uint32_t *lk) {
+    for (;;) {
+        uint32_t e = 0;
+        if (__hip_atomic_compare_exchange_strong(lk, &e, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+HDEV void h_release(uint32_t *lk) {
+    h_drain();
+    __hip_atomic_store(lk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// find-or-insert under the key's stripe lock (ONE lane at a time per wave).
+// Returns the slot, or -1 when the freelist is empty (E2BIG).  *inserted = a new slot.
+template <class KS>
+HDEV int32_t h_insert_locked(const HT &t, const KS &ks, uint64_t h, bool *inserted) {
+    *inserted = false;
+    uint32_t *lk = h_lock(t, h);
+    h_acquire(lk);
+    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32), K = t.K;
+    uint32_t p = (uint32_t)h & mask, freep = HT_EMPTY;
+    int32_t found = -1;
+    for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+        const uint64_t *r = h_rec(t, p);
+        const uint64_t w = h_ld(r);
+        const uint32_t s = (uint32_t)w;
+        if (s == HT_EMPTY) {
+            if (freep == HT_EMPTY) freep = p;
+            break;
+        }
+        if (s == HT_TOMB) {
+            if (freep == HT_EMPTY) freep = p;
+            continue;
+        }
+        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, K)) {
+            found = (int32_t)s;
+            break;
+        }
+    }
+    if (found >= 0) {
+        h_release(lk);
+        return found;
+    }
+    const int32_t idx = h_fl_pop(t);
+    if (idx < 0) {
+        h_release(lk);
+        return -1;
+    }
+    // claim a free bucket (another stripe may take the same one first: then probe on)
+    p = freep == HT_EMPTY ? ((uint32_t)h & mask) : freep;
+    uint64_t *r = nullptr;
+    bool was_empty = false;
+    for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+        uint64_t *q = h_rec(t, p);
+        const uint64_t w = h_ld(q);
+        const uint32_t s = (uint32_t)w;
+        if ((s == HT_EMPTY || s == HT_TOMB) && h_cas(q, w, ((uint64_t)tag << 32) | HT_BUSY)) {
+            r = q;
+            was_empty = s == HT_EMPTY;
+            break;
+        }
+    }
+    // live + busy <= E < ht_cap, so a free bucket always exists
+    const uint32_t nq = (K + 7) >> 3;
+    for (uint32_t q = 0; q < nq; q++) h_st(r + 1 + q, ks.word(q));
+    h_drain();
+    h_st(r, ((uint64_t)tag << 32) | (uint32_t)idx);
+    if (was_empty) __hip_atomic_fetch_add(&h_ctl(t)->used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h_release(lk);
+    *inserted = true;
+    return idx;
+}
+
+// delete under the stripe lock: the deleted slot or -1 (absent)
+template <class KS>
+HDEV int32_t h_delete_locked(const HT &t, const KS &ks, uint64_t h) {
+    uint32_t *lk = h_lock(t, h);
+    h_acquire(lk);
+    uint32_t p = 0;
+    const int32_t idx = h_find(t, ks, h, &p);
+    if (idx >= 0) {
+        uint64_t *r = h_rec(t, p);
+        h_st(r, (h_ld(r) & ~0xffffffffull) | HT_TOMB);
+        h_fl_push(t, idx);
+    }
+    h_release(lk);
+    return idx;
+}
+
+// key words taken from device bytes (host-side map operations)
+struct KeyBytes {
+    const uint8_t *p;
+    uint32_t K;
+    __device__ uint64_t word(uint32_t q) const {
+        uint64_t v = 0;
+        const uint32_t o = q * 8, c = K - o < 8 ? K - o : 8;
+        for (uint32_t i = 0; i < c; i++) v |= (uint64_t)p[o + i] << (8 * i);
+        return v;
+    }
+};
+// key words from a bucket record (rebuild)
+struct KeyRec {
+    const uint64_t *r;
+    __device__ uint64_t word(uint32_t q) const { return r[1 + q]; }
+};

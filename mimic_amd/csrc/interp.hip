@@ -30,6 +30,7 @@
 #include <algorithm>
 
 #include "layout.h"
+#include "hashmap.h"
 #include "../../include/mimic_amd.h"
 
 typedef uint16_t __attribute__((aligned(1))) u16u;
@@ -397,6 +398,29 @@ DEV void copy_into(const KParams &kp, const Lane &L, const Ref &src, uint8_t *ds
     }
 }
 
+// hash-map key words: derefMapKey (emulator_linux_helpers.go:449-471) copies the key out of VM
+// memory once, into the lane's key scratch in private memory (qword-interleaved like the stack)
+struct KeyPriv {
+    const uint64_t *p;
+    uint32_t stride;
+    __device__ uint64_t word(uint32_t q) const { return p[(size_t)q * stride]; }
+};
+DEV KeyPriv key_fetch(const KParams &kp, const Lane &L, const Ref &R, uint32_t K) {
+    uint64_t *p = (uint64_t *)kp.priv + (size_t)kp.priv_key_q * kp.priv_lanes + L.lane;
+    for (uint32_t q = 0; q * 8 < K; q++) {
+        const uint32_t c = K - q * 8 < 8 ? K - q * 8 : 8;
+        p[(size_t)q * kp.priv_lanes] = region_load(kp, L, R, R.off + q * 8, c);
+    }
+    return KeyPriv{p, kp.priv_lanes};
+}
+// values[cpu] + idx*S (hash: one values backing; per-CPU hash: cpu-major backings)
+DEV uint32_t hash_value_addr(const DMap &m, int32_t cpu, uint32_t idx) {
+    return m.backing_addr + (m.family == FAM_PERCPU_HASH ? (uint32_t)cpu * m.addr_period : 0u) + idx * m.value_size;
+}
+DEV uint8_t *hash_value_ptr(const KParams &kp, const DMap &m, int32_t cpu, uint32_t idx) {
+    return kp.arena + m.dev_off + (m.family == FAM_PERCPU_HASH ? (size_t)cpu * m.dev_stride : 0) + (size_t)idx * m.value_size;
+}
+
 struct HelperOut {
     int st;          // 0 or status
     uint64_t r0;     // new R0 (if set_r0)
@@ -433,7 +457,12 @@ DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint6
         o.set_r0 = true;
         return o;
     }
-    o.st = MIMIC_ERR_ENGINE_HELPER; // hash maps: not in this kernel build
+    // LinuxHashMap.Lookup :134-155 / LinuxPerCPUHashMap.Lookup :537-561
+    if (m.family == FAM_PERCPU_HASH && (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
+    const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
+    const int32_t idx = h_find(h_table(kp.arena, m), ks, h_hash(ks, m.key_size), nullptr);
+    o.r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
+    o.set_r0 = true;
     return o;
 }
 
@@ -461,7 +490,38 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
         o.set_r0 = true;
         return o;
     }
-    o.st = MIMIC_ERR_ENGINE_HELPER;
+    // LinuxHashMap.Update :158-203 / LinuxPerCPUHashMap.Update :564-612
+    if (m.family == FAM_PERCPU_HASH && (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
+    const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
+    const uint64_t h = h_hash(ks, m.key_size);
+    const HT t = h_table(kp.arena, m);
+    int32_t idx = h_find(t, ks, h, nullptr);
+    bool inserted = false;
+    if (idx < 0) {
+        // a new key: the lanes of this wave that insert take the stripe locks one at a time
+        uint64_t need = __ballot(1);
+        const uint32_t me = __lane_id();
+        while (need) {
+            if (me == (uint32_t)__builtin_ctzll(need)) idx = h_insert_locked(t, ks, h, &inserted);
+            need &= need - 1;
+        }
+    }
+    if (idx < 0) {
+        o.r0 = 7; // syscall.E2BIG: the freelist is empty
+        o.set_r0 = true;
+        return o;
+    }
+    if (inserted) { // keys.Write(keyOff, key) (the bytes of a found key are already there)
+        uint8_t *kd = kp.arena + m.keys_dev_off + (size_t)idx * m.key_size;
+        for (uint32_t q = 0; q * 8 < m.key_size; q++) {
+            const uint32_t c = m.key_size - q * 8 < 8 ? m.key_size - q * 8 : 8;
+            st_n(kd + q * 8, c, ks.word(q));
+        }
+    }
+    // re-resolved here (pure) so that no Ref stays live across the insert
+    copy_into(kp, L, resolve(kp, L, (uint32_t)r3), hash_value_ptr(kp, m, L.cpu, (uint32_t)idx), m.value_size);
+    o.r0 = 0;
+    o.set_r0 = true;
     return o;
 }
 
@@ -471,8 +531,20 @@ DEV HelperOut helper_delete(const KParams &kp, const Lane &L, uint64_t r1, uint6
     if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
     const DMap m = kp.maps[mid];
     if (m.family == FAM_ARRAY || m.family == FAM_PERCPU_ARRAY) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-    (void)r2;
-    o.st = MIMIC_ERR_ENGINE_HELPER;
+    Ref K = resolve(kp, L, (uint32_t)r2);
+    if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
+    // LinuxHashMap.Delete :225-255 / LinuxPerCPUHashMap.Delete :634-664 (absent key: nil)
+    const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
+    const uint64_t h = h_hash(ks, m.key_size);
+    const HT t = h_table(kp.arena, m);
+    uint64_t need = __ballot(1);
+    const uint32_t me = __lane_id();
+    while (need) {
+        if (me == (uint32_t)__builtin_ctzll(need)) h_delete_locked(t, ks, h);
+        need &= need - 1;
+    }
+    o.r0 = 0;
+    o.set_r0 = true;
     return o;
 }
 
@@ -662,7 +734,7 @@ DEV uint64_t alu32(uint32_t hi, uint64_t d, uint64_t x) {
 #define NREGS 11
 #define KEY_DONE 0xffffffffu
 
-extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(KParams kp) {
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(KParams kp) {
     // eBPF registers r0..r10 of every lane live in LDS, [wave][reg][lane] (8-byte words): a
     // wave-uniform register number addresses 64 consecutive words (conflict-free ds_read_b64),
     // and multi-register updates (exit, helpers) need no register-array copies.
@@ -955,6 +1027,85 @@ extern "C" __global__ void mimic_sum_u64_kernel(const uint8_t *base, uint64_t st
     uint64_t s = 0;
     for (uint32_t c = t / nvals; c < cpus; c += m) s += *(const uint64_t *)(base + (uint64_t)c * stride + 8ull * k);
     atomicAdd((unsigned long long *)&out[k], (unsigned long long)s);
+}
+
+// One host-side hash-map operation (mimic_map_update/lookup/delete), run by the same device code
+// the helpers use so that both sides share the index and the freelist.
+extern "C" __global__ void mimic_hash_op_kernel(uint8_t *arena, DMap m, uint32_t op, const uint8_t *key,
+                                                const uint8_t *val, int32_t cpu, int32_t *out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const KeyBytes ks{key, m.key_size};
+    const uint64_t h = h_hash(ks, m.key_size);
+    const HT t = h_table(arena, m);
+    int32_t idx;
+    if (op == 0) {
+        idx = h_find(t, ks, h, nullptr);
+    } else if (op == 1) {
+        idx = h_find(t, ks, h, nullptr);
+        bool ins = false;
+        if (idx < 0) idx = h_insert_locked(t, ks, h, &ins);
+        if (idx >= 0) {  // keys.Write + values[cpu].Write (emulator_linux_map_hash.go:188-200)
+            uint8_t *kd = arena + m.keys_dev_off + (size_t)idx * m.key_size;
+            for (uint32_t i = 0; i < m.key_size; i++) kd[i] = key[i];
+            uint8_t *vd = arena + m.dev_off + (m.family == FAM_PERCPU_HASH ? (size_t)cpu * m.dev_stride : 0) +
+                          (size_t)idx * m.value_size;
+            for (uint32_t i = 0; i < m.value_size; i++) vd[i] = val[i];
+        }
+    } else {
+        idx = h_delete_locked(t, ks, h);
+    }
+    *out = idx;
+}
+
+// Tombstone compaction: when live + deleted buckets pass 3/4 of the table, rebuild it in
+// place (one workgroup; launched before every batch, returns at once otherwise).
+extern "C" __global__ __launch_bounds__(1024) void mimic_hash_rebuild_kernel(uint8_t *arena, DMap m, uint32_t force) {
+    __shared__ uint32_t go, live;
+    const HT t = h_table(arena, m);
+    HashCtl *c = h_ctl(t);
+    if (threadIdx.x == 0) {
+        go = force || (uint64_t)c->used * 4 > (uint64_t)m.ht_cap * 3;
+        live = 0;
+    }
+    __syncthreads();
+    if (!go) return;
+    uint64_t *rec = h_rec(t, 0), *tmp = h_tmp(t);
+    const size_t words = (size_t)m.ht_cap * m.rec_q;
+    for (size_t i = threadIdx.x; i < words; i += blockDim.x) tmp[i] = rec[i];
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < m.ht_cap; p += blockDim.x) h_st(rec + (size_t)p * m.rec_q, ~0ull);
+    __syncthreads();
+    const uint32_t mask = m.ht_cap - 1, nq = m.rec_q - 1;
+    for (uint32_t p = threadIdx.x; p < m.ht_cap; p += blockDim.x) {
+        const uint64_t *t = tmp + (size_t)p * m.rec_q;
+        const uint64_t w = t[0];
+        if ((uint32_t)w >= HT_BUSY) continue;
+        const KeyRec kr{t};
+        const uint64_t h = h_hash(kr, m.key_size);
+        for (uint32_t q = (uint32_t)h & mask;; q = (q + 1) & mask) {
+            uint64_t *r = rec + (size_t)q * m.rec_q;
+            if (h_cas(r, ~0ull, ((uint64_t)(uint32_t)(w >> 32) << 32) | HT_BUSY)) {
+                for (uint32_t k = 0; k < nq; k++) h_st(r + 1 + k, t[1 + k]);
+                h_drain();
+                h_st(r, w);
+                break;
+            }
+        }
+        atomicAdd(&live, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) c->used = live;
+}
+
+extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
+                                    int32_t cpu, int32_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(mimic_hash_op_kernel, dim3(1), dim3(64), 0, st, arena, *m, op, key, val, cpu, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st) {
+    hipLaunchKernelGGL(mimic_hash_rebuild_kernel, dim3(1), dim3(1024), 0, st, arena, *m, force);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int mimic_launch_xdp(const KParams *kp, hipStream_t st) {

@@ -54,13 +54,29 @@ struct DMap {
     uint32_t ncpu;           // per-CPU: number of cpus (len(arrayMaps) / len(values))
     uint64_t dev_off;        // arena offset of cpu-0 backing
     uint64_t dev_stride;     // arena distance between cpu backings
-    // hash maps (device open-addressing index, see hashmap notes in engine.cpp)
-    uint64_t keys_dev_off;   // arena offset of the keys backing
+    // hash maps: device open-addressing index over the reference's key/value slots
+    // (hashmap.h).  The slot a key gets comes from the reference's FIFO freelist.
+    uint64_t keys_dev_off;   // arena offset of the VM-visible keys backing (E*K)
     uint32_t keys_addr;
-    uint32_t ht_cap;         // power of two
-    uint64_t ht_dev_off;     // arena offset of int32 slot table [ht_cap]
-    uint64_t fl_dev_off;     // arena offset of the freelist ring (int32 [E+1]) + head/len words
+    uint32_t ht_cap;         // buckets, power of two
+    uint64_t ht_dev_off;     // hash index region (hashmap.h): records | rebuild copy | locks | freelist | HashCtl
+    uint32_t rec_q;          // record size in qwords
+    uint32_t nlocks;         // power of two
+    uint32_t fl_cap;         // power of two >= 2(E+1)
+    uint32_t pad_h;
 };
+
+// freelist ring + table counters of one hash map (device, agent-scope atomics)
+struct HashCtl {
+    unsigned long long head;   // next ring position to pop
+    unsigned long long tail;   // next ring position to push
+    int32_t avail;             // free slots not yet claimed
+    uint32_t used;             // buckets that are not EMPTY (live + tombstones + busy)
+    uint32_t pad[2];
+};
+#define HT_EMPTY 0xffffffffu
+#define HT_TOMB 0xfffffffeu
+#define HT_BUSY 0xfffffffdu
 
 struct DProg {
     uint32_t base;   // first instruction in the concatenated instruction array
@@ -126,6 +142,8 @@ struct KParams {
     uint8_t *priv;              // per-lane private memory, qword-interleaved
     uint32_t priv_xdp_q;        // qword index of the xdp_md overlay
     uint32_t priv_frame_q;      // qword index of the saved-frame area
+    uint32_t priv_key_q;        // qword index of the hash-key scratch (ceil(K/8) words, max over hash maps)
+    uint32_t pad_k;
     uint64_t budget;
     // batch
     uint32_t n;

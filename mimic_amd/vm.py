@@ -172,7 +172,7 @@ class LinuxMap:
         """Per-key sum over vCPUs of a u64-valued map (device reduction)."""
         vm = self._vm
         if cpu_end is None:
-            cpu_end = vm.settings.vcpus if isinstance(self, LinuxPerCPUArrayMap) else 1
+            cpu_end = self.Indices()
         out = (C.c_uint64 * self.Spec.MaxEntries)()
         _check(vm.h, vm.lib.mimic_map_sum_u64(vm.h, self.id, cpu_begin, cpu_end, out, self.Spec.MaxEntries),
                "sum")
@@ -204,12 +204,68 @@ class LinuxPerCPUArrayMap(LinuxMap):  # emulator_linux_map_array.go:177-250
         return b"".join(i.to_bytes(4, "little") for i in range(self.Spec.MaxEntries))
 
 
+class LinuxHashMap(LinuxMap):  # emulator_linux_map_hash.go:21-255
+    """Exact-key map: a new key takes the head of a FIFO freelist of slots (0..E-1 initially);
+    a full freelist is E2BIG; Delete returns the slot to the tail."""
+
+    def _keys(self):
+        vm = self._vm
+        K, E = self.Spec.KeySize, self.Spec.MaxEntries
+        buf = C.create_string_buffer(max(K * E, 1))
+        n = C.c_uint32()
+        _check(vm.h, vm.lib.mimic_map_keys(vm.h, self.id, buf, max(K * E, 1), C.byref(n)), "keys")
+        return buf.raw[:K * n.value], n.value
+
+    def Keys(self, cpuid: int = 0) -> bytes:
+        return self._keys()[0]
+
+    def KeyList(self) -> List[bytes]:
+        raw, n = self._keys()
+        K = self.Spec.KeySize
+        return [raw[i * K:(i + 1) * K] for i in range(n)]
+
+    def Entries(self) -> List[Tuple[bytes, int]]:
+        """Live (key, slot) pairs (KeyToIndex), table order."""
+        vm = self._vm
+        K, E = self.Spec.KeySize, self.Spec.MaxEntries
+        kb = C.create_string_buffer(max(K * E, 1))
+        sl = (C.c_int32 * max(E, 1))()
+        n = C.c_uint32()
+        _check(vm.h, vm.lib.mimic_map_entries(vm.h, self.id, kb, sl, max(E, 1), C.byref(n)), "entries")
+        return [(kb.raw[i * K:(i + 1) * K], int(sl[i])) for i in range(n.value)]
+
+    def Contents(self) -> Dict[bytes, List[bytes]]:
+        """key -> [value bytes of cpu 0 .. Indices()-1] (one bulk read per cpu)."""
+        S = self.Spec.ValueSize
+        ents = self.Entries()
+        vals = [self.Values(c) for c in range(self.Indices())]
+        return {k: [v[s * S:(s + 1) * S] for v in vals] for k, s in ents}
+
+    def ValueOf(self, key: bytes, cpuid: int = 0) -> Optional[bytes]:
+        """The value bytes for key on a cpu (Lookup + MemoryController read), None if absent."""
+        a = self.Lookup(key, cpuid)
+        return None if a == 0 else self._vm.MemoryController.Read(a, self.Spec.ValueSize)
+
+
+class LinuxPerCPUHashMap(LinuxHashMap):  # emulator_linux_map_hash.go:417-664
+    def Indices(self) -> int:
+        return self._vm.settings.vcpus
+
+
+HASH_TYPES = (1, 13, 18, 19, 24, 25, 26, 28, 29)
+PERCPU_HASH_TYPES = (5, 21)
+
+
 def MapSpecToLinuxMap(spec: MapSpec) -> LinuxMap:  # emulator_linux_map.go:57-113
     t = int(spec.Type)
     if t in (2, 3, 8, 12, 14, 15, 16, 17, 20):
         return LinuxArrayMap(spec)
     if t == 6:
         return LinuxPerCPUArrayMap(spec)
+    if t in HASH_TYPES:
+        return LinuxHashMap(spec)
+    if t in PERCPU_HASH_TYPES:
+        return LinuxPerCPUHashMap(spec)
     raise MimicError(f"unsupported map type '{t}' in this engine build")
 
 

@@ -187,6 +187,122 @@ def prog_parse5(map_name: str = "flows", max_entries: int = 256) -> Program:
                    [dict(name=map_name, type=6, key_size=4, value_size=8, max_entries=max_entries)])
 
 
+def _flow_key_items():
+    """Parse the 5-tuple into a 16-byte key at r10-16: {saddr, daddr, sport|dport, proto, 0, 0, 0}
+    (IPv4; IPv6 addresses folded to 32 bits).  r7 = XDP_DROP; non-IP / truncated -> "out"."""
+    return [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),            # r2 = data
+        A.ldx(4, 3, 6, 4),            # r3 = data_end
+        A.mov64_imm(7, A.XDP_DROP),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 14),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(2, 5, 2, 12),           # ethertype (LE view)
+        A.jmp("jeq", 5, 0x0008, "ipv4"),
+        A.jmp("jeq", 5, 0xDD86, "ipv6"),
+        A.ja("out"),
+        "ipv4",
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 38),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(4, 1, 2, 26), A.stx(4, 10, -16, 1),     # saddr
+        A.ldx(4, 1, 2, 30), A.stx(4, 10, -12, 1),     # daddr
+        A.ldx(4, 1, 2, 34), A.stx(4, 10, -8, 1),      # sport | dport
+        A.ldx(1, 1, 2, 23), A.stx(4, 10, -4, 1),      # proto + 3 zero bytes
+        A.ja("track"),
+        "ipv6",
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 58),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(8, 1, 2, 22), A.ldx(8, 4, 2, 30), A.alu64("xor", 1, 4, reg=True),
+        A.mov64_reg(4, 1), A.alu64("rsh", 4, 32), A.alu64("xor", 1, 4, reg=True), A.stx(4, 10, -16, 1),
+        A.ldx(8, 1, 2, 38), A.ldx(8, 4, 2, 46), A.alu64("xor", 1, 4, reg=True),
+        A.mov64_reg(4, 1), A.alu64("rsh", 4, 32), A.alu64("xor", 1, 4, reg=True), A.stx(4, 10, -12, 1),
+        A.ldx(4, 1, 2, 54), A.stx(4, 10, -8, 1),
+        A.ldx(1, 1, 2, 20), A.stx(4, 10, -4, 1),
+        "track",
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -16),
+    ]
+
+
+def prog_flowtrack(map_name: str = "flows", max_entries: int = 131072, map_type: int = 1) -> Program:
+    """Config 4: insert the packet's 5-tuple key into a shared hash map if absent (BPF_NOEXIST;
+    the reference ignores the flags, Q10).  The value is a function of the key only, so the final
+    map contents do not depend on the order of the inserts.  XDP_PASS when the flow is (now)
+    tracked, XDP_DROP for non-IP / truncated frames or E2BIG (map full)."""
+    items = _flow_key_items() + [
+        A.ld_map_fd(1, map_name),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jne", 0, 0, "pass"),
+        A.ldx(8, 1, 10, -16),                          # value = mix(key)
+        A.ldx(8, 4, 10, -8),
+        A.alu64("mul", 1, 0x01000193),
+        A.alu64("xor", 1, 4, reg=True),
+        A.stx(8, 10, -24, 1),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -16),
+        A.mov64_reg(3, 10),
+        A.alu64("add", 3, -24),
+        A.ld_map_fd(1, map_name),
+        A.mov64_imm(4, 1),                             # BPF_NOEXIST
+        A.call(A.FN_MAP_UPDATE_ELEM),
+        A.jmp("jne", 0, 0, "out"),
+        "pass",
+        A.mov64_imm(7, A.XDP_PASS),
+        "out",
+        A.mov64_reg(0, 7),
+        A.exit_(),
+    ]
+    raw, rel = A.assemble(items)
+    return Program("xdp_flowtrack", raw, rel,
+                   [dict(name=map_name, type=map_type, key_size=16, value_size=8, max_entries=max_entries)])
+
+
+def prog_flowcount(map_name: str = "flowcnt", max_entries: int = 65536, delete_every: int = 0) -> Program:
+    """Per-CPU hash: count packets per 5-tuple key (lookup, then increment in place, or insert 1).
+    Each vCPU only touches its own values, so the final per-(key, cpu) counters do not depend on
+    the interleaving.  delete_every=d > 0: a packet whose key's first word % d == 0 deletes its
+    key again after counting (tombstones, freelist reuse)."""
+    items = _flow_key_items() + [
+        A.ld_map_fd(1, map_name),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jeq", 0, 0, "insert"),
+        A.ldx(8, 1, 0, 0),
+        A.alu64("add", 1, 1),
+        A.stx(8, 0, 0, 1),
+        A.ja("counted"),
+        "insert",
+        A.st(8, 10, -24, 1),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -16),
+        A.mov64_reg(3, 10),
+        A.alu64("add", 3, -24),
+        A.ld_map_fd(1, map_name),
+        A.mov64_imm(4, 0),
+        A.call(A.FN_MAP_UPDATE_ELEM),
+        A.jmp("jne", 0, 0, "out"),
+        "counted",
+        A.mov64_imm(7, A.XDP_PASS),
+    ]
+    if delete_every:
+        items += [
+            A.ldx(4, 1, 10, -16),
+            A.alu64("mod", 1, delete_every),
+            A.jmp("jne", 1, 0, "out"),
+            A.mov64_reg(2, 10),
+            A.alu64("add", 2, -16),
+            A.ld_map_fd(1, map_name),
+            A.call(A.FN_MAP_DELETE_ELEM),
+            A.mov64_imm(7, A.XDP_TX),
+        ]
+    items += ["out", A.mov64_reg(0, 7), A.exit_()]
+    raw, rel = A.assemble(items)
+    return Program("xdp_flowcount", raw, rel,
+                   [dict(name=map_name, type=5, key_size=16, value_size=8, max_entries=max_entries)])
+
+
 # ---------------------------------------------------------------------------------------------
 # packets
 # ---------------------------------------------------------------------------------------------
@@ -199,6 +315,8 @@ def _flow_pool(rng, n_flows: int = 65536):
         dst6=rng.integers(0, 256, (n_flows, 16), dtype=np.uint8),
         sport=rng.integers(1, 65536, n_flows).astype(np.uint16),
         dport=rng.integers(1, 65536, n_flows).astype(np.uint16),
+        # a flow keeps one L4 protocol: TCP 60 % / UDP 35 % / ICMP 5 %
+        proto=rng.choice(np.array([6, 17, 1]), n_flows, p=[0.60, 0.35, 0.05]).astype(np.uint8),
     )
 
 
@@ -218,8 +336,8 @@ def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: i
     # random payload bytes everywhere first (headers overwritten below)
     buf[:] = rng.integers(0, 256, total, dtype=np.uint8)
     kind = rng.choice(3, n, p=[0.90, 0.05, 0.05])           # ipv4 / ipv6 / arp
-    proto = rng.choice(np.array([6, 17, 1]), n, p=[0.60, 0.35, 0.05])
     flow = rng.integers(0, 65536, n)
+    proto = pool["proto"][flow]
     idx = off.astype(np.int64)
 
     def put(col, vals):
@@ -261,6 +379,8 @@ def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: i
     ok6 = lens[kind == 1] >= 58
     buf[v6[ok6] + 54] = (pool["sport"][f6[ok6]] >> 8).astype(np.uint8)
     buf[v6[ok6] + 55] = (pool["sport"][f6[ok6]] & 0xFF).astype(np.uint8)
+    buf[v6[ok6] + 56] = (pool["dport"][f6[ok6]] >> 8).astype(np.uint8)
+    buf[v6[ok6] + 57] = (pool["dport"][f6[ok6]] & 0xFF).astype(np.uint8)
     va = idx[kind == 2]
     buf[va + 14] = 0
     buf[va + 15] = 1

@@ -150,6 +150,16 @@ class OracleVM:
             raise OracleError("map_values")
         return buf.raw[:n]
 
+    def map_entries(self, mid: int) -> List[Tuple[bytes, int]]:
+        """Live (key, slot) pairs of a hash map (KeyToIndex)."""
+        _, K, _, E = self.specs[mid]
+        sl = (C.c_int32 * max(E, 1))()
+        kb = C.create_string_buffer(max(K * E, 1))
+        n = self.lib.orc_map_slots(self.h, mid, sl, kb, max(E, 1))
+        if n < 0:
+            raise OracleError("map_entries")
+        return [(kb.raw[i * K:(i + 1) * K], int(sl[i])) for i in range(n)]
+
     def map_addr(self, mid: int) -> int:
         return self.lib.orc_map_addr(self.h, mid)
 

@@ -370,6 +370,111 @@ case("tailcall_into_empty_program", tc_main, e(r0=1, status=PC_OOB, steps=5, err
      maps=[PA], extra_progs=[("empty", [])], prog_array=[("progs", 0, 1)])
 
 
+# hash maps (emulator_linux_map_hash.go): obj (8) | keys (E*K) | values (E*S); per-CPU hash:
+# V x values (E*S) | obj | keys.  A new key takes the freelist head (slots 0..E-1 initially,
+# :56-64, :179-186); Delete pushes the slot to the tail (:244-250); a full freelist is E2BIG.
+# Straight-line programs: steps = slots executed (the LD_IMM64 pad Nop counts, inst.go:82-84).
+H3 = dict(name="h", type=1, key_size=4, value_size=8, max_entries=3)
+H_KEYS, H_VALS = 0x10009, 0x10009 + 12 + 1
+
+
+def h_upd(key, val, m="h"):
+    return [A.st(4, 10, -4, key), A.st(8, 10, -16, val), A.mov64_reg(2, 10), A.alu64("add", 2, -4),
+            A.mov64_reg(3, 10), A.alu64("add", 3, -16), A.ld_map_fd(1, m), A.mov64_imm(4, 0), A.call(2)]
+
+
+def h_look(key, m="h"):
+    return [A.st(4, 10, -4, key), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, m), A.call(1)]
+
+
+def h_del(key, m="h"):
+    return [A.st(4, 10, -4, key), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, m), A.call(3)]
+
+
+def straight(name, items, r0, ref, **kw):
+    items = items + [A.exit_()]
+    case(name, items, e(r0=r0, steps=len(A.assemble(items)[0]) // 8), ref, **kw)
+
+
+straight("hash_lookup_absent_null", h_look(7), 0, "emulator_linux_map_hash.go:145-149", maps=[H3])
+straight("hash_update_returns_zero", h_upd(7, 100), 0, "emulator_linux_map_hash.go:158-203", maps=[H3])
+straight("hash_first_slot_address", h_upd(7, 100) + h_look(7), H_VALS,
+         "emulator_linux_map_hash.go:43-97 (obj @0x10000, keys @0x10009, values @0x10016), :152-154", maps=[H3])
+straight("hash_value_readback", h_upd(7, 100) + h_look(7) + [A.ldx(8, 0, 0, 0)], 100,
+         "emulator_linux_map_hash.go:196-200", maps=[H3])
+fifo = h_upd(1, 11) + h_upd(2, 22) + h_del(1) + h_upd(3, 33) + h_upd(4, 44)
+straight("hash_fifo_reuse_tail", fifo + h_look(4), H_VALS + 0,
+         "emulator_linux_map_hash.go:179-186, 244-250 (slot 0 returns to the tail)", maps=[H3])
+straight("hash_fifo_head_order", fifo + h_look(3), H_VALS + 16,
+         "emulator_linux_map_hash.go:61-64 (freelist 0,1,2 in order)", maps=[H3])
+straight("hash_fifo_value", fifo + h_look(4) + [A.ldx(8, 0, 0, 0)], 44, "emulator_linux_map_hash.go:196-200", maps=[H3])
+straight("hash_e2big_positive", h_upd(1, 1) + h_upd(2, 2) + h_upd(3, 3) + h_upd(4, 4), 7,
+         "emulator_linux_map_hash.go:181-184, helpers.go:549 (Q9)", maps=[H3])
+straight("hash_update_existing_keeps_slot",
+         h_upd(1, 1) + h_upd(2, 2) + h_upd(1, 5) + h_upd(3, 3) + h_look(1) + [A.ldx(8, 0, 0, 0)], 5,
+         "emulator_linux_map_hash.go:170-177 (found: same slot, no freelist pop)", maps=[H3])
+straight("hash_update_existing_then_full", h_upd(1, 1) + h_upd(2, 2) + h_upd(1, 5) + h_upd(3, 3) + h_upd(4, 4), 7,
+         "emulator_linux_map_hash.go:170-186", maps=[H3])
+straight("hash_delete_absent_zero", h_del(9), 0, "emulator_linux_map_hash.go:233-237", maps=[H3])
+straight("hash_delete_then_lookup_null", h_upd(1, 1) + h_del(1) + h_look(1), 0,
+         "emulator_linux_map_hash.go:239-244", maps=[H3])
+straight("hash_keys_backing_visible", h_upd(0x11223344, 1) + [A.ld_imm64(1, H_KEYS), A.ldx(4, 0, 1, 0)], 0x11223344,
+         "emulator_linux_map_hash.go:188-193 (keys PlainMemory is VM memory)", maps=[H3])
+straight("hash_keys_backing_second_slot",
+         h_upd(5, 1) + h_upd(0x0a0b0c0d, 2) + [A.ld_imm64(1, H_KEYS + 4), A.ldx(4, 0, 1, 0)], 0x0a0b0c0d,
+         "emulator_linux_map_hash.go:188-193", maps=[H3])
+straight("hash_host_update_then_lookup", h_look(5) + [A.ldx(8, 0, 0, 0)], 77, "emulator_linux_map_hash.go:158-203 (host Update)",
+         maps=[H3], map_init=[("h", k(5), (77).to_bytes(8, "little"), 0)])
+case("hash_object_not_vmmem", [A.ld_map_fd(1, "h"), A.ldx(4, 0, 1, 0), A.exit_()], e(status=NOTVMMEM, steps=3, err_pc=2),
+     "inst.go:308-311 (LinuxHashMap is not VMMem)", maps=[H3])
+case("hash_lookup_key_unresolved", [A.mov64_imm(2, 3), A.ld_map_fd(1, "h"), A.call(1), A.exit_()],
+     e(status=KEY, steps=4, err_pc=3), "emulator_linux_helpers.go:449-456", maps=[H3])
+case("hash_update_value_unresolved", [A.st(4, 10, -4, 1), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.mov64_imm(3, 3),
+                                      A.ld_map_fd(1, "h"), A.call(2), A.exit_()],
+     e(status=VALUE, steps=7, err_pc=6), "emulator_linux_helpers.go:525-530", maps=[H3])
+case("hash_delete_key_unresolved", [A.mov64_imm(2, 3), A.ld_map_fd(1, "h"), A.call(3), A.exit_()],
+     e(status=KEY, steps=4, err_pc=3), "emulator_linux_helpers.go:570-574", maps=[H3])
+case("hash_key_partly_outside_stack", [A.mov64_reg(2, 10), A.alu64("add", 2, -2), A.ld_map_fd(1, "h"), A.call(1), A.exit_()],
+     e(status=OK, r0=0, steps=6), "memory_plain.go:27-34 (4 key bytes at r10-2 are inside the 2 KiB stack)", maps=[H3])
+# 13-byte 5-tuple keys (K not a multiple of 8): keys backing 52 B, values @0x10009 + 53
+H13 = dict(name="h13", type=1, key_size=13, value_size=8, max_entries=4)
+H13_VALS = 0x10009 + 52 + 1
+
+
+def k13(last):
+    return [A.st(8, 10, -16, 0x01020304), A.st(4, 10, -8, 0x0a0b0c0d), A.st(1, 10, -4, last)]
+
+
+def h13_upd(last, val):
+    return k13(last) + [A.st(8, 10, -24, val), A.mov64_reg(2, 10), A.alu64("add", 2, -16), A.mov64_reg(3, 10),
+                        A.alu64("add", 3, -24), A.ld_map_fd(1, "h13"), A.mov64_imm(4, 0), A.call(2)]
+
+
+def h13_look(last):
+    return k13(last) + [A.mov64_reg(2, 10), A.alu64("add", 2, -16), A.ld_map_fd(1, "h13"), A.call(1)]
+
+
+straight("hash_key13_first_slot", h13_upd(0x55, 9) + h13_look(0x55), H13_VALS, "emulator_linux_map_hash.go:43-97, 152-154",
+         maps=[H13])
+straight("hash_key13_last_byte_distinguishes", h13_upd(0x55, 9) + h13_upd(0x56, 10) + h13_look(0x56) + [A.ldx(8, 0, 0, 0)],
+         10, "emulator_linux_map_hash.go:134-155 (exact key bytes)", maps=[H13])
+straight("hash_key13_miss", h13_upd(0x55, 9) + h13_look(0x57), 0, "emulator_linux_map_hash.go:145-149", maps=[H13])
+# per-CPU hash: values of cpu c @0x10000 + c*(E*S+1), obj after them, keys after the obj
+PH = dict(name="ph", type=5, key_size=4, value_size=4, max_entries=2)
+for cpu in (0, 1):
+    straight(f"percpu_hash_address_cpu{cpu}", h_upd(5, 3, "ph") + h_look(5, "ph"), 0x10000 + cpu * 9,
+             "emulator_linux_map_hash.go:439-500 (values per cpu first), :537-561", vcpus=2, maps=[PH], cpu=cpu)
+for cpu, val in ((0, 9), (1, 0)):
+    straight(f"percpu_hash_value_cpu{cpu}", h_look(5, "ph") + [A.ldx(4, 0, 0, 0)], val,
+             "emulator_linux_map_hash.go:564-612 (shared key table, per-cpu values)", vcpus=2, maps=[PH], cpu=cpu,
+             map_init=[("ph", k(5), k(9), 0)])
+straight("percpu_hash_keys_backing", h_upd(0x01020304, 3, "ph") + [A.ld_imm64(1, 0x10012 + 9), A.ldx(4, 0, 1, 0)], 0x01020304,
+         "emulator_linux_map_hash.go:484-494 (keys after the map object)", vcpus=2, maps=[PH], cpu=1)
+case("percpu_hash_object_not_vmmem", [A.ld_map_fd(1, "ph"), A.ldx(4, 0, 1, 0), A.exit_()], e(status=NOTVMMEM, steps=3, err_pc=2),
+     "inst.go:308-311", vcpus=2, maps=[PH])
+straight("percpu_hash_e2big", h_upd(1, 1, "ph") + h_upd(2, 2, "ph") + h_upd(3, 3, "ph"), 7,
+         "emulator_linux_map_hash.go:584-590", vcpus=2, maps=[PH])
+
 def main():
     out = os.path.join(HERE, "kat.json")
     with open(out, "w") as f:

@@ -26,6 +26,18 @@ class Scenario:
     max_tail_calls: int = 33
 
 
+HASH_TYPES = (1, 13, 18, 19, 24, 25, 26, 28, 29)
+PERCPU_HASH_TYPES = (5, 21)
+
+
+def ncpus(sc: Scenario, m: dict) -> int:
+    return sc.vcpus if m["type"] in (5, 6, 21) else 1
+
+
+def is_hash(m: dict) -> bool:
+    return m["type"] in HASH_TYPES + PERCPU_HASH_TYPES
+
+
 def build_oracle(sc: Scenario):
     import oracle
 
@@ -85,9 +97,14 @@ def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, ta
     out = vm.run_xdp_batch(pids[entry], buf.copy(), off, lens, cpu, headroom, tailroom, ingress, rxq, egress,
                            step_budget)
     out["maps"] = {}
+    out["hash"] = {}
     for m in sc.maps:
-        ncpu = sc.vcpus if m["type"] in (5, 6) else 1
-        out["maps"][m["name"]] = [vm.map_values(mids[m["name"]], c) for c in range(ncpu)]
+        vals = [vm.map_values(mids[m["name"]], c) for c in range(ncpus(sc, m))]
+        out["maps"][m["name"]] = vals
+        if is_hash(m):
+            S = m["value_size"]
+            out["hash"][m["name"]] = {k: [v[s * S:(s + 1) * S] for v in vals]
+                                      for k, s in vm.map_entries(mids[m["name"]])}
     vm.close()
     return out
 
@@ -106,16 +123,24 @@ def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=
     out = res.numpy(len(lens))
     out["pkt"] = batch.pkt_data.cpu().numpy()
     out["maps"] = {}
+    out["hash"] = {}
     for m in sc.maps:
-        ncpu = sc.vcpus if m["type"] in (5, 6) else 1
-        out["maps"][m["name"]] = [maps[m["name"]].Values(c) for c in range(ncpu)]
+        out["maps"][m["name"]] = [maps[m["name"]].Values(c) for c in range(ncpus(sc, m))]
+        if is_hash(m):
+            out["hash"][m["name"]] = maps[m["name"]].Contents()
     out["steps_total"] = vm.LastSteps()
     vm.close()
     return out
 
 
-def assert_same(o, e, check_pkt: bool = True, n: Optional[int] = None):
+def assert_same(o, e, check_pkt: bool = True, n: Optional[int] = None, hash_exact: bool = True,
+                check_steps: bool = True):
+    """hash_exact=False: compare hash maps by key (the slot a key gets depends on the order in
+    which concurrent vCPUs insert; the reference's processPool is no different).
+    check_steps=False: a packet's path (found vs inserted) may depend on that order too."""
     for k in ("r0", "status", "steps", "err_pc"):
+        if k == "steps" and not check_steps:
+            continue
         a = np.asarray(o[k])
         b = np.asarray(e[k])
         if n is not None:
@@ -127,6 +152,13 @@ def assert_same(o, e, check_pkt: bool = True, n: Optional[int] = None):
     if check_pkt:
         assert np.array_equal(o["pkt"][:len(e["pkt"])], e["pkt"][:len(o["pkt"])]), "packet memory differs"
     for name, vals in o["maps"].items():
+        if name in o.get("hash", {}):
+            oh, eh = o["hash"][name], e["hash"][name]
+            assert sorted(oh) == sorted(eh), f"hash map {name}: key sets differ ({len(oh)} vs {len(eh)} keys)"
+            for key in oh:
+                assert oh[key] == eh[key], f"hash map {name} key {key.hex()}: values differ"
+            if not hash_exact:
+                continue
         for c, v in enumerate(vals):
             assert v == e["maps"][name][c], f"map {name} cpu {c} differs"
 
