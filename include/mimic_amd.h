@@ -23,8 +23,10 @@
 #ifndef MIMIC_AMD_H
 #define MIMIC_AMD_H
 
+#if !defined(__HIPCC_RTC__)  /* hipRTC (the JIT kernels) provides these types itself */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -94,8 +96,12 @@ typedef struct {
     int32_t device;             /* HIP device ordinal */
     int32_t vcpu_begin;         /* this engine executes vCPUs [vcpu_begin, vcpu_begin+vcpu_count) */
     int32_t vcpu_count;         /* 0 = all */
-    int32_t reserved;
+    int32_t exec_mode;          /* MIMIC_EXEC_*: 0 = default (env MIMIC_EXEC=interp|jit, else JIT) */
 } mimic_vm_settings;
+
+#define MIMIC_EXEC_DEFAULT 0
+#define MIMIC_EXEC_INTERP 1   /* the batch interpreter kernel (interp.hip) */
+#define MIMIC_EXEC_JIT 2      /* per-program-set kernels generated from the loaded programs, hipRTC-compiled */
 
 typedef struct {
     const char *name;
@@ -185,6 +191,18 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch,
 int mimic_sync(mimic_vm *vm, void *hip_stream);
 /* Executed Step() count of the last completed mimic_run_xdp (sum over packets). */
 int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out);
+
+/* Execution mode the VM resolved to (MIMIC_EXEC_INTERP / MIMIC_EXEC_JIT). */
+int mimic_exec_mode(const mimic_vm *vm);
+/* The kernel the last batch ran on (a JIT VM runs batches whose step budget is below its
+ * loop-free kernels' step bound on the interpreter). */
+int mimic_last_exec(const mimic_vm *vm);
+/* JIT diagnostics (host only, no device): the kernel source generated for raw programs, and a
+ * hipRTC compile check of a source for gfx950. */
+long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, char *buf, size_t cap);
+int mimic_jit_check(const char *src, char *log, size_t cap, size_t *code_size);
+/* Compile the JIT kernel of raw programs into the MIMIC_JIT_CACHE directory (host only). */
+int mimic_jit_prebuild(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs);
 
 #ifdef __cplusplus
 }

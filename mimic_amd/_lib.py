@@ -31,7 +31,7 @@ MAP_F_DATASEC = 1
 class VMSettings(C.Structure):
     _fields_ = [("vcpus", C.c_int32), ("stack_frame_size", C.c_int32), ("stack_frame_count", C.c_int32),
                 ("max_tail_calls", C.c_int32), ("device", C.c_int32), ("vcpu_begin", C.c_int32),
-                ("vcpu_count", C.c_int32), ("reserved", C.c_int32)]
+                ("vcpu_count", C.c_int32), ("exec_mode", C.c_int32)]
 
 
 class MapSpecC(C.Structure):
@@ -67,6 +67,12 @@ EXPORTS = {
     "mimic_map_update": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32]),
     "mimic_map_lookup": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.POINTER(C.c_uint32)]),
     "mimic_map_delete": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "mimic_exec_mode": (C.c_int, [C.c_void_p]),
+    "mimic_last_exec": (C.c_int, [C.c_void_p]),
+    "mimic_jit_source_for": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_char_p,
+                                         C.c_size_t]),
+    "mimic_jit_check": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "mimic_jit_prebuild": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32]),
     "mimic_map_keys": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32)]),
     "mimic_map_entries": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_size_t,
                                     C.POINTER(C.c_uint32)]),

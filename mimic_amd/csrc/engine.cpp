@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -20,6 +21,7 @@
 
 #include "../../include/mimic_amd.h"
 #include "layout.h"
+#include "jit.h"
 
 extern "C" int mimic_launch_xdp(const KParams *kp, hipStream_t st);
 extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
@@ -77,6 +79,13 @@ struct mimic_vm {
     uint32_t lane_steps_cap = 0;
     uint32_t last_lanes = 0;
     hipStream_t last_stream = nullptr;
+    // execution
+    int exec_mode = MIMIC_EXEC_JIT;
+    std::vector<DInsn> h_all;   // predecoded instruction slots of every program (host copy)
+    std::vector<DProg> h_dp;
+    hipFunction_t jit_fn = nullptr;
+    JitInfo jit_info{};
+    int last_exec = 0;          // the kernel the last batch ran on
 };
 
 static int fail(mimic_vm *vm, int code, const char *fmt, ...) {
@@ -274,12 +283,12 @@ static DMap to_dmap(const HostMap &m) {
 
 static bool is_hash(const HostMap &m) { return m.family == FAM_HASH || m.family == FAM_PERCPU_HASH; }
 
-static int upload_tables(mimic_vm *vm) {
-    if (!vm->tables_dirty) return 0;
-    std::vector<DInsn> all;
-    std::vector<DProg> dp;
-    for (size_t pi = 0; pi < vm->progs.size(); pi++) {
-        auto &p = vm->progs[pi];
+// every program's slots with their predecoded facts, concatenated (interpreter + JIT input)
+static void build_host_tables(const std::vector<HostProg> &progs, std::vector<DInsn> &all, std::vector<DProg> &dp) {
+    all.clear();
+    dp.clear();
+    for (size_t pi = 0; pi < progs.size(); pi++) {
+        auto &p = progs[pi];
         DProg d{};
         d.base = (uint32_t)all.size();
         d.n = (uint32_t)p.ins.size();
@@ -292,6 +301,14 @@ static int upload_tables(mimic_vm *vm) {
             all.push_back(x);
         }
     }
+}
+
+static int upload_tables(mimic_vm *vm) {
+    if (!vm->tables_dirty) return 0;
+    build_host_tables(vm->progs, vm->h_all, vm->h_dp);
+    vm->jit_fn = nullptr;
+    std::vector<DInsn> all = vm->h_all;
+    std::vector<DProg> dp = vm->h_dp;
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
     std::vector<DMap> dm;
     for (auto &m : vm->maps) dm.push_back(to_dmap(m));
@@ -353,6 +370,40 @@ static HostRef host_resolve(const mimic_vm *vm, uint32_t a) {
     return R;
 }
 
+// cilium/ebpf v0.9.0 asm.Instruction.Unmarshal of raw slots + the Nop after LD_IMM64 (vm.go:102-112)
+static int decode_program(const uint8_t *raw, uint32_t n_slots, std::vector<DInsn> &out, std::string *err) {
+    out.assign(n_slots, DInsn{0, 0, 0});
+    for (uint32_t i = 0; i < n_slots; i++) {
+        const uint8_t *b = raw + 8ull * i;
+        uint32_t op = b[0], dst = b[1] & 0xf, src = b[1] >> 4;
+        uint16_t off = (uint16_t)(b[2] | (b[3] << 8));
+        int32_t imm;
+        memcpy(&imm, b + 4, 4);
+        DInsn d{};
+        d.w = op | (dst << 8) | (src << 12) | ((uint32_t)off << 16);
+        d.k = (uint64_t)(int64_t)imm;
+        if (op == 0x18) {
+            if (i + 1 >= n_slots) {
+                *err = "64bit immediate is missing second half";
+                return -1;
+            }
+            const uint8_t *c = b + 8;
+            if (c[0] | c[1] | c[2] | c[3]) {
+                *err = "64bit immediate has non-zero fields";
+                return -1;
+            }
+            uint32_t hi;
+            memcpy(&hi, c + 4, 4);
+            d.k = ((uint64_t)hi << 32) | (uint32_t)imm;
+            out[i] = d;
+            out[++i] = DInsn{0, 0, 0};
+            continue;
+        }
+        out[i] = d;
+    }
+    return 0;
+}
+
 extern "C" {
 
 int mimic_abi_version(void) { return MIMIC_ABI_VERSION; }
@@ -375,6 +426,15 @@ int mimic_vm_create(const mimic_vm_settings *settings, mimic_vm **out) {
         return MIMIC_EINVAL;
     }
     if (stack_size(vm) % 8 != 0 || stack_size(vm) > (1u << 20)) {
+        delete vm;
+        return MIMIC_EINVAL;
+    }
+    vm->exec_mode = settings->exec_mode;
+    if (vm->exec_mode == MIMIC_EXEC_DEFAULT) {
+        const char *e = getenv("MIMIC_EXEC");
+        vm->exec_mode = (e && !strcmp(e, "interp")) ? MIMIC_EXEC_INTERP : MIMIC_EXEC_JIT;
+    }
+    if (vm->exec_mode != MIMIC_EXEC_INTERP && vm->exec_mode != MIMIC_EXEC_JIT) {
         delete vm;
         return MIMIC_EINVAL;
     }
@@ -789,33 +849,10 @@ int mimic_program_load(mimic_vm *vm, const char *name, const void *insns, uint32
     if (n_slots >= (1u << MIMIC_PC_BITS) || total >= 0x7fffffffull) return fail(vm, MIMIC_EINVAL, "program too long");
     if (vm->progs.size() >= 65535) return fail(vm, MIMIC_EINVAL, "too many programs");
     hipSetDevice(vm->s.device);
-    const uint8_t *raw = (const uint8_t *)insns;
     HostProg p;
     p.name = name ? name : "";
-    p.ins.resize(n_slots);
-    // cilium/ebpf v0.9.0 asm.Instruction.Unmarshal + the Nop after LD_IMM64 (vm.go:102-112)
-    for (uint32_t i = 0; i < n_slots; i++) {
-        const uint8_t *b = raw + 8ull * i;
-        uint32_t op = b[0], dst = b[1] & 0xf, src = b[1] >> 4;
-        uint16_t off = (uint16_t)(b[2] | (b[3] << 8));
-        int32_t imm;
-        memcpy(&imm, b + 4, 4);
-        DInsn d{};
-        d.w = op | (dst << 8) | (src << 12) | ((uint32_t)off << 16);
-        d.k = (uint64_t)(int64_t)imm;
-        if (op == 0x18) {
-            if (i + 1 >= n_slots) return fail(vm, MIMIC_EINVAL, "64bit immediate is missing second half");
-            const uint8_t *c = b + 8;
-            if (c[0] | c[1] | c[2] | c[3]) return fail(vm, MIMIC_EINVAL, "64bit immediate has non-zero fields");
-            uint32_t hi;
-            memcpy(&hi, c + 4, 4);
-            d.k = ((uint64_t)hi << 32) | (uint32_t)imm;
-            p.ins[i] = d;
-            p.ins[++i] = DInsn{0, 0, 0};
-            continue;
-        }
-        p.ins[i] = d;
-    }
+    std::string derr;
+    if (decode_program((const uint8_t *)insns, n_slots, p.ins, &derr)) return fail(vm, MIMIC_EINVAL, "%s", derr.c_str());
     for (uint32_t r = 0; r < n_relocs; r++) {
         uint32_t s = relocs[r].slot;
         if (s >= n_slots) return fail(vm, MIMIC_EINVAL, "relocation slot %u out of range", s);
@@ -1012,7 +1049,23 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
-    if (mimic_launch_xdp(&kp, st)) return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    bool jit = vm->exec_mode == MIMIC_EXEC_JIT;
+    if (jit && !vm->jit_fn) {
+        std::string log;
+        if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, &vm->jit_info), &vm->jit_fn, &log))
+            return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
+    }
+    if (jit) {  // a loop-free kernel has no budget checks: tiny budgets run on the interpreter
+        const uint64_t bound = mimic_jit_step_bound(vm->jit_info, kp.max_tail_calls);
+        if (bound && kp.budget < bound) jit = false;
+    }
+    vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
+    if (jit) {
+        if (mimic_jit_launch(vm->jit_fn, &kp, st))
+            return fail(vm, MIMIC_EDEVICE, "JIT launch: %s", hipGetErrorString(hipGetLastError()));
+    } else if (mimic_launch_xdp(&kp, st)) {
+        return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    }
     vm->last_lanes = lanes;
     vm->last_stream = st;
     return 0;
@@ -1038,6 +1091,54 @@ int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out) {
     for (uint64_t v : h) t += v;
     *steps_out = t;
     return 0;
+}
+
+int mimic_exec_mode(const mimic_vm *vm) { return vm ? vm->exec_mode : MIMIC_EINVAL; }
+int mimic_last_exec(const mimic_vm *vm) { return vm ? vm->last_exec : MIMIC_EINVAL; }
+
+// The JIT kernel source for a set of raw programs (slots as mimic_program_load takes them; map
+// relocations do not change the code shape).  Returns the source length; copies it if it fits.
+// Host only: no device needed.
+long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, char *buf, size_t cap) {
+    std::vector<HostProg> hp(n_progs);
+    for (uint32_t p = 0; p < n_progs; p++) {
+        std::string err;
+        if (decode_program((const uint8_t *)progs[p], n_slots[p], hp[p].ins, &err)) return MIMIC_EINVAL;
+    }
+    std::vector<DInsn> all;
+    std::vector<DProg> dp;
+    build_host_tables(hp, all, dp);
+    const std::string src = mimic_jit_source(dp, all, nullptr);
+    if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);
+    return (long)src.size();
+}
+
+// Build the JIT kernel for raw programs into the MIMIC_JIT_CACHE directory (host only): a
+// later process that loads the same programs finds the code object there.
+int mimic_jit_prebuild(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs) {
+    std::vector<HostProg> hp(n_progs);
+    for (uint32_t p = 0; p < n_progs; p++) {
+        std::string err;
+        if (decode_program((const uint8_t *)progs[p], n_slots[p], hp[p].ins, &err)) return MIMIC_EINVAL;
+    }
+    std::vector<DInsn> all;
+    std::vector<DProg> dp;
+    build_host_tables(hp, all, dp);
+    std::string log;
+    return mimic_jit_prebuild_source(mimic_jit_source(dp, all, nullptr), &log) ? MIMIC_EINVAL : 0;
+}
+
+// hipRTC-compile a JIT source for gfx950 without loading it (host only).  0 = ok; the compiler
+// log is copied to log (if given).
+int mimic_jit_check(const char *src, char *log, size_t cap, size_t *code_size) {
+    std::string lg;
+    const int rc = mimic_jit_check_source(src ? src : "", &lg, code_size);
+    if (log && cap) {
+        const size_t n = std::min(cap - 1, lg.size());
+        memcpy(log, lg.data(), n);
+        log[n] = 0;
+    }
+    return rc ? MIMIC_EINVAL : 0;
 }
 
 }  // extern "C"

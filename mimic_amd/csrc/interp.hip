@@ -29,704 +29,7 @@
 #include <stdint.h>
 #include <algorithm>
 
-#include "layout.h"
-#include "hashmap.h"
-#include "../../include/mimic_amd.h"
-
-typedef uint16_t __attribute__((aligned(1))) u16u;
-typedef uint32_t __attribute__((aligned(1))) u32u;
-typedef uint64_t __attribute__((aligned(1))) u64u;
-
-#define DEV static __device__ __forceinline__
-
-// Read-only tables are read through the constant address space so that wave-uniform
-// indices become scalar (s_load) fetches through the scalar cache.
-#define CONST_AS __attribute__((address_space(4)))
-template <typename T>
-DEV T cget(const T *p, uint32_t i) {
-    static_assert(sizeof(T) % 4 == 0, "dword-sized tables only");
-    uint32_t w[sizeof(T) / 4];
-#if defined(__HIP_DEVICE_COMPILE__)
-    const CONST_AS uint32_t *q = (const CONST_AS uint32_t *)(p + i);
-#else
-    const uint32_t *q = (const uint32_t *)(p + i);  // host pass: never executed
-#endif
-#pragma unroll
-    for (unsigned k = 0; k < sizeof(T) / 4; k++) w[k] = q[k];
-    T out;
-    __builtin_memcpy(&out, w, sizeof(T));
-    return out;
-}
-
-enum RegionKind : uint32_t { RK_UNRES = 0, RK_STACK = 1, RK_XDP = 2, RK_GLOBAL = 3, RK_NOTVMMEM = 4, RK_NOTDATASEC = 5 };
-
-struct Ref {
-    uint32_t rk, off, limit;
-    int32_t map, sub, prog;
-    uint8_t *ptr;
-};
-
-struct Lane {
-    uint32_t lane;        // private-memory lane index
-    int32_t cpu;
-    uint32_t M;           // packet memory length H+L+T
-    uint8_t *pkt;         // packet memory (device)
-    uint32_t data, data_end, ingress, rxq, egress;
-    uint32_t xdp_dirty;
-    uint64_t sm0, sm1;    // stack words / granules already written in this process
-    uint32_t nframes, tailcalls;
-};
-
-static constexpr int EXIT_SIG = -1;
-
-// ---------------------------------------------------------------------------------------
-// raw loads / stores (unaligned accesses are legal on gfx950 global memory)
-// ---------------------------------------------------------------------------------------
-DEV uint64_t ld_n(const uint8_t *p, uint32_t n) {
-    switch (n) {
-    case 1: return *p;
-    case 2: return *(const u16u *)p;
-    case 4: return *(const u32u *)p;
-    case 8: return *(const u64u *)p;
-    default: {
-        uint64_t v = 0;
-        for (uint32_t i = n; i-- > 0;) v = (v << 8) | p[i];
-        return v;
-    }
-    }
-}
-DEV void st_n(uint8_t *p, uint32_t n, uint64_t v) {
-    switch (n) {
-    case 1: *p = (uint8_t)v; return;
-    case 2: *(u16u *)p = (uint16_t)v; return;
-    case 4: *(u32u *)p = (uint32_t)v; return;
-    case 8: *(u64u *)p = v; return;
-    default:
-        for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * i));
-    }
-}
-
-// private memory: byte offset o of lane l lives at priv + ((o>>3)*priv_lanes + l)*8 + (o&7)
-DEV uint8_t *priv_b(const KParams &kp, uint32_t lane, uint32_t o) {
-    return kp.priv + (((size_t)(o >> 3) * kp.priv_lanes + lane) << 3) + (o & 7);
-}
-DEV uint64_t priv_load(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n) {
-    if ((o & 7) + n <= 8) return ld_n(priv_b(kp, lane, o), n);
-    uint64_t v = 0;
-    for (uint32_t i = 0; i < n; i++) v |= (uint64_t)*priv_b(kp, lane, o + i) << (8 * i);
-    return v;
-}
-DEV void priv_store(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n, uint64_t v) {
-    if ((o & 7) + n <= 8) {
-        st_n(priv_b(kp, lane, o), n, v);
-        return;
-    }
-    for (uint32_t i = 0; i < n; i++) *priv_b(kp, lane, o + i) = (uint8_t)(v >> (8 * i));
-}
-
-// ---------------------------------------------------------------------------------------
-// stack (PlainMemory of StackFrameCount*StackFrameSize zero bytes, vm.go:208-210)
-//
-// The reference gives every process a fresh zeroed stack.  Instead of zeroing 2 KiB per
-// packet, validity is tracked per lane: sm0 has one bit per 8-byte word of the first 512
-// bytes (frames 0 and 1, where programs live), sm1 one bit per (1<<chunk_shift)-byte
-// granule of the rest.  Reads of never-written bytes return 0 without touching memory; the
-// first write to a word stores the whole zero-extended word.
-// ---------------------------------------------------------------------------------------
-#define STK_FINE 512u
-DEV bool stk_valid(const KParams &kp, const Lane &L, uint32_t o) {
-    return o < STK_FINE ? ((L.sm0 >> (o >> 3)) & 1) : ((L.sm1 >> ((o - STK_FINE) >> kp.chunk_shift)) & 1);
-}
-DEV void stk_touch(const KParams &kp, Lane &L, uint32_t o) {
-    if (o < STK_FINE) {
-        const uint32_t q = o >> 3;
-        if (!((L.sm0 >> q) & 1)) {
-            *(uint64_t *)priv_b(kp, L.lane, q << 3) = 0;
-            L.sm0 |= 1ull << q;
-        }
-    } else {
-        const uint32_t c = (o - STK_FINE) >> kp.chunk_shift;
-        if (!((L.sm1 >> c) & 1)) {
-            const uint32_t q0 = (STK_FINE + (c << kp.chunk_shift)) >> 3, nq = (1u << kp.chunk_shift) >> 3;
-            for (uint32_t q = 0; q < nq; q++) *(uint64_t *)priv_b(kp, L.lane, (q0 + q) << 3) = 0;
-            L.sm1 |= 1ull << c;
-        }
-    }
-}
-DEV uint64_t stack_load(const KParams &kp, const Lane &L, uint32_t o, uint32_t n) {
-    if ((o & 7) + n <= 8) {
-        if (!stk_valid(kp, L, o)) return 0;
-        return ld_n(priv_b(kp, L.lane, o), n);
-    }
-    uint64_t v = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t oo = o + i;
-        if (stk_valid(kp, L, oo)) v |= (uint64_t)*priv_b(kp, L.lane, oo) << (8 * i);
-    }
-    return v;
-}
-DEV void stack_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t v) {
-    if ((o & 7) + n <= 8) {
-        if (o < STK_FINE && !((L.sm0 >> (o >> 3)) & 1)) {
-            // first write to this word: store the whole word, zero-extended around the value
-            const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
-            *(uint64_t *)priv_b(kp, L.lane, o & ~7u) = (v & m) << (8 * (o & 7));
-            L.sm0 |= 1ull << (o >> 3);
-            return;
-        }
-        stk_touch(kp, L, o);
-        st_n(priv_b(kp, L.lane, o), n, v);
-        return;
-    }
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t oo = o + i;
-        stk_touch(kp, L, oo);
-        *priv_b(kp, L.lane, oo) = (uint8_t)(v >> (8 * i));
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// xdp_md (24-byte PlainMemory, context_xdp_md.go:56-105)
-// ---------------------------------------------------------------------------------------
-DEV uint32_t xdp_word(const Lane &L, uint32_t w) {
-    uint32_t v = 0;
-    v = w == 0 ? L.data : v;
-    v = w == 1 ? L.data_end : v;
-    v = w == 2 ? L.data : v;      // data_meta == data
-    v = w == 3 ? L.ingress : v;
-    v = w == 4 ? L.rxq : v;
-    v = w == 5 ? L.egress : v;
-    return v;
-}
-DEV uint64_t xdp_load(const KParams &kp, const Lane &L, uint32_t o, uint32_t n) {
-    if (L.xdp_dirty) return priv_load(kp, L.lane, kp.priv_xdp_q * 8 + o, n);
-    uint32_t w0 = o >> 2, sh = (o & 3) * 8;
-    uint64_t lo = (uint64_t)xdp_word(L, w0) | ((uint64_t)xdp_word(L, w0 + 1) << 32);
-    uint64_t hi = xdp_word(L, w0 + 2);
-    uint64_t v = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
-    return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
-}
-DEV void xdp_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t v) {
-    if (!L.xdp_dirty) {
-        for (uint32_t w = 0; w < 3; w++) {
-            uint64_t q = (uint64_t)xdp_word(L, 2 * w) | ((uint64_t)xdp_word(L, 2 * w + 1) << 32);
-            *(uint64_t *)priv_b(kp, L.lane, (kp.priv_xdp_q + w) * 8) = q;
-        }
-        L.xdp_dirty = 1;
-    }
-    priv_store(kp, L.lane, kp.priv_xdp_q * 8 + o, n, v);
-}
-
-// ---------------------------------------------------------------------------------------
-// MemoryController.GetEntry (memory_controller.go:117-145) over the lane's address space
-// ---------------------------------------------------------------------------------------
-DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
-    Ref R;
-    R.rk = RK_UNRES;
-    R.off = 0;
-    R.limit = 0;
-    R.map = -1;
-    R.sub = -1;
-    R.prog = -1;
-    R.ptr = nullptr;
-    const uint32_t St = kp.static_next;
-    if (a >= St) {
-        if (a - St <= kp.stack_size) {
-            R.rk = RK_STACK;
-            R.off = a - St;
-            R.limit = kp.stack_size;
-        } else {
-            const uint32_t P = St + kp.stack_size + 1;
-            if (a - P <= L.M) {
-                R.rk = RK_GLOBAL;
-                R.ptr = L.pkt;
-                R.off = a - P;
-                R.limit = L.M;
-            } else {
-                const uint32_t X = P + L.M + 1;
-                if (a - X <= MIMIC_XDP_MD_SIZE) {
-                    R.rk = RK_XDP;
-                    R.off = a - X;
-                    R.limit = MIMIC_XDP_MD_SIZE;
-                }
-            }
-        }
-        return R;
-    }
-    bool found = false;
-    for (uint32_t s = 0; s < kp.nsegs; s++) {
-        const Seg g = cget(kp.segs, s);
-        if (!found && a >= g.lo && a <= g.hi) {
-            found = true;
-            uint32_t off = a - g.lo;
-            switch (g.kind) {
-            case SEG_PLAIN:
-                R.rk = RK_GLOBAL;
-                R.ptr = kp.arena + g.dev_off;
-                R.off = off;
-                R.limit = g.size;
-                break;
-            case SEG_ARRAY_OBJ:
-                R.map = (int32_t)g.id;
-                R.rk = g.datasec ? RK_GLOBAL : RK_NOTDATASEC;
-                R.ptr = kp.arena + g.dev_off;
-                R.off = off;
-                R.limit = g.size;
-                break;
-            case SEG_MAP_OBJ:
-                R.map = (int32_t)g.id;
-                R.rk = RK_NOTVMMEM;
-                break;
-            case SEG_PROG:
-                R.prog = (int32_t)g.id;
-                R.rk = RK_NOTVMMEM;
-                break;
-            case SEG_PERCPU_ARRAY: {
-                uint32_t c = off / g.period, r = off - c * g.period;
-                R.ptr = kp.arena + g.dev_off + (size_t)c * g.dev_stride;
-                R.limit = g.size;
-                if (r <= 8) { // the sub-array LinuxArrayMap object of cpu c
-                    R.map = (int32_t)g.id;
-                    R.sub = (int32_t)c;
-                    R.rk = g.datasec ? RK_GLOBAL : RK_NOTDATASEC;
-                    R.off = r;
-                } else {
-                    R.rk = RK_GLOBAL;
-                    R.off = r - 9;
-                }
-                break;
-            }
-            case SEG_PERCPU_VALUES: {
-                uint32_t c = off / g.period, r = off - c * g.period;
-                R.rk = RK_GLOBAL;
-                R.ptr = kp.arena + g.dev_off + (size_t)c * g.dev_stride;
-                R.off = r;
-                R.limit = g.size;
-                break;
-            }
-            default: break;
-            }
-        }
-    }
-    return R;
-}
-
-DEV bool is_vmmem(uint32_t rk) { return rk == RK_STACK || rk == RK_XDP || rk == RK_GLOBAL || rk == RK_NOTDATASEC; }
-
-// VMMem.Load/Store after GetEntry (inst.go:298-363): returns 0 or a status
-DEV int mem_load(const KParams &kp, const Lane &L, const Ref &R, uint32_t n, uint64_t &v) {
-    if (R.rk == RK_UNRES) return MIMIC_ERR_MEM_UNRESOLVED;
-    if (R.rk == RK_NOTVMMEM) return MIMIC_ERR_MEM_NOT_VMMEM;
-    if (R.rk == RK_NOTDATASEC) return MIMIC_ERR_MEM_NOT_DATASEC;
-    if ((uint64_t)R.off + n > R.limit) return MIMIC_ERR_MEM_BOUNDS;
-    if (R.rk == RK_STACK) v = stack_load(kp, L, R.off, n);
-    else if (R.rk == RK_XDP) v = xdp_load(kp, L, R.off, n);
-    else v = ld_n(R.ptr + R.off, n);
-    return 0;
-}
-DEV int mem_store(const KParams &kp, Lane &L, const Ref &R, uint32_t n, uint64_t v) {
-    if (R.rk == RK_UNRES) return MIMIC_ERR_MEM_UNRESOLVED;
-    if (R.rk == RK_NOTVMMEM) return MIMIC_ERR_MEM_NOT_VMMEM;
-    if (R.rk == RK_NOTDATASEC) return MIMIC_ERR_MEM_NOT_DATASEC;
-    if ((uint64_t)R.off + n > R.limit) return MIMIC_ERR_MEM_BOUNDS;
-    if (R.rk == RK_STACK) stack_store(kp, L, R.off, n, v);
-    else if (R.rk == RK_XDP) xdp_store(kp, L, R.off, n, v);
-    else st_n(R.ptr + R.off, n, v);
-    return 0;
-}
-// VMMem.Read bounds check only (the bytes are consumed by the caller chunk-wise)
-DEV bool readable(const Ref &R, uint32_t n) {
-    if (!(R.rk == RK_STACK || R.rk == RK_XDP || R.rk == RK_GLOBAL)) return false;
-    return (uint64_t)R.off + n <= R.limit;
-}
-DEV uint64_t region_load(const KParams &kp, const Lane &L, const Ref &R, uint32_t off, uint32_t n) {
-    if (R.rk == RK_STACK) return stack_load(kp, L, off, n);
-    if (R.rk == RK_XDP) return xdp_load(kp, L, off, n);
-    return ld_n(R.ptr + off, n);
-}
-
-// ---------------------------------------------------------------------------------------
-// helpers (emulator_linux_helpers.go)
-// ---------------------------------------------------------------------------------------
-
-// regToMap, emulator_linux_helpers.go:415-447
-DEV bool reg_to_map(const KParams &kp, const Lane &L, uint64_t v, int32_t &map, int32_t &sub) {
-    Ref R = resolve(kp, L, (uint32_t)v);
-    if (R.rk == RK_UNRES) return false;
-    if (R.map >= 0) {
-        map = R.map;
-        sub = R.sub;
-        return true;
-    }
-    if (R.rk == RK_STACK || R.rk == RK_XDP || R.rk == RK_GLOBAL) {
-        uint64_t a;
-        if (mem_load(kp, L, R, 4, a)) return false;
-        Ref R2 = resolve(kp, L, (uint32_t)a);
-        if (R2.map >= 0) {
-            map = R2.map;
-            sub = R2.sub;
-            return true;
-        }
-    }
-    return false;
-}
-
-// array-family value address for key k; sub = concrete cpu sub-array (or -1 for a plain array)
-DEV uint32_t array_value_addr(const DMap &m, int32_t sub, uint32_t k) {
-    if (k >= m.max_entries) return 0;
-    uint32_t base = m.backing_addr + (sub > 0 ? (uint32_t)sub * m.addr_period : 0u);
-    return base + k * m.value_size;
-}
-DEV uint8_t *array_value_ptr(const KParams &kp, const DMap &m, int32_t sub, uint32_t k) {
-    return kp.arena + m.dev_off + (sub > 0 ? (size_t)sub * m.dev_stride : 0) + (size_t)k * m.value_size;
-}
-
-// memmove of n bytes from a VM region into the arena (map update, emulator_linux_map_array.go:112)
-DEV void copy_into(const KParams &kp, const Lane &L, const Ref &src, uint8_t *dst, uint32_t n) {
-    bool backward = src.rk == RK_GLOBAL && src.ptr + src.off < dst && dst < src.ptr + src.off + n;
-    if (!backward) {
-        for (uint32_t o = 0; o < n; o += 8) {
-            uint32_t c = n - o < 8 ? n - o : 8;
-            st_n(dst + o, c, region_load(kp, L, src, src.off + o, c));
-        }
-    } else {
-        for (uint32_t e = n; e > 0;) {
-            uint32_t c = e < 8 ? e : 8;
-            e -= c;
-            st_n(dst + e, c, region_load(kp, L, src, src.off + e, c));
-        }
-    }
-}
-
-// hash-map key words: derefMapKey (emulator_linux_helpers.go:449-471) copies the key out of VM
-// memory once, into the lane's key scratch in private memory (qword-interleaved like the stack)
-struct KeyPriv {
-    const uint64_t *p;
-    uint32_t stride;
-    __device__ uint64_t word(uint32_t q) const { return p[(size_t)q * stride]; }
-};
-DEV KeyPriv key_fetch(const KParams &kp, const Lane &L, const Ref &R, uint32_t K) {
-    uint64_t *p = (uint64_t *)kp.priv + (size_t)kp.priv_key_q * kp.priv_lanes + L.lane;
-    for (uint32_t q = 0; q * 8 < K; q++) {
-        const uint32_t c = K - q * 8 < 8 ? K - q * 8 : 8;
-        p[(size_t)q * kp.priv_lanes] = region_load(kp, L, R, R.off + q * 8, c);
-    }
-    return KeyPriv{p, kp.priv_lanes};
-}
-// values[cpu] + idx*S (hash: one values backing; per-CPU hash: cpu-major backings)
-DEV uint32_t hash_value_addr(const DMap &m, int32_t cpu, uint32_t idx) {
-    return m.backing_addr + (m.family == FAM_PERCPU_HASH ? (uint32_t)cpu * m.addr_period : 0u) + idx * m.value_size;
-}
-DEV uint8_t *hash_value_ptr(const KParams &kp, const DMap &m, int32_t cpu, uint32_t idx) {
-    return kp.arena + m.dev_off + (m.family == FAM_PERCPU_HASH ? (size_t)cpu * m.dev_stride : 0) + (size_t)idx * m.value_size;
-}
-
-struct HelperOut {
-    int st;          // 0 or status
-    uint64_t r0;     // new R0 (if set_r0)
-    bool set_r0;
-    bool tail;       // tail call taken
-    uint32_t new_prog;
-};
-
-// resolve the concrete array (sub-array) a LinuxMap reference names for this process
-// returns 0 ok, or MIMIC_ERR_HELPER_MAP_OP for per-CPU cpuid errors
-DEV int array_target(const DMap &m, int32_t sub, int32_t cpu, int32_t &which) {
-    if (m.family == FAM_PERCPU_ARRAY && sub < 0) {
-        if (cpu < 0 || (uint32_t)cpu >= m.ncpu) return MIMIC_ERR_HELPER_MAP_OP;
-        which = cpu;
-    } else {
-        which = sub;
-    }
-    return 0;
-}
-
-DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint64_t r2) { // :477-504
-    HelperOut o = {0, 0, false, false, 0};
-    int32_t mid, sub;
-    if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
-    Ref K = resolve(kp, L, (uint32_t)r2);
-    if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
-    if (m.family == FAM_ARRAY || m.family == FAM_PERCPU_ARRAY) {
-        int32_t which;
-        if (array_target(m, sub, L.cpu, which)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-        if (m.key_size != 4) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-        uint32_t k = (uint32_t)region_load(kp, L, K, K.off, 4);
-        o.r0 = array_value_addr(m, which, k);
-        o.set_r0 = true;
-        return o;
-    }
-    // LinuxHashMap.Lookup :134-155 / LinuxPerCPUHashMap.Lookup :537-561
-    if (m.family == FAM_PERCPU_HASH && (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-    const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
-    const int32_t idx = h_find(h_table(kp.arena, m), ks, h_hash(ks, m.key_size), nullptr);
-    o.r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
-    o.set_r0 = true;
-    return o;
-}
-
-DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint64_t r2, uint64_t r3) { // :506-555
-    HelperOut o = {0, 0, false, false, 0};
-    int32_t mid, sub;
-    if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
-    Ref K = resolve(kp, L, (uint32_t)r2);
-    if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
-    Ref V = resolve(kp, L, (uint32_t)r3);
-    if (!readable(V, m.value_size)) { o.st = MIMIC_ERR_HELPER_VALUE; return o; }
-    if (m.family == FAM_ARRAY || m.family == FAM_PERCPU_ARRAY) {
-        int32_t which;
-        if (array_target(m, sub, L.cpu, which)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-        if (m.key_size != 4) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-        uint32_t k = (uint32_t)region_load(kp, L, K, K.off, 4);
-        if (k >= m.max_entries) {
-            o.r0 = 7; // syscall.E2BIG returned as uint64(errno) (Q9)
-            o.set_r0 = true;
-            return o;
-        }
-        copy_into(kp, L, V, array_value_ptr(kp, m, which, k), m.value_size);
-        o.r0 = 0;
-        o.set_r0 = true;
-        return o;
-    }
-    // LinuxHashMap.Update :158-203 / LinuxPerCPUHashMap.Update :564-612
-    if (m.family == FAM_PERCPU_HASH && (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-    const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
-    const uint64_t h = h_hash(ks, m.key_size);
-    const HT t = h_table(kp.arena, m);
-    int32_t idx = h_find(t, ks, h, nullptr);
-    bool inserted = false;
-    if (idx < 0) {
-        // a new key: the lanes of this wave that insert take the stripe locks one at a time
-        uint64_t need = __ballot(1);
-        const uint32_t me = __lane_id();
-        while (need) {
-            if (me == (uint32_t)__builtin_ctzll(need)) idx = h_insert_locked(t, ks, h, &inserted);
-            need &= need - 1;
-        }
-    }
-    if (idx < 0) {
-        o.r0 = 7; // syscall.E2BIG: the freelist is empty
-        o.set_r0 = true;
-        return o;
-    }
-    if (inserted) { // keys.Write(keyOff, key) (the bytes of a found key are already there)
-        uint8_t *kd = kp.arena + m.keys_dev_off + (size_t)idx * m.key_size;
-        for (uint32_t q = 0; q * 8 < m.key_size; q++) {
-            const uint32_t c = m.key_size - q * 8 < 8 ? m.key_size - q * 8 : 8;
-            st_n(kd + q * 8, c, ks.word(q));
-        }
-    }
-    // re-resolved here (pure) so that no Ref stays live across the insert
-    copy_into(kp, L, resolve(kp, L, (uint32_t)r3), hash_value_ptr(kp, m, L.cpu, (uint32_t)idx), m.value_size);
-    o.r0 = 0;
-    o.set_r0 = true;
-    return o;
-}
-
-DEV HelperOut helper_delete(const KParams &kp, const Lane &L, uint64_t r1, uint64_t r2) { // :557-586
-    HelperOut o = {0, 0, false, false, 0};
-    int32_t mid, sub;
-    if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
-    if (m.family == FAM_ARRAY || m.family == FAM_PERCPU_ARRAY) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
-    Ref K = resolve(kp, L, (uint32_t)r2);
-    if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
-    // LinuxHashMap.Delete :225-255 / LinuxPerCPUHashMap.Delete :634-664 (absent key: nil)
-    const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
-    const uint64_t h = h_hash(ks, m.key_size);
-    const HT t = h_table(kp.arena, m);
-    uint64_t need = __ballot(1);
-    const uint32_t me = __lane_id();
-    while (need) {
-        if (me == (uint32_t)__builtin_ctzll(need)) h_delete_locked(t, ks, h);
-        need &= need - 1;
-    }
-    o.r0 = 0;
-    o.set_r0 = true;
-    return o;
-}
-
-DEV HelperOut helper_tailcall(const KParams &kp, const Lane &L, uint64_t r2, uint64_t r3) { // :649-738
-    HelperOut o = {0, 0, false, false, 0};
-    if (L.tailcalls >= kp.max_tail_calls) {
-        o.r0 = (uint64_t)(int64_t)-1; // -EPERM
-        o.set_r0 = true;
-        return o;
-    }
-    int32_t mid, sub;
-    if (!reg_to_map(kp, L, r2, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
-    if (m.type != MIMIC_MAP_PROG_ARRAY || m.key_size != 4 || m.family != FAM_ARRAY) {
-        o.st = MIMIC_ERR_HELPER_TAILCALL;
-        return o;
-    }
-    uint32_t slot = array_value_addr(m, -1, (uint32_t)r3);
-    Ref R = resolve(kp, L, slot);
-    if (R.rk == RK_UNRES) {
-        o.r0 = (uint64_t)(int64_t)-22; // -EINVAL
-        o.set_r0 = true;
-        return o;
-    }
-    if (!is_vmmem(R.rk)) { o.st = MIMIC_ERR_HELPER_TAILCALL; return o; }
-    uint64_t pa = 0;
-    if (mem_load(kp, L, R, 4, pa)) pa = 0; // the load error is ignored (:707-710)
-    Ref P = resolve(kp, L, (uint32_t)pa);
-    if (P.prog < 0) {
-        o.r0 = (uint64_t)(int64_t)-22;
-        o.set_r0 = true;
-        return o;
-    }
-    o.tail = true;
-    o.new_prog = (uint32_t)P.prog;
-    return o;
-}
-
-// emulatedLinuxHelpers classification (emulator_linux_helpers.go:28-204)
-DEV int helper_class(int32_t n) {
-    // 2 = linuxHelperCantEmulate, 1 = emulated by the reference, 0 = nil
-    switch (n) {
-    case 4: case 14: case 15: case 16: case 17: case 22: case 24: case 27: case 35: case 36: case 42:
-    case 45: case 46: case 47: case 55: case 56: case 67: case 69: case 80: case 112: case 113: case 114:
-    case 115: case 119: case 120: case 122: case 123: case 128: case 129: case 141: case 148: case 151:
-        return 2;
-    case 1: case 2: case 3: case 5: case 7: case 8: case 9: case 12: case 25: case 38: case 65: case 87:
-    case 88: case 89: case 125: case 160:
-        return 1;
-    default:
-        return 0;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// wave-wide minimum of a 32-bit key: DPP within each 16-lane row, then 4 readlanes
-// ---------------------------------------------------------------------------------------
-DEV uint32_t dpp_min(uint32_t v, int ctrl) {
-    uint32_t o;
-    switch (ctrl) {
-    case 0: o = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, 0xb1, 0xf, 0xf, false); break;
-    case 1: o = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, 0x4e, 0xf, 0xf, false); break;
-    case 2: o = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, 0x141, 0xf, 0xf, false); break;
-    default: o = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, 0x140, 0xf, 0xf, false); break;
-    }
-    return v < o ? v : o;
-}
-DEV uint32_t wave_min(uint32_t v) {
-    v = dpp_min(v, 0); // quad_perm [1,0,3,2]
-    v = dpp_min(v, 1); // quad_perm [2,3,0,1]
-    v = dpp_min(v, 2); // row_half_mirror
-    v = dpp_min(v, 3); // row_mirror
-    uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-    uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-    uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
-    uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-    a = a < b ? a : b;
-    c = c < d ? c : d;
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(a < c ? a : c));  // provably wave-uniform
-}
-
-// ---------------------------------------------------------------------------------------
-// conditional jumps (inst_gen.go:227-605, inst.go:205-241)
-// ---------------------------------------------------------------------------------------
-DEV bool jcond(uint32_t jop, uint64_t d, uint64_t s, bool w32) {
-    if (w32) {
-        uint32_t a = (uint32_t)d, b = (uint32_t)s;
-        int32_t sa = (int32_t)a, sb = (int32_t)b;
-        switch (jop) {
-        case 0x10: return a == b;
-        case 0x20: return a > b;
-        case 0x30: return a >= b;
-        case 0x40: return (a & b) == 0; // Q3 inverted JSET
-        case 0x50: return a != b;
-        case 0x60: return sa > sb;
-        case 0x70: return sa >= sb;
-        case 0xa0: return a < b;
-        case 0xb0: return a <= b;
-        case 0xc0: return sa < sb;
-        default: return sa <= sb; // 0xd0
-        }
-    }
-    int64_t sa = (int64_t)d, sb = (int64_t)s;
-    switch (jop) {
-    case 0x10: return d == s;
-    case 0x20: return d > s;
-    case 0x30: return d >= s;
-    case 0x40: return (d & s) == 0;
-    case 0x50: return d != s;
-    case 0x60: return sa > sb;
-    case 0x70: return sa >= sb;
-    case 0xa0: return d < s;
-    case 0xb0: return d <= s;
-    case 0xc0: return sa < sb;
-    default: return sa <= sb;
-    }
-}
-
-DEV bool is_cond_jop(uint32_t jop) {
-    switch (jop) {
-    case 0x10: case 0x20: case 0x30: case 0x40: case 0x50: case 0x60: case 0x70:
-    case 0xa0: case 0xb0: case 0xc0: case 0xd0:
-        return true;
-    default:
-        return false;
-    }
-}
-
-DEV uint32_t size_bytes(uint32_t op) {
-    switch (op & 0x18) {
-    case 0x00: return 4;
-    case 0x08: return 2;
-    case 0x10: return 1;
-    default: return 8;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// fast ALU ops (inst_gen.go:7-225, inst.go:86-136); the host only routes valid forms here
-// ---------------------------------------------------------------------------------------
-DEV uint64_t alu64(uint32_t hi, uint64_t d, uint64_t x) {
-    switch (hi) {
-    case 0x00: return d + x;
-    case 0x10: return d - x;
-    case 0x20: return d * x;
-    case 0x30: return d / x;   // K form, x != 0 (predecoded)
-    case 0x40: return d | x;
-    case 0x50: return d & x;
-    case 0x60: return x >= 64 ? 0 : d << x;
-    case 0x70: return x >= 64 ? 0 : d >> x;
-    case 0x80: return (uint64_t)(-(int64_t)d);
-    case 0x90: return d % x;
-    case 0xa0: return d ^ x;
-    case 0xb0: return x;
-    default: { // 0xc0 ARSH (x >= 0)
-        const int64_t a = (int64_t)d;
-        return (uint64_t)(x >= 64 ? (a < 0 ? -1 : 0) : (a >> x));
-    }
-    }
-}
-DEV uint64_t alu32(uint32_t hi, uint64_t d, uint64_t x) {
-    const uint32_t a = (uint32_t)d, b = (uint32_t)x;
-    switch (hi) {
-    case 0x00: return (uint32_t)(a + b);
-    case 0x10: return (uint32_t)(a - b);
-    case 0x20: return (uint32_t)(a * b);
-    case 0x30: return a / b;
-    case 0x40: return a | b;
-    case 0x50: return a & b;
-    case 0x60: return b >= 32 ? 0 : (uint32_t)(a << b);
-    case 0x70: return b >= 32 ? 0 : a >> b;
-    case 0x80: return (uint64_t)(int64_t)(int32_t)(0u - a);          // Q6: sign-extends
-    case 0x90: return a % b;
-    case 0xa0: return a ^ b;
-    case 0xb0: return b;
-    default: { // ARSH: the 64-bit shift count is not truncated; result sign-extends (Q5/Q6)
-        const int32_t sa = (int32_t)a;
-        return (uint64_t)(int64_t)(x >= 32 ? (sa < 0 ? -1 : 0) : (sa >> x));
-    }
-    }
-}
-
+#include "runtime.h"
 // ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------

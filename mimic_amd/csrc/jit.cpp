@@ -1,0 +1,562 @@
+// jit.cpp -- per-program-set JIT: the loaded eBPF programs become one straight-line HIP
+// kernel (compiled with hipRTC for gfx950 at the first run after a program load).
+//
+// The interpreter (interp.hip) pays for generality on every eBPF step. Each step runs:
+//   * a wave-wide minimum-PC reduction;
+//   * a scalar instruction fetch;
+//   * a dispatch switch;
+//   * LDS register traffic.
+// Here every instruction of every program is emitted once as HIP statements. Its registers,
+// offsets, immediates and opcode are compile-time constants, and r0..r10 are plain 64-bit
+// locals (VGPRs). Control flow is `goto` between basic blocks, and the GPU's own
+// divergence/reconvergence (EXEC masks) replaces min-PC scheduling. Semantics are those of
+// the interpreter, statement for statement: the same runtime.h functions resolve memory, run
+// the helpers and compute ALU/jump results, and the same predecoded error facts (layout.h
+// aux) decide what each slot does.
+//
+// Step accounting is exact per lane: `steps++` per instruction. The step budget (Run's
+// deadline) is checked once per basic block: a block whose end would exceed the budget is
+// executed by a "careful" copy that checks before every instruction.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <unistd.h>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/mimic_amd.h"
+#include "layout.h"
+#include "jit.h"
+
+namespace {
+
+#include "jit_headers.inc"  // kJitHeaderNames / kJitHeaderSrc / kJitHeaderCount (generated at build)
+
+struct Emitter {
+    std::string s;
+    void line(const char *fmt, ...) __attribute__((format(printf, 2, 3))) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        s += buf;
+        s += '\n';
+    }
+};
+
+struct ProgView {
+    uint32_t id, n, base;  // base: first slot in the concatenated instruction table (kp.insns)
+    const DInsn *ins;
+};
+
+uint32_t insn_op(const DInsn &x) { return x.w & 0xff; }
+uint32_t insn_dst(const DInsn &x) { return (x.w >> 8) & 0xf; }
+uint32_t insn_src(const DInsn &x) { return (x.w >> 12) & 0xf; }
+int32_t insn_off(const DInsn &x) { return (int16_t)(x.w >> 16); }
+
+// does the slot end a basic block (control leaves other than by falling through)?
+bool ends_block(const DInsn &x) {
+    switch (AUX_H(x.aux)) {
+    case H_ERR: case H_JA: case H_JCC: case H_EXIT: case H_CALL_LOCAL: return true;
+    case H_CALL: return (uint32_t)x.k == 12;  // a tail call may switch programs
+    default: return false;
+    }
+}
+
+int64_t jump_target(const DInsn &x, int64_t i) {
+    return insn_op(x) == 0x85 ? i + (int64_t)(int32_t)(uint32_t)x.k : i + insn_off(x) + 1;
+}
+
+class Gen {
+  public:
+    Gen(const std::vector<ProgView> &progs) : P(progs) {
+        for (auto &p : P)
+            for (uint32_t i = 0; i < p.n; i++) {
+                const DInsn &x = p.ins[i];
+                if (AUX_H(x.aux) == H_CALL && (uint32_t)x.k == 12) any_tail = true;
+                if (AUX_H(x.aux) == H_CALL_LOCAL) any_local = true;
+            }
+        // a frame pushed before a tail call returns into the NEW program (the saved PC is an
+        // index, vm.go:256-257): then any slot can be a return site
+        all_leaders = any_tail && any_local;
+        // loop-free programs without BPF-to-BPF calls run at most n steps per program (and at
+        // most MaxTailCalls+1 programs): with a budget at least that large, no block needs the
+        // careful copy (the engine falls back to the interpreter for smaller budgets)
+        bool back = false;
+        uint32_t mx = 0;
+        for (auto &p : P) {
+            mx = std::max(mx, p.n);
+            for (uint32_t i = 0; i < p.n; i++) {
+                const DInsn &x = p.ins[i];
+                const uint32_t h = AUX_H(x.aux);
+                if ((h == H_JA || h == H_JCC) && (x.aux & AUX_JT_OK) && jump_target(x, i) <= (int64_t)i) back = true;
+            }
+        }
+        careful_copies = back || any_local;
+        max_n = mx;
+    }
+
+    bool careful_copies = true;
+    uint32_t max_n = 0;
+    bool has_tail() const { return any_tail; }
+
+    std::string source() {
+        E.line("#include \"runtime.h\"");
+        E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
+        E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(KParams kp) {");
+        E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
+        E.line("  if (g >= kp.lanes) return;");
+        E.line("  Lane L;");
+        E.line("  L.lane = g;");
+        E.line("  L.cpu = (int32_t)(kp.vcpu_begin + g);");
+        E.line("  uint32_t ex_begin = 0, ex_count = 0;");
+        E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = kp.sched_start[g]; ex_count = kp.sched_start[g + 1] - ex_begin; }");
+        E.line("  uint64_t lane_steps = 0;");
+        E.line("  const uint32_t P = kp.static_next + kp.stack_size + 1;");
+        E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
+        E.line("    uint32_t i;");
+        E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
+        E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + g; if (ii >= kp.n) break; i = (uint32_t)ii; }");
+        E.line("    else { if (j >= ex_count) break; i = kp.sched_pkts[ex_begin + j]; }");
+        // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
+        E.line("    const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;");
+        E.line("    const uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;");
+        E.line("    const uint32_t len = kp.pkt_len[i];");
+        E.line("    L.pkt = kp.pkt_data + kp.pkt_off[i];");
+        E.line("    L.M = H + len + T;");
+        E.line("    for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;");
+        E.line("    for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;");
+        E.line("    L.data = P + H;");
+        E.line("    L.data_end = P + H + len;");
+        E.line("    L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);");
+        E.line("    L.rxq = (uint32_t)(kp.rxq_arr ? kp.rxq_arr[i] : kp.rxq);");
+        E.line("    L.egress = (uint32_t)(kp.egress_arr ? kp.egress_arr[i] : kp.egress);");
+        E.line("    L.sm0 = 0; L.sm1 = 0; L.xdp_dirty = 0; L.nframes = 0; L.tailcalls = 0;");
+        E.line("    uint64_t r0 = 0, r1 = P + L.M + 1, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0, r9 = 0;");
+        E.line("    uint64_t r10 = kp.static_next + kp.frame_size;");
+        E.line("    uint32_t steps = 0;");
+        E.line("    int st_ = 0;");
+        E.line("    int32_t epc_ = -1;");
+        E.line("    switch (kp.entry_prog) {");
+        for (auto &p : P) {
+            if (p.n == 0) E.line("    case %u: steps = 1; TERM(MIMIC_ERR_PC_OOB, 0);", p.id);  // vm.go:297-299
+            else E.line("    case %u: goto P%u_0;", p.id, p.id);
+        }
+        E.line("    default: TERM(MIMIC_ERR_PC_OOB, 0);");
+        E.line("    }");
+        for (auto &p : P) program(p);
+        E.line("  L_term:");
+        E.line("    if (kp.r0) kp.r0[i] = r0;");
+        E.line("    if (kp.status) kp.status[i] = (uint8_t)st_;");
+        E.line("    if (kp.steps) kp.steps[i] = steps;");
+        E.line("    if (kp.err_pc) kp.err_pc[i] = epc_;");
+        E.line("    lane_steps += steps;");
+        E.line("  }");
+        E.line("  if (kp.lane_steps) kp.lane_steps[g] = lane_steps;");
+        E.line("}");
+        return E.s;
+    }
+
+  private:
+    const std::vector<ProgView> &P;
+    Emitter E;
+    bool any_tail = false, any_local = false, all_leaders = false;
+
+    void program(const ProgView &p) {
+        if (p.n == 0) return;
+        std::set<uint32_t> lead = {0};
+        for (uint32_t i = 0; i < p.n; i++) {
+            const DInsn &x = p.ins[i];
+            const uint32_t h = AUX_H(x.aux);
+            if ((h == H_JA || h == H_JCC || h == H_CALL_LOCAL) && (x.aux & AUX_JT_OK))
+                lead.insert((uint32_t)jump_target(x, i));
+            if (ends_block(x) && i + 1 < p.n) lead.insert(i + 1);
+            if (all_leaders) lead.insert(i);
+        }
+        std::vector<uint32_t> L(lead.begin(), lead.end());
+        for (int careful = 0; careful < (careful_copies ? 2 : 1); careful++) {
+            for (size_t b = 0; b < L.size(); b++) {
+                const uint32_t s = L[b], e = b + 1 < L.size() ? L[b + 1] : p.n;
+                if (!careful) {
+                    E.line("  P%u_%u:", p.id, s);
+                    if (careful_copies) E.line("    if (steps + %uu > kp.budget) goto C%u_%u;", e - s, p.id, s);
+                } else {
+                    E.line("  C%u_%u:", p.id, s);
+                }
+                for (uint32_t i = s; i < e; i++) {
+                    if (careful) E.line("    if (steps == kp.budget) TERM(MIMIC_ERR_STEP_LIMIT, %u);", i);
+                    insn(p, i);
+                }
+                // falling off the end of the block
+                const DInsn &last = p.ins[e - 1];
+                if (!ends_block(last) || AUX_H(last.aux) == H_JCC ||
+                    (AUX_H(last.aux) == H_CALL && (uint32_t)last.k == 12))
+                    fall(p, e - 1);
+            }
+        }
+    }
+
+    // PC+1 after slot i (vm.go:328-337)
+    void fall(const ProgView &p, uint32_t i) {
+        if (p.ins[i].aux & AUX_FALL_OK) E.line("    goto P%u_%u;", p.id, i + 1);
+        else E.line("    TERM(MIMIC_ERR_PC_OOB, %u);", i);
+    }
+
+    // a taken jump / BPF-to-BPF call from slot i
+    void jump(const ProgView &p, uint32_t i) {
+        const DInsn &x = p.ins[i];
+        const int64_t t = jump_target(x, i);
+        if (x.aux & AUX_JT_OK) E.line("goto P%u_%u;", p.id, (uint32_t)t);
+        else if (x.aux & AUX_JT_NEG)  // the next Step indexes Instructions[-x] (vm.go:300)
+            E.line("{ if (steps == kp.budget) TERM(MIMIC_ERR_STEP_LIMIT, %" PRId64 "); steps++; TERM(MIMIC_PANIC_PC, %" PRId64 "); }", t, t);
+        else E.line("TERM(MIMIC_ERR_PC_OOB, %u);", i);
+    }
+
+    static std::string reg(uint32_t r) { return "r" + std::to_string(r); }
+    static std::string imm(uint64_t k) {
+        char b[40];
+        snprintf(b, sizeof b, "0x%" PRIx64 "ull", k);
+        return b;
+    }
+    std::string xop(const DInsn &x) { return (x.aux & AUX_X) ? reg(insn_src(x)) : imm(x.k); }
+    static std::string addr(uint32_t r, int32_t off) {
+        return "(uint32_t)(" + reg(r) + " + " + imm((uint64_t)(int64_t)off) + ")";
+    }
+
+    void insn(const ProgView &p, uint32_t i) {
+        const DInsn &x = p.ins[i];
+        const uint32_t op = insn_op(x), d = insn_dst(x), s = insn_src(x);
+        const int32_t off = insn_off(x);
+        const uint32_t h = AUX_H(x.aux);
+        if (h == H_LDIMM) E.line("    // %u: op 0x%02x dst r%u src r%u (imm from the table)", i, op, d, s);
+        else E.line("    // %u: op 0x%02x dst r%u src r%u off %d imm %" PRId64, i, op, d, s, off, (int64_t)x.k);
+        E.line("    steps++;");
+        switch (h) {
+        case H_NOP:
+            break;
+        case H_ERR:
+            E.line("    TERM(%u, %u);", AUX_ARG(x.aux), i);
+            break;
+        case H_ALU64:
+        case H_ALU32:
+            E.line("    %s = %s(0x%02xu, %s, %s);", reg(d).c_str(), h == H_ALU64 ? "alu64" : "alu32", op & 0xf0,
+                   reg(d).c_str(), xop(x).c_str());
+            break;
+        case H_LDIMM:  // read from the table: map relocations do not change the kernel source
+            E.line("    %s = cget(kp.insns, %uu).k;", reg(d).c_str(), p.base + i);
+            break;
+        case H_JA:
+            E.s += "    ";
+            jump(p, i);
+            break;
+        case H_JCC:
+            E.s += "    if (jcond(";
+            E.s += imm(AUX_ARG(x.aux)) + ", " + reg(d) + ", " + xop(x) + ((x.aux & AUX_W32) ? ", true)) " : ", false)) ");
+            jump(p, i);
+            break;
+        case H_LDX:
+            E.line("    { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, %s), %uu, v_); if (s_) TERM(s_, %u); %s = v_; }",
+                   addr(s, off).c_str(), AUX_SZ(x.aux), i, reg(d).c_str());
+            break;
+        case H_ST:
+        case H_STX:
+            E.line("    { const int s_ = mem_store(kp, L, resolve(kp, L, %s), %uu, %s); if (s_) TERM(s_, %u); }",
+                   addr(d, off).c_str(), AUX_SZ(x.aux), h == H_STX ? reg(s).c_str() : imm(x.k).c_str(), i);
+            break;
+        case H_EXIT:  // inst.go:277-296
+            if (!any_local) {
+                E.line("    TERM(MIMIC_OK, -1);");
+                break;
+            }
+            E.line("    if (L.nframes > 0) {");
+            E.line("      L.nframes--;");
+            E.line("      const uint32_t fq = kp.priv_frame_q + L.nframes * MIMIC_FRAME_QWORDS;");
+            E.line("      const uint32_t spc = (uint32_t)priv_load(kp, L.lane, fq * 8, 8);");
+            E.line("      r6 = priv_load(kp, L.lane, (fq + 1) * 8, 8);");
+            E.line("      r7 = priv_load(kp, L.lane, (fq + 2) * 8, 8);");
+            E.line("      r8 = priv_load(kp, L.lane, (fq + 3) * 8, 8);");
+            E.line("      r9 = priv_load(kp, L.lane, (fq + 4) * 8, 8);");
+            E.line("      r10 = r10 - kp.frame_size;");
+            E.line("      if (%uu <= spc + 1) TERM(MIMIC_ERR_PC_OOB, %u);", p.n, i);
+            E.line("      switch (spc + 1) {");
+            for (uint32_t a = 1; a < p.n; a++) {
+                const DInsn &c = p.ins[a - 1];
+                if (all_leaders || AUX_H(c.aux) == H_CALL_LOCAL) E.line("      case %u: goto P%u_%u;", a, p.id, a);
+            }
+            E.line("      default: TERM(MIMIC_ERR_ENGINE_HELPER, %u);", i);
+            E.line("      }");
+            E.line("    }");
+            E.line("    TERM(MIMIC_OK, -1);");
+            break;
+        case H_CALL_LOCAL:  // BPF-to-BPF, inst.go:244-258
+            E.line("    if (L.nframes >= MIMIC_MAX_FRAMES) TERM(MIMIC_ERR_CALL_DEPTH, %u);", i);
+            E.line("    { const uint32_t fq = kp.priv_frame_q + L.nframes * MIMIC_FRAME_QWORDS;");
+            E.line("      priv_store(kp, L.lane, fq * 8, 8, %uull);", i);
+            E.line("      priv_store(kp, L.lane, (fq + 1) * 8, 8, r6);");
+            E.line("      priv_store(kp, L.lane, (fq + 2) * 8, 8, r7);");
+            E.line("      priv_store(kp, L.lane, (fq + 3) * 8, 8, r8);");
+            E.line("      priv_store(kp, L.lane, (fq + 4) * 8, 8, r9);");
+            E.line("      L.nframes++;");
+            E.line("      r10 = r10 + kp.frame_size; }");
+            E.s += "    ";
+            jump(p, i);
+            break;
+        case H_CALL:
+            helper(p, i);
+            break;
+        default:
+            slow(p, i);
+            break;
+        }
+    }
+
+    void helper(const ProgView &p, uint32_t i) {  // emulator_linux_.go:125-194
+        const DInsn &x = p.ins[i];
+        switch ((uint32_t)x.k) {
+        case 1:
+            E.line("    { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
+            break;
+        case 2:
+            E.line("    { const HelperOut ho = helper_update(kp, L, r1, r2, r3); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
+            break;
+        case 3:
+            E.line("    { const HelperOut ho = helper_delete(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
+            break;
+        case 8:
+            E.line("    r0 = (uint64_t)(int64_t)L.cpu;");
+            break;
+        case 12:
+            E.line("    { const HelperOut ho = helper_tailcall(kp, L, r2, r3); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0;", i);
+            E.line("      if (ho.tail) {");
+            E.line("        L.tailcalls++;");
+            E.line("        switch (ho.new_prog) {");
+            for (auto &q : P) {
+                if (q.n == 0) E.line("        case %u: TERM(MIMIC_ERR_PC_OOB, %u);", q.id, i);
+                else E.line("        case %u: goto P%u_0;", q.id, q.id);
+            }
+            E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);
+            E.line("        }");
+            E.line("      }");
+            E.line("    }");
+            break;
+        default:  // 65: bpf_xdp_adjust_tail (emulator_linux_helpers.go:842-864)
+            E.line("    { const Ref R_ = resolve(kp, L, (uint32_t)r1);");
+            E.line("      if ((R_.rk == RK_GLOBAL || R_.rk == RK_STACK) && R_.map < 0 && R_.limit == 20) TERM(MIMIC_ERR_ENGINE_HELPER, %u);", i);
+            E.line("      r0 = (uint64_t)(int64_t)-22; }");
+            break;
+        }
+    }
+
+    // the interpreter's H_SLOW forms, specialised: per-lane-ordered errors and END
+    void slow(const ProgView &p, uint32_t i) {
+        (void)p;
+        const DInsn &x = p.ins[i];
+        const uint32_t op = insn_op(x), d = insn_dst(x), s = insn_src(x), cls = op & 7, hi = op & 0xf0;
+        const bool xsrc = (op & 0x08) != 0;
+        const int32_t off = insn_off(x);
+        if (cls == 1) {  // LDX with dst >= 10: the memory error comes first, inst.go:298-318
+            static const uint32_t szs[4] = {4, 2, 1, 8};
+            E.line("    { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, %s), %uu, v_); if (s_) TERM(s_, %u); }",
+                   addr(s, off).c_str(), szs[(op >> 3) & 3], i);
+            E.line("    TERM(%s, %u);", d > 10 ? "MIMIC_PANIC_BADREG" : "MIMIC_ERR_R10_WRITE", i);
+            return;
+        }
+        if (hi == 0xd0) {  // END, inst.go:138-198 (Q4)
+            if (d > 10) {
+                E.line("    TERM(MIMIC_PANIC_BADREG, %u);", i);
+                return;
+            }
+            const std::string D = reg(d);
+            std::string v = D;
+            if (x.k == 16) v = xsrc ? "(" + D + " & 0xffffull)" : "(((" + D + " >> 8) & 0xffull) | ((" + D + " & 0xffull) << 8))";
+            else if (x.k == 32) v = xsrc ? "(" + D + " & 0xffffffffull)" : "(uint64_t)__builtin_bswap32((uint32_t)" + D + ")";
+            else if (x.k == 64) v = xsrc ? "(" + D + " >> 32)" : "(uint64_t)__builtin_bswap32((uint32_t)(" + D + " >> 32))";
+            if (d == 10) E.line("    TERM(MIMIC_ERR_R10_WRITE, %u);", i);
+            else E.line("    %s = %s;", D.c_str(), v.c_str());
+            return;
+        }
+        // DIV / MOD with a register divisor (per-lane Go panic)
+        const bool is64 = cls == 7;
+        E.line("    if (%s == 0) TERM(MIMIC_PANIC_DIV0, %u);", is64 ? reg(s).c_str() : ("(uint32_t)" + reg(s)).c_str(), i);
+        if (d == 10) E.line("    TERM(MIMIC_ERR_R10_WRITE, %u);", i);
+        else E.line("    %s = %s(0x%02xu, %s, %s);", reg(d).c_str(), is64 ? "alu64" : "alu32", hi, reg(d).c_str(), reg(s).c_str());
+    }
+};
+
+// 128-bit name of a kernel source (+ compile options) for the on-disk code-object cache
+std::string cache_name(const std::string &src, const char *const *opts, int nopts) {
+    uint64_t a = 1469598103934665603ull, b = 0x9e3779b97f4a7c15ull;
+    auto mix = [&](const char *p, size_t n) {
+        for (size_t i = 0; i < n; i++) {
+            a = (a ^ (uint8_t)p[i]) * 1099511628211ull;
+            b = (b + (uint8_t)p[i]) * 0xff51afd7ed558ccdull;
+            b ^= b >> 29;
+        }
+    };
+    mix(src.data(), src.size());
+    for (int i = 0; i < nopts; i++) mix(opts[i], strlen(opts[i]) + 1);
+    int maj = 0, min = 0;
+    hiprtcVersion(&maj, &min);
+    char v[32];
+    snprintf(v, sizeof v, "rtc%d.%d", maj, min);
+    mix(v, strlen(v));
+    char out[48];
+    snprintf(out, sizeof out, "%016" PRIx64 "%016" PRIx64 ".hsaco", a, b);
+    return out;
+}
+
+// MIMIC_JIT_CACHE=dir keeps compiled kernels across processes (unset or empty: no disk cache)
+std::string cache_path(const std::string &name) {
+    const char *d = getenv("MIMIC_JIT_CACHE");
+    if (!d || !*d) return "";
+    return std::string(d) + "/" + name;
+}
+
+bool read_file(const std::string &path, std::vector<char> &out) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n > 0 && fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+    fclose(f);
+    return ok;
+}
+
+void write_file_atomic(const std::string &path, const std::vector<char> &data) {
+    const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+    FILE *f = fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+    fclose(f);
+    if (ok) rename(tmp.c_str(), path.c_str());
+    else remove(tmp.c_str());
+}
+
+const char *const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-label", "-Wno-unused-variable"};
+const int kNOpts = (int)(sizeof kOpts / sizeof *kOpts);
+
+// source -> gfx950 code object (hipRTC), through the disk cache when one is configured
+int build_code(const std::string &src, std::vector<char> &code, std::string *log) {
+    const std::string path = cache_path(cache_name(src, kOpts, kNOpts));
+    if (!path.empty() && read_file(path, code)) return 0;
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "mimic_jit.hip", kJitHeaderCount, kJitHeaderSrc, kJitHeaderNames) !=
+        HIPRTC_SUCCESS) {
+        *log = "hiprtcCreateProgram failed";
+        return -1;
+    }
+    const hiprtcResult rc = hiprtcCompileProgram(prog, kNOpts, kOpts);
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::string lg(ls + 1, '\0');
+    if (ls) hiprtcGetProgramLog(prog, &lg[0]);
+    if (rc != HIPRTC_SUCCESS) {
+        *log = "hipRTC: " + std::string(hiprtcGetErrorString(rc)) + "\n" + lg;
+        hiprtcDestroyProgram(&prog);
+        return -1;
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    code.resize(cs);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    if (!path.empty()) write_file_atomic(path, code);
+    return 0;
+}
+
+struct CacheKey {
+    int device;
+    std::string src;
+    bool operator<(const CacheKey &o) const { return device != o.device ? device < o.device : src < o.src; }
+};
+std::mutex g_mu;
+std::map<CacheKey, hipFunction_t> g_cache;
+
+}  // namespace
+
+std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, JitInfo *info) {
+    std::vector<ProgView> v;
+    for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
+    Gen g(v);
+    std::string src = g.source();
+    if (info) {
+        info->checks_budget = g.careful_copies;
+        info->max_n = g.max_n;
+        info->tail_calls = g.has_tail();
+    }
+    return src;
+}
+
+uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls) {
+    if (info.checks_budget) return 0;
+    // a jump to a negative PC counts one more Step than the slots executed
+    return (info.tail_calls ? (uint64_t)max_tail_calls + 1 : 1) * ((uint64_t)info.max_n + 1);
+}
+
+int mimic_jit_compile(int device, const std::string &src, hipFunction_t *fn, std::string *log) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const CacheKey key{device, src};
+    auto it = g_cache.find(key);
+    if (it != g_cache.end()) {
+        *fn = it->second;
+        return 0;
+    }
+    std::vector<char> code;
+    if (build_code(src, code, log)) return -1;
+    hipModule_t mod;
+    hipError_t e = hipModuleLoadData(&mod, code.data());
+    if (e != hipSuccess) {
+        *log = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
+        return -1;
+    }
+    e = hipModuleGetFunction(fn, mod, "mimic_jit_kernel");
+    if (e != hipSuccess) {
+        *log = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
+        return -1;
+    }
+    g_cache[key] = *fn;  // modules live for the process (shared by every VM with these programs)
+    return 0;
+}
+
+// compile into the disk cache only (no device): prewarming for later processes
+int mimic_jit_prebuild_source(const std::string &src, std::string *log) {
+    std::vector<char> code;
+    return build_code(src, code, log);
+}
+
+int mimic_jit_launch(hipFunction_t fn, const KParams *kp, hipStream_t st) {
+    const uint32_t blocks = (kp->lanes + 255) / 256;
+    if (blocks == 0) return 0;
+    KParams k = *kp;
+    void *args[] = {&k};
+    return hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
+}
+
+// compile only (no device needed): the hipRTC log, for build checks and tests
+int mimic_jit_check_source(const std::string &src, std::string *log, size_t *code_size) {
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "mimic_jit.hip", kJitHeaderCount, kJitHeaderSrc, kJitHeaderNames) !=
+        HIPRTC_SUCCESS)
+        return -1;
+    const hiprtcResult rc = hiprtcCompileProgram(prog, kNOpts, kOpts);
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::string lg(ls + 1, '\0');
+    if (ls) hiprtcGetProgramLog(prog, &lg[0]);
+    *log = lg;
+    if (code_size) hiprtcGetCodeSize(prog, code_size);
+    hiprtcDestroyProgram(&prog);
+    return rc == HIPRTC_SUCCESS ? 0 : -1;
+}

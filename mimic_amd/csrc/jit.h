@@ -1,0 +1,26 @@
+// jit.h -- per-program-set JIT kernels (jit.cpp): source generation, hipRTC build, launch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "layout.h"
+
+// HIP source of the kernel that runs the loaded programs (aux = predecoded facts)
+struct JitInfo {
+    bool checks_budget;  // the kernel has the per-block budget checks (loops / BPF-to-BPF calls)
+    uint32_t max_n;      // longest program
+    bool tail_calls;     // some program calls bpf_tail_call
+};
+std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, JitInfo *info);
+// 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
+// batch with a smaller budget must run on the interpreter
+uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);
+// hipRTC compile for gfx950 + module load on the current device (cached per device and source)
+int mimic_jit_compile(int device, const std::string &src, hipFunction_t *fn, std::string *log);
+int mimic_jit_launch(hipFunction_t fn, const KParams *kp, hipStream_t st);
+// hipRTC compile only, no device needed
+int mimic_jit_check_source(const std::string &src, std::string *log, size_t *code_size);
+// compile into the MIMIC_JIT_CACHE directory without a device (prewarming)
+int mimic_jit_prebuild_source(const std::string &src, std::string *log);

@@ -3,11 +3,13 @@
 The hot path shards with no exchange: rank r owns vCPUs [r*Vr, (r+1)*Vr) of one VM whose
 address layout is that of the full V = world*Vr machine, and its own packets.  The only
 collectives are setup/readout ones: the program bytes are broadcast from rank 0, and the
-per-CPU counters' per-key sums are all-reduced (the "sum over CPUs" view of a per-CPU map).
+per-CPU counters' per-key sums are all-reduced (the "sum over CPUs" view of a per-CPU map);
+a shared hash map is one replica per GPU whose (key, value) records are all-gathered and
+merged for the readout.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 
 def shard(vcpus_per_rank: int, rank: int) -> Tuple[int, int]:
@@ -46,3 +48,35 @@ def allreduce_max_f64(value: float, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allgather_records(records: bytes, rec_size: int, device) -> List[bytes]:
+    """All-gather variable-length byte blobs of fixed-size records (one per rank)."""
+    import torch
+    import torch.distributed as dist
+
+    ws = dist.get_world_size()
+    n = torch.tensor([len(records)], dtype=torch.int64, device=device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(ws)]
+    dist.all_gather(sizes, n)
+    mx = max(int(s.item()) for s in sizes)
+    buf = torch.zeros(max(mx, 1), dtype=torch.uint8, device=device)
+    if records:
+        buf[:len(records)].copy_(torch.frombuffer(bytearray(records), dtype=torch.uint8))
+    outs = [torch.zeros(max(mx, 1), dtype=torch.uint8, device=device) for _ in range(ws)]
+    dist.all_gather(outs, buf)
+    return [bytes(o[:int(s.item())].cpu().numpy().tobytes()) for o, s in zip(outs, sizes)]
+
+
+def merge_hash_replicas(contents: Dict[bytes, bytes], key_size: int, value_size: int, device) -> Dict[bytes, bytes]:
+    """Shared hash map over N GPUs kept as one replica per GPU (SURVEY 8(e) option 1): gather
+    every replica's (key, value) records and keep the first rank's value for each key.  Exact
+    for insert-if-absent programs whose values are a function of the key (cfg 4)."""
+    rs = key_size + value_size
+    mine = b"".join(k + v for k, v in sorted(contents.items()))
+    merged: Dict[bytes, bytes] = {}
+    for blob in allgather_records(mine, rs, device):
+        for o in range(0, len(blob), rs):
+            k, v = blob[o:o + key_size], blob[o + key_size:o + rs]
+            merged.setdefault(k, v)
+    return merged

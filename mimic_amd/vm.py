@@ -463,6 +463,14 @@ class VM:
         _check(self.h, self.lib.mimic_last_steps(self.h, C.byref(v)), "last steps")
         return v.value
 
+    def ExecMode(self) -> str:
+        """'jit' (per-program-set kernels, hipRTC) or 'interp' (the batch interpreter)."""
+        return {1: "interp", 2: "jit"}[self.lib.mimic_exec_mode(self.h)]
+
+    def LastExec(self) -> str:
+        """The kernel the last batch ran on."""
+        return {0: "none", 1: "interp", 2: "jit"}[self.lib.mimic_last_exec(self.h)]
+
 
 def NewVM(*opts) -> VM:  # vm.go:54-76
     emu = None

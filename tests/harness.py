@@ -57,8 +57,27 @@ def build_oracle(sc: Scenario):
     return vm, mids, pids
 
 
+def jit_prewarm(raws) -> None:
+    """MIMIC_JIT_PREWARM=1 (CPU host): compile the scenario's JIT kernel into the cache, skip."""
+    import ctypes as C
+
+    import pytest
+
+    from mimic_amd import _lib
+
+    lib = _lib.load()
+    bufs = [C.create_string_buffer(bytes(r), max(len(r), 1)) for r in raws]
+    arr = (C.c_void_p * max(len(raws), 1))(*[C.cast(b, C.c_void_p) for b in bufs])
+    ns = (C.c_uint32 * max(len(raws), 1))(*[len(r) // 8 for r in raws])
+    lib.mimic_jit_prebuild(arr, ns, len(raws))
+    pytest.skip("JIT prewarm")
+
+
 def build_engine(sc: Scenario, device: int = 0, shard=None):
     import mimic_amd as M
+
+    if os.environ.get("MIMIC_JIT_PREWARM"):
+        jit_prewarm([raw for _, raw, _ in sc.progs])
 
     emu = M.NewLinuxEmulator(M.OptMaxTailCalls(sc.max_tail_calls))
     opts = [M.VMOptEmulator(emu), M.VMOptSetvCPUs(sc.vcpus), M.VMOptDevice(device)]

@@ -81,3 +81,55 @@ def test_two_rank_shard_matches_single_process():
         assert total == want, (rank, total, want)
         assert mx == ws - 1
     assert sum(want) == N * ws
+
+
+def _hash_rank_main(rank, ws, port, q):
+    import torch.distributed as dist
+
+    import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    prog = W.prog_flowtrack(max_entries=8192)
+    vm = oracle.OracleVM(VPR * ws)
+    mid = vm.map_create("flows", 1, 16, 8, 8192)
+    pid = vm.prog_load("p", prog.raw, [(s, mid) for s, _ in prog.relocs])
+    buf, off, lens = W.make_packets(N, W.IMIX["sizes"], W.IMIX["weights"], seed=W.SEED + rank)
+    b0, cnt = D.shard(VPR, rank)
+    vm.run_xdp_batch(pid, buf, off, lens, b0 + W.schedule_cpu(N, cnt, "interleaved"), write_back=False)
+    vals = vm.map_values(mid, 0)
+    mine = {k: vals[s * 8:(s + 1) * 8] for k, s in vm.map_entries(mid)}
+    merged = D.merge_hash_replicas(mine, 16, 8, "cpu")
+    q.put((rank, sorted(merged.items())))
+    dist.destroy_process_group()
+
+
+def test_two_rank_hash_replicas_merge_to_single_process():
+    """cfg 4 over 2 ranks: one hash-map replica per rank, all-gathered and merged, equals one
+    process inserting every rank's packets (values are a function of the key)."""
+    ws = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hash_rank_main, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(ws)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    import oracle
+
+    prog = W.prog_flowtrack(max_entries=8192)
+    vm = oracle.OracleVM(VPR * ws)
+    mid = vm.map_create("flows", 1, 16, 8, 8192)
+    pid = vm.prog_load("p", prog.raw, [(s, mid) for s, _ in prog.relocs])
+    for r in range(ws):
+        buf, off, lens = W.make_packets(N, W.IMIX["sizes"], W.IMIX["weights"], seed=W.SEED + r)
+        vm.run_xdp_batch(pid, buf, off, lens, D.shard(VPR, r)[0] + W.schedule_cpu(N, VPR, "interleaved"),
+                         write_back=False)
+    vals = vm.map_values(mid, 0)
+    want = sorted((k, vals[s * 8:(s + 1) * 8]) for k, s in vm.map_entries(mid))
+    assert len(want) > 1000
+    for rank, got in res:
+        assert got == want, rank

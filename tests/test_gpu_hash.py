@@ -122,11 +122,12 @@ def test_tombstone_rebuild_between_batches(gpu):
     ovm.close()
 
 
-def test_hash_helpers_random_programs(gpu):
+@pytest.mark.parametrize("seed", range(12))
+def test_hash_helpers_random_programs(gpu, seed):
     """The fuzz generator's map calls against a per-CPU hash map with 4-byte keys, one vCPU."""
     from fuzz import random_program
 
-    for seed in range(12):
+    if True:
         rng = np.random.default_rng(7000 + seed)
         raw, rel = random_program(rng, n_body=int(rng.integers(20, 70)), map_name="m")
         mt = 5 if seed % 2 else 1
