@@ -12,7 +12,7 @@ ORC_HDR = os.path.join(ROOT, "oracle", "mimic_oracle.h")
 
 def _decls():
     txt = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*(mimic_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long|void|const char \*)\s*(mimic_\w+)\s*\(", txt, re.M)))
 
 
 def _enum(path, prefix):
