@@ -95,8 +95,9 @@ def cpu_baseline(cfg_name: str, min_seconds: float, vcpus_cpu: int = 8):
                        f"{vcpus_cpu} vCPUs, chunked), C oracle single-threaded, {dt:.1f} s")
 
 
-def read_pmc_traffic(cfg_name: str):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
+def read_pmc_traffic(cfg_name: str, kernel: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/*pmc*.json) of the
+    same workload and kernel (mimic_jit_kernel / mimic_xdp_kernel)."""
     import glob
 
     best = None
@@ -105,67 +106,36 @@ def read_pmc_traffic(cfg_name: str):
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("config") == cfg_name and d.get("bytes_per_launch"):
+        if d.get("config") == cfg_name and d.get("kernel") == kernel and d.get("bytes_per_launch"):
             best = d
     return best
 
 
-def host_resident_rate(vm, M, pid, buf, off, lens, sched, dev, chunks: int = 8, reps: int = 5):
-    """Packets start and end in host memory: H2D of packet bytes + descriptors, the kernel, D2H of
-    R0 + status, pipelined over `chunks` sub-batches.  Copies run on their own streams; the
-    kernels stay in order on one stream, so every vCPU still sees its packets in order."""
-    import torch
-
+def host_resident_rate(vm, M, pid, buf, off, lens, sched, dev, chunks: int = 0, reps: int = 5):
+    """Packets start and end in host memory: mimic_run_xdp_host pipelines sub-batches (H2D of
+    packet bytes + descriptors, the kernel, D2H of r0 + status) on separate streams.  The host
+    arrays are pinned once (hipHostRegister) like NIC / capture buffers would be."""
     n = len(lens)
-    h_buf = torch.from_numpy(buf).pin_memory()
-    h_off = torch.from_numpy(np.asarray(off, dtype=np.uint64).view(np.int64)).pin_memory()
-    h_len = torch.from_numpy(np.asarray(lens, dtype=np.uint32).view(np.int32)).pin_memory()
-    h_r0 = torch.empty(n, dtype=torch.int64).pin_memory()
-    h_st = torch.empty(n, dtype=torch.uint8).pin_memory()
-    d_buf = torch.empty_like(h_buf, device=dev)
-    d_off = torch.empty_like(h_off, device=dev)
-    d_len = torch.empty_like(h_len, device=dev)
-    d_r0 = torch.empty(n, dtype=torch.int64, device=dev)
-    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
-    s_h2d, s_k, s_d2h = (torch.cuda.Stream(device=dev) for _ in range(3))
-    bounds = np.linspace(0, n, chunks + 1).astype(np.int64)
-    offs = np.asarray(off, dtype=np.int64)
-    ends = offs + np.asarray(lens, dtype=np.int64)
-
-    def one_pass():
-        for c in range(chunks):
-            a, b = int(bounds[c]), int(bounds[c + 1])
-            if a == b:
-                continue
-            lo, hi = int(offs[a]), int(ends[b - 1])
-            e_in = torch.cuda.Event()
-            with torch.cuda.stream(s_h2d):
-                d_buf[lo:hi].copy_(h_buf[lo:hi], non_blocking=True)
-                d_off[a:b].copy_(h_off[a:b], non_blocking=True)
-                d_len[a:b].copy_(h_len[a:b], non_blocking=True)
-                e_in.record(s_h2d)
-            s_k.wait_event(e_in)
-            sub = M.XDPBatch(d_buf, d_off[a:b], d_len[a:b], ingress=1, schedule=sched)
-            res = M.XDPResults(d_r0[a:b], d_st[a:b], None, None)
-            vm.RunXDPBatch(pid, sub, res, stream=s_k, sync=False)
-            e_k = torch.cuda.Event()
-            e_k.record(s_k)
-            s_d2h.wait_event(e_k)
-            with torch.cuda.stream(s_d2h):
-                h_r0[a:b].copy_(d_r0[a:b], non_blocking=True)
-                h_st[a:b].copy_(d_st[a:b], non_blocking=True)
-
-    one_pass()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        one_pass()
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    r0 = np.empty(n, np.uint64)
+    st = np.empty(n, np.uint8)
+    arrs = (buf, off, lens, r0, st)
+    for a in arrs:
+        vm.HostRegister(a)
+    try:
+        vm.RunXDPHost(pid, buf, off, lens, schedule=sched, ingress=1, chunks=chunks, r0=r0, status=st)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            vm.RunXDPHost(pid, buf, off, lens, schedule=sched, ingress=1, chunks=chunks, r0=r0, status=st)
+        dt = time.perf_counter() - t0
+    finally:
+        for a in arrs:
+            vm.HostUnregister(a)
     moved = int(buf.nbytes) + 12 * n + 9 * n
     return {"value": round(n * reps / dt / 1e6, 3), "unit": "Mpkts/s", "chunks": chunks,
             "pcie_bytes_per_batch": moved, "pcie_GBps": round(moved * reps / dt / 1e9, 2),
-            "ok_frac": float((h_st.numpy() == 0).mean())}
+            "ok_frac": float((st == 0).mean())}
 
 
 def main():
@@ -273,7 +243,7 @@ def main():
         avg_launch_s = float(np.mean(kern_ms)) / 1e3
         alg = algorithmic_bytes(lens, vpg, prog.maps)
         achieved = alg / avg_launch_s
-        pmc = read_pmc_traffic(args.config)
+        pmc = read_pmc_traffic(args.config, "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel")
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",
             "value": round(value, 3),

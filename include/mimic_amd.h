@@ -192,6 +192,32 @@ int mimic_sync(mimic_vm *vm, void *hip_stream);
 /* Executed Step() count of the last completed mimic_run_xdp (sum over packets). */
 int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out);
 
+/* Host-resident batches: packets start and end in host memory (captured pcap, ctx JSON, NIC
+ * buffers).  The engine pipelines the batch in sub-batches: H2D of packet bytes + descriptors,
+ * the kernel, D2H of r0/status (and of the packet memory when pkt_out is set), on separate
+ * streams so that copies overlap kernels.  vCPU assignment is that of the whole batch.
+ * Host memory should be pinned (mimic_host_register) for the copies to run asynchronously. */
+typedef struct {
+    uint32_t n;
+    uint32_t schedule;            /* MIMIC_SCHED_*; CHUNKED runs as the equivalent EXPLICIT schedule */
+    const uint8_t *pkt_data;      /* host */
+    const uint64_t *pkt_off;      /* host, [n] */
+    const uint32_t *pkt_len;      /* host, [n] */
+    uint32_t headroom_all, tailroom_all;
+    int32_t ingress_all, rxq_all, egress_all;
+    int32_t pad;
+    const int32_t *cpu;           /* host, EXPLICIT */
+    uint64_t step_budget;
+    uint8_t *pkt_out;             /* optional host: packet memory after the run (needs ascending pkt_off) */
+    uint64_t *r0;                 /* host, [n] */
+    uint8_t *status;              /* host, [n] */
+} mimic_xdp_host_batch;
+/* chunks = number of sub-batches (0: about 16 MiB of packet memory each) */
+int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks);
+/* Pin / unpin host memory for DMA (hipHostRegister / hipHostUnregister). */
+int mimic_host_register(void *p, size_t bytes);
+int mimic_host_unregister(void *p);
+
 /* Execution mode the VM resolved to (MIMIC_EXEC_INTERP / MIMIC_EXEC_JIT). */
 int mimic_exec_mode(const mimic_vm *vm);
 /* The kernel the last batch ran on (a JIT VM runs batches whose step budget is below its

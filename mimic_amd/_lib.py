@@ -58,6 +58,15 @@ class XDPResults(C.Structure):
     _fields_ = [("r0", C.c_void_p), ("status", C.c_void_p), ("steps", C.c_void_p), ("err_pc", C.c_void_p)]
 
 
+class XDPHostBatch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("schedule", C.c_uint32), ("pkt_data", C.c_void_p),
+                ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p),
+                ("headroom_all", C.c_uint32), ("tailroom_all", C.c_uint32),
+                ("ingress_all", C.c_int32), ("rxq_all", C.c_int32), ("egress_all", C.c_int32), ("pad", C.c_int32),
+                ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("pkt_out", C.c_void_p),
+                ("r0", C.c_void_p), ("status", C.c_void_p)]
+
+
 EXPORTS = {
     "mimic_abi_version": (C.c_int, []),
     "mimic_last_error": (C.c_char_p, [C.c_void_p]),
@@ -68,6 +77,9 @@ EXPORTS = {
     "mimic_map_lookup": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.POINTER(C.c_uint32)]),
     "mimic_map_delete": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "mimic_exec_mode": (C.c_int, [C.c_void_p]),
+    "mimic_run_xdp_host": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPHostBatch), C.c_uint32]),
+    "mimic_host_register": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "mimic_host_unregister": (C.c_int, [C.c_void_p]),
     "mimic_last_exec": (C.c_int, [C.c_void_p]),
     "mimic_jit_source_for": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_char_p,
                                          C.c_size_t]),

@@ -23,7 +23,7 @@
 #include "layout.h"
 #include "jit.h"
 
-extern "C" int mimic_launch_xdp(const KParams *kp, hipStream_t st);
+extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st);
 extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
                                     int32_t cpu, int32_t *out, hipStream_t st);
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
@@ -86,7 +86,29 @@ struct mimic_vm {
     hipFunction_t jit_fn = nullptr;
     JitInfo jit_info{};
     int last_exec = 0;          // the kernel the last batch ran on
+    // launch parameters of JIT kernels in device memory: a ring of slots written by
+    // stream-ordered copies from pinned host memory (a repeated batch reuses its slot)
+    static constexpr int KP_SLOTS = 64;
+    KParams *d_kp = nullptr, *h_kp = nullptr;
+    hipEvent_t kp_ev[KP_SLOTS] = {};
+    bool kp_used[KP_SLOTS] = {};
+    int kp_next = 0, kp_last = -1;
+    hipStream_t kp_last_stream = nullptr;
+    // host-resident pipeline (mimic_run_xdp_host): NB rotating device staging slots
+    static constexpr int NB = 3;
+    struct Slot {
+        uint8_t *buf = nullptr;
+        uint64_t *r0 = nullptr;
+        uint8_t *st = nullptr;
+        hipEvent_t e_in = nullptr, e_k = nullptr, e_out = nullptr;
+        bool used = false;
+    } slot[NB];
+    size_t hp_cap_bytes = 0, hp_cap_n = 0, hp_cap_desc = 0;
+    uint64_t *hp_off = nullptr;   // whole-batch descriptors (one copy each per batch)
+    uint32_t *hp_len = nullptr;
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
 };
+
 
 static int fail(mimic_vm *vm, int code, const char *fmt, ...) {
     if (vm) {
@@ -105,6 +127,27 @@ static int fail(mimic_vm *vm, int code, const char *fmt, ...) {
         hipError_t e_ = (call);                                                                 \
         if (e_ != hipSuccess) return fail((vm), MIMIC_EDEVICE, "%s: %s", #call, hipGetErrorString(e_)); \
     } while (0)
+
+// the device copy of kp for a JIT launch on stream st (see mimic_vm::d_kp)
+static int kp_slot(mimic_vm *vm, const KParams &kp, hipStream_t st, const KParams **out) {
+    if (!vm->d_kp) {
+        HIP_OK(vm, hipMalloc(&vm->d_kp, sizeof(KParams) * mimic_vm::KP_SLOTS));
+        HIP_OK(vm, hipHostMalloc(&vm->h_kp, sizeof(KParams) * mimic_vm::KP_SLOTS));
+        for (auto &e : vm->kp_ev) HIP_OK(vm, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    int slot = vm->kp_last;
+    if (slot < 0 || st != vm->kp_last_stream || memcmp(&vm->h_kp[slot], &kp, sizeof kp) != 0) {
+        slot = vm->kp_next;
+        vm->kp_next = (slot + 1) % mimic_vm::KP_SLOTS;
+        if (vm->kp_used[slot]) HIP_OK(vm, hipEventSynchronize(vm->kp_ev[slot]));  // its last kernel is done
+        vm->h_kp[slot] = kp;
+        HIP_OK(vm, hipMemcpyAsync(vm->d_kp + slot, vm->h_kp + slot, sizeof kp, hipMemcpyHostToDevice, st));
+        vm->kp_last = slot;
+        vm->kp_last_stream = st;
+    }
+    *out = vm->d_kp + slot;
+    return slot;
+}
 
 static uint32_t stack_size(const mimic_vm *vm) {
     return (uint32_t)(vm->s.stack_frame_size * vm->s.stack_frame_count);
@@ -459,6 +502,21 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_sched_start);
     hipFree(vm->d_sched_pkts);
     hipFree(vm->d_lane_steps);
+    hipFree(vm->d_kp);
+    if (vm->h_kp) hipHostFree(vm->h_kp);
+    for (auto &sl : vm->slot) {
+        hipFree(sl.buf);
+        hipFree(sl.r0);
+        hipFree(sl.st);
+        for (hipEvent_t e : {sl.e_in, sl.e_k, sl.e_out})
+            if (e) hipEventDestroy(e);
+    }
+    hipFree(vm->hp_off);
+    hipFree(vm->hp_len);
+    if (vm->s_h2d) hipStreamDestroy(vm->s_h2d);
+    if (vm->s_d2h) hipStreamDestroy(vm->s_d2h);
+    for (auto &e : vm->kp_ev)
+        if (e) hipEventDestroy(e);
     if (vm->stream) hipStreamDestroy(vm->stream);
     delete vm;
 }
@@ -912,16 +970,25 @@ int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out) {
     return 0;
 }
 
-// the batch form of NewProcess / SetCPUID / Run / Cleanup
+// the batch form of NewProcess / SetCPUID / Run / Cleanup.  shift: for an INTERLEAVED
+// sub-batch, the index of its first packet in the whole batch (vCPU of packet k = (shift+k) % V)
+static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
+                        hipStream_t st_in, uint64_t shift);
+
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                   void *hip_stream) {
+    return run_xdp_impl(vm, prog_id, b, res, (hipStream_t)hip_stream, 0);
+}
+
+static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
+                        hipStream_t st_in, uint64_t first_index) {
     if (!vm || !b || !res) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
     hipSetDevice(vm->s.device);
     int rc = upload_tables(vm);
     if (rc) return rc;
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
+    hipStream_t st = st_in ? st_in : vm->stream;
     const uint32_t lanes = (uint32_t)vm->s.vcpu_count;
     const uint32_t S = stack_size(vm);
     // private memory: stack | xdp_md overlay | saved frames, qword-interleaved over lanes
@@ -1001,7 +1068,8 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
         kp.per_lane = lanes ? (uint32_t)(((uint64_t)b->n + lanes - 1) / lanes) : 0;
         break;
     case MIMIC_SCHED_INTERLEAVED:
-        kp.per_lane = lanes ? (uint32_t)(((uint64_t)b->n + lanes - 1) / lanes) : 0;
+        kp.sched_shift = lanes ? (uint32_t)(first_index % lanes) : 0;
+        kp.per_lane = lanes ? (uint32_t)(((uint64_t)b->n + kp.sched_shift + lanes - 1) / lanes) : 0;
         break;
     case MIMIC_SCHED_EXPLICIT: {
         if (!b->cpu && b->n) return fail(vm, MIMIC_EINVAL, "explicit schedule needs cpu[]");
@@ -1060,11 +1128,17 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, cons
         if (bound && kp.budget < bound) jit = false;
     }
     vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
-    if (jit) {
-        if (mimic_jit_launch(vm->jit_fn, &kp, st))
-            return fail(vm, MIMIC_EDEVICE, "JIT launch: %s", hipGetErrorString(hipGetLastError()));
-    } else if (mimic_launch_xdp(&kp, st)) {
-        return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    if (jit && vm->jit_info.kp_by_value) {  // parameters in the kernarg segment
+        if (mimic_jit_launch(vm->jit_fn, vm->jit_info, &kp, nullptr, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    } else {                                // parameters read from a device copy
+        const KParams *dkp = nullptr;
+        const int slot = kp_slot(vm, kp, st, &dkp);
+        if (slot < 0) return slot;
+        if (jit ? mimic_jit_launch(vm->jit_fn, vm->jit_info, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+        HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));
+        vm->kp_used[slot] = true;
     }
     vm->last_lanes = lanes;
     vm->last_stream = st;
@@ -1139,6 +1213,137 @@ int mimic_jit_check(const char *src, char *log, size_t cap, size_t *code_size) {
         log[n] = 0;
     }
     return rc ? MIMIC_EINVAL : 0;
+}
+
+int mimic_host_register(void *p, size_t bytes) {
+    if (!p || !bytes) return MIMIC_EINVAL;
+    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? 0 : MIMIC_EDEVICE;
+}
+
+int mimic_host_unregister(void *p) {
+    if (!p) return MIMIC_EINVAL;
+    return hipHostUnregister(p) == hipSuccess ? 0 : MIMIC_EDEVICE;
+}
+
+int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks) {
+    if (!vm || !hb) return MIMIC_EINVAL;
+    const uint32_t n = hb->n;
+    if (n == 0) return 0;
+    if (!hb->pkt_data || !hb->pkt_off || !hb->pkt_len || !hb->r0 || !hb->status)
+        return fail(vm, MIMIC_EINVAL, "missing host arrays");
+    hipSetDevice(vm->s.device);
+    const uint64_t room = (uint64_t)hb->headroom_all + hb->tailroom_all;
+    if (chunks == 0) {  // auto: ~16 MiB of packet memory per sub-batch (copies of that size run at link rate)
+        uint64_t bytes = 0;
+        for (uint32_t i = 0; i < n; i++) bytes += hb->pkt_len[i] + room;
+        chunks = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(2, bytes >> 24));
+    }
+    chunks = std::max<uint32_t>(1, std::min(chunks, n));
+    // per sub-batch: the host byte window [lo, hi) holding its packets
+    std::vector<uint32_t> bnd(chunks + 1);
+    for (uint32_t c = 0; c <= chunks; c++) bnd[c] = (uint32_t)((uint64_t)n * c / chunks);
+    std::vector<uint64_t> lo(chunks, ~0ull), hi(chunks, 0);
+    size_t max_bytes = 0, max_n = 0;
+    bool ascending = true;
+    for (uint32_t c = 0; c < chunks; c++) {
+        for (uint32_t i = bnd[c]; i < bnd[c + 1]; i++) {
+            lo[c] = std::min<uint64_t>(lo[c], hb->pkt_off[i]);
+            hi[c] = std::max<uint64_t>(hi[c], hb->pkt_off[i] + hb->pkt_len[i] + room);
+            if (i && hb->pkt_off[i] < hb->pkt_off[i - 1] + hb->pkt_len[i - 1] + room) ascending = false;
+        }
+        max_bytes = std::max<size_t>(max_bytes, hi[c] - lo[c]);
+        max_n = std::max<size_t>(max_n, bnd[c + 1] - bnd[c]);
+    }
+    if (hb->pkt_out && !ascending) return fail(vm, MIMIC_EINVAL, "pkt_out needs ascending, non-overlapping packets");
+    // CHUNKED over the whole batch = EXPLICIT with cpu(i) = vcpu_begin + i / ceil(n / lanes)
+    std::vector<int32_t> cpu_chunked;
+    uint32_t sched = hb->schedule;
+    const int32_t *cpu = hb->cpu;
+    if (sched == MIMIC_SCHED_CHUNKED) {
+        const uint32_t lanes = (uint32_t)vm->s.vcpu_count;
+        const uint64_t per = ((uint64_t)n + lanes - 1) / lanes;
+        cpu_chunked.resize(n);
+        for (uint32_t i = 0; i < n; i++) cpu_chunked[i] = vm->s.vcpu_begin + (int32_t)(i / per);
+        cpu = cpu_chunked.data();
+        sched = MIMIC_SCHED_EXPLICIT;
+    }
+    if (sched == MIMIC_SCHED_EXPLICIT && !cpu) return fail(vm, MIMIC_EINVAL, "explicit schedule needs cpu[]");
+    if (!vm->s_h2d) {
+        HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_h2d, hipStreamNonBlocking));
+        HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_d2h, hipStreamNonBlocking));
+        for (auto &sl : vm->slot)
+            for (hipEvent_t *e : {&sl.e_in, &sl.e_k, &sl.e_out}) HIP_OK(vm, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    if (n > vm->hp_cap_desc) {
+        HIP_OK(vm, hipDeviceSynchronize());
+        hipFree(vm->hp_off);
+        hipFree(vm->hp_len);
+        vm->hp_off = nullptr;
+        vm->hp_len = nullptr;
+        HIP_OK(vm, hipMalloc(&vm->hp_off, 8ull * n));
+        HIP_OK(vm, hipMalloc(&vm->hp_len, 4ull * n));
+        vm->hp_cap_desc = n;
+    }
+    if (max_bytes > vm->hp_cap_bytes || max_n > vm->hp_cap_n) {
+        HIP_OK(vm, hipDeviceSynchronize());
+        for (auto &sl : vm->slot) {
+            hipFree(sl.buf);
+            hipFree(sl.r0);
+            hipFree(sl.st);
+            HIP_OK(vm, hipMalloc(&sl.buf, std::max<size_t>(max_bytes, 1)));
+            HIP_OK(vm, hipMalloc(&sl.r0, max_n * 8));
+            HIP_OK(vm, hipMalloc(&sl.st, max_n));
+            sl.used = false;
+        }
+        vm->hp_cap_bytes = max_bytes;
+        vm->hp_cap_n = max_n;
+    }
+    // descriptors of the whole batch first (two copies), then one packet-bytes copy per sub-batch;
+    // the previous batch's kernels may still read hp_off / hp_len
+    for (auto &sl : vm->slot)
+        if (sl.used) HIP_OK(vm, hipStreamWaitEvent(vm->s_h2d, sl.e_k, 0));
+    HIP_OK(vm, hipMemcpyAsync(vm->hp_off, hb->pkt_off, 8ull * n, hipMemcpyHostToDevice, vm->s_h2d));
+    HIP_OK(vm, hipMemcpyAsync(vm->hp_len, hb->pkt_len, 4ull * n, hipMemcpyHostToDevice, vm->s_h2d));
+    for (uint32_t c = 0; c < chunks; c++) {
+        auto &sl = vm->slot[c % mimic_vm::NB];
+        const uint32_t a = bnd[c], m = bnd[c + 1] - bnd[c];
+        if (m == 0) continue;
+        if (sl.used) HIP_OK(vm, hipStreamWaitEvent(vm->s_h2d, sl.e_out, 0));  // the slot's last D2H is done
+        HIP_OK(vm, hipMemcpyAsync(sl.buf, hb->pkt_data + lo[c], hi[c] - lo[c], hipMemcpyHostToDevice, vm->s_h2d));
+        HIP_OK(vm, hipEventRecord(sl.e_in, vm->s_h2d));
+        HIP_OK(vm, hipStreamWaitEvent(vm->stream, sl.e_in, 0));
+        mimic_xdp_batch b{};
+        b.n = m;
+        b.schedule = sched;
+        b.pkt_data = sl.buf - lo[c];  // offsets stay those of the host batch
+        b.pkt_off = vm->hp_off + a;
+        b.pkt_len = vm->hp_len + a;
+        b.headroom_all = hb->headroom_all;
+        b.tailroom_all = hb->tailroom_all;
+        b.ingress_all = hb->ingress_all;
+        b.rxq_all = hb->rxq_all;
+        b.egress_all = hb->egress_all;
+        b.cpu = sched == MIMIC_SCHED_EXPLICIT ? cpu + a : nullptr;
+        b.step_budget = hb->step_budget;
+        mimic_xdp_results r{};
+        r.r0 = sl.r0;
+        r.status = sl.st;
+        int rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a);
+        if (rc) return rc;
+        HIP_OK(vm, hipEventRecord(sl.e_k, vm->stream));
+        HIP_OK(vm, hipStreamWaitEvent(vm->s_d2h, sl.e_k, 0));
+        HIP_OK(vm, hipMemcpyAsync(hb->r0 + a, sl.r0, 8ull * m, hipMemcpyDeviceToHost, vm->s_d2h));
+        HIP_OK(vm, hipMemcpyAsync(hb->status + a, sl.st, m, hipMemcpyDeviceToHost, vm->s_d2h));
+        if (hb->pkt_out) {
+            const uint64_t plo = hb->pkt_off[a], phi = hb->pkt_off[a + m - 1] + hb->pkt_len[a + m - 1] + room;
+            HIP_OK(vm, hipMemcpyAsync(hb->pkt_out + plo, sl.buf + (plo - lo[c]), phi - plo, hipMemcpyDeviceToHost, vm->s_d2h));
+        }
+        HIP_OK(vm, hipEventRecord(sl.e_out, vm->s_d2h));
+        sl.used = true;
+    }
+    HIP_OK(vm, hipStreamSynchronize(vm->s_d2h));
+    vm->last_stream = nullptr;
+    return 0;
 }
 
 }  // extern "C"

@@ -37,7 +37,8 @@
 #define NREGS 11
 #define KEY_DONE 0xffffffffu
 
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(KParams kp) {
+extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams *__restrict__ kpp) {
+    const KParams &kp = *kpp;  // device copy (engine.cpp kp_slot): fields load where used
     // eBPF registers r0..r10 of every lane live in LDS, [wave][reg][lane] (8-byte words): a
     // wave-uniform register number addresses 64 consecutive words (conflict-free ds_read_b64),
     // and multi-register updates (exit, helpers) need no register-array copies.
@@ -68,7 +69,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                 uint64_t ii = (uint64_t)g * kp.per_lane + j;
                 if (ii < kp.n) i = (uint32_t)ii;
             } else if (kp.sched == SCHED_INTERLEAVED) {
-                uint64_t ii = (uint64_t)j * kp.lanes + g;
+                uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift);
                 if (ii < kp.n) i = (uint32_t)ii;
             } else if (j < ex_count) {
                 i = kp.sched_pkts[ex_begin + j];
@@ -84,6 +85,9 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         L.sm0 = 0;
         L.sm1 = 0;
         L.xdp_dirty = 0;
+        L.t_n = 0;
+        L.t_lo = 0;
+        L.t_ptr = nullptr;
         L.nframes = 0;
         L.tailcalls = 0;
         L.M = 0;
@@ -221,7 +225,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                         break;
                     case H_CALL: {  // helpers, emulator_linux_.go:125-194
                         const int32_t hn = (int32_t)(uint32_t)k;
-                        HelperOut ho = {0, 0, false, false, 0};
+                        HelperOut ho = {0, 0, false, false, 0, 0, 0, nullptr};
                         if (hn == 1) ho = helper_lookup(kp, L, REG(1), REG(2));
                         else if (hn == 2) ho = helper_update(kp, L, REG(1), REG(2), REG(3));
                         else if (hn == 3) ho = helper_delete(kp, L, REG(1), REG(2));
@@ -236,6 +240,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                         st = ho.st;
                         if (!st) {
                             if (ho.set_r0) REG(0) = ho.r0;
+                            if (ho.t_n) { L.t_lo = ho.t_lo; L.t_n = ho.t_n; L.t_ptr = ho.t_ptr; }
                             if (ho.tail) {  // PC = -1, then Step's bounds check on the new program
                                 const DProg np = kp.progs[ho.new_prog];
                                 L.tailcalls++;
@@ -411,10 +416,10 @@ extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mimic_launch_xdp(const KParams *kp, hipStream_t st) {
+extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st) {
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
-    hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, *kp);
+    hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -80,6 +80,13 @@ int64_t jump_target(const DInsn &x, int64_t i) {
 class Gen {
   public:
     Gen(const std::vector<ProgView> &progs) : P(progs) {
+        // tuning knobs (environment; they change the generated source, hence the cache key)
+        const char *f = getenv("MIMIC_JIT_FAST");
+        fast_paths = !(f && f[0] == '0');
+        const char *sg = getenv("MIMIC_JIT_STAGE");
+        stage = !(sg && sg[0] == '0');
+        const char *k = getenv("MIMIC_JIT_KP");
+        kp_by_value = !(k && !strcmp(k, "ptr"));
         for (auto &p : P)
             for (uint32_t i = 0; i < p.n; i++) {
                 const DInsn &x = p.ins[i];
@@ -108,14 +115,43 @@ class Gen {
 
     bool careful_copies = true;
     uint32_t max_n = 0;
+    bool fast_paths = true;    // MIMIC_JIT_FAST=0: every access through resolve()
+    bool stage = true;         // MIMIC_JIT_STAGE=0: no LDS packet window
+    bool kp_by_value = true;   // MIMIC_JIT_KP=ptr: launch parameters read from a device copy
     bool has_tail() const { return any_tail; }
 
     std::string source() {
+        // stage packets in LDS only when some access is expected to hit the packet
+        if (stage) {
+            bool any = false;
+            for (auto &p : P) {
+                ctx_hints(p);
+                for (uint32_t i = 0; i < p.n; i++) {
+                    const DInsn &x = p.ins[i];
+                    const uint32_t h = AUX_H(x.aux);
+                    if (h == H_LDX && hint(insn_src(x)) == HINT_PKT) any = true;
+                    if ((h == H_ST || h == H_STX) && hint(insn_dst(x)) == HINT_PKT) any = true;
+                }
+            }
+            stage = any && fast_paths;
+        }
         E.line("#include \"runtime.h\"");
         E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
-        E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(KParams kp) {");
+        // KParams is read through a pointer to device memory: fields are then loaded (scalar)
+        // where they are used instead of all being preloaded into SGPRs from the kernarg
+        // segment (which spilled and cost VGPRs / occupancy)
+        if (kp_by_value) {
+            E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(KParams kp) {");
+        } else {
+            E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");
+            E.line("  const KParams &kp = *kpp;");
+        }
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
         E.line("  if (g >= kp.lanes) return;");
+        if (stage && fast_paths) {
+            E.line("  __shared__ PWin pwin_;");
+            E.line("  const uint32_t tl_ = threadIdx.x;");
+        }
         E.line("  Lane L;");
         E.line("  L.lane = g;");
         E.line("  L.cpu = (int32_t)(kp.vcpu_begin + g);");
@@ -126,7 +162,7 @@ class Gen {
         E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
         E.line("    uint32_t i;");
         E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
-        E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + g; if (ii >= kp.n) break; i = (uint32_t)ii; }");
+        E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else { if (j >= ex_count) break; i = kp.sched_pkts[ex_begin + j]; }");
         // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
         E.line("    const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;");
@@ -141,7 +177,8 @@ class Gen {
         E.line("    L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);");
         E.line("    L.rxq = (uint32_t)(kp.rxq_arr ? kp.rxq_arr[i] : kp.rxq);");
         E.line("    L.egress = (uint32_t)(kp.egress_arr ? kp.egress_arr[i] : kp.egress);");
-        E.line("    L.sm0 = 0; L.sm1 = 0; L.xdp_dirty = 0; L.nframes = 0; L.tailcalls = 0;");
+        if (stage && fast_paths) E.line("    const uint32_t W_ = win_stage(pwin_, tl_, L.pkt, L.M);");
+        E.line("    L.sm0 = 0; L.sm1 = 0; L.xdp_dirty = 0; L.nframes = 0; L.tailcalls = 0; L.t_lo = 0; L.t_n = 0; L.t_ptr = nullptr;");
         E.line("    uint64_t r0 = 0, r1 = P + L.M + 1, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0, r9 = 0;");
         E.line("    uint64_t r10 = kp.static_next + kp.frame_size;");
         E.line("    uint32_t steps = 0;");
@@ -174,6 +211,7 @@ class Gen {
 
     void program(const ProgView &p) {
         if (p.n == 0) return;
+        ctx_hints(p);
         std::set<uint32_t> lead = {0};
         for (uint32_t i = 0; i < p.n; i++) {
             const DInsn &x = p.ins[i];
@@ -233,6 +271,98 @@ class Gen {
         return "(uint32_t)(" + reg(r) + " + " + imm((uint64_t)(int64_t)off) + ")";
     }
 
+    // Memory access fast paths.  The base register hints which per-process entry the address
+    // most likely falls in (r10: the stack; a copy of the entry r1: xdp_md; anything else: the
+    // packet).  The fast path is taken only when the access lies inside that entry, where it is
+    // exactly what GetEntry + VMMem.Load/Store would do.  Every other access (other entries, map
+    // values, errors) goes through the generic resolve().  Hints never change results.
+    enum Hint { HINT_PKT, HINT_STACK, HINT_CTX };
+    Hint hint(uint32_t base) const {
+        if (base == 10) return HINT_STACK;
+        if (base < 11 && ctx_reg[base]) return HINT_CTX;
+        return HINT_PKT;
+    }
+    bool ctx_reg[11] = {};
+
+    // registers that only ever hold the context pointer: r1 (never written: helpers keep it,
+    // Q8) and registers whose every write is `mov rX, r1`
+    void ctx_hints(const ProgView &p) {
+        bool written[11] = {}, other[11] = {};
+        for (uint32_t i = 0; i < p.n; i++) {
+            const DInsn &x = p.ins[i];
+            const uint32_t h = AUX_H(x.aux), d = insn_dst(x), op = insn_op(x);
+            bool writes = h == H_ALU64 || h == H_ALU32 || h == H_LDIMM || h == H_LDX || h == H_SLOW;
+            if (h == H_CALL || h == H_CALL_LOCAL) { written[0] = other[0] = true; }
+            if (h == H_CALL_LOCAL) for (int r = 1; r <= 5; r++) written[r] = other[r] = true;
+            if (!writes || d > 10) continue;
+            written[d] = true;
+            if (!(op == 0xbf && insn_src(x) == 1)) other[d] = true;
+        }
+        for (int r = 0; r < 11; r++) ctx_reg[r] = false;
+        if (written[1] || any_tail) return;
+        ctx_reg[1] = true;
+        for (int r = 2; r < 10; r++) ctx_reg[r] = written[r] && !other[r];
+    }
+
+    void load(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &dst) {
+        if (!fast_paths) {
+            E.line("    { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, %s), %uu, v_); if (s_) TERM(s_, %u); %s = v_; }",
+                   addr(base, off).c_str(), n, i, dst.c_str());
+            return;
+        }
+        E.line("    { const uint32_t a_ = %s; uint64_t v_ = 0;", addr(base, off).c_str());
+        switch (hint(base)) {
+        case HINT_STACK:
+            E.line("      const uint32_t o_ = a_ - kp.static_next;");
+            E.line("      if ((uint64_t)o_ + %uu <= kp.stack_size) v_ = stack_load(kp, L, o_, %uu);", n, n);
+            break;
+        case HINT_CTX:
+            E.line("      const uint32_t o_ = a_ - (P + L.M + 1);");
+            E.line("      if ((uint64_t)o_ + %uu <= MIMIC_XDP_MD_SIZE) v_ = xdp_load(kp, L, o_, %uu);", n, n);
+            break;
+        default:
+            E.line("      const uint32_t o_ = a_ - P;");
+            if (stage) E.line("      if ((uint64_t)o_ + %uu <= W_) v_ = win_load(pwin_, tl_, o_, %uu); else", n, n);
+            E.line("      if ((uint64_t)o_ + %uu <= L.M) v_ = ld_n(L.pkt + o_, %uu);", n, n);
+            break;
+        }
+        E.line("      else { const int s_ = mem_load(kp, L, resolve(kp, L, a_), %uu, v_); if (s_) TERM(s_, %u); }", n, i);
+        E.line("      %s = v_; }", dst.c_str());
+    }
+
+    void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val) {
+        if (!fast_paths) {
+            E.line("    { const int s_ = mem_store(kp, L, resolve(kp, L, %s), %uu, %s); if (s_) TERM(s_, %u); }",
+                   addr(base, off).c_str(), n, val.c_str(), i);
+            return;
+        }
+        E.line("    { const uint32_t a_ = %s;", addr(base, off).c_str());
+        switch (hint(base)) {
+        case HINT_STACK:
+            E.line("      const uint32_t o_ = a_ - kp.static_next;");
+            E.line("      if ((uint64_t)o_ + %uu <= kp.stack_size) stack_store(kp, L, o_, %uu, %s);", n, n, val.c_str());
+            break;
+        case HINT_CTX:
+            E.line("      const uint32_t o_ = a_ - (P + L.M + 1);");
+            E.line("      if ((uint64_t)o_ + %uu <= MIMIC_XDP_MD_SIZE) xdp_store(kp, L, o_, %uu, %s);", n, n, val.c_str());
+            break;
+        default:
+            E.line("      const uint32_t o_ = a_ - P;");
+            if (stage)
+                E.line("      if ((uint64_t)o_ + %uu <= L.M) { st_n(L.pkt + o_, %uu, %s); if (o_ < W_) win_store(pwin_, tl_, W_, o_, %uu, %s); }",
+                       n, n, val.c_str(), n, val.c_str());
+            else E.line("      if ((uint64_t)o_ + %uu <= L.M) st_n(L.pkt + o_, %uu, %s);", n, n, val.c_str());
+            break;
+        }
+        if (stage)  // a store that reaches the packet through another hint must update the window too
+            E.line("      else { const Ref R_ = resolve(kp, L, a_); const int s_ = mem_store(kp, L, R_, %uu, %s); if (s_) TERM(s_, %u);"
+                   " if (R_.ptr == L.pkt && R_.rk == RK_GLOBAL && R_.off < W_) win_store(pwin_, tl_, W_, R_.off, %uu, %s); } }",
+                   n, val.c_str(), i, n, val.c_str());
+        else
+            E.line("      else { const int s_ = mem_store(kp, L, resolve(kp, L, a_), %uu, %s); if (s_) TERM(s_, %u); } }", n,
+                   val.c_str(), i);
+    }
+
     void insn(const ProgView &p, uint32_t i) {
         const DInsn &x = p.ins[i];
         const uint32_t op = insn_op(x), d = insn_dst(x), s = insn_src(x);
@@ -265,13 +395,11 @@ class Gen {
             jump(p, i);
             break;
         case H_LDX:
-            E.line("    { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, %s), %uu, v_); if (s_) TERM(s_, %u); %s = v_; }",
-                   addr(s, off).c_str(), AUX_SZ(x.aux), i, reg(d).c_str());
+            load(i, s, off, AUX_SZ(x.aux), reg(d));
             break;
         case H_ST:
         case H_STX:
-            E.line("    { const int s_ = mem_store(kp, L, resolve(kp, L, %s), %uu, %s); if (s_) TERM(s_, %u); }",
-                   addr(d, off).c_str(), AUX_SZ(x.aux), h == H_STX ? reg(s).c_str() : imm(x.k).c_str(), i);
+            store(i, d, off, AUX_SZ(x.aux), h == H_STX ? reg(s) : imm(x.k));
             break;
         case H_EXIT:  // inst.go:277-296
             if (!any_local) {
@@ -324,7 +452,8 @@ class Gen {
         const DInsn &x = p.ins[i];
         switch ((uint32_t)x.k) {
         case 1:
-            E.line("    { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
+            E.line("    { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0;", i);
+            E.line("      if (ho.t_n) { L.t_lo = ho.t_lo; L.t_n = ho.t_n; L.t_ptr = ho.t_ptr; } }");
             break;
         case 2:
             E.line("    { const HelperOut ho = helper_update(kp, L, r1, r2, r3); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
@@ -495,6 +624,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->checks_budget = g.careful_copies;
         info->max_n = g.max_n;
         info->tail_calls = g.has_tail();
+        info->kp_by_value = g.kp_by_value;
     }
     return src;
 }
@@ -536,11 +666,12 @@ int mimic_jit_prebuild_source(const std::string &src, std::string *log) {
     return build_code(src, code, log);
 }
 
-int mimic_jit_launch(hipFunction_t fn, const KParams *kp, hipStream_t st) {
+int mimic_jit_launch(hipFunction_t fn, const JitInfo &info, const KParams *kp, const KParams *d_kp, hipStream_t st) {
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
-    KParams k = *kp;
-    void *args[] = {&k};
+    const KParams *p = d_kp;
+    KParams v = *kp;
+    void *args[] = {info.kp_by_value ? (void *)&v : (void *)&p};
     return hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
 }
 

@@ -12,6 +12,7 @@ struct JitInfo {
     bool checks_budget;  // the kernel has the per-block budget checks (loops / BPF-to-BPF calls)
     uint32_t max_n;      // longest program
     bool tail_calls;     // some program calls bpf_tail_call
+    bool kp_by_value;    // the kernel takes KParams by value (else a pointer to a device copy)
 };
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, JitInfo *info);
 // 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
@@ -19,7 +20,8 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
 uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);
 // hipRTC compile for gfx950 + module load on the current device (cached per device and source)
 int mimic_jit_compile(int device, const std::string &src, hipFunction_t *fn, std::string *log);
-int mimic_jit_launch(hipFunction_t fn, const KParams *kp, hipStream_t st);
+// d_kp: the launch parameters in device memory
+int mimic_jit_launch(hipFunction_t fn, const JitInfo &info, const KParams *kp, const KParams *d_kp, hipStream_t st);
 // hipRTC compile only, no device needed
 int mimic_jit_check_source(const std::string &src, std::string *log, size_t *code_size);
 // compile into the MIMIC_JIT_CACHE directory without a device (prewarming)

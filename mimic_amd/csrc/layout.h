@@ -149,7 +149,7 @@ struct KParams {
     uint32_t n;
     uint32_t sched;
     uint32_t per_lane;          // CHUNKED: chunk; INTERLEAVED/EXPLICIT: max packets per lane
-    uint32_t pad0;
+    uint32_t sched_shift;       // INTERLEAVED: index of packet 0 in the whole batch, mod lanes (sub-batches)
     uint8_t *pkt_data;
     const uint64_t *pkt_off;
     const uint32_t *pkt_len;

@@ -55,6 +55,11 @@ struct Lane {
     uint32_t xdp_dirty;
     uint64_t sm0, sm1;    // stack words / granules already written in this process
     uint32_t nframes, tailcalls;
+    // one-entry translation cache of a static plain region (a map value backing, set by the
+    // lookup helper): addresses in [t_lo, t_lo + t_n) resolve to t_ptr + (a - t_lo) without
+    // the segment scan.  Static entries never move, so an entry stays exact; t_n = 0 = empty.
+    uint32_t t_lo, t_n;
+    uint8_t *t_ptr;
 };
 
 static constexpr int EXIT_SIG = -1;
@@ -233,6 +238,13 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
         }
         return R;
     }
+    if (a - L.t_lo < L.t_n) {
+        R.rk = RK_GLOBAL;
+        R.ptr = L.t_ptr;
+        R.off = a - L.t_lo;
+        R.limit = L.t_n - 1;
+        return R;
+    }
     bool found = false;
     for (uint32_t s = 0; s < kp.nsegs; s++) {
         const Seg g = cget(kp.segs, s);
@@ -407,7 +419,16 @@ struct HelperOut {
     bool set_r0;
     bool tail;       // tail call taken
     uint32_t new_prog;
+    uint32_t t_lo, t_n;  // translation-cache entry for the returned value's region (t_n = 0: none)
+    uint8_t *t_ptr;
 };
+
+// the map descriptor: scalar loads when every active lane names the same map (the usual case)
+DEV DMap load_map(const KParams &kp, int32_t mid) {
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(mid);
+    if (__ballot(mid != m0) == 0) return cget(kp.maps, (uint32_t)m0);
+    return kp.maps[mid];
+}
 
 // resolve the concrete array (sub-array) a LinuxMap reference names for this process
 // returns 0 ok, or MIMIC_ERR_HELPER_MAP_OP for per-CPU cpuid errors
@@ -422,10 +443,10 @@ DEV int array_target(const DMap &m, int32_t sub, int32_t cpu, int32_t &which) {
 }
 
 DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint64_t r2) { // :477-504
-    HelperOut o = {0, 0, false, false, 0};
+    HelperOut o = {0, 0, false, false, 0, 0, 0, nullptr};
     int32_t mid, sub;
     if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
+    const DMap m = load_map(kp, mid);
     Ref K = resolve(kp, L, (uint32_t)r2);
     if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
     if (m.family == FAM_ARRAY || m.family == FAM_PERCPU_ARRAY) {
@@ -435,6 +456,11 @@ DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint6
         uint32_t k = (uint32_t)region_load(kp, L, K, K.off, 4);
         o.r0 = array_value_addr(m, which, k);
         o.set_r0 = true;
+        if (o.r0) {  // the values backing of that (sub-)array: [base, base + E*S] (inclusive end)
+            o.t_lo = m.backing_addr + (which > 0 ? (uint32_t)which * m.addr_period : 0u);
+            o.t_n = m.max_entries * m.value_size + 1;
+            o.t_ptr = array_value_ptr(kp, m, which, 0);
+        }
         return o;
     }
     // LinuxHashMap.Lookup :134-155 / LinuxPerCPUHashMap.Lookup :537-561
@@ -443,14 +469,19 @@ DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint6
     const int32_t idx = h_find(h_table(kp.arena, m), ks, h_hash(ks, m.key_size), nullptr);
     o.r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
     o.set_r0 = true;
+    if (idx >= 0) {
+        o.t_lo = hash_value_addr(m, L.cpu, 0);
+        o.t_n = m.max_entries * m.value_size + 1;
+        o.t_ptr = hash_value_ptr(kp, m, L.cpu, 0);
+    }
     return o;
 }
 
 DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint64_t r2, uint64_t r3) { // :506-555
-    HelperOut o = {0, 0, false, false, 0};
+    HelperOut o = {0, 0, false, false, 0, 0, 0, nullptr};
     int32_t mid, sub;
     if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
+    const DMap m = load_map(kp, mid);
     Ref K = resolve(kp, L, (uint32_t)r2);
     if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
     Ref V = resolve(kp, L, (uint32_t)r3);
@@ -506,10 +537,10 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
 }
 
 DEV HelperOut helper_delete(const KParams &kp, const Lane &L, uint64_t r1, uint64_t r2) { // :557-586
-    HelperOut o = {0, 0, false, false, 0};
+    HelperOut o = {0, 0, false, false, 0, 0, 0, nullptr};
     int32_t mid, sub;
     if (!reg_to_map(kp, L, r1, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
+    const DMap m = load_map(kp, mid);
     if (m.family == FAM_ARRAY || m.family == FAM_PERCPU_ARRAY) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
     Ref K = resolve(kp, L, (uint32_t)r2);
     if (!readable(K, m.key_size)) { o.st = MIMIC_ERR_HELPER_KEY; return o; }
@@ -529,7 +560,7 @@ DEV HelperOut helper_delete(const KParams &kp, const Lane &L, uint64_t r1, uint6
 }
 
 DEV HelperOut helper_tailcall(const KParams &kp, const Lane &L, uint64_t r2, uint64_t r3) { // :649-738
-    HelperOut o = {0, 0, false, false, 0};
+    HelperOut o = {0, 0, false, false, 0, 0, 0, nullptr};
     if (L.tailcalls >= kp.max_tail_calls) {
         o.r0 = (uint64_t)(int64_t)-1; // -EPERM
         o.set_r0 = true;
@@ -537,7 +568,7 @@ DEV HelperOut helper_tailcall(const KParams &kp, const Lane &L, uint64_t r2, uin
     }
     int32_t mid, sub;
     if (!reg_to_map(kp, L, r2, mid, sub)) { o.st = MIMIC_ERR_HELPER_MAP_PTR; return o; }
-    const DMap m = kp.maps[mid];
+    const DMap m = load_map(kp, mid);
     if (m.type != MIMIC_MAP_PROG_ARRAY || m.key_size != 4 || m.family != FAM_ARRAY) {
         o.st = MIMIC_ERR_HELPER_TAILCALL;
         return o;
@@ -707,3 +738,40 @@ DEV uint64_t alu32(uint32_t hi, uint64_t d, uint64_t x) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// JIT packet window: the first bytes of each lane's packet memory staged in LDS, qword-
+// interleaved across the block's lanes ([q][lane]: uniform offsets are conflict-free).  The
+// window is a copy of global packet memory: every packet store updates both.
+// ---------------------------------------------------------------------------------------
+#define PWIN_Q 8u        // qwords per lane (64 bytes)
+#define PWIN_LANES 256u  // block size
+typedef uint64_t PWin[PWIN_Q][PWIN_LANES];
+
+// stage pkt[0, W) with W = min(M, 64) rounded down to whole qwords; returns W
+DEV uint32_t win_stage(PWin &w, uint32_t tl, const uint8_t *pkt, uint32_t M) {
+    const uint32_t W = M >= PWIN_Q * 8 ? PWIN_Q * 8 : (M & ~7u);
+#pragma unroll
+    for (uint32_t q = 0; q < PWIN_Q; q++)
+        if (q * 8 < W) w[q][tl] = *(const u64u *)(pkt + q * 8);
+    return W;
+}
+// n bytes at offset o, o + n <= W
+DEV uint64_t win_load(const PWin &w, uint32_t tl, uint32_t o, uint32_t n) {
+    const uint32_t q = o >> 3, sh = (o & 7) * 8;
+    uint64_t v = w[q][tl] >> sh;
+    if (sh + 8 * n > 64) v |= w[q + 1][tl] << (64 - sh);
+    return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
+}
+// mirror a packet store of n bytes at offset o (o < W) into the window
+DEV void win_store(PWin &w, uint32_t tl, uint32_t W, uint32_t o, uint32_t n, uint64_t v) {
+    const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+    v &= m;
+    const uint32_t q = o >> 3, sh = (o & 7) * 8;
+    w[q][tl] = (w[q][tl] & ~(m << sh)) | (v << sh);
+    if (sh + 8 * n > 64 && (q + 1) * 8 < W) {
+        const uint32_t bits = sh + 8 * n - 64;
+        const uint64_t m1 = (1ull << bits) - 1;
+        w[q + 1][tl] = (w[q + 1][tl] & ~m1) | (v >> (64 - sh));
+    }
+}

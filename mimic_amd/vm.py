@@ -415,48 +415,53 @@ class VM:
     def RunXDPBatch(self, prog_id: int, batch: "XDPBatch", results: Optional["XDPResults"] = None,
                     stream=None, sync: bool = True) -> "XDPResults":
         """N x {NewProcess, SetCPUID, Run, read R0, Cleanup} on the GPU."""
-        import torch
-
-        dev = batch.pkt_data.device
         if results is None:
-            results = XDPResults.empty(batch.n, dev)
-        b = L.XDPBatch()
-        b.n = batch.n
-        b.schedule = batch.schedule
-        b.pkt_data = batch.pkt_data.data_ptr()
-        b.pkt_off = batch.pkt_off.data_ptr()
-        b.pkt_len = batch.pkt_len.data_ptr()
-        b.headroom = batch.headroom.data_ptr() if isinstance(batch.headroom, torch.Tensor) else None
-        b.headroom_all = 0 if isinstance(batch.headroom, torch.Tensor) else int(batch.headroom)
-        b.tailroom = batch.tailroom.data_ptr() if isinstance(batch.tailroom, torch.Tensor) else None
-        b.tailroom_all = 0 if isinstance(batch.tailroom, torch.Tensor) else int(batch.tailroom)
-        for fld, val in (("ingress_ifindex", batch.ingress), ("rx_queue_index", batch.rxq),
-                         ("egress_ifindex", batch.egress)):
-            allname = {"ingress_ifindex": "ingress_all", "rx_queue_index": "rxq_all",
-                       "egress_ifindex": "egress_all"}[fld]
-            if isinstance(val, torch.Tensor):
-                setattr(b, fld, val.data_ptr())
-                setattr(b, allname, 0)
-            else:
-                setattr(b, fld, None)
-                setattr(b, allname, int(val))
-        cpu_host = None
-        if batch.schedule == L.SCHED_EXPLICIT:
-            import numpy as np
-            cpu_host = np.ascontiguousarray(np.asarray(batch.cpu, dtype=np.int32))
-            b.cpu = cpu_host.ctypes.data
-        else:
-            b.cpu = None
-        b.step_budget = batch.step_budget
-        def ptr(t):
-            return t.data_ptr() if t is not None else None
-
-        r = L.XDPResults(ptr(results.r0), ptr(results.status), ptr(results.steps), ptr(results.err_pc))
+            results = XDPResults.empty(batch.n, batch.pkt_data.device)
+        b = batch._c()
+        r = results._c()
         st = stream.cuda_stream if stream is not None else None
-        _check(self.h, self.lib.mimic_run_xdp(self.h, prog_id, C.byref(b), C.byref(r), st), "RunXDPBatch")
+        rc = self.lib.mimic_run_xdp(self.h, prog_id, b, r, st)
+        if rc:
+            _check(self.h, rc, "RunXDPBatch")
         if sync:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
         return results
+
+    def RunXDPHost(self, prog_id: int, buf, off, lens, schedule=L.SCHED_INTERLEAVED, cpu=None, headroom: int = 0,
+                   tailroom: int = 0, ingress: int = 0, rxq: int = 0, egress: int = 0, step_budget: int = 0,
+                   chunks: int = 0, pkt_out=None, r0=None, status=None):
+        """A batch resident in HOST memory (numpy arrays): the engine pipelines H2D copies, the
+        kernels and the D2H copies of r0/status (and of the packet memory into pkt_out).
+        Returns (r0 uint64[n], status uint8[n]).  Register the arrays (HostRegister) for
+        asynchronous copies."""
+        import numpy as np
+
+        n = len(lens)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        r0 = np.empty(n, np.uint64) if r0 is None else r0
+        status = np.empty(n, np.uint8) if status is None else status
+        hb = L.XDPHostBatch()
+        hb.n, hb.schedule = n, schedule
+        hb.pkt_data, hb.pkt_off, hb.pkt_len = buf.ctypes.data, off.ctypes.data, lens.ctypes.data
+        hb.headroom_all, hb.tailroom_all = headroom, tailroom
+        hb.ingress_all, hb.rxq_all, hb.egress_all = ingress, rxq, egress
+        cpu_arr = None
+        if cpu is not None:
+            cpu_arr = np.ascontiguousarray(cpu, dtype=np.int32)
+            hb.cpu = cpu_arr.ctypes.data
+        hb.step_budget = step_budget
+        hb.pkt_out = pkt_out.ctypes.data if pkt_out is not None else None
+        hb.r0, hb.status = r0.ctypes.data, status.ctypes.data
+        _check(self.h, self.lib.mimic_run_xdp_host(self.h, prog_id, C.byref(hb), chunks), "RunXDPHost")
+        return r0, status
+
+    def HostRegister(self, arr) -> None:
+        """Pin a numpy array's memory for DMA (hipHostRegister)."""
+        _check(self.h, self.lib.mimic_host_register(arr.ctypes.data, arr.nbytes), "host register")
+
+    def HostUnregister(self, arr) -> None:
+        _check(self.h, self.lib.mimic_host_unregister(arr.ctypes.data), "host unregister")
 
     def LastSteps(self) -> int:
         v = C.c_uint64()
@@ -558,6 +563,44 @@ class XDPBatch:
     def n(self) -> int:
         return int(self.pkt_len.numel())
 
+    def _c(self):
+        """The mimic_xdp_batch of this batch (built once; a batch is not modified after use)."""
+        cached = getattr(self, "_cstruct", None)
+        if cached is not None:
+            return cached
+        import torch
+
+        b = L.XDPBatch()
+        b.n = self.n
+        b.schedule = self.schedule
+        b.pkt_data = self.pkt_data.data_ptr()
+        b.pkt_off = self.pkt_off.data_ptr()
+        b.pkt_len = self.pkt_len.data_ptr()
+        b.headroom = self.headroom.data_ptr() if isinstance(self.headroom, torch.Tensor) else None
+        b.headroom_all = 0 if isinstance(self.headroom, torch.Tensor) else int(self.headroom)
+        b.tailroom = self.tailroom.data_ptr() if isinstance(self.tailroom, torch.Tensor) else None
+        b.tailroom_all = 0 if isinstance(self.tailroom, torch.Tensor) else int(self.tailroom)
+        for fld, allname, val in (("ingress_ifindex", "ingress_all", self.ingress), ("rx_queue_index", "rxq_all", self.rxq),
+                                  ("egress_ifindex", "egress_all", self.egress)):
+            if isinstance(val, torch.Tensor):
+                setattr(b, fld, val.data_ptr())
+                setattr(b, allname, 0)
+            else:
+                setattr(b, fld, None)
+                setattr(b, allname, int(val))
+        self._cpu_host = None
+        if self.schedule == L.SCHED_EXPLICIT:
+            import numpy as np
+
+            self._cpu_host = np.ascontiguousarray(np.asarray(self.cpu, dtype=np.int32))
+            b.cpu = self._cpu_host.ctypes.data
+        else:
+            b.cpu = None
+        b.step_budget = self.step_budget
+        self._cstruct = C.byref(b)
+        self._cstruct_obj = b
+        return self._cstruct
+
     @staticmethod
     def layout(lengths: Sequence[int], headroom=0, tailroom=0, align: int = 64):
         """Offsets of each packet memory (H+L+T) in one buffer, each aligned to `align`."""
@@ -622,6 +665,16 @@ class XDPBatch:
 class XDPResults:
     def __init__(self, r0, status, steps, err_pc):
         self.r0, self.status, self.steps, self.err_pc = r0, status, steps, err_pc
+
+    def _c(self):
+        cached = getattr(self, "_cstruct", None)
+        if cached is None:
+            def ptr(t):
+                return t.data_ptr() if t is not None else None
+
+            self._cstruct_obj = L.XDPResults(ptr(self.r0), ptr(self.status), ptr(self.steps), ptr(self.err_pc))
+            cached = self._cstruct = C.byref(self._cstruct_obj)
+        return cached
 
     @classmethod
     def empty(cls, n: int, device, full: bool = True):

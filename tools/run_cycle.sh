@@ -1,0 +1,12 @@
+# one build->measure cycle: GPU tests in both engines, host/launch probes, benches
+set -e
+mkdir -p gpurun_out/$TAG
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/$TAG/tests_jit.log 2>&1 || { tail -40 gpurun_out/$TAG/tests_jit.log; exit 1; }
+tail -1 gpurun_out/$TAG/tests_jit.log
+MIMIC_EXEC=interp timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/$TAG/tests_interp.log 2>&1 || { tail -40 gpurun_out/$TAG/tests_interp.log; exit 1; }
+tail -1 gpurun_out/$TAG/tests_interp.log
+timeout -k 10 300 python tools/host_probe.py > gpurun_out/$TAG/hp.log 2>&1
+timeout -k 10 120 python tools/launch_probe.py >> gpurun_out/$TAG/hp.log 2>&1
+grep -v amdgpu.ids gpurun_out/$TAG/hp.log
+bash tools/run_bench.sh
