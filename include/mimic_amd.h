@@ -69,7 +69,10 @@ enum mimic_status {
     MIMIC_ERR_STEP_LIMIT = 22,       /* step budget (stands for Run's ctx deadline, vm.go:344-350) */
     MIMIC_ERR_CALL_DEPTH = 23,       /* > MIMIC_MAX_FRAMES nested BPF-to-BPF calls */
     MIMIC_ERR_ENGINE_HELPER = 24,    /* helper the reference emulates but this engine does not */
-    MIMIC_ERR_NO_CPU = 25
+    MIMIC_ERR_NO_CPU = 25,
+    MIMIC_ERR_CTX_ACCESS = 26,       /* __sk_buff / bpf_sock / bpf_flow_keys field error, emulator_linux_sk_buff.go */
+    MIMIC_PANIC_SLICE = 27,          /* Go slice-bounds panic in those accessors */
+    MIMIC_ERR_CTX_LOAD = 28          /* Context.Load failed (SKBuffFromBytes error, out of address space) */
 };
 
 /* Linux map types (ebpf.MapType). */

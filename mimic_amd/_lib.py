@@ -20,7 +20,8 @@ STATUS_NAMES = [
     "ERR_HELPER_KEY", "ERR_HELPER_VALUE", "ERR_HELPER_MAP_OP", "ERR_HELPER_TAILCALL",
     "ERR_HELPER_UNIMPLEMENTED", "ERR_HELPER_CANT_EMULATE", "ERR_LDABS", "PANIC_DIV0",
     "PANIC_SHIFT", "PANIC_BADREG", "PANIC_CALLX", "PANIC_PC", "PANIC_HELPER_NEG",
-    "ERR_STEP_LIMIT", "ERR_CALL_DEPTH", "ERR_ENGINE_HELPER", "ERR_NO_CPU",
+    "ERR_STEP_LIMIT", "ERR_CALL_DEPTH", "ERR_ENGINE_HELPER", "ERR_NO_CPU", "ERR_CTX_ACCESS", "PANIC_SLICE",
+    "ERR_CTX_LOAD",
 ]
 STATUS = {n: i for i, n in enumerate(STATUS_NAMES)}
 

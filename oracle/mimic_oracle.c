@@ -35,7 +35,7 @@
 /* objects registered in the memory controller                               */
 /* ------------------------------------------------------------------------- */
 
-typedef enum { K_PLAIN, K_ARRAY, K_PERCPU_ARRAY, K_HASH, K_PERCPU_HASH, K_PROG } objkind;
+typedef enum { K_PLAIN, K_ARRAY, K_PERCPU_ARRAY, K_HASH, K_PERCPU_HASH, K_PROG, K_SKB, K_SK, K_FK } objkind;
 
 typedef struct {
     uint8_t *b;
@@ -103,6 +103,8 @@ struct orc_vm {
     int nprogs;
     plain_mem **scratch;
     int nscratch;
+    void **leaks;   /* sk_buff contexts' sock / flow_keys / packet objects: never freed by Cleanup */
+    int nleaks, cap_leaks;
     char err[256];
 };
 
@@ -123,6 +125,7 @@ struct orc_proc {
     /* xdp_md context (context_xdp_md.go:22-34) */
     int has_ctx;
     plain_mem *pkt, *xdpmd;
+    struct skb_state *skb;  /* sk_buff context (context_sk_buff.go:20-29) */
 };
 
 static void set_err(orc_vm *vm, const char *fmt, ...) {
@@ -289,10 +292,13 @@ static void pm_free(plain_mem *m) {
     free(m);
 }
 
+static int skb_access(void *obj, objkind kind, uint32_t off, int n, uint64_t *v, int load);
+
 /* VMMem dispatch for an entry: PlainMemory or LinuxArrayMap (emulator_linux_map_array.go:134-168).
  * Returns ORC_ERR_MEM_NOT_VMMEM for objects that do not implement VMMem. */
 static int vm_load(entry *e, uint32_t off, int n, uint64_t *v) {
     if (e->kind == K_PLAIN) return pm_load((plain_mem *)e->obj, off, n, v);
+    if (e->kind == K_SKB || e->kind == K_SK || e->kind == K_FK) return skb_access(e->obj, e->kind, off, n, v, 1);
     if (e->kind == K_ARRAY) {
         orc_map *m = (orc_map *)e->obj;
         if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
@@ -302,6 +308,7 @@ static int vm_load(entry *e, uint32_t off, int n, uint64_t *v) {
 }
 static int vm_store(entry *e, uint32_t off, uint64_t v, int n) {
     if (e->kind == K_PLAIN) return pm_store((plain_mem *)e->obj, off, v, n);
+    if (e->kind == K_SKB || e->kind == K_SK || e->kind == K_FK) return skb_access(e->obj, e->kind, off, n, &v, 0);
     if (e->kind == K_ARRAY) {
         orc_map *m = (orc_map *)e->obj;
         if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
@@ -311,6 +318,7 @@ static int vm_store(entry *e, uint32_t off, uint64_t v, int n) {
 }
 static int vm_read(entry *e, uint32_t off, uint8_t *out, uint32_t n) {
     if (e->kind == K_PLAIN) return pm_read((plain_mem *)e->obj, off, out, n);
+    if (e->kind == K_SKB || e->kind == K_SK || e->kind == K_FK) return ORC_ERR_CTX_ACCESS; /* "not implemented" */
     if (e->kind == K_ARRAY) {
         orc_map *m = (orc_map *)e->obj;
         if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
@@ -320,6 +328,7 @@ static int vm_read(entry *e, uint32_t off, uint8_t *out, uint32_t n) {
 }
 static int vm_write(entry *e, uint32_t off, const uint8_t *in, uint32_t n) {
     if (e->kind == K_PLAIN) return pm_write((plain_mem *)e->obj, off, in, n);
+    if (e->kind == K_SKB || e->kind == K_SK || e->kind == K_FK) return ORC_ERR_CTX_ACCESS;
     if (e->kind == K_ARRAY) {
         orc_map *m = (orc_map *)e->obj;
         if (!m->spec->datasec) return ORC_ERR_MEM_NOT_DATASEC;
@@ -327,7 +336,7 @@ static int vm_write(entry *e, uint32_t off, const uint8_t *in, uint32_t n) {
     }
     return ORC_ERR_MEM_NOT_VMMEM;
 }
-static int is_vmmem(objkind k) { return k == K_PLAIN || k == K_ARRAY; }
+static int is_vmmem(objkind k) { return k == K_PLAIN || k == K_ARRAY || k == K_SKB || k == K_SK || k == K_FK; }
 static int is_linuxmap(objkind k) { return k == K_ARRAY || k == K_PERCPU_ARRAY || k == K_HASH || k == K_PERCPU_HASH; }
 
 /* ------------------------------------------------------------------------- */
@@ -375,6 +384,8 @@ void orc_vm_free(orc_vm *vm) {
     }
     for (int i = 0; i < vm->nscratch; i++) pm_free(vm->scratch[i]);
     free(vm->scratch);
+    for (int i = 0; i < vm->nleaks; i++) free(vm->leaks[i]);
+    free(vm->leaks);
     free(vm->maps);
     free(vm->progs);
     free(vm->e);
@@ -1202,12 +1213,33 @@ static int h_st(orc_proc *p, const insn *i, int reg) {
     return vm_store(e, off, s, size_bytes(i->op));
 }
 
-/* LinuxEmulator.CustomInstruction, emulator_linux_.go:198-288 (XDP path: R6 is never a *SKBuff) */
+/* LinuxEmulator.CustomInstruction, emulator_linux_.go:198-288: LD_ABS / LD_IND read the
+ * __sk_buff's packet (R6 must resolve to the *SKBuff entry), R0 = big-endian load at
+ * skb.data + [src] + imm, then R1-R5 are clobbered.  Every failure is one error status. */
+static uint32_t skb_data_addr(void *skb);
 static int h_custom(orc_proc *p, const insn *i) {
     switch (i->op) {
     case 0x20: case 0x28: case 0x30: case 0x38:
-    case 0x40: case 0x48: case 0x50: case 0x58:
-        return ORC_ERR_LDABS;
+    case 0x40: case 0x48: case 0x50: case 0x58: {
+        uint32_t off;
+        entry *e = mc_get(p->vm, (uint32_t)p->R.r[6], &off);
+        if (!e || e->kind != K_SKB) return ORC_ERR_LDABS;
+        uint32_t addr = skb_data_addr(e->obj) + (uint32_t)i->k;
+        if (i->op & 0x40) {
+            uint64_t s;
+            GET(i->src, s); /* Registers.Get panics on a bad register (vm.go:431-432) */
+            addr = skb_data_addr(e->obj) + (uint32_t)s + (uint32_t)i->k;
+        }
+        entry *pe = mc_get(p->vm, addr, &off);
+        if (!pe || !is_vmmem(pe->kind)) return ORC_ERR_LDABS;
+        uint64_t v;
+        int rc = vm_load(pe, off, size_bytes(i->op), &v);
+        if (rc == ORC_PANIC_SLICE) return rc; /* a Go panic propagates as a panic */
+        if (rc) return ORC_ERR_LDABS;
+        p->R.r[0] = v;
+        for (int r = 1; r <= 5; r++) p->R.r[r] = 0;
+        return 0;
+    }
     }
     return ORC_ERR_UNSUPPORTED_OP;
 }
@@ -1410,6 +1442,481 @@ int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_resul
         if (out->steps) out->steps[i] = steps;
         if (out->err_pc) out->err_pc[i] = st == ORC_OK ? -1 : epc;
         if (b->write_back) memcpy(mem, p->pkt->b, H + L + T);
+        orc_proc_free(p);
+    }
+    return 0;
+}
+
+/* ========================================================================= */
+/* sk_buff context: context_sk_buff.go + emulator_linux_sk_buff.go           */
+/* ========================================================================= */
+
+/* A net.IP as the reference holds it: kind 0 = make(net.IP, n) (zeros, cap n), 1 = nil
+ * (cap 0), 2 = a slice of gopacket's copy of the packet starting at byte `off` (cap = L - off;
+ * Go lets s[a:b] reach up to the capacity, so reads may run past the address). */
+typedef struct {
+    int kind;
+    uint32_t off, n;
+} go_ip;
+
+typedef struct sk_state { /* SK, emulator_linux_sk_buff.go:700-720 */
+    uint32_t bound_dev_if, family, sock_type, protocol, mark, priority;
+    go_ip src4, src6, dst4, dst6;
+    uint32_t src_port, dst_port, state;
+    int32_t rx_queue_mapping;
+    const uint8_t *pkt; /* gopacket's copy of the packet (immutable) */
+    uint32_t L;
+} sk_state;
+
+typedef struct fk_state { /* FlowKeys, :1003-1019 */
+    uint16_t nhoff, thoff, addr_proto;
+    uint8_t is_frag, is_first_frag, is_encap, ip_proto;
+    uint16_t n_proto, sport, dport;
+    uint32_t flags, flow_label;
+} fk_state;
+
+typedef struct skb_state { /* SKBuff, :35-103 */
+    uint32_t len;
+    uint16_t queue_mapping;
+    uint8_t pkt_type;
+    int vlan_present;
+    uint16_t tc_index;
+    uint32_t priority;
+    int32_t skb_iif;
+    uint32_t hash;
+    uint16_t vlan_proto, vlan_tci;
+    uint32_t napi_id, mark;
+    uint16_t protocol;
+    uint8_t cb[48];
+    int64_t tstamp;     /* time.Time as Unix seconds; the zero Time is -62135596800 */
+    uint32_t head, data, tail, end;
+    uint32_t sk_addr, fk_addr, dev_ifindex;
+    sk_state *sk;
+    fk_state *fk;
+    plain_mem *pkt;
+} skb_state;
+
+static uint32_t skb_data_addr(void *skb) { return ((skb_state *)skb)->data; }
+
+static uint64_t to_size(uint64_t v, int n) {
+    return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
+}
+
+/* b2i over n bytes, big endian (the convertAccess helpers) */
+static uint64_t be_bytes(const uint8_t *b, int n) {
+    uint64_t v = 0;
+    for (int k = 0; k < n; k++) v = (v << 8) | b[k];
+    return v;
+}
+
+/* copy(v, ip[start:start+n]) then b2i: a slice-bounds panic when start+n exceeds the capacity */
+static int ip_load(const sk_state *sk, const go_ip *ip, uint64_t start, int n, uint64_t *v) {
+    uint64_t cap = ip->kind == 0 ? ip->n : ip->kind == 1 ? 0 : (uint64_t)sk->L - ip->off;
+    if (start + (uint64_t)n > cap) return ORC_PANIC_SLICE;
+    uint8_t b[8] = {0};
+    if (ip->kind == 2)
+        for (int k = 0; k < n; k++) b[k] = sk->pkt[ip->off + start + k];
+    *v = be_bytes(b, n);
+    return 0;
+}
+
+#define RO() do { if (!load) return ORC_ERR_CTX_ACCESS; } while (0)
+
+/* SKBuff.convertAccess, emulator_linux_sk_buff.go:295-676 */
+static int skb_convert(skb_state *s, uint32_t off, int n, uint64_t *v, int load) {
+    uint64_t val = *v;
+    switch (off) {
+    case 0: RO(); *v = to_size(s->len, n); return 0;                            /* len */
+    case 4: RO(); *v = to_size(s->pkt_type & 7, n); return 0;                   /* pkt_type */
+    case 8: if (load) *v = to_size(s->mark, n); else s->mark = (uint32_t)to_size(val, n); return 0;
+    case 12: if (load) *v = to_size(s->queue_mapping, n); else s->queue_mapping = (uint16_t)to_size(val, n); return 0;
+    case 16: RO(); *v = to_size(s->protocol, n); return 0;
+    case 20: RO(); *v = s->vlan_present ? 1 : 0; return 0;
+    case 24: RO(); *v = to_size(s->vlan_tci, n); return 0;
+    case 28: RO(); *v = to_size(s->vlan_proto, n); return 0;
+    case 32: if (load) *v = to_size(s->priority, n); else s->priority = (uint32_t)to_size(val, n); return 0;
+    case 36: RO(); *v = to_size((uint64_t)(int64_t)s->skb_iif, n); return 0;  /* ingress_ifindex */
+    case 40: RO(); *v = to_size(s->dev_ifindex, n); return 0;                 /* ifindex */
+    case 44: if (load) *v = to_size(s->tc_index, n); else s->tc_index = (uint16_t)to_size(val, n); return 0;
+    case 68: RO(); *v = to_size(s->hash, n); return 0;
+    case 72: /* tc_classid: native u16 at cb[6:8] */
+        if (load) *v = (uint64_t)(s->cb[6] | (s->cb[7] << 8));
+        else { s->cb[6] = (uint8_t)val; s->cb[7] = (uint8_t)(val >> 8); }
+        return 0;
+    case 76: RO(); *v = to_size(s->data, n); return 0;                         /* data */
+    case 80: RO(); *v = (uint64_t)s->cb[32] | ((uint64_t)s->cb[33] << 8) | ((uint64_t)s->cb[34] << 16) |
+                        ((uint64_t)s->cb[35] << 24); return 0;                  /* data_end: cb[32:36] */
+    case 84: RO(); *v = to_size(s->napi_id, n); return 0;
+    case 88: RO(); *v = to_size(s->sk->family, n); return 0;
+    case 132: RO(); *v = to_size(s->sk->dst_port, n); return 0;                /* remote_port */
+    case 136: RO(); *v = to_size(s->sk->src_port, n); return 0;                /* local_port */
+    case 140: RO(); *v = (uint64_t)(s->cb[36] | (s->cb[37] << 8)); return 0;  /* data_meta: cb[36:38] */
+    case 144: case 148: RO(); *v = s->fk_addr; return 0;                       /* flow_keys */
+    case 152: case 156:                                                         /* tstamp */
+        if (load) *v = (uint64_t)s->tstamp; else s->tstamp = (int64_t)val;
+        return 0;
+    case 160: RO(); *v = (uint64_t)s->cb[0] | ((uint64_t)s->cb[1] << 8) | ((uint64_t)s->cb[2] << 16) |
+                         ((uint64_t)s->cb[3] << 24); return 0;                  /* wire_len: cb[0:4] */
+    case 164: case 176: case 184: case 188: return ORC_ERR_CTX_ACCESS;        /* gso_segs/gso_size/hwtstamp: "not yet implemented" */
+    case 168: case 172: RO(); *v = s->sk_addr; return 0;                       /* sk */
+    }
+    if (off >= 48 && off < 68) {   /* cb[5]: load = cb[offset:size] -> low > high -> panic; store = no-op */
+        if (load) return ORC_PANIC_SLICE;
+        return 0;
+    }
+    if (off >= 92 && off < 96) { RO(); return ip_load(s->sk, &s->sk->dst4, off - 92, n, v); }   /* remote_ip4 */
+    if (off >= 96 && off < 100) { RO(); return ip_load(s->sk, &s->sk->src4, off - 96, n, v); }  /* local_ip4 */
+    if (off >= 100 && off < 116) { RO(); return ip_load(s->sk, &s->sk->dst6, off - 100, n, v); } /* remote_ip6 */
+    if (off >= 116 && off < 132) { RO(); return ip_load(s->sk, &s->sk->src6, off - 116, n, v); } /* local_ip6 */
+    return ORC_ERR_CTX_ACCESS; /* "invalid offset" */
+}
+
+/* SK.convertAccess, :772-918 */
+static int sk_convert(sk_state *s, uint32_t off, int n, uint64_t *v, int load) {
+    uint64_t val = *v;
+    switch (off) {
+    case 0: if (load) *v = to_size(s->bound_dev_if, n); else s->bound_dev_if = (uint32_t)to_size(val, n); return 0;
+    case 4: RO(); *v = to_size(s->family, n); return 0;
+    case 8: RO(); *v = to_size(s->sock_type, n); return 0;
+    case 12: RO(); *v = to_size(s->protocol, n); return 0;
+    case 16: if (load) *v = to_size(s->mark, n); else s->mark = (uint32_t)to_size(val, n); return 0;
+    case 20: if (load) *v = to_size(s->priority, n); else s->priority = (uint32_t)to_size(val, n); return 0;
+    case 44: RO(); *v = to_size(s->src_port, n); return 0;
+    case 48: RO(); *v = to_size(s->dst_port, n); return 0;
+    case 72: RO(); *v = to_size(s->state, n); return 0;
+    case 76: RO(); *v = to_size((uint64_t)(int64_t)s->rx_queue_mapping, n); return 0;
+    }
+    if (off >= 24 && off < 28) { RO(); return ip_load(s, &s->src4, off - 24, n, v); }
+    if (off >= 28 && off < 44) { RO(); return ip_load(s, &s->src6, off - 28, n, v); }
+    if (off >= 52 && off < 56) { RO(); return ip_load(s, &s->dst4, off - 52, n, v); }
+    if (off >= 56 && off < 72) {   /* dst_ipv6: start := offset - 17*4 (:889), a uint32 that wraps below 68 */
+        RO();
+        uint32_t start = off - 68;
+        return ip_load(s, &s->dst6, (uint64_t)start, n, v);
+    }
+    return ORC_ERR_CTX_ACCESS;
+}
+
+/* FlowKeys.convertAccess, :1031-1175 */
+static int fk_convert(fk_state *f, uint32_t off, int n, uint64_t *v, int load) {
+    uint64_t val = *v;
+#define FK_FIELD(fld, T) do { if (load) *v = to_size(f->fld, n); else f->fld = (T)to_size(val, n); return 0; } while (0)
+    switch (off) {
+    case 0: case 1: FK_FIELD(nhoff, uint16_t);
+    case 2: case 3: FK_FIELD(thoff, uint16_t);
+    case 4: case 5: FK_FIELD(addr_proto, uint16_t);
+    case 6: FK_FIELD(is_frag, uint8_t);
+    case 7: FK_FIELD(is_first_frag, uint8_t);
+    case 8: FK_FIELD(is_encap, uint8_t);
+    case 9: FK_FIELD(ip_proto, uint8_t);
+    case 10: case 11: FK_FIELD(n_proto, uint16_t);
+    case 12: case 13: FK_FIELD(sport, uint16_t);
+    case 14: case 15: FK_FIELD(dport, uint16_t);
+    case 32: case 33: case 34: case 35: FK_FIELD(flags, uint32_t);
+    case 36: case 37: case 38: case 39: FK_FIELD(flow_label, uint32_t);
+    }
+#undef FK_FIELD
+    if (off >= 16 && off < 32) return ORC_PANIC_SLICE; /* ip[offset:...] on a 16-byte slice, offset >= 16 */
+    return ORC_ERR_CTX_ACCESS;
+}
+
+static int skb_access(void *obj, objkind kind, uint32_t off, int n, uint64_t *v, int load) {
+    if (kind == K_SKB) return skb_convert((skb_state *)obj, off, n, v, load);
+    if (kind == K_SK) return sk_convert((sk_state *)obj, off, n, v, load);
+    return fk_convert((fk_state *)obj, off, n, v, load);
+}
+
+/* ---- SKBuffFromBytes (:108-265) over gopacket v1.1.19's eager decoding ------------------
+ * gopacket is not vendored (go.mod pins v1.1.19); its decoders are restated for the layers
+ * that decide the SKBuff fields: Ethernet (+802.3 length), Dot1Q/QinQ, IPv4 (+options),
+ * IPv6 (+Routing / Destination-options headers), TCP, UDP, and UDP tunnels that would add a
+ * second link / network layer (VXLAN 4789, Geneve 6081, GTPv1-U 2152).  Other layers
+ * (ARP, LLC, ICMP, payloads) end the walk; they set no field.  Parity for this walk is
+ * unpinned: no reference test calls SKBuffFromBytes. */
+typedef struct {
+    const uint8_t *pkt;
+    uint32_t L;
+    int err;                /* a second link / network / transport layer */
+    int link, net, trans;
+    uint16_t protocol, vlan_proto, vlan_tci;
+    int vlan_present;
+    uint32_t family;
+    go_ip s4, d4, s6, d6;
+    uint32_t sport, dport;
+} skb_walk;
+
+static uint16_t rd16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+static void walk_ethertype(skb_walk *w, uint32_t t, uint32_t o, uint32_t len);
+static void walk_ethernet(skb_walk *w, uint32_t o, uint32_t len);
+static void walk_ip(skb_walk *w, uint32_t o, uint32_t len);
+
+static void walk_tcp(skb_walk *w, uint32_t o, uint32_t len) {
+    /* decodeTCP adds the layer even when DecodeFromBytes fails; ports are read first */
+    if (w->trans++) { w->err = 1; return; }
+    if (len >= 20) {
+        w->sport = rd16(w->pkt + o);
+        w->dport = rd16(w->pkt + o + 2);
+    }
+}
+
+static void walk_udp(skb_walk *w, uint32_t o, uint32_t len) {
+    if (w->trans++) { w->err = 1; return; }
+    if (len < 8) return;
+    const uint8_t *d = w->pkt + o;
+    w->sport = rd16(d);
+    w->dport = rd16(d + 2);
+    uint32_t ulen = rd16(d + 4), plen;
+    if (ulen >= 8) plen = (ulen > len ? len : ulen) - 8;
+    else if (ulen == 0) plen = len - 8;
+    else return; /* "UDP packet too small" */
+    if (plen == 0) return;
+    uint32_t po = o + 8;
+    /* NextLayerType: the destination port's layer type unless it is LayerTypePayload, else the
+     * source port's (udp.go); gopacket's UDPPortLayerType table (ports.go) */
+    static const uint32_t known[] = {53, 123, 4789, 67, 68, 546, 547, 5060, 6343, 6081, 3784, 2152, 623, 1812};
+    uint32_t port = w->sport;
+    for (unsigned k = 0; k < sizeof known / sizeof *known; k++)
+        if (w->dport == known[k]) port = w->dport;
+    const uint8_t *q = w->pkt + po;
+    if (port == 4789) {        /* VXLAN: 8-byte header, then Ethernet */
+        if (plen < 8) return;
+        walk_ethernet(w, po + 8, plen - 8);
+    } else if (port == 6081) { /* Geneve: 8 + options, then the protocol's EthernetType */
+        if (plen < 8) return;
+        uint32_t hl = 8 + (q[0] & 0x3f) * 4u;
+        if (plen < hl) return;
+        walk_ethertype(w, rd16(q + 2), po + hl, plen - hl);
+    } else if (port == 2152) { /* GTPv1-U: 8 bytes (+4 with E/S/PN), then IPv4 / IPv6 */
+        if (plen < 8) return;
+        uint32_t hl = (q[0] & 0x07) ? 12 : 8;
+        if ((q[0] & 0x04) || plen <= hl) return; /* extension headers: not restated */
+        walk_ip(w, po + hl, plen - hl);
+    }
+}
+
+static void walk_proto(skb_walk *w, uint32_t proto, uint32_t o, uint32_t len) {
+    if (len == 0) return; /* NextDecoder with an empty payload decodes nothing */
+    switch (proto) {
+    case 6: walk_tcp(w, o, len); return;
+    case 17: walk_udp(w, o, len); return;
+    case 4: case 41: walk_ip(w, o, len); return; /* IPIP / IPv6-in-IP: a second network layer */
+    }
+}
+
+static void walk_ipv4(skb_walk *w, uint32_t o, uint32_t len) {
+    if (w->net++) { w->err = 1; return; }
+    w->family = 2; /* AF_INET */
+    if (len < 20) { w->s4.kind = 1; w->d4.kind = 1; return; } /* SrcIP / DstIP stay nil */
+    const uint8_t *d = w->pkt + o;
+    w->s4.kind = 2; w->s4.off = o + 12;
+    w->d4.kind = 2; w->d4.off = o + 16;
+    uint32_t ihl = d[0] & 0x0f, tl = rd16(d + 2);
+    uint32_t ff = rd16(d + 6);
+    if (tl == 0) tl = len;
+    if (tl < 20 || ihl < 5 || ihl * 4 > tl) return;
+    uint32_t dl = len;
+    if (len > tl) dl = tl;
+    else if (len < tl && ihl * 4 > len) return;
+    /* options, ip4.go: a malformed option ends the decode */
+    uint32_t q = 20;
+    while (q < ihl * 4) {
+        uint8_t t = d[q];
+        if (t == 0) break;
+        if (t == 1) { q++; continue; }
+        if (ihl * 4 - q < 2) return;
+        uint8_t ol = d[q + 1];
+        if (ihl * 4 - q < ol) return;
+        if (ol <= 2) return;
+        q += ol;
+    }
+    if ((ff & 0x2000) || (ff & 0x1fff)) return; /* a fragment: LayerTypeFragment */
+    walk_proto(w, d[9], o + ihl * 4, dl - ihl * 4);
+}
+
+static void walk_ipv6(skb_walk *w, uint32_t o, uint32_t len) {
+    if (w->net++) { w->err = 1; return; }
+    w->family = 10; /* AF_INET6 */
+    if (len < 40) { w->s6.kind = 1; w->d6.kind = 1; return; }
+    const uint8_t *d = w->pkt + o;
+    w->s6.kind = 2; w->s6.off = o + 8;
+    w->d6.kind = 2; w->d6.off = o + 24;
+    uint32_t next = d[6], plen = rd16(d + 4);
+    if (next == 0) return;  /* Hop-by-Hop / jumbograms: not restated */
+    if (plen == 0) return;  /* "IPv6 length 0, but next header is ..." */
+    uint32_t po = o + 40, pl = len - 40;
+    if (pl > plen) pl = plen;
+    for (int guard = 0; guard < 16; guard++) {
+        if (next == 43 || next == 60) { /* Routing / Destination options: (d[1]+1)*8 bytes */
+            if (pl < 2) return;
+            uint32_t hl = (w->pkt[po + 1] + 1u) * 8;
+            if (pl < hl) return;
+            next = w->pkt[po];
+            po += hl;
+            pl -= hl;
+            continue;
+        }
+        if (next == 44) return; /* Fragment */
+        break;
+    }
+    walk_proto(w, next, po, pl);
+}
+
+static void walk_ip(skb_walk *w, uint32_t o, uint32_t len) { /* decodeIPv4orIPv6 */
+    if (len == 0) return;
+    uint32_t v = w->pkt[o] >> 4;
+    if (v == 4) walk_ipv4(w, o, len);
+    else if (v == 6) walk_ipv6(w, o, len);
+}
+
+static void walk_dot1q(skb_walk *w, uint32_t o, uint32_t len) {
+    if (len < 4) return;
+    const uint8_t *d = w->pkt + o;
+    w->vlan_proto = rd16(d + 2); /* Dot1Q.Type: the inner EthernetType (:182) */
+    w->vlan_tci = rd16(d);
+    w->vlan_present = 1;
+    walk_ethertype(w, rd16(d + 2), o + 4, len - 4);
+}
+
+/* LLC (llc.go) and SNAP: 802.3 frames reach a network layer through LLC 0xAA/0xAA + SNAP */
+static void walk_llc(skb_walk *w, uint32_t o, uint32_t len) {
+    if (len < 3) return;
+    const uint8_t *d = w->pkt + o;
+    uint32_t hl = 3;
+    if (!(d[2] & 1) || (d[2] & 3) == 1) {  /* I- or S-format: 2-byte control */
+        if (len < 4) return;
+        hl = 4;
+    }
+    if ((d[0] & 0xfe) != 0xaa || (d[1] & 0xfe) != 0xaa) return;  /* not SNAP */
+    if (len - hl == 0) return;
+    if (len - hl < 5) return;
+    walk_ethertype(w, rd16(d + hl + 3), o + hl + 5, len - hl - 5);
+}
+
+static void walk_ethertype(skb_walk *w, uint32_t t, uint32_t o, uint32_t len) {
+    if (len == 0) return;
+    switch (t) {
+    case 0x0000: walk_llc(w, o, len); return;
+    case 0x0800: case 0x86DD: walk_ip(w, o, len); return;
+    case 0x8100: case 0x88a8: walk_dot1q(w, o, len); return;
+    case 0x6558: walk_ethernet(w, o, len); return; /* transparent Ethernet bridging */
+    }
+}
+
+static void walk_ethernet(skb_walk *w, uint32_t o, uint32_t len) {
+    if (len < 14) return; /* "Ethernet packet too small": no layer */
+    if (w->link++) { w->err = 1; return; }
+    const uint8_t *d = w->pkt + o;
+    uint32_t t = rd16(d + 12);
+    uint32_t pl = len - 14;
+    if (t < 0x0600) { /* 802.3 length: EthernetTypeLLC (0); the payload is trimmed to the length */
+        if (pl > t) pl = t;
+        t = 0;
+    }
+    if (w->link == 1) w->protocol = (uint16_t)t;
+    walk_ethertype(w, t, o + 14, pl);
+}
+
+/* LinuxContextSKBuff.Load, context_sk_buff.go:42-107.  Returns 0 or ORC_ERR_CTX_LOAD. */
+static int skb_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t ifindex) {
+    orc_vm *vm = p->vm;
+    skb_walk w;
+    memset(&w, 0, sizeof w);
+    w.pkt = pkt;
+    w.L = L;
+    w.s4.n = w.d4.n = 4;
+    w.s6.n = w.d6.n = 16;
+    walk_ethernet(&w, 0, L);
+    if (w.err) return ORC_ERR_CTX_LOAD; /* "handling of multiple ... layers not supported" */
+    skb_state *s = (skb_state *)calloc(1, sizeof *s);
+    sk_state *sk = (sk_state *)calloc(1, sizeof *sk);
+    fk_state *fk = (fk_state *)calloc(1, sizeof *fk);
+    plain_mem *pm = (plain_mem *)calloc(1, sizeof *pm);
+    uint8_t *copy = (uint8_t *)malloc(L ? L : 1);   /* gopacket's copy (NoCopy false) */
+    memcpy(copy, pkt, L);
+    pm->len = 32 + L + 64;
+    pm->b = (uint8_t *)calloc(pm->len, 1);
+    pm->big_endian = 1; /* ByteOrder: binary.BigEndian (:116-119) */
+    memcpy(pm->b + 32, pkt, L);
+    sk->family = w.family;
+    sk->src4 = w.s4; sk->dst4 = w.d4; sk->src6 = w.s6; sk->dst6 = w.d6;
+    sk->src_port = w.sport;
+    sk->dst_port = w.dport;
+    sk->state = 7; /* BPF_TCP_CLOSE */
+    sk->pkt = copy;
+    sk->L = L;
+    s->len = L;
+    s->protocol = w.protocol;
+    s->vlan_proto = w.vlan_proto;
+    s->vlan_tci = w.vlan_tci;
+    s->vlan_present = w.vlan_present;
+    s->tstamp = -62135596800ll; /* time.Time{}.Unix() */
+    s->dev_ifindex = ifindex;
+    s->sk = sk;
+    s->fk = fk;
+    s->pkt = pm;
+    /* head = 0 + 32, data = 0 + 32, tail = len, end = len (skb_reset_tail_pointer before the reserve) */
+    s->head = 32;
+    s->data = 32;
+    s->tail = L;
+    s->end = L;
+    /* the reference keeps these objects alive after Cleanup (only the sk_buff entry is deleted) */
+    void *objs[] = {sk, fk, pm, pm->b, copy};
+    if (vm->nleaks + 5 > vm->cap_leaks) {
+        vm->cap_leaks = vm->cap_leaks ? 2 * vm->cap_leaks + 5 : 64;
+        vm->leaks = (void **)realloc(vm->leaks, sizeof(void *) * (size_t)vm->cap_leaks);
+    }
+    for (int k = 0; k < 5; k++) vm->leaks[vm->nleaks++] = objs[k];
+    p->skb = s;
+    uint32_t sa, ska, fka, pa;
+    if (mc_add(vm, s, K_SKB, 192, &sa)) return ORC_ERR_CTX_LOAD;
+    if (mc_add(vm, sk, K_SK, 80, &ska)) return ORC_ERR_CTX_LOAD;
+    s->sk_addr = ska;
+    if (mc_add(vm, fk, K_FK, 40, &fka)) return ORC_ERR_CTX_LOAD;
+    s->fk_addr = fka;
+    if (mc_add(vm, pm, K_PLAIN, pm->len, &pa)) return ORC_ERR_CTX_LOAD;
+    s->head += pa;
+    s->data += pa;
+    s->tail += pa;
+    s->end += pa;
+    /* computeDataPointers (:269-281): cb[28:32] = data, cb[32:36] = end, native order */
+    for (int k = 0; k < 4; k++) {
+        s->cb[28 + k] = (uint8_t)(s->data >> (8 * k));
+        s->cb[32 + k] = (uint8_t)(s->end >> (8 * k));
+    }
+    p->R.r[1] = sa;
+    return 0;
+}
+
+int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_results *out) {
+    if (prog_id < 0 || prog_id >= vm->nprogs) {
+        set_err(vm, "no program with id '%d' is loaded", prog_id);
+        return -1;
+    }
+    uint64_t budget = b->step_budget ? b->step_budget : DEFAULT_BUDGET;
+    for (uint32_t i = 0; i < b->n; i++) {
+        uint32_t L = b->pkt_len[i];
+        uint8_t *mem = b->pkt_data + b->pkt_off[i];
+        orc_proc *p = proc_new(vm, prog_id);
+        uint32_t steps = 0;
+        int32_t epc = -1;
+        int st = skb_load(p, mem + 32, L, b->ifindex);
+        if (!st) {
+            if (orc_proc_set_cpu(p, b->cpu ? b->cpu[i] : 0)) st = ORC_ERR_NO_CPU;
+            else st = run(p, budget, &steps, &epc);
+        }
+        if (out->r0) out->r0[i] = p->R.r[0];
+        if (out->status) out->status[i] = (uint8_t)st;
+        if (out->steps) out->steps[i] = steps;
+        if (out->err_pc) out->err_pc[i] = st == ORC_OK ? -1 : epc;
+        if (b->write_back && p->skb) memcpy(mem, p->skb->pkt->b, 32 + L + 64);
+        /* Process.Cleanup (vm.go:363-374) + LinuxContextSKBuff.Cleanup (context_sk_buff.go:110-119):
+         * the stack and the sk_buff entry only; the sock, flow keys and packet entries stay */
+        if (p->skb) {
+            mc_del_obj(vm, p->skb);
+            free(p->skb);
+            p->skb = NULL;
+        }
         orc_proc_free(p);
     }
     return 0;

@@ -53,6 +53,10 @@ enum {
     ORC_ERR_CALL_DEPTH = 23,      /* engine bound on BPF-to-BPF frames (reference: unbounded) */
     ORC_ERR_ENGINE_HELPER = 24,   /* helper the reference emulates but the engine does not */
     ORC_ERR_NO_CPU = 25,          /* never produced by the batch runner (cpu always set) */
+    ORC_ERR_CTX_ACCESS = 26,      /* __sk_buff / bpf_sock / bpf_flow_keys Load/Store error (read-only, invalid offset,
+                                     not implemented), emulator_linux_sk_buff.go convertAccess */
+    ORC_PANIC_SLICE = 27,         /* Go slice-bounds panic inside convertAccess (cb loads, IP slices, flow_keys IP) */
+    ORC_ERR_CTX_LOAD = 28,        /* NewProcess: Context.Load failed (SKBuffFromBytes error, out of memory) */
     ORC_STATUS_COUNT
 };
 
@@ -149,6 +153,21 @@ typedef struct {
 } orc_results;
 
 int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_results *out);
+
+/* sk_buff batches (LinuxContextSKBuff, context_sk_buff.go): packet i is pkt_len[i] bytes at
+ * pkt_data + pkt_off[i] + 32; the process sees packet memory [pkt_off[i], +32+L+64) (headroom
+ * 32, tailroom 64, emulator_linux_sk_buff.go:113-121), written back when write_back is set. */
+typedef struct {
+    uint32_t n;
+    uint8_t *pkt_data;
+    const uint64_t *pkt_off;
+    const uint32_t *pkt_len;
+    uint32_t ifindex;       /* NetDev.IFIndex (ctx "dev") */
+    const int32_t *cpu;
+    uint64_t step_budget;
+    int write_back;
+} orc_skb_batch;
+int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_results *out);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,11 @@ class _Batch(C.Structure):
                 ("write_back", C.c_int)]
 
 
+class _SkbBatch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("pkt_data", C.c_void_p), ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p),
+                ("ifindex", C.c_uint32), ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("write_back", C.c_int)]
+
+
 class _Results(C.Structure):
     _fields_ = [("r0", C.c_void_p), ("status", C.c_void_p), ("steps", C.c_void_p), ("err_pc", C.c_void_p)]
 
@@ -69,6 +74,7 @@ def load(build: bool = True) -> C.CDLL:
         "orc_proc_set_reg": (None, [C.c_void_p, C.c_int, C.c_uint64]),
         "orc_proc_call_helper": (C.c_int, [C.c_void_p, C.c_int32]),
         "orc_run_xdp_batch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(_Batch), C.POINTER(_Results)]),
+        "orc_run_skb_batch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(_SkbBatch), C.POINTER(_Results)]),
     }
     for n, (r, a) in sig.items():
         f = getattr(lib, n)
@@ -234,6 +240,26 @@ class OracleVM:
                      out["err_pc"].ctypes.data)
         rc = self.lib.orc_run_xdp_batch(self.h, prog_id, C.byref(b), C.byref(r))
         if rc:
+            raise OracleError(self.err())
+        out["pkt"] = buf
+        return out
+
+    def run_skb_batch(self, prog_id: int, buf: np.ndarray, off: np.ndarray, lens: np.ndarray, cpu: np.ndarray,
+                      ifindex: int = 0, step_budget: int = 0, write_back: bool = True):
+        """Sequential sk_buff-context run: packet i is lens[i] bytes at buf[off[i] + 32:]; the
+        process's packet memory [off[i], off[i] + 96 + L) is written back if write_back."""
+        n = len(lens)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        cpu = np.ascontiguousarray(cpu, dtype=np.int32)
+        b = _SkbBatch(n, buf.ctypes.data, off.ctypes.data, lens.ctypes.data, ifindex, cpu.ctypes.data, step_budget,
+                      int(write_back))
+        out = {"r0": np.zeros(n, np.uint64), "status": np.zeros(n, np.uint8), "steps": np.zeros(n, np.uint32),
+               "err_pc": np.zeros(n, np.int32)}
+        r = _Results(out["r0"].ctypes.data, out["status"].ctypes.data, out["steps"].ctypes.data,
+                     out["err_pc"].ctypes.data)
+        if self.lib.orc_run_skb_batch(self.h, prog_id, C.byref(b), C.byref(r)):
             raise OracleError(self.err())
         out["pkt"] = buf
         return out
