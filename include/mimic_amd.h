@@ -190,6 +190,39 @@ int mimic_stack_addr(mimic_vm *vm, uint32_t *addr_out);
  * Enqueued on `hip_stream` (a hipStream_t, NULL = the vm's own stream); returns when enqueued. */
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch,
                   const mimic_xdp_results *results, void *hip_stream);
+/* One batch of sk_buff processes (LinuxContextSKBuff, context_sk_buff.go:20-119).  DEVICE
+ * pointers as in mimic_xdp_batch.  Process i's packet memory is pkt_data[pkt_off[i] ..
+ * pkt_off[i]+32+L+64) with the packet's L = pkt_len[i] bytes at +32 (SKBuffFromBytes'
+ * headroom / tailroom, emulator_linux_sk_buff.go:108-121); the engine zeroes the room bytes
+ * and runs the program on that memory IN PLACE (BigEndian scalar accesses).  A packet whose
+ * Load fails (a second link / network / transport layer) gets MIMIC_ERR_CTX_LOAD and its
+ * memory is not touched.  Cleanup leaks the sock / flow-keys / packet entries exactly as the
+ * reference does (context_sk_buff.go:110-119), so their addresses keep growing across
+ * batches until mimic_skb_release. */
+#define MIMIC_CTX_XDP 0
+#define MIMIC_CTX_SKB 1
+typedef struct {
+    uint32_t n;
+    uint32_t schedule;          /* MIMIC_SCHED_* */
+    uint8_t *pkt_data;
+    const uint64_t *pkt_off;
+    const uint32_t *pkt_len;
+    uint32_t ifindex;           /* LinuxContextSKBuff.Dev.IFIndex (__sk_buff.ifindex) */
+    int32_t pad;
+    const int32_t *cpu;         /* HOST array for MIMIC_SCHED_EXPLICIT */
+    uint64_t step_budget;       /* 0 = MIMIC default */
+} mimic_skb_batch;
+
+/* Batch form of: for each packet i { p := vm.NewProcess(prog, &LinuxContextSKBuff{Packet: pkt_i,
+ * Dev: &NetDev{IFIndex}}); p.SetCPUID(cpu(i)); p.Run(ctx); r0[i] = p.Registers.R0; p.Cleanup() }
+ * (vm.go:198-374, context_sk_buff.go:42-119).  Enqueued on `hip_stream` like mimic_run_xdp. */
+int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *batch,
+                  const mimic_xdp_results *results, void *hip_stream);
+/* Drop the sock / flow-keys / packet entries earlier sk_buff processes leaked: the state of a
+ * fresh VM with the same maps and programs (no reference counterpart; the reference never
+ * frees them).  Needed before adding maps / programs or running xdp_md batches again. */
+int mimic_skb_release(mimic_vm *vm);
+
 /* Wait for all work the vm enqueued on `hip_stream` (NULL = own stream). */
 int mimic_sync(mimic_vm *vm, void *hip_stream);
 /* Executed Step() count of the last completed mimic_run_xdp (sum over packets). */
@@ -232,6 +265,10 @@ long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uin
 int mimic_jit_check(const char *src, char *log, size_t cap, size_t *code_size);
 /* Compile the JIT kernel of raw programs into the MIMIC_JIT_CACHE directory (host only). */
 int mimic_jit_prebuild(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs);
+/* The same for the kernel of a batch context (MIMIC_CTX_XDP / MIMIC_CTX_SKB). */
+long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
+                              char *buf, size_t cap);
+int mimic_jit_prebuild_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind);
 
 #ifdef __cplusplus
 }

@@ -1,9 +1,9 @@
 """mimic_amd -- MI355X-native batch eBPF engine behind dylandreimerink/mimic's Process.Run surface.
 
-Product path: hand-written gfx950 HIP interpreter (csrc/interp.hip) + C++ host engine
-(csrc/engine.cpp) behind the C ABI in include/mimic_amd.h, bound here with ctypes.
+Product path: per-program gfx950 JIT kernels (csrc/jit.cpp, hipRTC) and the hand-written batch
+interpreter (csrc/interp.hip) + C++ host engine (csrc/engine.cpp) behind the C ABI in include/mimic_amd.h, bound here with ctypes.
 """
-from .vm import (E2BIG, LinuxArrayMap, LinuxContextXDP, LinuxEmulator, LinuxHashMap, LinuxMap, LinuxPerCPUArrayMap,
+from .vm import (E2BIG, LinuxArrayMap, LinuxContextSKBuff, LinuxContextXDP, NetDev, SKBBatch, LinuxEmulator, LinuxHashMap, LinuxMap, LinuxPerCPUArrayMap,
                  LinuxPerCPUHashMap, MapSpec, MapSpecToLinuxMap, MapType, MimicError, NewLinuxEmulator, NewVM, OptMaxTailCalls, Process,
                  ProgramSpec, UnmarshalContextJSON, VM, VMOptDevice, VMOptEmulator, VMOptSetvCPUs, VMOptShard,
                  XDPBatch, XDPResults)

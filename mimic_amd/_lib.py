@@ -55,6 +55,15 @@ class XDPBatch(C.Structure):
                 ("cpu", C.c_void_p), ("step_budget", C.c_uint64)]
 
 
+class SKBBatch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("schedule", C.c_uint32), ("pkt_data", C.c_void_p),
+                ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p), ("ifindex", C.c_uint32), ("pad", C.c_int32),
+                ("cpu", C.c_void_p), ("step_budget", C.c_uint64)]
+
+
+CTX_XDP, CTX_SKB = 0, 1
+
+
 class XDPResults(C.Structure):
     _fields_ = [("r0", C.c_void_p), ("status", C.c_void_p), ("steps", C.c_void_p), ("err_pc", C.c_void_p)]
 
@@ -99,6 +108,11 @@ EXPORTS = {
     "mimic_mem_load": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(C.c_uint64)]),
     "mimic_stack_addr": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "mimic_run_xdp": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPBatch), C.POINTER(XDPResults), C.c_void_p]),
+    "mimic_run_skb": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(SKBBatch), C.POINTER(XDPResults), C.c_void_p]),
+    "mimic_skb_release": (C.c_int, [C.c_void_p]),
+    "mimic_jit_source_for_ctx": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32,
+                                             C.c_char_p, C.c_size_t]),
+    "mimic_jit_prebuild_ctx": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32]),
     "mimic_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mimic_last_steps": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }

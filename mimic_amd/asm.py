@@ -49,6 +49,19 @@ FN_TAIL_CALL = 12
 FN_XDP_ADJUST_TAIL = 65
 
 XDP_ABORTED, XDP_DROP, XDP_PASS, XDP_TX, XDP_REDIRECT = range(5)
+TC_ACT_OK, TC_ACT_SHOT = 0, 2
+
+# __sk_buff field offsets (include/uapi/linux/bpf.h; SKBuff.convertAccess, emulator_linux_sk_buff.go:295-676)
+SKB = dict(len=0, pkt_type=4, mark=8, queue_mapping=12, protocol=16, vlan_present=20, vlan_tci=24, vlan_proto=28,
+           priority=32, ingress_ifindex=36, ifindex=40, tc_index=44, cb=48, hash=68, tc_classid=72, data=76,
+           data_end=80, napi_id=84, family=88, remote_ip4=92, local_ip4=96, remote_ip6=100, local_ip6=116,
+           remote_port=132, local_port=136, data_meta=140, flow_keys=144, tstamp=152, wire_len=160, gso_segs=164,
+           sk=168, gso_size=176, hwtstamp=184)
+# struct bpf_sock (SK.convertAccess :772-918) and struct bpf_flow_keys (:1031-1175)
+SOCK = dict(bound_dev_if=0, family=4, type=8, protocol=12, mark=16, priority=20, src_ip4=24, src_ip6=28,
+            src_port=44, dst_port=48, dst_ip4=52, dst_ip6=56, state=72, rx_queue_mapping=76)
+FLOW_KEYS = dict(nhoff=0, thoff=2, addr_proto=4, is_frag=6, is_first_frag=7, is_encap=8, ip_proto=9, n_proto=10,
+                 sport=12, dport=14, ipv4_src=16, ipv4_dst=20, ipv6_src=16, flags=32, flow_label=36)
 
 
 @dataclass
@@ -179,6 +192,16 @@ def jmp(op: str, dst: int, src_or_imm: int, off: Union[int, str], reg: bool = Fa
 def jmp32(op: str, dst: int, src_or_imm: int, off: Union[int, str], reg: bool = False) -> Insn:
     return Insn(JMP32 | JMP_OPS[op] | (X if reg else K), dst, src_or_imm if reg else 0, off,
                 0 if reg else src_or_imm)
+
+
+def ld_abs(size: int, imm: int) -> Insn:
+    """LD_ABS: R0 = ntoh(*(size *)(skb->data + imm)), R1-R5 clobbered (emulator_linux_.go:200-238)."""
+    return Insn(LD | ABS | SIZE_BYTES[size], 0, 0, 0, imm)
+
+
+def ld_ind(size: int, src: int, imm: int) -> Insn:
+    """LD_IND: R0 = ntoh(*(size *)(skb->data + src + imm)) (emulator_linux_.go:240-284)."""
+    return Insn(LD | IND | SIZE_BYTES[size], 0, src, 0, imm)
 
 
 def ja(off: Union[int, str]) -> Insn:

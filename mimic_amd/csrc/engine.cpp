@@ -22,6 +22,7 @@
 #include "../../include/mimic_amd.h"
 #include "layout.h"
 #include "jit.h"
+#include "skb.h"
 
 extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st);
 extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
@@ -29,6 +30,11 @@ extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, 
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
+extern "C" size_t mimic_skb_scan_bytes(uint32_t n);
+extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
+                                     uint32_t n, SkbRec *rec, uint64_t *foot, uint64_t *prefix, void *scan_tmp,
+                                     size_t scan_bytes, uint64_t *state, uint64_t init_base, uint32_t use_init,
+                                     hipStream_t st);
 
 namespace {
 
@@ -83,8 +89,8 @@ struct mimic_vm {
     int exec_mode = MIMIC_EXEC_JIT;
     std::vector<DInsn> h_all;   // predecoded instruction slots of every program (host copy)
     std::vector<DProg> h_dp;
-    hipFunction_t jit_fn = nullptr;
-    JitInfo jit_info{};
+    hipFunction_t jit_fn[2] = {nullptr, nullptr};   // per CtxKind, generated on first use
+    JitInfo jit_info[2]{};
     int last_exec = 0;          // the kernel the last batch ran on
     // launch parameters of JIT kernels in device memory: a ring of slots written by
     // stream-ordered copies from pinned host memory (a repeated batch reuses its slot)
@@ -107,6 +113,14 @@ struct mimic_vm {
     uint64_t *hp_off = nullptr;   // whole-batch descriptors (one copy each per batch)
     uint32_t *hp_len = nullptr;
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    // sk_buff batches (skb.h): per-packet records, footprints, their prefix, scan scratch, and
+    // the device word pair {next leak address, this batch's leak base}
+    SkbRec *d_skb_rec = nullptr;
+    uint64_t *d_skb_foot = nullptr, *d_skb_prefix = nullptr, *d_skb_state = nullptr;
+    void *d_skb_scan = nullptr;
+    size_t skb_cap = 0, skb_scan_cap = 0;
+    bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
+    hipStream_t skb_stream = nullptr;
 };
 
 
@@ -296,7 +310,8 @@ static uint32_t predecode(const DInsn &x, int64_t i, int64_t n) {
         if (dst == 10) return err(MIMIC_ERR_R10_WRITE);
         return a | H_LDIMM;
     }
-    if ((op & 0xe0) == 0x20 || (op & 0xe0) == 0x40) return err(MIMIC_ERR_LDABS);
+    if ((op & 0xe0) == 0x20 || (op & 0xe0) == 0x40)  // LD_ABS / LD_IND: CustomInstruction
+        return a | H_LDABS | ((op & 0x40) ? AUX_X : 0) | (sz(op) << 24);
     return err(MIMIC_ERR_UNSUPPORTED_OP);
 }
 
@@ -349,7 +364,7 @@ static void build_host_tables(const std::vector<HostProg> &progs, std::vector<DI
 static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     build_host_tables(vm->progs, vm->h_all, vm->h_dp);
-    vm->jit_fn = nullptr;
+    vm->jit_fn[0] = vm->jit_fn[1] = nullptr;
     std::vector<DInsn> all = vm->h_all;
     std::vector<DProg> dp = vm->h_dp;
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
@@ -513,6 +528,11 @@ void mimic_vm_destroy(mimic_vm *vm) {
     }
     hipFree(vm->hp_off);
     hipFree(vm->hp_len);
+    hipFree(vm->d_skb_rec);
+    hipFree(vm->d_skb_foot);
+    hipFree(vm->d_skb_prefix);
+    hipFree(vm->d_skb_state);
+    hipFree(vm->d_skb_scan);
     if (vm->s_h2d) hipStreamDestroy(vm->s_h2d);
     if (vm->s_d2h) hipStreamDestroy(vm->s_d2h);
     for (auto &e : vm->kp_ev)
@@ -524,6 +544,8 @@ void mimic_vm_destroy(mimic_vm *vm) {
 // MapSpecToLinuxMap (emulator_linux_map.go:57-113) + Init + AddMap
 int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id) {
     if (!vm || !spec || !map_id) return MIMIC_EINVAL;
+    if (vm->skb_leaked)   // first fit would now place it in the freed stack / sk_buff hole or after the leaks
+        return fail(vm, MIMIC_ENOTSUP, "adding maps after sk_buff batches is not supported (mimic_skb_release first)");
     hipSetDevice(vm->s.device);
     std::string name = spec->name ? spec->name : "";
     for (auto &m : vm->maps)
@@ -902,6 +924,8 @@ int mimic_map_addr(mimic_vm *vm, uint32_t id, uint32_t *addr_out) {
 int mimic_program_load(mimic_vm *vm, const char *name, const void *insns, uint32_t n_slots,
                        const mimic_reloc *relocs, uint32_t n_relocs, uint32_t *prog_id) {
     if (!vm || (!insns && n_slots) || !prog_id) return MIMIC_EINVAL;
+    if (vm->skb_leaked)
+        return fail(vm, MIMIC_ENOTSUP, "adding programs after sk_buff batches is not supported (mimic_skb_release first)");
     uint64_t total = n_slots;
     for (auto &q : vm->progs) total += q.ins.size();
     if (n_slots >= (1u << MIMIC_PC_BITS) || total >= 0x7fffffffull) return fail(vm, MIMIC_EINVAL, "program too long");
@@ -972,19 +996,86 @@ int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out) {
 
 // the batch form of NewProcess / SetCPUID / Run / Cleanup.  shift: for an INTERLEAVED
 // sub-batch, the index of its first packet in the whole batch (vCPU of packet k = (shift+k) % V)
+struct SkbRun {     // the sk_buff part of a batch (mimic_run_skb)
+    uint32_t ifindex;
+};
+
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
-                        hipStream_t st_in, uint64_t shift);
+                        hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr);
 
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                   void *hip_stream) {
     return run_xdp_impl(vm, prog_id, b, res, (hipStream_t)hip_stream, 0);
 }
 
+// Batch form of NewProcess(prog, &LinuxContextSKBuff{Packet, Dev}) + SetCPUID + Run + Cleanup
+int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, const mimic_xdp_results *res,
+                  void *hip_stream) {
+    if (!vm || !sb || !res) return MIMIC_EINVAL;
+    mimic_xdp_batch b{};
+    b.n = sb->n;
+    b.schedule = sb->schedule;
+    b.pkt_data = sb->pkt_data;
+    b.pkt_off = sb->pkt_off;
+    b.pkt_len = sb->pkt_len;
+    b.cpu = sb->cpu;
+    b.step_budget = sb->step_budget;
+    const SkbRun r{sb->ifindex};
+    return run_xdp_impl(vm, prog_id, &b, res, (hipStream_t)hip_stream, 0, &r);
+}
+
+int mimic_skb_release(mimic_vm *vm) {
+    if (!vm) return MIMIC_EINVAL;
+    hipSetDevice(vm->s.device);
+    if (vm->skb_stream) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
+    vm->skb_leaked = false;
+    return 0;
+}
+
+// the sk_buff records, footprints and leak addresses of a batch (skb.hip), on stream st
+static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st) {
+    const uint32_t n = b->n;
+    if (vm->skb_stream && vm->skb_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
+    if (n > vm->skb_cap || !vm->d_skb_state) {
+        HIP_OK(vm, hipStreamSynchronize(st));
+        hipFree(vm->d_skb_rec);
+        hipFree(vm->d_skb_foot);
+        hipFree(vm->d_skb_prefix);
+        vm->d_skb_rec = nullptr;
+        vm->d_skb_foot = vm->d_skb_prefix = nullptr;
+        const size_t cap = std::max<size_t>(n, 1024);
+        HIP_OK(vm, hipMalloc(&vm->d_skb_rec, cap * sizeof(SkbRec)));
+        HIP_OK(vm, hipMalloc(&vm->d_skb_foot, cap * 8));
+        HIP_OK(vm, hipMalloc(&vm->d_skb_prefix, cap * 8));
+        if (!vm->d_skb_state) HIP_OK(vm, hipMalloc(&vm->d_skb_state, 16));
+        vm->skb_cap = cap;
+    }
+    const size_t sb = mimic_skb_scan_bytes(std::max<uint32_t>(n, 1));
+    if (sb > vm->skb_scan_cap) {
+        HIP_OK(vm, hipStreamSynchronize(st));
+        hipFree(vm->d_skb_scan);
+        vm->d_skb_scan = nullptr;
+        HIP_OK(vm, hipMalloc(&vm->d_skb_scan, std::max<size_t>(sb, 256)));
+        vm->skb_scan_cap = std::max<size_t>(sb, 256);
+    }
+    // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
+    const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
+    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, vm->d_skb_rec, vm->d_skb_foot, vm->d_skb_prefix,
+                              vm->d_skb_scan, vm->skb_scan_cap, vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
+        return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
+    if (n) vm->skb_leaked = true;
+    vm->skb_stream = st;
+    return 0;
+}
+
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
-                        hipStream_t st_in, uint64_t first_index) {
+                        hipStream_t st_in, uint64_t first_index, const SkbRun *skb) {
     if (!vm || !b || !res) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
+    if (!skb && vm->skb_leaked)   // the xdp entries would land in the freed hole or after the leaks
+        return fail(vm, MIMIC_ENOTSUP, "xdp_md batches after sk_buff batches are not supported (mimic_skb_release first)");
+    const uint32_t ctx = skb ? CTX_SKB : CTX_XDP;
     hipSetDevice(vm->s.device);
     int rc = upload_tables(vm);
     if (rc) return rc;
@@ -1110,6 +1201,15 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     default:
         return fail(vm, MIMIC_EINVAL, "unknown schedule %u", b->schedule);
     }
+    if (skb) {
+        rc = skb_prepare(vm, b, st);
+        if (rc) return rc;
+        kp.ctx_kind = CTX_SKB;
+        kp.skb_ifindex = skb->ifindex;
+        kp.skb_rec = vm->d_skb_rec;
+        kp.skb_prefix = vm->d_skb_prefix;
+        kp.skb_base = vm->d_skb_state + 1;
+    }
     // compact hash tables whose buckets are mostly tombstones (device-side check, no host sync)
     for (auto &m : vm->maps) {
         if (!is_hash(m)) continue;
@@ -1118,24 +1218,26 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
     bool jit = vm->exec_mode == MIMIC_EXEC_JIT;
-    if (jit && !vm->jit_fn) {
+    if (jit && !vm->jit_fn[ctx]) {
         std::string log;
-        if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, &vm->jit_info), &vm->jit_fn, &log))
+        if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx]),
+                              &vm->jit_fn[ctx], &log))
             return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
     }
+    const JitInfo &ji = vm->jit_info[ctx];
     if (jit) {  // a loop-free kernel has no budget checks: tiny budgets run on the interpreter
-        const uint64_t bound = mimic_jit_step_bound(vm->jit_info, kp.max_tail_calls);
+        const uint64_t bound = mimic_jit_step_bound(ji, kp.max_tail_calls);
         if (bound && kp.budget < bound) jit = false;
     }
     vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
-    if (jit && vm->jit_info.kp_by_value) {  // parameters in the kernarg segment
-        if (mimic_jit_launch(vm->jit_fn, vm->jit_info, &kp, nullptr, st))
+    if (jit && ji.kp_by_value) {  // parameters in the kernarg segment
+        if (mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, nullptr, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     } else {                                // parameters read from a device copy
         const KParams *dkp = nullptr;
         const int slot = kp_slot(vm, kp, st, &dkp);
         if (slot < 0) return slot;
-        if (jit ? mimic_jit_launch(vm->jit_fn, vm->jit_info, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
+        if (jit ? mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));
         vm->kp_used[slot] = true;
@@ -1174,6 +1276,12 @@ int mimic_last_exec(const mimic_vm *vm) { return vm ? vm->last_exec : MIMIC_EINV
 // relocations do not change the code shape).  Returns the source length; copies it if it fits.
 // Host only: no device needed.
 long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, char *buf, size_t cap) {
+    return mimic_jit_source_for_ctx(progs, n_slots, n_progs, MIMIC_CTX_XDP, buf, cap);
+}
+
+long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
+                              char *buf, size_t cap) {
+    if (ctx_kind != MIMIC_CTX_XDP && ctx_kind != MIMIC_CTX_SKB) return MIMIC_EINVAL;
     std::vector<HostProg> hp(n_progs);
     for (uint32_t p = 0; p < n_progs; p++) {
         std::string err;
@@ -1182,7 +1290,7 @@ long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uin
     std::vector<DInsn> all;
     std::vector<DProg> dp;
     build_host_tables(hp, all, dp);
-    const std::string src = mimic_jit_source(dp, all, nullptr);
+    const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr);
     if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);
     return (long)src.size();
 }
@@ -1190,6 +1298,11 @@ long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uin
 // Build the JIT kernel for raw programs into the MIMIC_JIT_CACHE directory (host only): a
 // later process that loads the same programs finds the code object there.
 int mimic_jit_prebuild(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs) {
+    return mimic_jit_prebuild_ctx(progs, n_slots, n_progs, MIMIC_CTX_XDP);
+}
+
+int mimic_jit_prebuild_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind) {
+    if (ctx_kind != MIMIC_CTX_XDP && ctx_kind != MIMIC_CTX_SKB) return MIMIC_EINVAL;
     std::vector<HostProg> hp(n_progs);
     for (uint32_t p = 0; p < n_progs; p++) {
         std::string err;
@@ -1199,7 +1312,7 @@ int mimic_jit_prebuild(const void *const *progs, const uint32_t *n_slots, uint32
     std::vector<DProg> dp;
     build_host_tables(hp, all, dp);
     std::string log;
-    return mimic_jit_prebuild_source(mimic_jit_source(dp, all, nullptr), &log) ? MIMIC_EINVAL : 0;
+    return mimic_jit_prebuild_source(mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr), &log) ? MIMIC_EINVAL : 0;
 }
 
 // hipRTC-compile a JIT source for gfx950 without loading it (host only).  0 = ok; the compiler

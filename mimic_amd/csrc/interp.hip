@@ -92,6 +92,9 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
         L.tailcalls = 0;
         L.M = 0;
         L.pkt = nullptr;
+        L.rec = nullptr;
+        L.pa = P;
+        L.ka = 0;
         // a process ends here: results straight to HBM (Run's return + p.Registers.R0)
 #define TERM(st_, epc_)                                                \
         do {                                                           \
@@ -102,7 +105,21 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
             lane_steps += steps;                                       \
             key = KEY_DONE;                                            \
         } while (0)
-        if (i != 0xffffffffu) {
+        if (i != 0xffffffffu && kp.ctx_kind == CTX_SKB) {   // LinuxContextSKBuff.Load (skb.h)
+            uint64_t r1 = 0;
+            const int ls = skb_load(kp, L, i, r1);
+            REG(10) = kp.static_next + kp.frame_size;
+            if (ls) {
+                TERM(ls, -1);
+            } else {
+                REG(1) = r1;
+                key = pbase;
+                if (pn == 0) {
+                    steps = 1;
+                    TERM(MIMIC_ERR_PC_OOB, 0);
+                }
+            }
+        } else if (i != 0xffffffffu) {
             const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;
             const uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;
             const uint32_t len = kp.pkt_len[i];
@@ -258,6 +275,18 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
                     case H_ERR:
                         st = (int)AUX_ARG(aux);
                         break;
+                    case H_LDABS: {  // emulator_linux_.go:198-288
+                        const bool ind = (aux & AUX_X) != 0;
+                        const uint32_t x = (uint32_t)k + (ind ? (uint32_t)REG(src < NREGS ? src : 10) : 0u);
+                        uint64_t v = 0;
+                        st = ld_abs(kp, L, REG(6), x, AUX_SZ(aux), ind && src > 10, v);
+                        if (!st) {
+                            REG(0) = v;
+#pragma unroll
+                            for (int q = 1; q <= 5; q++) REG(q) = 0;
+                        }
+                        break;
+                    }
                     default: {  // H_SLOW: rare forms whose error order is per lane, and END
                         const uint32_t cls = op & 7, hi = op & 0xf0;
                         const bool xsrc = (op & 0x08) != 0;

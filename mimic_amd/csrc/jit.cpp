@@ -79,7 +79,7 @@ int64_t jump_target(const DInsn &x, int64_t i) {
 
 class Gen {
   public:
-    Gen(const std::vector<ProgView> &progs) : P(progs) {
+    Gen(const std::vector<ProgView> &progs, uint32_t ctx_kind) : P(progs), ctx(ctx_kind) {
         // tuning knobs (environment; they change the generated source, hence the cache key)
         const char *f = getenv("MIMIC_JIT_FAST");
         fast_paths = !(f && f[0] == '0');
@@ -87,6 +87,8 @@ class Gen {
         stage = !(sg && sg[0] == '0');
         const char *k = getenv("MIMIC_JIT_KP");
         kp_by_value = !(k && !strcmp(k, "ptr"));
+        const char *sh = getenv("MIMIC_JIT_SHARE");
+        share = !(sh && sh[0] == '0');
         for (auto &p : P)
             for (uint32_t i = 0; i < p.n; i++) {
                 const DInsn &x = p.ins[i];
@@ -118,7 +120,9 @@ class Gen {
     bool fast_paths = true;    // MIMIC_JIT_FAST=0: every access through resolve()
     bool stage = true;         // MIMIC_JIT_STAGE=0: no LDS packet window
     bool kp_by_value = true;   // MIMIC_JIT_KP=ptr: launch parameters read from a device copy
+    bool share = true;         // MIMIC_JIT_SHARE=0: slow paths inlined at every site
     bool has_tail() const { return any_tail; }
+    uint32_t ctx = CTX_XDP;    // the batch context this kernel is generated for
 
     std::string source() {
         // stage packets in LDS only when some access is expected to hit the packet
@@ -131,10 +135,12 @@ class Gen {
                     const uint32_t h = AUX_H(x.aux);
                     if (h == H_LDX && hint(insn_src(x)) == HINT_PKT) any = true;
                     if ((h == H_ST || h == H_STX) && hint(insn_dst(x)) == HINT_PKT) any = true;
+                    if (h == H_LDABS && ctx == CTX_SKB) any = true;
                 }
             }
             stage = any && fast_paths;
         }
+        E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#include \"runtime.h\"");
         E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
         // KParams is read through a pointer to device memory: fields are then loaded (scalar)
@@ -159,31 +165,47 @@ class Gen {
         E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = kp.sched_start[g]; ex_count = kp.sched_start[g + 1] - ex_begin; }");
         E.line("  uint64_t lane_steps = 0;");
         E.line("  const uint32_t P = kp.static_next + kp.stack_size + 1;");
+        if (ctx == CTX_SKB) E.line("  const uint32_t SK_ = P;   // the sk_buff entry (skb.h)");
+        // operands of the shared slow-path blocks (G_*): address, size, value, PC, return site
+        E.line("  uint32_t ga_ = 0, gn_ = 0, gret_ = 0; int32_t gpc_ = 0; uint64_t gv_ = 0;");
         E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
         E.line("    uint32_t i;");
         E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else { if (j >= ex_count) break; i = kp.sched_pkts[ex_begin + j]; }");
-        // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
-        E.line("    const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;");
-        E.line("    const uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;");
-        E.line("    const uint32_t len = kp.pkt_len[i];");
-        E.line("    L.pkt = kp.pkt_data + kp.pkt_off[i];");
-        E.line("    L.M = H + len + T;");
-        E.line("    for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;");
-        E.line("    for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;");
-        E.line("    L.data = P + H;");
-        E.line("    L.data_end = P + H + len;");
-        E.line("    L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);");
-        E.line("    L.rxq = (uint32_t)(kp.rxq_arr ? kp.rxq_arr[i] : kp.rxq);");
-        E.line("    L.egress = (uint32_t)(kp.egress_arr ? kp.egress_arr[i] : kp.egress);");
-        if (stage && fast_paths) E.line("    const uint32_t W_ = win_stage(pwin_, tl_, L.pkt, L.M);");
+        if (ctx == CTX_SKB) {
+            // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107, skb.h)
+            E.line("    uint64_t r1 = 0;");
+            E.line("    const int ls_ = skb_load(kp, L, i, r1);");
+            // the window starts at the packet (skb.data = packet memory + 32)
+            if (stage && fast_paths)
+                E.line("    const uint32_t W_ = ls_ ? 0u : win_stage(pwin_, tl_, L.pkt + SKB_HEADROOM, L.M - SKB_HEADROOM);");
+        } else {
+            // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
+            E.line("    const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;");
+            E.line("    const uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;");
+            E.line("    const uint32_t len = kp.pkt_len[i];");
+            E.line("    L.pkt = kp.pkt_data + kp.pkt_off[i];");
+            E.line("    L.M = H + len + T;");
+            E.line("    L.pa = P;");
+            E.line("    L.rec = nullptr;");
+            E.line("    for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;");
+            E.line("    for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;");
+            E.line("    L.data = P + H;");
+            E.line("    L.data_end = P + H + len;");
+            E.line("    L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);");
+            E.line("    L.rxq = (uint32_t)(kp.rxq_arr ? kp.rxq_arr[i] : kp.rxq);");
+            E.line("    L.egress = (uint32_t)(kp.egress_arr ? kp.egress_arr[i] : kp.egress);");
+            if (stage && fast_paths) E.line("    const uint32_t W_ = win_stage(pwin_, tl_, L.pkt, L.M);");
+            E.line("    uint64_t r1 = P + L.M + 1;");
+        }
         E.line("    L.sm0 = 0; L.sm1 = 0; L.xdp_dirty = 0; L.nframes = 0; L.tailcalls = 0; L.t_lo = 0; L.t_n = 0; L.t_ptr = nullptr;");
-        E.line("    uint64_t r0 = 0, r1 = P + L.M + 1, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0, r9 = 0;");
+        E.line("    uint64_t r0 = 0, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0, r9 = 0;");
         E.line("    uint64_t r10 = kp.static_next + kp.frame_size;");
         E.line("    uint32_t steps = 0;");
         E.line("    int st_ = 0;");
         E.line("    int32_t epc_ = -1;");
+        if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
         E.line("    switch (kp.entry_prog) {");
         for (auto &p : P) {
             if (p.n == 0) E.line("    case %u: steps = 1; TERM(MIMIC_ERR_PC_OOB, 0);", p.id);  // vm.go:297-299
@@ -192,6 +214,8 @@ class Gen {
         E.line("    default: TERM(MIMIC_ERR_PC_OOB, 0);");
         E.line("    }");
         for (auto &p : P) program(p);
+        E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
+        shared_blocks();
         E.line("  L_term:");
         E.line("    if (kp.r0) kp.r0[i] = r0;");
         E.line("    if (kp.status) kp.status[i] = (uint8_t)st_;");
@@ -207,6 +231,14 @@ class Gen {
   private:
     const std::vector<ProgView> &P;
     Emitter E;
+    // packet-entry fast paths: the entry's address, the window's offset in packet memory, and
+    // the byte order of scalar accesses (sk_buff packets are BigEndian PlainMemory)
+    const char *pa() const { return ctx == CTX_SKB ? "L.pa" : "P"; }
+    uint32_t wb() const { return ctx == CTX_SKB ? SKB_HEADROOM_J : 0u; }
+    std::string ord(const std::string &v, uint32_t n) const {
+        return ctx == CTX_SKB && n > 1 ? "bswap_n(" + v + ", " + std::to_string(n) + "u)" : v;
+    }
+    static constexpr uint32_t SKB_HEADROOM_J = 32;
     bool any_tail = false, any_local = false, all_leaders = false;
 
     void program(const ProgView &p) {
@@ -293,74 +325,174 @@ class Gen {
             const uint32_t h = AUX_H(x.aux), d = insn_dst(x), op = insn_op(x);
             bool writes = h == H_ALU64 || h == H_ALU32 || h == H_LDIMM || h == H_LDX || h == H_SLOW;
             if (h == H_CALL || h == H_CALL_LOCAL) { written[0] = other[0] = true; }
-            if (h == H_CALL_LOCAL) for (int r = 1; r <= 5; r++) written[r] = other[r] = true;
+            if (h == H_CALL_LOCAL || h == H_LDABS) for (int r = 0; r <= 5; r++) written[r] = other[r] = true;
             if (!writes || d > 10) continue;
             written[d] = true;
             if (!(op == 0xbf && insn_src(x) == 1)) other[d] = true;
         }
         for (int r = 0; r < 11; r++) ctx_reg[r] = false;
-        if (written[1] || any_tail) return;
-        ctx_reg[1] = true;
+        // after a tail call r1 is whatever the caller left there (usually the context): a wrong
+        // hint only costs the fast path, the address check keeps every access exact
+        ctx_reg[1] = !written[1];
         for (int r = 2; r < 10; r++) ctx_reg[r] = written[r] && !other[r];
     }
 
-    void load(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &dst) {
-        if (!fast_paths) {
-            E.line("    { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, %s), %uu, v_); if (s_) TERM(s_, %u); %s = v_; }",
-                   addr(base, off).c_str(), n, i, dst.c_str());
-            return;
+    // ---- shared slow paths ------------------------------------------------------------------
+    // The generic forms (resolve + VMMem access, helpers, LD_ABS) are large.  Instead of one copy
+    // per instruction, every site jumps to one shared block per form with its operands in
+    // ga_/gn_/gv_/gpc_ and its return label number in gret_; the block ends in a switch back to
+    // the site.  Kernels stay small (instruction cache, hipRTC time), and lanes of one wave
+    // that take the slow path at different sites run it together.
+    enum Blk { B_LD, B_ST, B_ABS, B_H1, B_H2, B_H3, B_H12, B_COUNT };
+    std::vector<std::string> rets[B_COUNT];
+    static const char *blk_name(int b) {
+        static const char *n[] = {"G_LD", "G_ST", "G_ABS", "G_H1", "G_H2", "G_H3", "G_H12"};
+        return n[b];
+    }
+    // a jump to block b from slot i, with `set` run before; returns the return label to place
+    std::string to_blk(int b, uint32_t i, const std::string &set) {
+        const uint32_t k = (uint32_t)rets[b].size();
+        std::string lbl = std::string("R") + blk_name(b) + "_" + std::to_string(k);
+        rets[b].push_back(lbl);
+        E.line("      %s gpc_ = %u; gret_ = %uu; goto %s; %s:;", set.c_str(), i, k, blk_name(b), lbl.c_str());
+        return lbl;
+    }
+    void ret_switch(int b) {
+        E.line("    switch (gret_) {");
+        for (size_t k = 0; k < rets[b].size(); k++) E.line("    case %zu: goto %s;", k, rets[b][k].c_str());
+        E.line("    default: TERM(MIMIC_ERR_ENGINE_HELPER, gpc_);");
+        E.line("    }");
+    }
+    void shared_blocks() {
+        if (!rets[B_LD].empty()) {
+            E.line("  G_LD: { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, ga_), gn_, v_); if (s_) TERM(s_, gpc_); gv_ = v_; }");
+            ret_switch(B_LD);
         }
-        E.line("    { const uint32_t a_ = %s; uint64_t v_ = 0;", addr(base, off).c_str());
+        if (!rets[B_ST].empty()) {
+            E.line("  G_ST: { const Ref R_ = resolve(kp, L, ga_); const int s_ = mem_store(kp, L, R_, gn_, gv_); if (s_) TERM(s_, gpc_);");
+            if (stage)  // a store that reaches the packet must update the window too
+                E.line("    if (R_.ptr == L.pkt && (R_.rk == RK_GLOBAL || R_.rk == RK_BEPKT)) win_store_rel(pwin_, tl_, W_, R_.off, %uu, gn_, %s); }",
+                       wb(), ctx == CTX_SKB ? "bswap_n(gv_, gn_)" : "gv_");
+            else E.line("    }");
+            ret_switch(B_ST);
+        }
+        if (!rets[B_ABS].empty()) {
+            E.line("  G_ABS: { uint64_t v_ = 0; const int s_ = ld_abs(kp, L, r6, ga_, gn_, false, v_); if (s_) TERM(s_, gpc_); gv_ = v_; }");
+            ret_switch(B_ABS);
+        }
+        if (!rets[B_H1].empty()) {
+            E.line("  G_H1: { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0;");
+            E.line("    if (ho.t_n) { L.t_lo = ho.t_lo; L.t_n = ho.t_n; L.t_ptr = ho.t_ptr; } }");
+            ret_switch(B_H1);
+        }
+        if (!rets[B_H2].empty()) {
+            E.line("  G_H2: { const HelperOut ho = helper_update(kp, L, r1, r2, r3); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0; }");
+            ret_switch(B_H2);
+        }
+        if (!rets[B_H3].empty()) {
+            E.line("  G_H3: { const HelperOut ho = helper_delete(kp, L, r1, r2); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0; }");
+            ret_switch(B_H3);
+        }
+        if (!rets[B_H12].empty()) {
+            E.line("  G_H12: { const HelperOut ho = helper_tailcall(kp, L, r2, r3); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0;");
+            E.line("    if (ho.tail) {");
+            E.line("      L.tailcalls++;");
+            E.line("      switch (ho.new_prog) {");
+            for (auto &q : P) {
+                if (q.n == 0) E.line("      case %u: TERM(MIMIC_ERR_PC_OOB, gpc_);", q.id);
+                else E.line("      case %u: goto P%u_0;", q.id, q.id);
+            }
+            E.line("      default: TERM(MIMIC_ERR_PC_OOB, gpc_);");
+            E.line("      }");
+            E.line("    } }");
+            ret_switch(B_H12);
+        }
+    }
+
+    // fast-path conditions and values for an access of n bytes at address ga_ (see hint())
+    struct Fast {
+        std::string cond, val, store;
+    };
+    std::vector<Fast> fast_forms(uint32_t base, uint32_t n, const std::string &v) {
+        std::vector<Fast> f;
+        if (!fast_paths) return f;
+        const std::string N = std::to_string(n) + "u";
         switch (hint(base)) {
         case HINT_STACK:
-            E.line("      const uint32_t o_ = a_ - kp.static_next;");
-            E.line("      if ((uint64_t)o_ + %uu <= kp.stack_size) v_ = stack_load(kp, L, o_, %uu);", n, n);
+            f.push_back({"(uint64_t)(uint32_t)(ga_ - kp.static_next) + " + N + " <= kp.stack_size",
+                         "stack_load(kp, L, ga_ - kp.static_next, " + N + ")",
+                         "stack_store(kp, L, ga_ - kp.static_next, " + N + ", " + v + ")"});
             break;
         case HINT_CTX:
-            E.line("      const uint32_t o_ = a_ - (P + L.M + 1);");
-            E.line("      if ((uint64_t)o_ + %uu <= MIMIC_XDP_MD_SIZE) v_ = xdp_load(kp, L, o_, %uu);", n, n);
-            break;
-        default:
-            E.line("      const uint32_t o_ = a_ - P;");
-            if (stage) E.line("      if ((uint64_t)o_ + %uu <= W_) v_ = win_load(pwin_, tl_, o_, %uu); else", n, n);
-            E.line("      if ((uint64_t)o_ + %uu <= L.M) v_ = ld_n(L.pkt + o_, %uu);", n, n);
+            if (ctx == CTX_XDP)
+                f.push_back({"(uint64_t)(uint32_t)(ga_ - (P + L.M + 1)) + " + N + " <= MIMIC_XDP_MD_SIZE",
+                             "xdp_load(kp, L, ga_ - (P + L.M + 1), " + N + ")",
+                             "xdp_store(kp, L, ga_ - (P + L.M + 1), " + N + ", " + v + ")"});
+            break;  // sk_buff fields: see skb_ctx_fast()
+        default: {
+            const std::string o = "(uint32_t)(ga_ - " + std::string(pa()) + ")";
+            if (stage) {
+                const std::string wo = "(uint32_t)(ga_ - " + std::string(pa()) + " - " + std::to_string(wb()) + "u)";
+                f.push_back({"(uint64_t)" + wo + " + " + N + " <= W_", ord("win_load(pwin_, tl_, " + wo + ", " + N + ")", n), ""});
+            }
+            f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord("ld_n(L.pkt + " + o + ", " + N + ")", n),
+                         "{ st_n(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
+                             (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
             break;
         }
-        E.line("      else { const int s_ = mem_load(kp, L, resolve(kp, L, a_), %uu, v_); if (s_) TERM(s_, %u); }", n, i);
-        E.line("      %s = v_; }", dst.c_str());
+        }
+        return f;
+    }
+
+    void load(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &dst) {
+        E.line("    ga_ = %s;", addr(base, off).c_str());
+        std::string pre = "    ";
+        for (auto &f : fast_forms(base, n, "")) {
+            E.line("%sif (%s) %s = %s;", pre.c_str(), f.cond.c_str(), dst.c_str(), f.val.c_str());
+            pre = "    else ";
+        }
+        if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {  // __sk_buff field: convertAccess directly
+            E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
+                   "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, 0, true);"
+                   " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
+            pre = "    else ";
+        }
+        if (share) {
+            E.line("%s{", pre.c_str());
+            to_blk(B_LD, i, "gn_ = " + std::to_string(n) + "u;");
+            E.line("      %s = gv_; }", dst.c_str());
+        } else {
+            E.line("%s{ uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, ga_), %uu, v_); if (s_) TERM(s_, %u); %s = v_; }",
+                   pre.c_str(), n, i, dst.c_str());
+        }
     }
 
     void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val) {
-        if (!fast_paths) {
-            E.line("    { const int s_ = mem_store(kp, L, resolve(kp, L, %s), %uu, %s); if (s_) TERM(s_, %u); }",
-                   addr(base, off).c_str(), n, val.c_str(), i);
-            return;
+        E.line("    ga_ = %s;", addr(base, off).c_str());
+        std::string pre = "    ";
+        for (auto &f : fast_forms(base, n, val)) {
+            if (f.store.empty()) continue;
+            E.line("%sif (%s) { %s; }", pre.c_str(), f.cond.c_str(), f.store.c_str());
+            pre = "    else ";
         }
-        E.line("    { const uint32_t a_ = %s;", addr(base, off).c_str());
-        switch (hint(base)) {
-        case HINT_STACK:
-            E.line("      const uint32_t o_ = a_ - kp.static_next;");
-            E.line("      if ((uint64_t)o_ + %uu <= kp.stack_size) stack_store(kp, L, o_, %uu, %s);", n, n, val.c_str());
-            break;
-        case HINT_CTX:
-            E.line("      const uint32_t o_ = a_ - (P + L.M + 1);");
-            E.line("      if ((uint64_t)o_ + %uu <= MIMIC_XDP_MD_SIZE) xdp_store(kp, L, o_, %uu, %s);", n, n, val.c_str());
-            break;
-        default:
-            E.line("      const uint32_t o_ = a_ - P;");
+        if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {
+            E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
+                   "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, %s, false);"
+                   " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
+            pre = "    else ";
+        }
+        if (share) {
+            E.line("%s{", pre.c_str());
+            to_blk(B_ST, i, "gn_ = " + std::to_string(n) + "u; gv_ = " + val + ";");
+            E.line("    }");
+        } else {
+            E.line("%s{ const Ref R_ = resolve(kp, L, ga_); const int s_ = mem_store(kp, L, R_, %uu, %s); if (s_) TERM(s_, %u);",
+                   pre.c_str(), n, val.c_str(), i);
             if (stage)
-                E.line("      if ((uint64_t)o_ + %uu <= L.M) { st_n(L.pkt + o_, %uu, %s); if (o_ < W_) win_store(pwin_, tl_, W_, o_, %uu, %s); }",
-                       n, n, val.c_str(), n, val.c_str());
-            else E.line("      if ((uint64_t)o_ + %uu <= L.M) st_n(L.pkt + o_, %uu, %s);", n, n, val.c_str());
-            break;
+                E.line("      if (R_.ptr == L.pkt && (R_.rk == RK_GLOBAL || R_.rk == RK_BEPKT)) win_store_rel(pwin_, tl_, W_, R_.off, %uu, %uu, %s); }",
+                       wb(), n, ord(val, n).c_str());
+            else E.line("    }");
         }
-        if (stage)  // a store that reaches the packet through another hint must update the window too
-            E.line("      else { const Ref R_ = resolve(kp, L, a_); const int s_ = mem_store(kp, L, R_, %uu, %s); if (s_) TERM(s_, %u);"
-                   " if (R_.ptr == L.pkt && R_.rk == RK_GLOBAL && R_.off < W_) win_store(pwin_, tl_, W_, R_.off, %uu, %s); } }",
-                   n, val.c_str(), i, n, val.c_str());
-        else
-            E.line("      else { const int s_ = mem_store(kp, L, resolve(kp, L, a_), %uu, %s); if (s_) TERM(s_, %u); } }", n,
-                   val.c_str(), i);
     }
 
     void insn(const ProgView &p, uint32_t i) {
@@ -442,6 +574,9 @@ class Gen {
         case H_CALL:
             helper(p, i);
             break;
+        case H_LDABS:
+            ldabs(p, i);
+            break;
         default:
             slow(p, i);
             break;
@@ -450,7 +585,14 @@ class Gen {
 
     void helper(const ProgView &p, uint32_t i) {  // emulator_linux_.go:125-194
         const DInsn &x = p.ins[i];
-        switch ((uint32_t)x.k) {
+        const uint32_t h = (uint32_t)x.k;
+        if (share && (h == 1 || h == 2 || h == 3 || h == 12)) {
+            E.line("    {");
+            to_blk(h == 1 ? B_H1 : h == 2 ? B_H2 : h == 3 ? B_H3 : B_H12, i, "");
+            E.line("    }");
+            return;
+        }
+        switch (h) {
         case 1:
             E.line("    { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0;", i);
             E.line("      if (ho.t_n) { L.t_lo = ho.t_lo; L.t_n = ho.t_n; L.t_ptr = ho.t_ptr; } }");
@@ -484,6 +626,42 @@ class Gen {
             E.line("      r0 = (uint64_t)(int64_t)-22; }");
             break;
         }
+    }
+
+    // LD_ABS / LD_IND (emulator_linux_.go:198-288).  Fast path: R6 is this process's sk_buff
+    // and the bytes lie in its packet memory -- then the generic answer is exactly a BigEndian
+    // load at packet offset 32 + x (entries are disjoint, so nothing else can match first).
+    void ldabs(const ProgView &p, uint32_t i) {
+        const DInsn &x = p.ins[i];
+        const uint32_t n = AUX_SZ(x.aux), s = insn_src(x);
+        const bool ind = (x.aux & AUX_X) != 0;
+        if (ind && s > 10) {  // Registers.Get panics (after the R6 check)
+            E.line("    { uint64_t v_ = 0; const int s_ = ld_abs(kp, L, r6, 0u, %uu, true, v_); TERM(s_ ? s_ : MIMIC_PANIC_BADREG, %u); }", n, i);
+            return;
+        }
+        const std::string N = std::to_string(n) + "u";
+        E.line("    ga_ = (uint32_t)%s%s;", imm(x.k).c_str(), ind ? (" + (uint32_t)" + reg(s)).c_str() : "");
+        std::string pre = "    ";
+        if (ctx == CTX_SKB && fast_paths) {
+            E.line("    if ((uint32_t)r6 - SK_ <= SKB_STRUCT_SIZE && (uint64_t)(uint32_t)(%uu + ga_) + %s <= L.M) {", SKB_HEADROOM_J, N.c_str());
+            if (stage)
+                E.line("      if ((uint64_t)ga_ + %s <= W_) r0 = %s; else r0 = %s;", N.c_str(),
+                       ord("win_load(pwin_, tl_, ga_, " + N + ")", n).c_str(),
+                       ord("ld_n(L.pkt + (uint32_t)(" + std::to_string(SKB_HEADROOM_J) + "u + ga_), " + N + ")", n).c_str());
+            else
+                E.line("      r0 = %s;", ord("ld_n(L.pkt + (uint32_t)(" + std::to_string(SKB_HEADROOM_J) + "u + ga_), " + N + ")", n).c_str());
+            E.line("    }");
+            pre = "    else ";
+        }
+        if (share) {
+            E.line("%s{", pre.c_str());
+            to_blk(B_ABS, i, "gn_ = " + N + ";");
+            E.line("      r0 = gv_; }");
+        } else {
+            E.line("%s{ uint64_t v_ = 0; const int s_ = ld_abs(kp, L, r6, ga_, %s, false, v_); if (s_) TERM(s_, %u); r0 = v_; }",
+                   pre.c_str(), N.c_str(), i);
+        }
+        E.line("    r1 = 0; r2 = 0; r3 = 0; r4 = 0; r5 = 0;");
     }
 
     // the interpreter's H_SLOW forms, specialised: per-lane-ordered errors and END
@@ -615,10 +793,11 @@ std::map<CacheKey, hipFunction_t> g_cache;
 
 }  // namespace
 
-std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, JitInfo *info) {
+std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
+                             JitInfo *info) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
-    Gen g(v);
+    Gen g(v, ctx_kind);
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;

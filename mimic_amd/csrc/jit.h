@@ -14,7 +14,9 @@ struct JitInfo {
     bool tail_calls;     // some program calls bpf_tail_call
     bool kp_by_value;    // the kernel takes KParams by value (else a pointer to a device copy)
 };
-std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, JitInfo *info);
+// ctx_kind: CtxKind of the batches the kernel runs
+std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
+                             JitInfo *info);
 // 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
 // batch with a smaller budget must run on the interpreter
 uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);

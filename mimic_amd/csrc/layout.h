@@ -105,6 +105,7 @@ enum Handler : uint32_t {
     H_EXIT = 11,
     H_CALL = 12,       // helper 1/2/3/8/12/65
     H_CALL_LOCAL = 13, // BPF-to-BPF
+    H_LDABS = 14,      // LD_ABS / LD_IND (AUX_X = IND); R6 must be the sk_buff (emulator_linux_.go:198-288)
 };
 #define AUX_H(a) ((a) & 0xffu)
 #define AUX_FALL_OK (1u << 8)    // PC+1 < len(Instructions)
@@ -121,6 +122,10 @@ struct DInsn {
 };
 
 enum Sched : uint32_t { SCHED_CHUNKED = 0, SCHED_INTERLEAVED = 1, SCHED_EXPLICIT = 2 };
+
+// context of a batch: LinuxContextXDP (context_xdp_md.go) or LinuxContextSKBuff (context_sk_buff.go)
+enum CtxKind : uint32_t { CTX_XDP = 0, CTX_SKB = 1 };
+struct SkbRec;
 
 struct KParams {
     // program / static memory
@@ -169,4 +174,11 @@ struct KParams {
     uint32_t *steps;
     int32_t *err_pc;
     uint64_t *lane_steps;          // optional: per-lane executed steps (insns/s accounting)
+    // sk_buff batches (skb.h): per-packet records, exclusive prefix of the leak footprints,
+    // and the device word holding the first leak address of this batch
+    uint32_t ctx_kind;             // CtxKind
+    uint32_t skb_ifindex;          // NetDev.IFIndex
+    SkbRec *skb_rec;
+    const uint64_t *skb_prefix;
+    const uint64_t *skb_base;
 };

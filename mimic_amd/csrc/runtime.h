@@ -11,6 +11,7 @@
 
 #include "layout.h"
 #include "hashmap.h"
+#include "skb.h"
 #include "../../include/mimic_amd.h"
 
 typedef uint16_t __attribute__((aligned(1))) u16u;
@@ -38,7 +39,19 @@ DEV T cget(const T *p, uint32_t i) {
     return out;
 }
 
-enum RegionKind : uint32_t { RK_UNRES = 0, RK_STACK = 1, RK_XDP = 2, RK_GLOBAL = 3, RK_NOTVMMEM = 4, RK_NOTDATASEC = 5 };
+enum RegionKind : uint32_t {
+    RK_UNRES = 0, RK_STACK = 1, RK_XDP = 2, RK_GLOBAL = 3, RK_NOTVMMEM = 4, RK_NOTDATASEC = 5,
+    RK_SKB = 6, RK_SK = 7, RK_FK = 8,   // *SKBuff / *SK / *FlowKeys: VMMem via convertAccess
+    RK_BEPKT = 9                         // sk_buff packet: PlainMemory with ByteOrder BigEndian
+};
+
+// The context kind of a batch.  A JIT kernel is generated for one kind and defines
+// MIMIC_CTX_FIXED, so that the other kind's code folds away; the interpreter reads kp.ctx_kind.
+#ifdef MIMIC_CTX_FIXED
+#define CTX_SKB_MODE(kp) (MIMIC_CTX_FIXED == CTX_SKB)
+#else
+#define CTX_SKB_MODE(kp) ((kp).ctx_kind == CTX_SKB)
+#endif
 
 struct Ref {
     uint32_t rk, off, limit;
@@ -60,6 +73,10 @@ struct Lane {
     // the segment scan.  Static entries never move, so an entry stays exact; t_n = 0 = empty.
     uint32_t t_lo, t_n;
     uint8_t *t_ptr;
+    // the packet entry's address (xdp: P; sk_buff: Pa) and the sk_buff context
+    uint32_t pa;
+    uint32_t ka;          // sock entry (flow keys at ka + 81)
+    SkbRec *rec;          // this process's SKBuff / SK / FlowKeys state (HBM, per packet)
 };
 
 static constexpr int EXIT_SIG = -1;
@@ -220,6 +237,28 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
             R.rk = RK_STACK;
             R.off = a - St;
             R.limit = kp.stack_size;
+        } else if (CTX_SKB_MODE(kp)) {
+            // sk_buff right after the stack; this process's sock / flow keys / packet at its
+            // leak position.  Earlier processes' leaked entries are not visible.
+            const uint32_t Sk = St + kp.stack_size + 1;
+            if (a - Sk <= SKB_STRUCT_SIZE) {
+                R.rk = RK_SKB;
+                R.off = a - Sk;
+                R.limit = SKB_STRUCT_SIZE;
+            } else if (L.rec && a - L.ka <= SKB_SK_SIZE) {
+                R.rk = RK_SK;
+                R.off = a - L.ka;
+                R.limit = SKB_SK_SIZE;
+            } else if (L.rec && a - (L.ka + SKB_SK_SIZE + 1) <= SKB_FK_SIZE) {
+                R.rk = RK_FK;
+                R.off = a - (L.ka + SKB_SK_SIZE + 1);
+                R.limit = SKB_FK_SIZE;
+            } else if (L.rec && a - L.pa <= L.M) {
+                R.rk = RK_BEPKT;
+                R.ptr = L.pkt;
+                R.off = a - L.pa;
+                R.limit = L.M;
+            }
         } else {
             const uint32_t P = St + kp.stack_size + 1;
             if (a - P <= L.M) {
@@ -303,16 +342,43 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
     return R;
 }
 
-DEV bool is_vmmem(uint32_t rk) { return rk == RK_STACK || rk == RK_XDP || rk == RK_GLOBAL || rk == RK_NOTDATASEC; }
+DEV bool is_vmmem(uint32_t rk) {
+    return rk == RK_STACK || rk == RK_XDP || rk == RK_GLOBAL || rk == RK_NOTDATASEC || rk == RK_SKB || rk == RK_SK ||
+           rk == RK_FK || rk == RK_BEPKT;
+}
+
+// big-endian scalar of n bytes (binary.BigEndian.Uint16/32/64)
+DEV uint64_t bswap_n(uint64_t v, uint32_t n) {
+    switch (n) {
+    case 2: return __builtin_bswap16((uint16_t)v);
+    case 4: return __builtin_bswap32((uint32_t)v);
+    case 8: return __builtin_bswap64(v);
+    default: return v;
+    }
+}
+
+// SKBuff / SK / FlowKeys .Load / .Store (convertAccess): no PlainMemory bounds check
+DEV int skb_access(const KParams &kp, const Lane &L, const Ref &R, uint32_t n, uint64_t &v, bool load) {
+    SkbRes o;
+    if (R.rk == RK_SKB)
+        o = skb_convert(L.rec, kp.skb_ifindex, L.pa + SKB_HEADROOM, L.pa + (L.M - SKB_HEADROOM - SKB_TAILROOM), L.ka,
+                        L.ka + SKB_SK_SIZE + 1, R.off, n, v, load);
+    else if (R.rk == RK_SK) o = sk_convert(L.rec, R.off, n, v, load);
+    else o = fk_convert(L.rec, R.off, n, v, load);
+    if (load) v = o.v;
+    return o.st;
+}
 
 // VMMem.Load/Store after GetEntry (inst.go:298-363): returns 0 or a status
 DEV int mem_load(const KParams &kp, const Lane &L, const Ref &R, uint32_t n, uint64_t &v) {
     if (R.rk == RK_UNRES) return MIMIC_ERR_MEM_UNRESOLVED;
     if (R.rk == RK_NOTVMMEM) return MIMIC_ERR_MEM_NOT_VMMEM;
     if (R.rk == RK_NOTDATASEC) return MIMIC_ERR_MEM_NOT_DATASEC;
+    if (R.rk == RK_SKB || R.rk == RK_SK || R.rk == RK_FK) return skb_access(kp, L, R, n, v, true);
     if ((uint64_t)R.off + n > R.limit) return MIMIC_ERR_MEM_BOUNDS;
     if (R.rk == RK_STACK) v = stack_load(kp, L, R.off, n);
     else if (R.rk == RK_XDP) v = xdp_load(kp, L, R.off, n);
+    else if (R.rk == RK_BEPKT) v = bswap_n(ld_n(R.ptr + R.off, n), n);
     else v = ld_n(R.ptr + R.off, n);
     return 0;
 }
@@ -320,15 +386,18 @@ DEV int mem_store(const KParams &kp, Lane &L, const Ref &R, uint32_t n, uint64_t
     if (R.rk == RK_UNRES) return MIMIC_ERR_MEM_UNRESOLVED;
     if (R.rk == RK_NOTVMMEM) return MIMIC_ERR_MEM_NOT_VMMEM;
     if (R.rk == RK_NOTDATASEC) return MIMIC_ERR_MEM_NOT_DATASEC;
+    if (R.rk == RK_SKB || R.rk == RK_SK || R.rk == RK_FK) return skb_access(kp, L, R, n, v, false);
     if ((uint64_t)R.off + n > R.limit) return MIMIC_ERR_MEM_BOUNDS;
     if (R.rk == RK_STACK) stack_store(kp, L, R.off, n, v);
     else if (R.rk == RK_XDP) xdp_store(kp, L, R.off, n, v);
+    else if (R.rk == RK_BEPKT) st_n(R.ptr + R.off, n, bswap_n(v, n));
     else st_n(R.ptr + R.off, n, v);
     return 0;
 }
 // VMMem.Read bounds check only (the bytes are consumed by the caller chunk-wise)
 DEV bool readable(const Ref &R, uint32_t n) {
-    if (!(R.rk == RK_STACK || R.rk == RK_XDP || R.rk == RK_GLOBAL)) return false;
+    // SKBuff / SK / FlowKeys .Read is "not implemented" (an error)
+    if (!(R.rk == RK_STACK || R.rk == RK_XDP || R.rk == RK_GLOBAL || R.rk == RK_BEPKT)) return false;
     return (uint64_t)R.off + n <= R.limit;
 }
 DEV uint64_t region_load(const KParams &kp, const Lane &L, const Ref &R, uint32_t off, uint32_t n) {
@@ -350,8 +419,8 @@ DEV bool reg_to_map(const KParams &kp, const Lane &L, uint64_t v, int32_t &map, 
         sub = R.sub;
         return true;
     }
-    if (R.rk == RK_STACK || R.rk == RK_XDP || R.rk == RK_GLOBAL) {
-        uint64_t a;
+    if (is_vmmem(R.rk)) {
+        uint64_t a = 0;
         if (mem_load(kp, L, R, 4, a)) return false;
         Ref R2 = resolve(kp, L, (uint32_t)a);
         if (R2.map >= 0) {
@@ -375,7 +444,7 @@ DEV uint8_t *array_value_ptr(const KParams &kp, const DMap &m, int32_t sub, uint
 
 // memmove of n bytes from a VM region into the arena (map update, emulator_linux_map_array.go:112)
 DEV void copy_into(const KParams &kp, const Lane &L, const Ref &src, uint8_t *dst, uint32_t n) {
-    bool backward = src.rk == RK_GLOBAL && src.ptr + src.off < dst && dst < src.ptr + src.off + n;
+    bool backward = (src.rk == RK_GLOBAL || src.rk == RK_BEPKT) && src.ptr + src.off < dst && dst < src.ptr + src.off + n;
     if (!backward) {
         for (uint32_t o = 0; o < n; o += 8) {
             uint32_t c = n - o < 8 ? n - o : 8;
@@ -610,6 +679,46 @@ DEV int helper_class(int32_t n) {
     }
 }
 
+// LD_ABS / LD_IND (LinuxEmulator.CustomInstruction, emulator_linux_.go:198-288): R6 must resolve
+// to the *SKBuff entry; R0 = Load(size) at skb.data + x (x = imm, or src + imm for LD_IND) in
+// whatever entry that address falls in; then R1-R5 = 0 (done by the caller).  A register
+// source > 10 panics after the R6 check (the caller passes bad_src).
+DEV int ld_abs(const KParams &kp, const Lane &L, uint64_t r6, uint32_t x, uint32_t n, bool bad_src, uint64_t &v) {
+    const Ref S = resolve(kp, L, (uint32_t)r6);
+    if (S.rk != RK_SKB) return MIMIC_ERR_LDABS;
+    if (bad_src) return MIMIC_PANIC_BADREG;
+    const Ref P = resolve(kp, L, L.pa + SKB_HEADROOM + x);
+    if (!is_vmmem(P.rk)) return MIMIC_ERR_LDABS;
+    const int rc = mem_load(kp, L, P, n, v);
+    if (rc == MIMIC_PANIC_SLICE) return rc;   // a Go panic stays a panic
+    return rc ? MIMIC_ERR_LDABS : 0;
+}
+
+// NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107) for packet i: the entries
+// of the skb.h layout, zeroed headroom / tailroom, R1 = the sk_buff address.  Returns 0 or
+// MIMIC_ERR_CTX_LOAD (SKBuffFromBytes failed, or AddEntry ran out of 32-bit address space;
+// then the packet memory is left untouched, as the reference never writes it).
+DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1) {
+    SkbRec *rec = kp.skb_rec + i;
+    const uint32_t lw = rec->len;
+    L.pkt = kp.pkt_data + kp.pkt_off[i];
+    L.rec = nullptr;
+    L.ka = 0;
+    L.pa = 0;
+    L.M = 0;
+    if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
+    const uint64_t ka = *kp.skb_base + kp.skb_prefix[i];
+    if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
+    L.rec = rec;
+    L.ka = (uint32_t)ka;
+    L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
+    L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
+    for (uint32_t b = 0; b < SKB_HEADROOM; b += 8) *(u64u *)(L.pkt + b) = 0;
+    for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
+    r1 = kp.static_next + kp.stack_size + 1;
+    return 0;
+}
+
 // ---------------------------------------------------------------------------------------
 // wave-wide minimum of a 32-bit key: DPP within each 16-lane row, then 4 readlanes
 // ---------------------------------------------------------------------------------------
@@ -773,5 +882,15 @@ DEV void win_store(PWin &w, uint32_t tl, uint32_t W, uint32_t o, uint32_t n, uin
         const uint32_t bits = sh + 8 * n - 64;
         const uint64_t m1 = (1ull << bits) - 1;
         w[q + 1][tl] = (w[q + 1][tl] & ~m1) | (v >> (64 - sh));
+    }
+}
+// mirror a packet store of n bytes at packet-memory offset o into a window that covers packet
+// memory [wb, wb + W): the part of the store that overlaps the window, if any
+DEV void win_store_rel(PWin &w, uint32_t tl, uint32_t W, uint32_t o, uint32_t wb, uint32_t n, uint64_t v) {
+    if (o >= wb) {
+        if (o - wb < W) win_store(w, tl, W, o - wb, n, v);
+    } else if (o + n > wb && W > 0) {
+        const uint32_t d = wb - o;
+        win_store(w, tl, W, 0, n - d, v >> (8 * d));
     }
 }

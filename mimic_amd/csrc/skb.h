@@ -1,0 +1,450 @@
+// skb.h -- the sk_buff context on the device (LinuxContextSKBuff, context_sk_buff.go:42-119,
+// and SKBuff / SK / FlowKeys, emulator_linux_sk_buff.go).
+//
+// One SkbRec per packet holds everything the reference keeps in its SKBuff, SK and FlowKeys
+// objects: the fields SKBuffFromBytes derives from the packet headers, the fields a program
+// may store into, and a 40-byte copy of the IP-address bytes.  SK's net.IP fields are slices
+// of gopacket's private copy of the packet, so reads see the ORIGINAL bytes even after the
+// program has rewritten its packet memory.
+//
+//   mimic_skb_prep_kernel (skb.hip)    : header walk -> SkbRec[i] + address footprint[i]
+//   exclusive scan of the footprints   : where packet i's leaked entries sit
+//   JIT / interpreter kernels          : context load, then __sk_buff / bpf_sock / flow_keys
+//                                        accesses via skb_access(); LD_ABS / LD_IND
+//
+// Address layout of one sequential reference run (memory_controller.go:58-112 first fit).
+// NewProcess adds the stack at St.  Load then adds the sk_buff (192 B) right after it, and
+// then the sock (80 B), flow keys (40 B) and packet (32 + L + 64 B).  Cleanup deletes the
+// stack and the sk_buff only (context_sk_buff.go:110-119).  So the next process reuses
+// [St, St+S+193) exactly, while the sock / flow-keys / packet entries of every earlier
+// process stay allocated:
+//   Sk = St + S + 1                 sk_buff [Sk, Sk+192]        same for every packet
+//   Ka = leak_base + prefix_i       sock    [Ka, Ka+80]
+//   Fa = Ka + 81                    flow    [Fa, Fa+40]
+//   Pa = Fa + 41                    packet  [Pa, Pa+96+L]       data = Pa+32, data_end = Pa+L
+// where prefix_i sums (219 + L_j) over the earlier packets whose Load succeeded.
+#pragma once
+#include <stdint.h>
+
+#define SKB_STRUCT_SIZE 192u     // SKBuff.Size(), emulator_linux_sk_buff.go:679-681
+#define SKB_SK_SIZE 80u          // SK.Size()
+#define SKB_FK_SIZE 40u          // FlowKeys.Size()
+#define SKB_HEADROOM 32u         // :113
+#define SKB_TAILROOM 64u         // :116
+#define SKB_FOOT_FIXED 219u      // (80+1) + (40+1) + (96+1): address span of one packet's leaks
+#define SKB_LOAD_FAILED 0x80000000u
+#define SKB_SNAP 40u
+#define SKB_REC_BYTES 160u
+
+// net.IP as the reference holds it: kind 0 = make(net.IP, n) (zeros, cap n), 1 = nil,
+// 2 = gopacket's packet copy from byte `off` (cap = L - off: Go slices may read past n)
+struct SkbIP {
+    uint32_t off;
+    uint8_t kind, n, pad[2];
+};
+
+struct SkbRec {  // 160 bytes
+    // ---- derived at load (read-only for the program) ----
+    uint32_t len;              // L | SKB_LOAD_FAILED
+    uint16_t protocol, vlan_proto, vlan_tci;
+    uint8_t vlan_present, family;   // family: SK.Family (AF_UNSPEC 0 / AF_INET 2 / AF_INET6 10)
+    uint32_t sport, dport;     // SK.SrcPort / DstPort
+    SkbIP ip[4];               // SK srcIP4, dstIP4, srcIP6, dstIP6
+    uint32_t snap_base;
+    uint8_t snap[SKB_SNAP];    // packet bytes [snap_base, snap_base + 40) (0 beyond L)
+    // ---- writable state ----
+    uint32_t mark, priority;   // SKBuff.markOrReservedTailroom, priority
+    uint16_t queue_mapping, tc_index;
+    uint8_t cb6, cb7, pad1[2];   // cb[6:8] (tc_classid)
+    int64_t tstamp;            // time.Time as Unix seconds
+    uint32_t sk_bound_dev_if, sk_mark, sk_priority;
+    // FlowKeys, :1003-1019
+    uint16_t fk_nhoff, fk_thoff, fk_addr_proto;
+    uint8_t fk_is_frag, fk_is_first_frag, fk_is_encap, fk_ip_proto;
+    uint16_t fk_n_proto, fk_sport, fk_dport;
+    uint32_t fk_flags, fk_flow_label;
+    uint32_t pad2;
+};
+
+#define SKB_TSTAMP_ZERO (-62135596800ll)   // time.Time{}.Unix()
+
+#ifndef SKB_DEV
+#define SKB_DEV static __device__ __forceinline__
+#endif
+// the field accessors are big switches reached from every generic memory access of a JIT
+// kernel: out of line (value arguments and results only, so no scratch) to keep the kernels
+// small and their hipRTC compile fast
+#define SKB_COLD static __device__ __noinline__
+
+struct SkbRes {
+    uint64_t v;
+    int st;   // 0 or a status
+};
+
+SKB_DEV uint16_t skb_rd16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+// ---------------------------------------------------------------------------------------
+// SKBuffFromBytes (emulator_linux_sk_buff.go:108-265) over gopacket v1.1.19's eager decode
+// (gopacket.NewPacket(data, LayerTypeEthernet, Default)).  Only the layers that set SKBuff
+// fields or lead to another such layer are walked: Ethernet (+802.3 length -> LLC/SNAP),
+// Dot1Q / QinQ, IPv4 (+options, fragments stop), IPv6 (+Routing / Destination options),
+// TCP, UDP and the UDP tunnels that decode another link / network layer (VXLAN 4789, Geneve
+// 6081, GTPv1-U 2152), IPIP / IPv6-in-IP.  A second link, network or transport layer is the
+// reference's "handling of multiple ... layers not supported" error.  The walk is iterative
+// (a small state machine) rather than recursive.  Returns 0, or 1 for that error.
+// ---------------------------------------------------------------------------------------
+enum { SW_DONE, SW_ETH, SW_ETYPE, SW_LLC, SW_DOT1Q, SW_IP, SW_PROTO };
+
+SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
+    uint32_t st = SW_ETH, o = 0, len = L, t = 0;
+    uint32_t link = 0, net = 0, trans = 0;
+    for (uint32_t guard = 0; guard < L + 64; guard++) {  // each Dot1Q step consumes 4 bytes
+        switch (st) {
+        case SW_ETH: {
+            if (len < 14) return 0;      // "Ethernet packet too small": no layer
+            if (link++) return 1;
+            t = skb_rd16(pkt + o + 12);
+            uint32_t pl = len - 14;
+            if (t < 0x0600) {            // 802.3 length field: EthernetTypeLLC, payload trimmed
+                if (pl > t) pl = t;
+                t = 0;
+            }
+            r.protocol = (uint16_t)t;    // skb.protocol = EthernetType (:187)
+            o += 14;
+            len = pl;
+            st = SW_ETYPE;
+            break;
+        }
+        case SW_ETYPE:
+            if (len == 0) return 0;
+            switch (t) {
+            case 0x0000: st = SW_LLC; break;
+            case 0x0800: case 0x86DD: st = SW_IP; break;
+            case 0x8100: case 0x88a8: st = SW_DOT1Q; break;
+            case 0x6558: st = SW_ETH; break;   // transparent Ethernet bridging
+            default: return 0;
+            }
+            break;
+        case SW_LLC: {   // LLC + SNAP (llc.go)
+            if (len < 3) return 0;
+            const uint8_t *d = pkt + o;
+            uint32_t hl = 3;
+            if (!(d[2] & 1) || (d[2] & 3) == 1) {   // I- or S-format: 2-byte control
+                if (len < 4) return 0;
+                hl = 4;
+            }
+            if ((d[0] & 0xfe) != 0xaa || (d[1] & 0xfe) != 0xaa) return 0;
+            if (len - hl < 5) return 0;
+            t = skb_rd16(d + hl + 3);
+            o += hl + 5;
+            len -= hl + 5;
+            st = SW_ETYPE;
+            break;
+        }
+        case SW_DOT1Q: {
+            if (len < 4) return 0;
+            const uint8_t *d = pkt + o;
+            r.vlan_proto = skb_rd16(d + 2);   // Dot1Q.Type (:182)
+            r.vlan_tci = skb_rd16(d);
+            r.vlan_present = 1;
+            t = skb_rd16(d + 2);
+            o += 4;
+            len -= 4;
+            st = SW_ETYPE;
+            break;
+        }
+        case SW_IP: {    // decodeIPv4orIPv6
+            if (len == 0) return 0;
+            const uint32_t v = pkt[o] >> 4;
+            const uint8_t *d = pkt + o;
+            if (v == 4) {
+                if (net++) return 1;
+                r.family = 2;
+                if (len < 20) {  // SrcIP / DstIP stay nil
+                    r.ip[0].kind = 1;
+                    r.ip[1].kind = 1;
+                    return 0;
+                }
+                r.ip[0].kind = 2; r.ip[0].off = o + 12;
+                r.ip[1].kind = 2; r.ip[1].off = o + 16;
+                const uint32_t ihl = d[0] & 0x0f, ff = skb_rd16(d + 6);
+                uint32_t tl = skb_rd16(d + 2);
+                if (tl == 0) tl = len;   // TSO
+                if (tl < 20 || ihl < 5 || ihl * 4 > tl) return 0;
+                uint32_t dl = len;
+                if (len > tl) dl = tl;
+                else if (len < tl && ihl * 4 > len) return 0;
+                for (uint32_t q = 20; q < ihl * 4;) {   // options: a malformed one ends the decode
+                    const uint8_t ot = d[q];
+                    if (ot == 0) break;
+                    if (ot == 1) { q++; continue; }
+                    if (ihl * 4 - q < 2) return 0;
+                    const uint8_t ol = d[q + 1];
+                    if (ihl * 4 - q < ol) return 0;
+                    if (ol <= 2) return 0;
+                    q += ol;
+                }
+                if ((ff & 0x2000) || (ff & 0x1fff)) return 0;   // a fragment
+                t = d[9];
+                o += ihl * 4;
+                len = dl - ihl * 4;
+                st = SW_PROTO;
+            } else if (v == 6) {
+                if (net++) return 1;
+                r.family = 10;
+                if (len < 40) {
+                    r.ip[2].kind = 1;
+                    r.ip[3].kind = 1;
+                    return 0;
+                }
+                r.ip[2].kind = 2; r.ip[2].off = o + 8;
+                r.ip[3].kind = 2; r.ip[3].off = o + 24;
+                uint32_t next = d[6];
+                const uint32_t plen = skb_rd16(d + 4);
+                if (next == 0) return 0;   // Hop-by-Hop / jumbograms: not restated
+                if (plen == 0) return 0;
+                uint32_t po = o + 40, pl = len - 40;
+                if (pl > plen) pl = plen;
+                for (int k = 0; k < 16; k++) {
+                    if (next == 43 || next == 60) {   // Routing / Destination options
+                        if (pl < 2) return 0;
+                        const uint32_t hl = (pkt[po + 1] + 1u) * 8;
+                        if (pl < hl) return 0;
+                        next = pkt[po];
+                        po += hl;
+                        pl -= hl;
+                        continue;
+                    }
+                    if (next == 44) return 0;  // Fragment
+                    break;
+                }
+                t = next;
+                o = po;
+                len = pl;
+                st = SW_PROTO;
+            } else {
+                return 0;
+            }
+            break;
+        }
+        case SW_PROTO:
+            if (len == 0) return 0;
+            if (t == 6) {            // TCP: the layer is added even when its decode fails
+                if (trans++) return 1;
+                if (len >= 20) {
+                    r.sport = skb_rd16(pkt + o);
+                    r.dport = skb_rd16(pkt + o + 2);
+                }
+                return 0;
+            }
+            if (t == 4 || t == 41) { st = SW_IP; break; }
+            if (t != 17) return 0;
+            {                        // UDP (udp.go) and the tunnels behind it
+                if (trans++) return 1;
+                if (len < 8) return 0;
+                const uint8_t *d = pkt + o;
+                r.sport = skb_rd16(d);
+                r.dport = skb_rd16(d + 2);
+                const uint32_t ulen = skb_rd16(d + 4);
+                uint32_t plen;
+                if (ulen >= 8) plen = (ulen > len ? len : ulen) - 8;
+                else if (ulen == 0) plen = len - 8;
+                else return 0;
+                if (plen == 0) return 0;
+                // NextLayerType: the destination port's type unless it is Payload, else the
+                // source port's (gopacket's UDPPortLayerType table)
+                uint32_t port = r.sport;
+                switch (r.dport) {
+                case 53: case 123: case 4789: case 67: case 68: case 546: case 547: case 5060: case 6343:
+                case 6081: case 3784: case 2152: case 623: case 1812:
+                    port = r.dport;
+                    break;
+                default:
+                    break;
+                }
+                const uint32_t po = o + 8;
+                const uint8_t *q = pkt + po;
+                if (port == 4789) {          // VXLAN, then Ethernet
+                    if (plen < 8) return 0;
+                    o = po + 8;
+                    len = plen - 8;
+                    st = SW_ETH;
+                } else if (port == 6081) {   // Geneve: 8 + options, then the protocol type
+                    if (plen < 8) return 0;
+                    const uint32_t hl = 8 + (q[0] & 0x3f) * 4u;
+                    if (plen < hl) return 0;
+                    t = skb_rd16(q + 2);
+                    o = po + hl;
+                    len = plen - hl;
+                    st = SW_ETYPE;
+                } else if (port == 2152) {   // GTPv1-U, then IPv4 / IPv6
+                    if (plen < 8) return 0;
+                    const uint32_t hl = (q[0] & 0x07) ? 12 : 8;
+                    if ((q[0] & 0x04) || plen <= hl) return 0;
+                    o = po + hl;
+                    len = plen - hl;
+                    st = SW_IP;
+                } else {
+                    return 0;
+                }
+            }
+            break;
+        default:
+            return 0;
+        }
+    }
+    return 0;
+}
+
+// SKBuffFromBytes + the parts of LinuxContextSKBuff.Load that do not depend on addresses
+SKB_DEV void skb_init(const uint8_t *pkt, uint32_t L, SkbRec &r) {
+    uint64_t *w = (uint64_t *)&r;
+    for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) w[q] = 0;
+    r.ip[0].n = 4; r.ip[1].n = 4; r.ip[2].n = 16; r.ip[3].n = 16;   // make(net.IP, 4/16)
+    r.tstamp = SKB_TSTAMP_ZERO;
+    const int err = skb_walk(pkt, L, r);
+    r.len = L | (err ? SKB_LOAD_FAILED : 0u);
+    // the one IP slice window programs can read (IPv4: src..dst+11, IPv6: src..dst+23)
+    uint32_t b = r.family == 10 && r.ip[2].kind == 2 ? r.ip[2].off : (r.ip[0].kind == 2 ? r.ip[0].off : 0u);
+    r.snap_base = b;
+    for (uint32_t k = 0; k < SKB_SNAP; k++) r.snap[k] = b + k < L ? pkt[b + k] : 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// convertAccess (SKBuff :295-676, SK :772-918, FlowKeys :1031-1175).  Status codes are those
+// of include/mimic_amd.h; loads return the value in v, stores take it from v.
+// ---------------------------------------------------------------------------------------
+SKB_DEV uint64_t skb_to_size(uint64_t v, uint32_t n) { return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1)); }
+
+// copy(v, ip[start:start+n]); b2i(v): a slice-bounds panic past the capacity
+SKB_DEV int skb_ip_load(const SkbRec &r, uint32_t which, uint64_t start, uint32_t n, uint64_t &v) {
+    const SkbIP ip = r.ip[which];
+    const uint64_t cap = ip.kind == 0 ? ip.n : ip.kind == 1 ? 0 : (uint64_t)(r.len & ~SKB_LOAD_FAILED) - ip.off;
+    if (start + n > cap) return 27;   // MIMIC_PANIC_SLICE
+    uint64_t x = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t b = ip.kind == 2 ? r.snap[ip.off - r.snap_base + (uint32_t)start + k] : 0u;
+        x = (x << 8) | b;
+    }
+    v = x;
+    return 0;
+}
+
+#define SKB_RO() do { if (!load) return 26; } while (0)   // errReadOnly -> MIMIC_ERR_CTX_ACCESS
+
+// SKBuff.convertAccess; data = skb.data, end = skb.end, ka/fa = sock / flow-keys addresses
+SKB_DEV int skb_convert_(SkbRec &r, uint32_t ifindex, uint32_t data, uint32_t end, uint32_t ka, uint32_t fa,
+                         uint32_t off, uint32_t n, uint64_t &v, bool load) {
+    const uint64_t val = v;
+    switch (off) {
+    case 0: SKB_RO(); v = skb_to_size(r.len & ~SKB_LOAD_FAILED, n); return 0;
+    case 4: SKB_RO(); v = 0; return 0;                                   // pkt_type & 7 (never set)
+    case 8: if (load) v = skb_to_size(r.mark, n); else r.mark = (uint32_t)skb_to_size(val, n); return 0;
+    case 12: if (load) v = skb_to_size(r.queue_mapping, n); else r.queue_mapping = (uint16_t)skb_to_size(val, n); return 0;
+    case 16: SKB_RO(); v = skb_to_size(r.protocol, n); return 0;
+    case 20: SKB_RO(); v = r.vlan_present ? 1 : 0; return 0;
+    case 24: SKB_RO(); v = skb_to_size(r.vlan_tci, n); return 0;
+    case 28: SKB_RO(); v = skb_to_size(r.vlan_proto, n); return 0;
+    case 32: if (load) v = skb_to_size(r.priority, n); else r.priority = (uint32_t)skb_to_size(val, n); return 0;
+    case 36: SKB_RO(); v = 0; return 0;                                  // ingress_ifindex: skbIIF (0)
+    case 40: SKB_RO(); v = skb_to_size(ifindex, n); return 0;            // dev.IFIndex
+    case 44: if (load) v = skb_to_size(r.tc_index, n); else r.tc_index = (uint16_t)skb_to_size(val, n); return 0;
+    case 68: SKB_RO(); v = 0; return 0;                                  // hash (never set)
+    case 72:                                                             // tc_classid: native u16 at cb[6:8]
+        if (load) v = (uint64_t)(r.cb6 | (r.cb7 << 8));
+        else { r.cb6 = (uint8_t)val; r.cb7 = (uint8_t)(val >> 8); }
+        return 0;
+    case 76: SKB_RO(); v = skb_to_size(data, n); return 0;
+    case 80: SKB_RO(); v = end; return 0;                                // data_end: cb[32:36]
+    case 84: SKB_RO(); v = 0; return 0;                                  // napi_id
+    case 88: SKB_RO(); v = skb_to_size(r.family, n); return 0;           // sk.Family
+    case 132: SKB_RO(); v = skb_to_size(r.dport, n); return 0;           // remote_port
+    case 136: SKB_RO(); v = skb_to_size(r.sport, n); return 0;           // local_port
+    case 140: SKB_RO(); v = 0; return 0;                                 // data_meta: cb[36:38]
+    case 144: case 148: SKB_RO(); v = fa; return 0;                      // flow_keys
+    case 152: case 156:                                                  // tstamp
+        if (load) v = (uint64_t)r.tstamp; else r.tstamp = (int64_t)val;
+        return 0;
+    case 160: SKB_RO(); v = 0; return 0;                                 // wire_len: cb[0:4]
+    case 164: case 176: case 184: case 188: return 26;                   // "not yet implemented"
+    case 168: case 172: SKB_RO(); v = ka; return 0;                      // sk
+    default: break;
+    }
+    if (off >= 48 && off < 68) {   // cb[5]: a load slices cb[offset:size] (low > high): panic
+        if (load) return 27;
+        return 0;
+    }
+    if (off >= 92 && off < 96) { SKB_RO(); return skb_ip_load(r, 1, off - 92, n, v); }     // remote_ip4
+    if (off >= 96 && off < 100) { SKB_RO(); return skb_ip_load(r, 0, off - 96, n, v); }    // local_ip4
+    if (off >= 100 && off < 116) { SKB_RO(); return skb_ip_load(r, 3, off - 100, n, v); }  // remote_ip6
+    if (off >= 116 && off < 132) { SKB_RO(); return skb_ip_load(r, 2, off - 116, n, v); }  // local_ip6
+    return 26;   // "invalid offset"
+}
+
+// SK.convertAccess
+SKB_DEV int sk_convert_(SkbRec &r, uint32_t off, uint32_t n, uint64_t &v, bool load) {
+    const uint64_t val = v;
+    switch (off) {
+    case 0: if (load) v = skb_to_size(r.sk_bound_dev_if, n); else r.sk_bound_dev_if = (uint32_t)skb_to_size(val, n); return 0;
+    case 4: SKB_RO(); v = skb_to_size(r.family, n); return 0;
+    case 8: SKB_RO(); v = 0; return 0;                                   // type
+    case 12: SKB_RO(); v = 0; return 0;                                  // protocol
+    case 16: if (load) v = skb_to_size(r.sk_mark, n); else r.sk_mark = (uint32_t)skb_to_size(val, n); return 0;
+    case 20: if (load) v = skb_to_size(r.sk_priority, n); else r.sk_priority = (uint32_t)skb_to_size(val, n); return 0;
+    case 44: SKB_RO(); v = skb_to_size(r.sport, n); return 0;
+    case 48: SKB_RO(); v = skb_to_size(r.dport, n); return 0;
+    case 72: SKB_RO(); v = skb_to_size(7, n); return 0;                  // state: BPF_TCP_CLOSE
+    case 76: SKB_RO(); v = 0; return 0;                                  // rx_queue_mapping
+    default: break;
+    }
+    if (off >= 24 && off < 28) { SKB_RO(); return skb_ip_load(r, 0, off - 24, n, v); }
+    if (off >= 28 && off < 44) { SKB_RO(); return skb_ip_load(r, 2, off - 28, n, v); }
+    if (off >= 52 && off < 56) { SKB_RO(); return skb_ip_load(r, 1, off - 52, n, v); }
+    if (off >= 56 && off < 72) { SKB_RO(); return skb_ip_load(r, 3, (uint64_t)(uint32_t)(off - 68), n, v); }  // start wraps below 68
+    return 26;
+}
+
+// FlowKeys.convertAccess: each field answers for every offset it covers
+#define FK_RW(fld, T) do { if (load) v = skb_to_size(r.fld, n); else r.fld = (T)skb_to_size(val, n); return 0; } while (0)
+SKB_DEV int fk_convert_(SkbRec &r, uint32_t off, uint32_t n, uint64_t &v, bool load) {
+    const uint64_t val = v;
+    switch (off) {
+    case 0: case 1: FK_RW(fk_nhoff, uint16_t);
+    case 2: case 3: FK_RW(fk_thoff, uint16_t);
+    case 4: case 5: FK_RW(fk_addr_proto, uint16_t);
+    case 6: FK_RW(fk_is_frag, uint8_t);
+    case 7: FK_RW(fk_is_first_frag, uint8_t);
+    case 8: FK_RW(fk_is_encap, uint8_t);
+    case 9: FK_RW(fk_ip_proto, uint8_t);
+    case 10: case 11: FK_RW(fk_n_proto, uint16_t);
+    case 12: case 13: FK_RW(fk_sport, uint16_t);
+    case 14: case 15: FK_RW(fk_dport, uint16_t);
+    case 32: case 33: case 34: case 35: FK_RW(fk_flags, uint32_t);
+    case 36: case 37: case 38: case 39: FK_RW(fk_flow_label, uint32_t);
+    default: break;
+    }
+    if (off >= 16 && off < 32) return 27;   // ip[offset:...] of a 16-byte slice
+    return 26;
+}
+#undef FK_RW
+#undef SKB_RO
+
+SKB_COLD SkbRes skb_convert(SkbRec *r, uint32_t ifindex, uint32_t data, uint32_t end, uint32_t ka, uint32_t fa,
+                            uint32_t off, uint32_t n, uint64_t v, bool load) {
+    SkbRes o;
+    o.st = skb_convert_(*r, ifindex, data, end, ka, fa, off, n, v, load);
+    o.v = v;
+    return o;
+}
+SKB_COLD SkbRes sk_convert(SkbRec *r, uint32_t off, uint32_t n, uint64_t v, bool load) {
+    SkbRes o;
+    o.st = sk_convert_(*r, off, n, v, load);
+    o.v = v;
+    return o;
+}
+SKB_COLD SkbRes fk_convert(SkbRec *r, uint32_t off, uint32_t n, uint64_t v, bool load) {
+    SkbRes o;
+    o.st = fk_convert_(*r, off, n, v, load);
+    o.v = v;
+    return o;
+}

@@ -1,0 +1,64 @@
+// skb.hip -- context construction for sk_buff batches (LinuxContextSKBuff.Load,
+// context_sk_buff.go:42-107, over SKBuffFromBytes, emulator_linux_sk_buff.go:108-265).
+//
+// Three stream-ordered steps before the program kernel (JIT or interpreter) runs:
+//   1. mimic_skb_prep_kernel: one thread per packet walks the headers once and writes the
+//      packet's SkbRec (skb.h) and its leak footprint (219 + L, or 0 when Load fails);
+//   2. an exclusive scan of the footprints (hipCUB): packet i's sock / flow-keys / packet
+//      entries start at leak_base + prefix[i], exactly where a sequential reference run's
+//      first-fit AddEntry puts them (Cleanup leaks them, so they pile up);
+//   3. mimic_skb_advance_kernel: publishes this batch's leak_base and moves the VM's leak
+//      cursor past the batch (device-side: no host round trip between batches).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "runtime.h"
+
+// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them
+extern "C" __global__ __launch_bounds__(256) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
+                                                                       const uint64_t *__restrict__ pkt_off,
+                                                                       const uint32_t *__restrict__ pkt_len,
+                                                                       uint32_t n, SkbRec *__restrict__ rec,
+                                                                       uint64_t *__restrict__ foot) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t L = pkt_len[i];
+    SkbRec r;
+    skb_init(pkt_data + pkt_off[i] + SKB_HEADROOM, L, r);
+    rec[i] = r;
+    foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
+}
+
+// state[0] = the VM's next leak address, state[1] = this batch's leak base
+extern "C" __global__ void mimic_skb_advance_kernel(uint64_t *state, const uint64_t *prefix, const uint64_t *foot,
+                                                    uint32_t n, uint64_t init_base, uint32_t use_init) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t base = use_init ? init_base : state[0];
+    state[1] = base;
+    state[0] = base + (n ? prefix[n - 1] + foot[n - 1] : 0ull);
+}
+
+extern "C" size_t mimic_skb_scan_bytes(uint32_t n) {
+    size_t bytes = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n) !=
+        hipSuccess)
+        return 0;
+    return bytes;
+}
+
+extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
+                                     uint32_t n, SkbRec *rec, uint64_t *foot, uint64_t *prefix, void *scan_tmp,
+                                     size_t scan_bytes, uint64_t *state, uint64_t init_base, uint32_t use_init,
+                                     hipStream_t st) {
+    if (n) {
+        hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pkt_data, pkt_off, pkt_len, n,
+                           rec, foot);
+        if (hipGetLastError() != hipSuccess) return -1;
+        size_t bytes = scan_bytes;
+        if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, (const uint64_t *)foot, prefix, (int)n, st) != hipSuccess)
+            return -1;
+    }
+    hipLaunchKernelGGL(mimic_skb_advance_kernel, dim3(1), dim3(64), 0, st, state, prefix, foot, n, init_base, use_init);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -284,12 +284,35 @@ class LinuxContextXDP:  # context_xdp_md.go:22-34
     Name: str = ""
 
 
+@dataclass
+class NetDev:  # emulator_linux_sk_buff.go:962-964
+    IFIndex: int = 0
+
+
+@dataclass
+class LinuxContextSKBuff:  # context_sk_buff.go:20-29
+    """An sk_buff context.  The reference also accepts a user-given SK / FlowKeys (JSON "sock" /
+    "flowKeys"); this engine builds them from the packet (the reference's default) only."""
+    Packet: bytes = b""
+    Dev: Optional[NetDev] = None
+    Name: str = ""
+
+
 def UnmarshalContextJSON(text: str):
-    """context.go:57-71 + context_xdp_md.go:10-19 (xdp_md only)."""
+    """context.go:57-71 + context_xdp_md.go:10-19 + context_sk_buff.go:8-17."""
     obj = json.loads(text)
-    if obj.get("type") != "xdp_md":
-        raise MimicError(f"no context unmarshaller registered for type '{obj.get('type')}'")
+    typ = obj.get("type")
     c = obj.get("ctx") or {}
+    if typ == "sk_buff":
+        if c.get("sock") is not None or c.get("flowKeys") is not None:
+            raise MimicError("sk_buff contexts with a custom sock / flowKeys are not supported by this engine")
+        pkt = c.get("packet")
+        dev = c.get("dev")
+        return LinuxContextSKBuff(Packet=base64.b64decode(pkt) if pkt else b"",
+                                  Dev=NetDev(int(dev.get("ifIndex", 0))) if dev is not None else None,
+                                  Name=obj.get("name", ""))
+    if typ != "xdp_md":
+        raise MimicError(f"no context unmarshaller registered for type '{typ}'")
     pkt = c.get("packet")
     return LinuxContextXDP(Headroom=int(c.get("headroom", 0)), Tailroom=int(c.get("tailroom", 0)),
                            Packet=base64.b64decode(pkt) if pkt else b"",
@@ -406,7 +429,7 @@ class VM:
         _check(self.h, self.lib.mimic_stack_addr(self.h, C.byref(a)), "stack addr")
         return a.value
 
-    def NewProcess(self, entrypoint: int, ctx: Optional[LinuxContextXDP]) -> "Process":  # vm.go:198-235
+    def NewProcess(self, entrypoint: int, ctx=None) -> "Process":  # vm.go:198-235
         if entrypoint >= len(self.programs):
             raise MimicError(f"no program with id '{entrypoint}' is loaded")
         return Process(self, entrypoint, ctx)
@@ -426,6 +449,24 @@ class VM:
         if sync:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
         return results
+
+    def RunSKBBatch(self, prog_id: int, batch: "SKBBatch", results: Optional["XDPResults"] = None,
+                    stream=None, sync: bool = True) -> "XDPResults":
+        """N x {NewProcess(LinuxContextSKBuff), SetCPUID, Run, read R0, Cleanup} on the GPU."""
+        if results is None:
+            results = XDPResults.empty(batch.n, batch.pkt_data.device)
+        st = stream.cuda_stream if stream is not None else None
+        rc = self.lib.mimic_run_skb(self.h, prog_id, batch._c(), results._c(), st)
+        if rc:
+            _check(self.h, rc, "RunSKBBatch")
+        if sync:
+            _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
+        return results
+
+    def SKBRelease(self) -> None:
+        """Forget the sock / flow-keys / packet entries earlier sk_buff processes leaked (a fresh
+        VM with the same maps and programs)."""
+        _check(self.h, self.lib.mimic_skb_release(self.h), "skb release")
 
     def RunXDPHost(self, prog_id: int, buf, off, lens, schedule=L.SCHED_INTERLEAVED, cpu=None, headroom: int = 0,
                    tailroom: int = 0, ingress: int = 0, rxq: int = 0, egress: int = 0, step_budget: int = 0,
@@ -501,7 +542,7 @@ class Registers:
 class Process:
     """Single process = a one-packet batch on the GPU (the Process.Run drop-in)."""
 
-    def __init__(self, vm: VM, prog_id: int, ctx: Optional[LinuxContextXDP]):
+    def __init__(self, vm: VM, prog_id: int, ctx=None):
         self.VM = vm
         self.prog_id = prog_id
         self.Context = ctx
@@ -528,11 +569,16 @@ class Process:
         ctx = self.Context or LinuxContextXDP()
         if self.cpuID < 0 or self.cpuID >= self.VM.settings.vcpus:
             raise MimicError("process has no valid CPU ID (SetCPUID first)")
-        batch = XDPBatch.from_packets([ctx.Packet], device=f"cuda:{self.VM.settings.device}",
-                                      headroom=ctx.Headroom, tailroom=ctx.Tailroom, ingress=ctx.IngessIfIndex,
-                                      rxq=ctx.RxQueueIndex, egress=ctx.EgressIfIndex,
-                                      schedule=L.SCHED_EXPLICIT, cpu=[self.cpuID], step_budget=step_budget)
-        res = self.VM.RunXDPBatch(self.prog_id, batch)
+        dev = f"cuda:{self.VM.settings.device}"
+        if isinstance(ctx, LinuxContextSKBuff):
+            batch = SKBBatch.from_packets([ctx.Packet], device=dev, ifindex=ctx.Dev.IFIndex if ctx.Dev else 0,
+                                          schedule=L.SCHED_EXPLICIT, cpu=[self.cpuID], step_budget=step_budget)
+            res = self.VM.RunSKBBatch(self.prog_id, batch)
+        else:
+            batch = XDPBatch.from_packets([ctx.Packet], device=dev, headroom=ctx.Headroom, tailroom=ctx.Tailroom,
+                                          ingress=ctx.IngessIfIndex, rxq=ctx.RxQueueIndex, egress=ctx.EgressIfIndex,
+                                          schedule=L.SCHED_EXPLICIT, cpu=[self.cpuID], step_budget=step_budget)
+            res = self.VM.RunXDPBatch(self.prog_id, batch)
         self.Registers.R0 = int(res.r0[0].item()) & 0xFFFFFFFFFFFFFFFF
         self.Steps = int(res.steps[0].item())
         self.Status = int(res.status[0].item())
@@ -659,6 +705,74 @@ class XDPBatch:
         h = int(self.headroom[i].item()) if not np.isscalar(self.headroom) else int(self.headroom)
         t_ = int(self.tailroom[i].item()) if not np.isscalar(self.tailroom) else int(self.tailroom)
         n = h + int(self.pkt_len[i].item()) + t_
+        return bytes(self.pkt_data[o:o + n].cpu().numpy().tobytes())
+
+
+class SKBBatch:
+    """A batch of sk_buff contexts resident on the GPU (see mimic_skb_batch): packet memory i is
+    32 + L + 64 bytes at pkt_off[i], the packet at +32."""
+    HEADROOM, TAILROOM = 32, 64
+
+    def __init__(self, pkt_data, pkt_off, pkt_len, ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+        self.pkt_data, self.pkt_off, self.pkt_len = pkt_data, pkt_off, pkt_len
+        self.ifindex, self.schedule, self.cpu, self.step_budget = ifindex, schedule, cpu, step_budget
+
+    @property
+    def n(self) -> int:
+        return int(self.pkt_len.numel())
+
+    def _c(self):
+        cached = getattr(self, "_cstruct", None)
+        if cached is not None:
+            return cached
+        b = L.SKBBatch()
+        b.n, b.schedule = self.n, self.schedule
+        b.pkt_data, b.pkt_off, b.pkt_len = self.pkt_data.data_ptr(), self.pkt_off.data_ptr(), self.pkt_len.data_ptr()
+        b.ifindex = int(self.ifindex)
+        self._cpu_host = None
+        if self.schedule == L.SCHED_EXPLICIT:
+            import numpy as np
+
+            self._cpu_host = np.ascontiguousarray(np.asarray(self.cpu, dtype=np.int32))
+            b.cpu = self._cpu_host.ctypes.data
+        else:
+            b.cpu = None
+        b.step_budget = self.step_budget
+        self._cstruct_obj = b
+        self._cstruct = C.byref(b)
+        return self._cstruct
+
+    @classmethod
+    def layout(cls, lengths: Sequence[int], align: int = 64):
+        return XDPBatch.layout(lengths, cls.HEADROOM, cls.TAILROOM, align)
+
+    @classmethod
+    def from_packets(cls, packets: Sequence[bytes], device="cuda", ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None,
+                     step_budget=0):
+        import numpy as np
+
+        lens = np.asarray([len(p) for p in packets], dtype=np.uint32)
+        off, total = cls.layout(lens)
+        buf = np.zeros(max(total, 1), dtype=np.uint8)
+        for i, p in enumerate(packets):
+            o = int(off[i]) + cls.HEADROOM
+            buf[o:o + len(p)] = np.frombuffer(bytes(p), dtype=np.uint8)
+        return cls.from_numpy(buf, off, lens, device, ifindex, schedule, cpu, step_budget)
+
+    @classmethod
+    def from_numpy(cls, buf, off, lens, device="cuda", ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+        import numpy as np
+        import torch
+
+        def t(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=dt))).to(device)
+
+        return cls(t(buf, np.uint8), t(np.asarray(off, dtype=np.uint64).view(np.int64), np.int64),
+                   t(np.asarray(lens, dtype=np.uint32).view(np.int32), np.int32), ifindex, schedule, cpu, step_budget)
+
+    def packet_bytes(self, i: int) -> bytes:
+        o = int(self.pkt_off[i].item())
+        n = self.HEADROOM + int(self.pkt_len[i].item()) + self.TAILROOM
         return bytes(self.pkt_data[o:o + n].cpu().numpy().tobytes())
 
 

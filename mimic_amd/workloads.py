@@ -320,14 +320,16 @@ def _flow_pool(rng, n_flows: int = 65536):
     )
 
 
-def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: int = 64):
+def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: int = 64, headroom: int = 0,
+                 tailroom: int = 0):
     """Synthetic frames -> (buf uint8[total], off uint64[n], lens uint32[n]).  Vectorised over
-    packet kinds; every packet memory starts at a multiple of `align` bytes."""
+    packet kinds; every packet memory (headroom + L + tailroom bytes, the frame at +headroom)
+    starts at a multiple of `align` bytes."""
     rng = np.random.Generator(np.random.PCG64(seed))
     pool = _flow_pool(rng)
     w = np.asarray(weights, dtype=np.float64)
     lens = np.asarray(sizes, dtype=np.int64)[rng.choice(len(sizes), n, p=w / w.sum())]
-    slot = (lens + align - 1) // align * align
+    slot = (headroom + lens + tailroom + align - 1) // align * align
     off = np.zeros(n, dtype=np.int64)
     if n > 1:
         off[1:] = np.cumsum(slot)[:-1]
@@ -338,7 +340,7 @@ def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: i
     kind = rng.choice(3, n, p=[0.90, 0.05, 0.05])           # ipv4 / ipv6 / arp
     flow = rng.integers(0, 65536, n)
     proto = pool["proto"][flow]
-    idx = off.astype(np.int64)
+    idx = off.astype(np.int64) + headroom
 
     def put(col, vals):
         vals = np.asarray(vals, dtype=np.uint8)
@@ -376,6 +378,9 @@ def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: i
     for k in range(16):
         buf[v6 + 22 + k] = pool["src6"][f6, k]
         buf[v6 + 38 + k] = pool["dst6"][f6, k]
+    plen6 = np.maximum(lens[kind == 1] - 54, 0).astype(np.uint16)   # IPv6 payload length
+    buf[v6 + 18] = (plen6 >> 8).astype(np.uint8)
+    buf[v6 + 19] = (plen6 & 0xFF).astype(np.uint8)
     ok6 = lens[kind == 1] >= 58
     buf[v6[ok6] + 54] = (pool["sport"][f6[ok6]] >> 8).astype(np.uint8)
     buf[v6[ok6] + 55] = (pool["sport"][f6[ok6]] & 0xFF).astype(np.uint8)
@@ -399,3 +404,339 @@ def schedule_cpu(n: int, vcpus: int, mode: str = "chunked") -> np.ndarray:
         chunk = -(-n // vcpus)
         return (i // chunk).astype(np.int32)
     return (i % vcpus).astype(np.int32)
+
+
+# ---------------------------------------------------------------------------------------------
+# sk_buff workloads (config 5: context_sk_buff.go path)
+# ---------------------------------------------------------------------------------------------
+SKB_HEADROOM, SKB_TAILROOM = 32, 64
+
+
+def make_skb_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: int = 64, variety: float = 0.0):
+    """sk_buff batch input: packet memory i = 32 + L + 64 bytes at off[i], the frame at +32.
+    variety > 0 replaces that fraction of the frames with header variants (VLAN / QinQ, IPv4
+    options and fragments, bad lengths, 802.3 + LLC/SNAP, IPv6 extension headers, UDP tunnels
+    and IPIP that give the reference's "multiple layers" Load error, truncated frames)."""
+    buf, off, lens = make_packets(n, sizes, weights, seed, align, SKB_HEADROOM, SKB_TAILROOM)
+    if variety > 0:
+        rng = np.random.Generator(np.random.PCG64(seed ^ 0x5B5B))
+        pick = np.nonzero(rng.random(n) < variety)[0]
+        for i in pick:
+            L = int(lens[i])
+            o = int(off[i]) + SKB_HEADROOM
+            f = skb_variant(rng, L)               # truncated variants are shorter than L
+            buf[o:o + len(f)] = np.frombuffer(f, dtype=np.uint8)
+            lens[i] = len(f)
+    return buf, off, lens
+
+
+def _ipv4(rng, proto, payload_len, ihl=5, frag=0, tl=None, opts=b""):
+    total = 4 * ihl + payload_len if tl is None else tl
+    h = bytes([0x40 | ihl, 0]) + int(total & 0xFFFF).to_bytes(2, "big") + b"\x12\x34" + int(frag).to_bytes(2, "big")
+    h += bytes([64, proto, 0, 0]) + bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+    opts = (opts + b"\x00" * 40)[:4 * ihl - 20]
+    return h + opts
+
+
+def _ipv6(rng, nh, plen):
+    return (bytes([0x60, 0, 0, 0]) + int(plen & 0xFFFF).to_bytes(2, "big") + bytes([nh, 64]) +
+            bytes(rng.integers(0, 256, 32, dtype=np.uint8)))
+
+
+def _l4(rng, proto, sport=None, dport=None, ulen=None):
+    sp = int(rng.integers(1, 65536)) if sport is None else sport
+    dp = int(rng.integers(1, 65536)) if dport is None else dport
+    if proto == 6:
+        return sp.to_bytes(2, "big") + dp.to_bytes(2, "big") + bytes(rng.integers(0, 256, 8, dtype=np.uint8)) + \
+            b"\x50\x10" + bytes(6)
+    return sp.to_bytes(2, "big") + dp.to_bytes(2, "big") + int(ulen or 0).to_bytes(2, "big") + b"\x00\x00"
+
+
+def skb_variant(rng, L: int) -> bytes:
+    """One frame of length L (truncated variants: at most L) whose headers exercise a corner of
+    SKBuffFromBytes' walk."""
+    mac = bytes(rng.integers(0, 256, 12, dtype=np.uint8))
+    k = int(rng.integers(0, 16))
+    proto = int(rng.choice([6, 17, 1]))
+    if k == 0:    # 802.1Q VLAN + IPv4
+        f = mac + b"\x81\x00" + int(rng.integers(0, 65536)).to_bytes(2, "big") + b"\x08\x00" + \
+            _ipv4(rng, proto, max(L - 38, 0)) + _l4(rng, proto, ulen=max(L - 38, 0))
+    elif k == 1:  # QinQ (802.1ad + 802.1Q) + IPv6
+        f = mac + b"\x88\xa8\x00\x05\x81\x00\x00\x07\x86\xdd" + _ipv6(rng, proto, max(L - 62, 0)) + _l4(rng, proto)
+    elif k == 2:  # IPv4 with options (NOP, record-route-ish, bad option)
+        ihl = int(rng.integers(6, 16))
+        opts = bytes(rng.choice([b"\x01\x01\x01\x01", b"\x07\x07\x04\x00\x00\x00\x00\x00", b"\x44\x01",
+                                 b"\x00\x00\x00\x00"]))
+        f = mac + b"\x08\x00" + _ipv4(rng, proto, max(L - 14 - 4 * ihl, 0), ihl=ihl, opts=opts) + _l4(rng, proto)
+    elif k == 3:  # fragments
+        f = mac + b"\x08\x00" + _ipv4(rng, proto, max(L - 34, 0), frag=int(rng.choice([0x2000, 0x0010, 0x4000]))) + \
+            _l4(rng, proto)
+    elif k == 4:  # total length 0 / < 20 / larger than the frame
+        f = mac + b"\x08\x00" + _ipv4(rng, proto, 0, tl=int(rng.choice([0, 12, 19, 20, 4000]))) + _l4(rng, proto)
+    elif k == 5:  # VXLAN: a second Ethernet layer -> Load error
+        inner = mac + b"\x08\x00" + _ipv4(rng, 17, 8) + _l4(rng, 17)
+        f = mac + b"\x08\x00" + _ipv4(rng, 17, 16 + len(inner)) + _l4(rng, 17, dport=4789, ulen=16 + len(inner)) + \
+            b"\x08\x00\x00\x00\x00\x00\x01\x00" + inner
+    elif k == 6:  # Geneve carrying IPv4: a second network layer -> Load error
+        f = mac + b"\x08\x00" + _ipv4(rng, 17, 44) + _l4(rng, 17, dport=6081, ulen=44) + \
+            b"\x00\x00\x08\x00\x00\x00\x10\x00" + _ipv4(rng, 6, 20) + _l4(rng, 6)
+    elif k == 7:  # GTP-U from a non-tunnel source port towards 2152
+        f = mac + b"\x08\x00" + _ipv4(rng, 17, 56) + _l4(rng, 17, dport=2152, ulen=56) + b"\x30\xff\x00\x28" + \
+            bytes(4) + _ipv4(rng, 6, 20) + _l4(rng, 6)
+    elif k == 8:  # IPIP -> Load error
+        f = mac + b"\x08\x00" + _ipv4(rng, 4, 40) + _ipv4(rng, 6, 20) + _l4(rng, 6)
+    elif k == 9:  # 802.3 length + LLC/SNAP + IPv4
+        f = mac + int(max(min(L - 14, 1500), 0)).to_bytes(2, "big") + b"\xaa\xaa\x03\x00\x00\x00\x08\x00" + \
+            _ipv4(rng, proto, max(L - 42, 0)) + _l4(rng, proto)
+    elif k == 10:  # IPv6 + routing header + UDP
+        f = mac + b"\x86\xdd" + _ipv6(rng, 43, max(L - 54, 0)) + b"\x11\x00\x00\x00\x00\x00\x00\x00" + \
+            _l4(rng, 17, ulen=max(L - 62, 0))
+    elif k == 11:  # IPv6 fragment / hop-by-hop
+        f = mac + b"\x86\xdd" + _ipv6(rng, int(rng.choice([0, 44, 60])), max(L - 54, 0)) + bytes(8) + _l4(rng, 6)
+    elif k == 12:  # truncated frames: short Ethernet, short IPv4 / IPv6 headers
+        f = (mac + b"\x08\x00" + _ipv4(rng, proto, 20) + _l4(rng, proto))[:int(rng.integers(0, 40))]
+        if rng.random() < 0.5:
+            f = (mac + b"\x86\xdd" + _ipv6(rng, 6, 20))[:int(rng.integers(14, 54))]
+        return f[:L]
+    elif k == 13:  # UDP length field variants (0, < 8, larger than the frame)
+        f = mac + b"\x08\x00" + _ipv4(rng, 17, max(L - 34, 0)) + _l4(rng, 17, dport=53, ulen=int(rng.choice([0, 5, 8, 9000])))
+    elif k == 14:  # ARP / unknown ethertypes
+        f = mac + bytes(rng.choice([b"\x08\x06", b"\x88\xcc", b"\x65\x58"])) + bytes(rng.integers(0, 256, 46, dtype=np.uint8))
+    else:          # random bytes after a valid IPv4 header
+        f = mac + b"\x08\x00" + bytes(rng.integers(0, 256, 40, dtype=np.uint8))
+    f = f[:L] + bytes(rng.integers(0, 256, max(L - len(f), 0), dtype=np.uint8))
+    return f
+
+
+def _count(idx: int, stats: str):
+    """stats[idx] += 1 through the lookup helper (per-CPU array): 10 slots, r1-r5 / r0 clobbered."""
+    return [
+        A.st(4, 10, -20, idx),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -20),
+        A.ld_map_fd(1, stats),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jeq", 0, 0, 3),
+        A.ldx(8, 1, 0, 0),
+        A.alu64("add", 1, 1),
+        A.stx(8, 0, 0, 1),
+    ]
+
+
+def _tail(idx: int, progs: str):
+    return [A.mov64_reg(1, 6), A.ld_map_fd(2, progs), A.mov64_imm(3, idx), A.call(A.FN_TAIL_CALL)]
+
+
+def skb_programs(progs: str = "progs", flows: str = "flows", stats: str = "stats", flow_entries: int = 65536):
+    """Config 5: a ~230-slot tc-style classifier over the sk_buff context as a chain of five
+    programs joined by tail calls (prog array), with hash-map flow lookups and per-CPU counters.
+
+      skb_entry   __sk_buff field loads / stores, protocol dispatch -> tail call 1 / 2 / 3
+      skb_ipv4    LD_ABS / LD_IND header parse -> 5-tuple key, flow lookup -> tail call 4
+      skb_ipv6    LD_ABS DW address fold -> key, flow lookup -> tail call 4
+      skb_other   counter, verdict
+      skb_verdict direct packet access (BigEndian memory), tc_classid / priority / flow_keys,
+                  verdict from the fields earlier programs wrote
+
+    Packets of one wavefront take different chains (branch-divergence stress).  Returns
+    (list of Program, map specs, prog-array entries [(map, key, program index)])."""
+    S = A.SKB
+    entry = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 7, 6, S["len"]),
+        A.ldx(4, 8, 6, S["protocol"]),
+        A.ldx(4, 9, 6, S["vlan_present"]),
+        A.stx(4, 6, S["mark"], 7),                 # mark = len
+        A.ldx(4, 2, 6, S["ifindex"]),
+        A.alu64("add", 9, 2, reg=True),
+        A.stx(2, 6, S["queue_mapping"], 9),
+        A.ldx(4, 2, 6, S["family"]),
+        A.ldx(4, 3, 6, S["remote_port"]),
+        A.alu64("lsh", 2, 16),
+        A.alu64("or", 2, 3, reg=True),
+        A.stx(4, 6, S["tc_index"], 2),
+        A.ldx(8, 2, 6, S["tstamp"]),
+        A.alu64("add", 2, 7, reg=True),
+        A.stx(8, 6, S["tstamp"], 2),
+        *_count(0, stats),
+        A.mov64_imm(3, 3),
+        A.jmp("jne", 8, 0x0800, "not4"),
+        A.mov64_imm(3, 1),
+        A.ja("go"),
+        "not4",
+        A.jmp("jne", 8, 0x86DD, "go"),
+        A.mov64_imm(3, 2),
+        "go",
+        A.mov64_reg(1, 6),
+        A.ld_map_fd(2, progs),
+        A.call(A.FN_TAIL_CALL),
+        A.mov64_imm(0, A.TC_ACT_OK),               # the tail call failed
+        A.exit_(),
+    ]
+    ipv4 = [
+        A.mov64_reg(6, 1),
+        A.ld_abs(1, 14),                           # version / IHL
+        A.mov64_reg(7, 0),
+        A.alu64("and", 7, 0x0F),
+        A.alu64("lsh", 7, 2),                      # r7 = IHL * 4
+        A.jmp("jlt", 7, 20, "bad"),
+        A.ld_abs(1, 23),                           # protocol
+        A.stx(4, 10, -4, 0),
+        A.ld_abs(4, 26),                           # saddr (host order)
+        A.stx(4, 10, -16, 0),
+        A.ld_abs(4, 30),                           # daddr
+        A.stx(4, 10, -12, 0),
+        A.ld_ind(2, 7, 14),                        # sport
+        A.mov64_reg(8, 0),
+        A.alu64("lsh", 8, 16),
+        A.ld_ind(2, 7, 16),                        # dport
+        A.alu64("or", 8, 0, reg=True),
+        A.stx(4, 10, -8, 8),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -16),
+        A.ld_map_fd(1, flows),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.mov64_imm(9, 1),                         # stats index: miss
+        A.mov64_imm(8, 0),
+        A.jmp("jeq", 0, 0, "miss"),
+        A.ldx(8, 8, 0, 0),                         # flow value
+        A.mov64_imm(9, 2),                         # hit
+        "miss",
+        A.stx(4, 10, -20, 9),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -20),
+        A.ld_map_fd(1, stats),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jeq", 0, 0, 3),
+        A.ldx(8, 1, 0, 0),
+        A.alu64("add", 1, 1),
+        A.stx(8, 0, 0, 1),
+        A.mov64_reg(1, 8),
+        A.alu64("and", 1, 7),
+        A.stx(4, 6, S["priority"], 1),             # priority = flow value & 7
+        A.ldx(4, 2, 6, S["local_ip4"]),            # SK's view of the addresses
+        A.ldx(4, 3, 6, S["remote_ip4"]),
+        A.alu64("xor", 2, 3, reg=True),
+        A.ldx(4, 3, 6, S["mark"]),
+        A.alu64("xor", 3, 2, reg=True),
+        A.stx(4, 6, S["mark"], 3),
+        *_tail(4, progs),
+        "bad",
+        A.mov64_imm(0, A.TC_ACT_SHOT),
+        A.exit_(),
+    ]
+    ipv6 = [
+        A.mov64_reg(6, 1),
+        A.ld_abs(8, 22),                           # saddr[0:8]
+        A.mov64_reg(7, 0),
+        A.ld_abs(8, 30),                           # saddr[8:16]
+        A.alu64("xor", 7, 0, reg=True),
+        A.mov64_reg(8, 7),
+        A.alu64("rsh", 8, 32),
+        A.alu64("xor", 7, 8, reg=True),
+        A.stx(4, 10, -16, 7),
+        A.ld_abs(8, 38),                           # daddr
+        A.mov64_reg(7, 0),
+        A.ld_abs(8, 46),
+        A.alu64("xor", 7, 0, reg=True),
+        A.mov64_reg(8, 7),
+        A.alu64("rsh", 8, 32),
+        A.alu64("xor", 7, 8, reg=True),
+        A.stx(4, 10, -12, 7),
+        A.ld_abs(4, 54),                           # sport | dport
+        A.stx(4, 10, -8, 0),
+        A.ld_abs(1, 20),                           # next header
+        A.stx(4, 10, -4, 0),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -16),
+        A.ld_map_fd(1, flows),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.mov64_imm(8, 0),
+        A.jmp("jeq", 0, 0, 1),
+        A.ldx(8, 8, 0, 0),
+        *_count(3, stats),
+        A.stx(4, 6, S["priority"], 8),
+        *_tail(4, progs),
+        A.mov64_imm(0, A.TC_ACT_SHOT),
+        A.exit_(),
+    ]
+    other = [
+        A.mov64_reg(6, 1),
+        *_count(4, stats),
+        A.ldx(4, 0, 6, S["vlan_tci"]),
+        A.alu64("and", 0, 1),
+        A.exit_(),
+    ]
+    verdict = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, S["data"]),
+        A.ldx(4, 3, 6, S["data_end"]),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 14),
+        A.mov64_imm(9, 0),
+        A.jmp("jgt", 4, 3, "nodata", reg=True),
+        A.ldx(2, 9, 2, 12),                        # ethertype, BigEndian packet memory
+        A.ldx(1, 4, 2, 0),
+        A.alu64("xor", 4, 0xFF),
+        A.stx(1, 2, 0, 4),                         # rewrite the first destination-MAC byte
+        "nodata",
+        A.stx(2, 6, S["tc_classid"], 9),
+        A.ldx(4, 7, 6, S["mark"]),
+        A.ldx(4, 8, 6, S["priority"]),
+        A.ldx(4, 3, 6, S["local_port"]),
+        A.ldx(4, 1, 6, S["flow_keys"]),
+        A.stx(2, 1, A.FLOW_KEYS["sport"], 3),
+        A.ldx(2, 3, 1, A.FLOW_KEYS["sport"]),
+        A.alu64("xor", 7, 8, reg=True),
+        A.alu64("xor", 7, 3, reg=True),
+        A.ldx(4, 3, 6, S["queue_mapping"]),
+        A.alu64("add", 7, 3, reg=True),
+        *_count(5, stats),
+        A.mov64_imm(0, A.TC_ACT_OK),
+        A.jmp("jset", 7, 1, 1),                    # Q3: taken when (r7 & 1) == 0
+        A.mov64_imm(0, A.TC_ACT_SHOT),
+        A.exit_(),
+    ]
+    out = []
+    for name, items in (("skb_entry", entry), ("skb_ipv4", ipv4), ("skb_ipv6", ipv6), ("skb_other", other),
+                        ("skb_verdict", verdict)):
+        raw, rel = A.assemble(items)
+        out.append(Program(name, raw, rel, []))
+    maps = [dict(name=progs, type=3, key_size=4, value_size=4, max_entries=8),
+            dict(name=flows, type=1, key_size=16, value_size=8, max_entries=flow_entries),
+            dict(name=stats, type=6, key_size=4, value_size=8, max_entries=8)]
+    prog_array = [(progs, k, k) for k in (1, 2, 3, 4)]
+    return out, maps, prog_array
+
+
+def skb_flow_keys(buf, off, lens, every: int = 3, limit: int = 4096):
+    """Keys the cfg-5 programs build for some of the batch's IPv4 / IPv6 frames (plain Ethernet):
+    the hash map is pre-populated with every `every`-th distinct key, up to `limit`, value =
+    a function of the key.  Returns [(key bytes, value bytes)]."""
+    import struct
+
+    keys = {}
+    for i in range(len(lens)):
+        L = int(lens[i])
+        o = int(off[i]) + SKB_HEADROOM
+        f = bytes(buf[o:o + L])
+        if L < 14:
+            continue
+        et = int.from_bytes(f[12:14], "big")
+        if et == 0x0800 and L >= 38:
+            ihl = (f[14] & 0x0F) * 4
+            if ihl < 20 or 14 + ihl + 4 > L + SKB_TAILROOM or 14 + ihl + 4 > L:
+                continue
+            k = struct.pack("<IIII", int.from_bytes(f[26:30], "big"), int.from_bytes(f[30:34], "big"),
+                            (int.from_bytes(f[14 + ihl:16 + ihl], "big") << 16) | int.from_bytes(f[16 + ihl:18 + ihl], "big"),
+                            f[23])
+        elif et == 0x86DD and L >= 58:
+            def fold(a, b):
+                x = int.from_bytes(f[a:a + 8], "big") ^ int.from_bytes(f[b:b + 8], "big")
+                return (x ^ (x >> 32)) & 0xFFFFFFFF
+            k = struct.pack("<IIII", fold(22, 30), fold(38, 46), int.from_bytes(f[54:58], "big"), f[20])
+        else:
+            continue
+        keys.setdefault(k, None)
+    sel = list(keys)[::every][:limit]
+    return [(k, (int.from_bytes(k[:8], "little") * 0x9E3779B1 & (2**64 - 1)).to_bytes(8, "little")) for k in sel]

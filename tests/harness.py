@@ -57,7 +57,7 @@ def build_oracle(sc: Scenario):
     return vm, mids, pids
 
 
-def jit_prewarm(raws) -> None:
+def jit_prewarm(raws, ctx: int = 0) -> None:
     """MIMIC_JIT_PREWARM=1 (CPU host): compile the scenario's JIT kernel into the cache, skip."""
     import ctypes as C
 
@@ -69,15 +69,15 @@ def jit_prewarm(raws) -> None:
     bufs = [C.create_string_buffer(bytes(r), max(len(r), 1)) for r in raws]
     arr = (C.c_void_p * max(len(raws), 1))(*[C.cast(b, C.c_void_p) for b in bufs])
     ns = (C.c_uint32 * max(len(raws), 1))(*[len(r) // 8 for r in raws])
-    lib.mimic_jit_prebuild(arr, ns, len(raws))
+    lib.mimic_jit_prebuild_ctx(arr, ns, len(raws), ctx)
     pytest.skip("JIT prewarm")
 
 
-def build_engine(sc: Scenario, device: int = 0, shard=None):
+def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0):
     import mimic_amd as M
 
     if os.environ.get("MIMIC_JIT_PREWARM"):
-        jit_prewarm([raw for _, raw, _ in sc.progs])
+        jit_prewarm([raw for _, raw, _ in sc.progs], ctx)
 
     emu = M.NewLinuxEmulator(M.OptMaxTailCalls(sc.max_tail_calls))
     opts = [M.VMOptEmulator(emu), M.VMOptSetvCPUs(sc.vcpus), M.VMOptDevice(device)]
@@ -185,3 +185,77 @@ def assert_same(o, e, check_pkt: bool = True, n: Optional[int] = None, hash_exac
 def single(sc: Scenario, packet: bytes = b"\x00" * 64, cpu: int = 0, **kw):
     buf, off, lens = packets_to_buffer([packet], kw.pop("headroom", 0), kw.pop("tailroom", 0))
     return buf, off, lens, np.array([cpu], dtype=np.int32)
+
+
+# ---------------------------------------------------------------------------------------------
+# sk_buff batches (LinuxContextSKBuff): packet memory i = 32 + L + 64 bytes at off[i]
+# ---------------------------------------------------------------------------------------------
+SKB_ROOM = (32, 64)
+
+
+def skb_packets_to_buffer(packets: Sequence[bytes], align: int = 64):
+    return packets_to_buffer(packets, SKB_ROOM[0], SKB_ROOM[1], align)
+
+
+def _splits(n: int, splits):
+    if not splits:
+        return [(0, n)]
+    cuts = [0] + [int(s) for s in splits] + [n]
+    return [(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1)]
+
+
+def _map_readout(sc, read_values, read_hash):
+    maps, hashes = {}, {}
+    for m in sc.maps:
+        vals = [read_values(m["name"], c) for c in range(ncpus(sc, m))]
+        maps[m["name"]] = vals
+        if is_hash(m):
+            hashes[m["name"]] = read_hash(m, vals)
+    return maps, hashes
+
+
+def run_oracle_skb(sc: Scenario, buf, off, lens, cpu, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
+                   splits=None):
+    """Sequential reference semantics; `splits` = indices where a new batch (same VM) starts."""
+    vm, mids, pids = build_oracle(sc)
+    buf = np.array(buf, dtype=np.uint8, copy=True)
+    parts = []
+    for a, b in _splits(len(lens), splits):
+        parts.append(vm.run_skb_batch(pids[entry], buf, off[a:b], lens[a:b], cpu[a:b], ifindex, step_budget))
+    out = {k: np.concatenate([p[k] for p in parts]) for k in ("r0", "status", "steps", "err_pc")}
+    out["pkt"] = buf
+
+    def hread(m, vals):
+        S = m["value_size"]
+        return {k: [v[s * S:(s + 1) * S] for v in vals] for k, s in vm.map_entries(mids[m["name"]])}
+
+    out["maps"], out["hash"] = _map_readout(sc, lambda name, c: vm.map_values(mids[name], c), hread)
+    vm.close()
+    return out
+
+
+def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
+                   schedule=None, splits=None, device: int = 0):
+    import torch
+
+    import mimic_amd as M
+
+    vm, maps, pids = build_engine(sc, device, ctx=1)
+    if schedule is None:
+        schedule = M.SCHED_EXPLICIT
+    dev = f"cuda:{device}"
+    full = M.SKBBatch.from_numpy(buf, off, lens, device=dev, ifindex=ifindex)
+    parts = []
+    for a, b in _splits(len(lens), splits):
+        sub = M.SKBBatch(full.pkt_data, full.pkt_off[a:b], full.pkt_len[a:b], ifindex, schedule,
+                         None if cpu is None else np.asarray(cpu)[a:b], step_budget)
+        parts.append(vm.RunSKBBatch(pids[entry], sub).numpy(b - a))
+    out = {k: np.concatenate([p[k] for p in parts]) for k in ("r0", "status", "steps", "err_pc")}
+    torch.cuda.synchronize(device)
+    out["pkt"] = full.pkt_data.cpu().numpy()
+    out["maps"], out["hash"] = _map_readout(sc, lambda name, c: maps[name].Values(c),
+                                            lambda m, vals: maps[m["name"]].Contents())
+    out["steps_total"] = vm.LastSteps()
+    out["last_exec"] = vm.LastExec()
+    vm.close()
+    return out

@@ -1,0 +1,31 @@
+"""sk_buff known-answer vectors (tests/golden/kat_skb.json) -> harness scenarios."""
+import json
+import os
+
+import numpy as np
+
+from harness import Scenario, skb_packets_to_buffer
+
+KAT_SKB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kat_skb.json")
+
+
+def load_cases():
+    with open(KAT_SKB_PATH) as f:
+        return json.load(f)["cases"]
+
+
+def scenario(c):
+    return Scenario(vcpus=1, progs=[("main", bytes.fromhex(c["raw"]), [])])
+
+
+def inputs(c):
+    buf, off, lens = skb_packets_to_buffer([bytes.fromhex(p) for p in c["packets"]])
+    return dict(buf=buf, off=off, lens=lens, cpu=np.zeros(len(lens), dtype=np.int32), ifindex=c["ifindex"])
+
+
+def check(c, out):
+    for i, ex in enumerate(c["expect"]):
+        got = {"status": int(out["status"][i]), "err_pc": int(out["err_pc"][i]),
+               "r0": int(out["r0"][i]) & ((1 << 64) - 1), "steps": int(out["steps"][i])}
+        for k, v in ex.items():
+            assert got[k] == v, f"{c['name']} ({c['ref']}) packet {i}: {k} = {got[k]:#x} expected {v:#x} (got {got})"

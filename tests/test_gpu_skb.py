@@ -1,0 +1,141 @@
+"""GPU parity for the sk_buff context (config 5): the HIP engine vs the CPU oracle, bit-exact,
+through the C ABI (mimic_run_skb).  Covers the hand-derived vectors of kat_skb.json, random
+programs over header variants, the config-5 tail-call chain with hash / per-CPU maps, the
+leaked-entry address layout across batches, and the API rules around it."""
+import numpy as np
+import pytest
+
+import kat_skb
+from fuzz_skb import random_skb_program
+from harness import Scenario, assert_same, run_engine_skb, run_oracle_skb
+from mimic_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+CASES = kat_skb.load_cases()
+
+
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_skb_kat(gpu, c):
+    sc = kat_skb.scenario(c)
+    inp = kat_skb.inputs(c)
+    e = run_engine_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"])
+    kat_skb.check(c, e)
+    o = run_oracle_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"])
+    assert_same(o, e)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_skb_fuzz(gpu, seed):
+    rng = np.random.default_rng(7000 + seed)
+    raw, rel = random_skb_program(rng, n_ops=int(rng.integers(3, 16)))
+    sc = Scenario(vcpus=8, progs=[("fz", raw, rel)])
+    buf, off, lens = W.make_skb_packets(96, sizes=(14, 40, 64, 128, 576), weights=(1, 1, 3, 2, 1), seed=seed,
+                                        variety=0.6)
+    cpu = rng.integers(0, 8, len(lens)).astype(np.int32)
+    o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=3, step_budget=5000)
+    e = run_engine_skb(sc, buf, off, lens, cpu, ifindex=3, step_budget=5000)
+    assert_same(o, e)
+
+
+def _cfg5(vcpus: int, buf, off, lens):
+    progs, maps, pa = W.skb_programs()
+    init = [("flows", k, v, 0) for k, v in W.skb_flow_keys(buf, off, lens)]
+    return Scenario(vcpus=vcpus, maps=maps, progs=[(p.name, p.raw, p.relocs) for p in progs], prog_array=pa,
+                    map_init=init)
+
+
+@pytest.mark.parametrize("variety", [0.0, 0.3])
+def test_cfg5_chain_small(gpu, variety):
+    buf, off, lens = W.make_skb_packets(4096, **W.IMIX, variety=variety)
+    sc = _cfg5(64, buf, off, lens)
+    cpu = W.schedule_cpu(len(lens), 64, "chunked")
+    o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=2)
+    e = run_engine_skb(sc, buf, off, lens, cpu, ifindex=2)
+    assert_same(o, e)
+    ok = o["status"] == 0
+    assert ok.mean() > 0.5
+    assert set(np.unique(o["r0"][ok])) <= {0, 1, 2}
+
+
+def test_cfg5_multi_batch_leaks(gpu):
+    """Three batches on one VM: the leaked sock / flow-keys / packet entries of earlier batches
+    move every later process's addresses (data, data_end, sk, flow_keys)."""
+    buf, off, lens = W.make_skb_packets(3000, **W.IMIX, variety=0.2)
+    sc = _cfg5(32, buf, off, lens)
+    cpu = W.schedule_cpu(len(lens), 32, "interleaved")
+    o = run_oracle_skb(sc, buf, off, lens, cpu, splits=[1000, 2100])
+    e = run_engine_skb(sc, buf, off, lens, cpu, splits=[1000, 2100])
+    assert_same(o, e)
+
+
+def test_leaked_addresses_across_batches(gpu):
+    """r0 = skb->data for every packet, in two batches on one VM."""
+    from mimic_amd import asm as A
+
+    raw, _ = A.assemble([A.ldx(4, 0, 1, A.SKB["data"]), A.exit_()])
+    sc = Scenario(vcpus=4, progs=[("d", raw, [])])
+    buf, off, lens = W.make_skb_packets(500, sizes=(60, 300, 1500), weights=(2, 1, 1), variety=0.3)
+    cpu = W.schedule_cpu(len(lens), 4, "chunked")
+    o = run_oracle_skb(sc, buf, off, lens, cpu, splits=[233])
+    e = run_engine_skb(sc, buf, off, lens, cpu, splits=[233])
+    assert_same(o, e)
+    ok = o["status"] == 0
+    assert len(np.unique(o["r0"][ok])) == ok.sum()   # every process got a fresh packet entry
+
+
+@pytest.mark.slow
+def test_cfg5_large(gpu):
+    """Config 5 shape at 262 144 IMIX packets, 65 536 vCPUs: exact against the oracle."""
+    n, V = 1 << 18, 1 << 16
+    buf, off, lens = W.make_skb_packets(n, **W.IMIX, variety=0.05)
+    sc = _cfg5(V, buf, off, lens)
+    cpu = W.schedule_cpu(n, V, "chunked")
+    o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=1)
+    e = run_engine_skb(sc, buf, off, lens, cpu, ifindex=1)
+    assert_same(o, e)
+
+
+def test_skb_api_rules(gpu):
+    """xdp_md batches, new maps and new programs are refused while sk_buff leaks exist (first
+    fit would place them in the freed stack / sk_buff hole); SKBRelease resets the VM's layout."""
+    import mimic_amd as M
+    from mimic_amd import asm as A
+
+    raw, _ = A.assemble([A.mov64_imm(0, 2), A.exit_()])
+    emu = M.NewLinuxEmulator()
+    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(2))
+    pid = vm.AddProgram(M.ProgramSpec("p", raw, []))
+    sb = M.SKBBatch.from_packets([bytes(64)] * 4, device="cuda:0")
+    r = vm.RunSKBBatch(pid, sb)
+    assert r.numpy(4)["r0"].tolist() == [2] * 4
+    xb = M.XDPBatch.from_packets([bytes(64)], device="cuda:0")
+    with pytest.raises(M.MimicError):
+        vm.RunXDPBatch(pid, xb)
+    with pytest.raises(M.MimicError):
+        vm.AddProgram(M.ProgramSpec("q", raw, []))
+    vm.SKBRelease()
+    assert vm.RunXDPBatch(pid, xb).numpy(1)["r0"].tolist() == [2]
+    vm.close()
+
+
+def test_process_run_skb(gpu):
+    """Process.Run with a LinuxContextSKBuff: one process at a time, leaks accumulate like the
+    reference's (the second process's skb->sk is 219 + L above the first's)."""
+    import mimic_amd as M
+    from mimic_amd import asm as A
+
+    raw, _ = A.assemble([A.ldx(4, 0, 1, A.SKB["sk"]), A.exit_()])
+    emu = M.NewLinuxEmulator()
+    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(1))
+    pid = vm.AddProgram(M.ProgramSpec("p", raw, []))
+    got = []
+    for L in (64, 100):
+        p = vm.NewProcess(pid, M.LinuxContextSKBuff(Packet=bytes(L), Dev=M.NetDev(3)))
+        p.SetCPUID(0)
+        p.Run()
+        got.append(p.Registers.R0)
+    assert got[1] - got[0] == 219 + 64
+    ctx = M.UnmarshalContextJSON('{"name": "x", "type": "sk_buff", "ctx": {"packet": "AAAA", "dev": {"ifIndex": 4}}}')
+    assert isinstance(ctx, M.LinuxContextSKBuff) and ctx.Dev.IFIndex == 4 and ctx.Packet == b"\0\0\0"
+    vm.close()

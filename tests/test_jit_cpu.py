@@ -16,15 +16,15 @@ from mimic_amd import asm as A
 from mimic_amd import workloads as W
 
 
-def _source(raws):
+def _source(raws, ctx: int = _lib.CTX_XDP):
     lib = _lib.load()
     bufs = [C.create_string_buffer(bytes(r), max(len(r), 1)) for r in raws]
     arr = (C.c_void_p * len(raws))(*[C.cast(b, C.c_void_p) for b in bufs])
     ns = (C.c_uint32 * len(raws))(*[len(r) // 8 for r in raws])
-    n = lib.mimic_jit_source_for(arr, ns, len(raws), None, 0)
+    n = lib.mimic_jit_source_for_ctx(arr, ns, len(raws), ctx, None, 0)
     assert n > 0
     buf = C.create_string_buffer(n + 1)
-    assert lib.mimic_jit_source_for(arr, ns, len(raws), buf, n + 1) == n
+    assert lib.mimic_jit_source_for_ctx(arr, ns, len(raws), ctx, buf, n + 1) == n
     return buf.value.decode()
 
 
@@ -66,3 +66,20 @@ def test_tail_calls_and_local_calls_compile():
     src = _source([main, other, b""])
     assert "case 1: goto P1_0;" in src and "MIMIC_ERR_PC_OOB" in src
     _compiles(src)
+
+
+def test_skb_chain_kernel_compiles():
+    """Config 5's tail-call chain as an sk_buff-context kernel: BigEndian packet fast paths and
+    LD_ABS / LD_IND over the LDS window starting at skb->data."""
+    progs, _, _ = W.skb_programs()
+    src = _source([p.raw for p in progs], _lib.CTX_SKB)
+    assert "#define MIMIC_CTX_FIXED 1" in src and "skb_load(kp, L, i, r1)" in src
+    assert "ld_abs(kp, L, r6" in src and "bswap_n(" in src
+    assert _compiles(src) > 0
+
+
+def test_skb_and_xdp_kernels_differ_only_in_context():
+    p = W.prog_classifier()
+    x, s = _source([p.raw]), _source([p.raw], _lib.CTX_SKB)
+    assert "#define MIMIC_CTX_FIXED 0" in x and "#define MIMIC_CTX_FIXED 1" in s
+    _compiles(s)
