@@ -269,6 +269,14 @@ int mimic_jit_prebuild(const void *const *progs, const uint32_t *n_slots, uint32
 long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
                               char *buf, size_t cap);
 int mimic_jit_prebuild_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind);
+/* Compile a kernel source (as mimic_jit_source_for_ctx returns it) into the MIMIC_JIT_CACHE
+ * directory (host only; a no-op when it is already there).  Lets a test session or a deploy
+ * step build many kernels in parallel processes before any device is touched. */
+int mimic_jit_cache_source(const char *src);
+/* hipRTC-compile a source and copy the gfx950 code object (an ELF whose AMDGPU metadata note
+ * holds the kernel's register, scratch and LDS usage) into code (when it fits); its size in
+ * *code_size.  Host only. */
+int mimic_jit_code(const char *src, void *code, size_t cap, size_t *code_size);
 
 #ifdef __cplusplus
 }

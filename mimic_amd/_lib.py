@@ -113,6 +113,8 @@ EXPORTS = {
     "mimic_jit_source_for_ctx": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32,
                                              C.c_char_p, C.c_size_t]),
     "mimic_jit_prebuild_ctx": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32]),
+    "mimic_jit_cache_source": (C.c_int, [C.c_char_p]),
+    "mimic_jit_code": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "mimic_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mimic_last_steps": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }

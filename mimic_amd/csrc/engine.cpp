@@ -364,6 +364,17 @@ static void build_host_tables(const std::vector<HostProg> &progs, std::vector<DI
 static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     build_host_tables(vm->progs, vm->h_all, vm->h_dp);
+    // map hints of LD_IMM64 constants that are array-family map objects (AUX_MAPHINT)
+    for (auto &x : vm->h_all) {
+        if (AUX_H(x.aux) != H_LDIMM || x.k > 0xffffffffull) continue;
+        for (size_t m = 0; m < vm->maps.size() && m < 0xfffe; m++) {
+            const HostMap &hm = vm->maps[m];
+            if (hm.obj_addr == (uint32_t)x.k && (hm.family == FAM_ARRAY || hm.family == FAM_PERCPU_ARRAY)) {
+                x.aux = (x.aux & 0xffffu) | ((uint32_t)(m + 1) << 16);
+                break;
+            }
+        }
+    }
     vm->jit_fn[0] = vm->jit_fn[1] = nullptr;
     std::vector<DInsn> all = vm->h_all;
     std::vector<DProg> dp = vm->h_dp;
@@ -1080,7 +1091,12 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     int rc = upload_tables(vm);
     if (rc) return rc;
     hipStream_t st = st_in ? st_in : vm->stream;
-    const uint32_t lanes = (uint32_t)vm->s.vcpu_count;
+    const uint32_t cpu_lanes = (uint32_t)vm->s.vcpu_count;
+    // EXPLICIT batches may hold processes whose CPU ID is unset (-1) or V: two extra lanes
+    bool extra = false;
+    if (b->schedule == MIMIC_SCHED_EXPLICIT && b->cpu)
+        for (uint32_t i = 0; i < b->n && !extra; i++) extra = b->cpu[i] == -1 || b->cpu[i] == vm->s.vcpus;
+    const uint32_t lanes = cpu_lanes + (extra ? 2u : 0u);
     const uint32_t S = stack_size(vm);
     // private memory: stack | xdp_md overlay | saved frames, qword-interleaved over lanes
     const uint32_t stack_q = S / 8;
@@ -1128,6 +1144,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.total_vcpus = (uint32_t)vm->s.vcpus;
     kp.vcpu_begin = (uint32_t)vm->s.vcpu_begin;
     kp.lanes = lanes;
+    kp.cpu_lanes = cpu_lanes;
     kp.priv_lanes = vm->priv_lanes;
     kp.priv = vm->priv;
     kp.priv_xdp_q = xdp_q;
@@ -1166,9 +1183,15 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (!b->cpu && b->n) return fail(vm, MIMIC_EINVAL, "explicit schedule needs cpu[]");
         // stable counting sort of packets by vCPU (each vCPU runs its packets in order)
         std::vector<uint32_t> start(lanes + 1, 0), pk(b->n);
+        std::vector<uint32_t> lane_of(b->n);
         for (uint32_t i = 0; i < b->n; i++) {
-            int64_t c = (int64_t)b->cpu[i] - vm->s.vcpu_begin;
-            if (c < 0 || c >= (int64_t)lanes) return fail(vm, MIMIC_EINVAL, "packet %u: cpu %d not on this engine", i, b->cpu[i]);
+            const int32_t id = b->cpu[i];
+            int64_t c = (int64_t)id - vm->s.vcpu_begin;
+            if (id == -1) c = cpu_lanes;                       // SetCPUID never called (vm.go:214)
+            else if (id == vm->s.vcpus) c = cpu_lanes + 1;     // accepted by SetCPUID (vm.go:273)
+            else if (c < 0 || c >= (int64_t)cpu_lanes)
+                return fail(vm, MIMIC_EINVAL, "packet %u: cpu %d not on this engine", i, id);
+            lane_of[i] = (uint32_t)c;
             start[c + 1]++;
         }
         uint32_t mx = 0;
@@ -1177,7 +1200,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             start[c + 1] += start[c];
         }
         std::vector<uint32_t> fill(start.begin(), start.end() - 1);
-        for (uint32_t i = 0; i < b->n; i++) pk[fill[b->cpu[i] - vm->s.vcpu_begin]++] = i;
+        for (uint32_t i = 0; i < b->n; i++) pk[fill[lane_of[i]]++] = i;
         hipStreamSynchronize(st);
         if (start.size() > vm->sched_cap_start) {
             hipFree(vm->d_sched_start);
@@ -1230,10 +1253,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (bound && kp.budget < bound) jit = false;
     }
     vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
-    if (jit && ji.kp_by_value) {  // parameters in the kernarg segment
-        if (mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, nullptr, st))
-            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
-    } else {                                // parameters read from a device copy
+    {  // launch parameters are read from a device copy
         const KParams *dkp = nullptr;
         const int slot = kp_slot(vm, kp, st, &dkp);
         if (slot < 0) return slot;
@@ -1326,6 +1346,22 @@ int mimic_jit_check(const char *src, char *log, size_t cap, size_t *code_size) {
         log[n] = 0;
     }
     return rc ? MIMIC_EINVAL : 0;
+}
+
+int mimic_jit_cache_source(const char *src) {
+    if (!src) return MIMIC_EINVAL;
+    std::string log;
+    return mimic_jit_prebuild_source(src, &log) ? MIMIC_EINVAL : 0;
+}
+
+int mimic_jit_code(const char *src, void *code, size_t cap, size_t *code_size) {
+    if (!src || !code_size) return MIMIC_EINVAL;
+    std::vector<char> co;
+    std::string log;
+    if (mimic_jit_build_code(src, co, &log)) return MIMIC_EINVAL;
+    *code_size = co.size();
+    if (code && cap >= co.size()) memcpy(code, co.data(), co.size());
+    return 0;
 }
 
 int mimic_host_register(void *p, size_t bytes) {

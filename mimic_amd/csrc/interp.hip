@@ -50,7 +50,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
     const bool lane_valid = g < kp.lanes;
     Lane L;
     L.lane = g;
-    L.cpu = (int32_t)(kp.vcpu_begin + g);
+    L.cpu = lane_cpu(kp, g);
 
     uint32_t ex_begin = 0, ex_count = 0;
     if (lane_valid && kp.sched == SCHED_EXPLICIT) {

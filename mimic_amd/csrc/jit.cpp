@@ -83,12 +83,10 @@ class Gen {
         // tuning knobs (environment; they change the generated source, hence the cache key)
         const char *f = getenv("MIMIC_JIT_FAST");
         fast_paths = !(f && f[0] == '0');
+        const char *cm = getenv("MIMIC_JIT_COLD");   // call | inline (default: by kernel size)
+        cold_mode = !cm ? 0 : !strcmp(cm, "call") ? 1 : !strcmp(cm, "inline") ? 2 : 0;
         const char *sg = getenv("MIMIC_JIT_STAGE");
         stage = !(sg && sg[0] == '0');
-        const char *k = getenv("MIMIC_JIT_KP");
-        kp_by_value = !(k && !strcmp(k, "ptr"));
-        const char *sh = getenv("MIMIC_JIT_SHARE");
-        share = !(sh && sh[0] == '0');
         for (auto &p : P)
             for (uint32_t i = 0; i < p.n; i++) {
                 const DInsn &x = p.ins[i];
@@ -118,9 +116,11 @@ class Gen {
     bool careful_copies = true;
     uint32_t max_n = 0;
     bool fast_paths = true;    // MIMIC_JIT_FAST=0: every access through resolve()
+    int cold_mode = 0;         // MIMIC_JIT_COLD: 0 auto, 1 call, 2 inline
+    bool cold_inline = true;   // the cold paths are inlined at every site (else called)
+    uint32_t cold_sites = 0;
+    static constexpr uint32_t kColdInlineSites = 48;
     bool stage = true;         // MIMIC_JIT_STAGE=0: no LDS packet window
-    bool kp_by_value = true;   // MIMIC_JIT_KP=ptr: launch parameters read from a device copy
-    bool share = true;         // MIMIC_JIT_SHARE=0: slow paths inlined at every site
     bool has_tail() const { return any_tail; }
     uint32_t ctx = CTX_XDP;    // the batch context this kernel is generated for
 
@@ -140,36 +140,57 @@ class Gen {
             }
             stage = any && fast_paths;
         }
+        // cold paths: inlined at each site for small kernels (best register allocation), called
+        // for large ones (hipRTC time grows with every inlined copy)
+        uint32_t sites = 0;
+        for (auto &p : P)
+            for (uint32_t i = 0; i < p.n; i++) {
+                const uint32_t h = AUX_H(p.ins[i].aux);
+                if (h == H_LDX || h == H_ST || h == H_STX || h == H_CALL || h == H_LDABS || h == H_SLOW) sites++;
+            }
+        if (careful_copies) sites *= 2;
+        cold_sites = sites;
+        cold_inline = cold_mode == 2 || (cold_mode == 0 && sites <= kColdInlineSites);
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
+        E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         E.line("#include \"runtime.h\"");
         E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
-        // KParams is read through a pointer to device memory: fields are then loaded (scalar)
-        // where they are used instead of all being preloaded into SGPRs from the kernarg
-        // segment (which spilled and cost VGPRs / occupancy)
-        if (kp_by_value) {
-            E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(KParams kp) {");
-        } else {
-            E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");
-            E.line("  const KParams &kp = *kpp;");
-        }
+        // Around a cold call the lane state and the argument / result registers go through the
+        // Spill record (runtime.h); only what a cold path can change comes back.
+        E.line("#define SPILL() do { sp_.L = L; sp_.r[0] = r0; sp_.r[1] = r1; sp_.r[2] = r2; sp_.r[3] = r3; sp_.r[4] = r4; "
+               "sp_.r[5] = r5; sp_.r[6] = r6; } while (0)");
+        E.line("#define FILL() do { r0 = sp_.r[0]; r1 = sp_.r[1]; r2 = sp_.r[2]; r3 = sp_.r[3]; r4 = sp_.r[4]; r5 = sp_.r[5]; "
+               "L.sm0 = sp_.L.sm0; L.sm1 = sp_.L.sm1; L.xdp_dirty = sp_.L.xdp_dirty; L.t_lo = sp_.L.t_lo; L.t_n = sp_.L.t_n; "
+               "L.t_ptr = sp_.L.t_ptr; } while (0)");
+        E.line("#define COLD_CALL(call_, pc_) do { SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
+        // KParams is read through a pointer to a device copy: fields are loaded (scalar) where
+        // they are used instead of all being preloaded into SGPRs from the kernarg segment
+        // (which spills SGPRs and costs VGPRs / occupancy)
+        E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");
+        E.line("  const KParams &kp = *kpp;");
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
         E.line("  if (g >= kp.lanes) return;");
         if (stage && fast_paths) {
             E.line("  __shared__ PWin pwin_;");
-            E.line("  const uint32_t tl_ = threadIdx.x;");
+            E.line("  const uint32_t tl0_ = threadIdx.x;");
         }
         E.line("  Lane L;");
+        E.line("  Spill sp_;");
         E.line("  L.lane = g;");
-        E.line("  L.cpu = (int32_t)(kp.vcpu_begin + g);");
+        E.line("  L.cpu = lane_cpu(kp, g);");
         E.line("  uint32_t ex_begin = 0, ex_count = 0;");
         E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = kp.sched_start[g]; ex_count = kp.sched_start[g + 1] - ex_begin; }");
         E.line("  uint64_t lane_steps = 0;");
         E.line("  const uint32_t P = kp.static_next + kp.stack_size + 1;");
         if (ctx == CTX_SKB) E.line("  const uint32_t SK_ = P;   // the sk_buff entry (skb.h)");
-        // operands of the shared slow-path blocks (G_*): address, size, value, PC, return site
-        E.line("  uint32_t ga_ = 0, gn_ = 0, gret_ = 0; int32_t gpc_ = 0; uint64_t gv_ = 0;");
+        E.line("  uint32_t ga_ = 0;   // the address of the current memory access");
         E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
         E.line("    uint32_t i;");
+        // The lane's private-memory and LDS addresses are loop-invariant; hoisted out of the packet
+        // loop they would stay live (one VGPR pair per stack slot) through every packet.  An opaque
+        // per-iteration copy of the lane index keeps each address next to its use.
+        E.line("    { uint32_t ln_ = g; asm volatile(\"\" : \"+v\"(ln_)); L.lane = ln_; }");
+        if (stage && fast_paths) E.line("    uint32_t tl_ = tl0_; asm volatile(\"\" : \"+v\"(tl_));");
         E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else { if (j >= ex_count) break; i = kp.sched_pkts[ex_begin + j]; }");
@@ -215,7 +236,6 @@ class Gen {
         E.line("    }");
         for (auto &p : P) program(p);
         E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
-        shared_blocks();
         E.line("  L_term:");
         E.line("    if (kp.r0) kp.r0[i] = r0;");
         E.line("    if (kp.status) kp.status[i] = (uint8_t)st_;");
@@ -240,6 +260,7 @@ class Gen {
     }
     static constexpr uint32_t SKB_HEADROOM_J = 32;
     bool any_tail = false, any_local = false, all_leaders = false;
+    uint32_t blk_start = 0;   // first slot of the basic block being emitted
 
     void program(const ProgView &p) {
         if (p.n == 0) return;
@@ -257,6 +278,7 @@ class Gen {
         for (int careful = 0; careful < (careful_copies ? 2 : 1); careful++) {
             for (size_t b = 0; b < L.size(); b++) {
                 const uint32_t s = L[b], e = b + 1 < L.size() ? L[b + 1] : p.n;
+                blk_start = s;
                 if (!careful) {
                     E.line("  P%u_%u:", p.id, s);
                     if (careful_copies) E.line("    if (steps + %uu > kp.budget) goto C%u_%u;", e - s, p.id, s);
@@ -337,78 +359,6 @@ class Gen {
         for (int r = 2; r < 10; r++) ctx_reg[r] = written[r] && !other[r];
     }
 
-    // ---- shared slow paths ------------------------------------------------------------------
-    // The generic forms (resolve + VMMem access, helpers, LD_ABS) are large.  Instead of one copy
-    // per instruction, every site jumps to one shared block per form with its operands in
-    // ga_/gn_/gv_/gpc_ and its return label number in gret_; the block ends in a switch back to
-    // the site.  Kernels stay small (instruction cache, hipRTC time), and lanes of one wave
-    // that take the slow path at different sites run it together.
-    enum Blk { B_LD, B_ST, B_ABS, B_H1, B_H2, B_H3, B_H12, B_COUNT };
-    std::vector<std::string> rets[B_COUNT];
-    static const char *blk_name(int b) {
-        static const char *n[] = {"G_LD", "G_ST", "G_ABS", "G_H1", "G_H2", "G_H3", "G_H12"};
-        return n[b];
-    }
-    // a jump to block b from slot i, with `set` run before; returns the return label to place
-    std::string to_blk(int b, uint32_t i, const std::string &set) {
-        const uint32_t k = (uint32_t)rets[b].size();
-        std::string lbl = std::string("R") + blk_name(b) + "_" + std::to_string(k);
-        rets[b].push_back(lbl);
-        E.line("      %s gpc_ = %u; gret_ = %uu; goto %s; %s:;", set.c_str(), i, k, blk_name(b), lbl.c_str());
-        return lbl;
-    }
-    void ret_switch(int b) {
-        E.line("    switch (gret_) {");
-        for (size_t k = 0; k < rets[b].size(); k++) E.line("    case %zu: goto %s;", k, rets[b][k].c_str());
-        E.line("    default: TERM(MIMIC_ERR_ENGINE_HELPER, gpc_);");
-        E.line("    }");
-    }
-    void shared_blocks() {
-        if (!rets[B_LD].empty()) {
-            E.line("  G_LD: { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, ga_), gn_, v_); if (s_) TERM(s_, gpc_); gv_ = v_; }");
-            ret_switch(B_LD);
-        }
-        if (!rets[B_ST].empty()) {
-            E.line("  G_ST: { const Ref R_ = resolve(kp, L, ga_); const int s_ = mem_store(kp, L, R_, gn_, gv_); if (s_) TERM(s_, gpc_);");
-            if (stage)  // a store that reaches the packet must update the window too
-                E.line("    if (R_.ptr == L.pkt && (R_.rk == RK_GLOBAL || R_.rk == RK_BEPKT)) win_store_rel(pwin_, tl_, W_, R_.off, %uu, gn_, %s); }",
-                       wb(), ctx == CTX_SKB ? "bswap_n(gv_, gn_)" : "gv_");
-            else E.line("    }");
-            ret_switch(B_ST);
-        }
-        if (!rets[B_ABS].empty()) {
-            E.line("  G_ABS: { uint64_t v_ = 0; const int s_ = ld_abs(kp, L, r6, ga_, gn_, false, v_); if (s_) TERM(s_, gpc_); gv_ = v_; }");
-            ret_switch(B_ABS);
-        }
-        if (!rets[B_H1].empty()) {
-            E.line("  G_H1: { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0;");
-            E.line("    if (ho.t_n) { L.t_lo = ho.t_lo; L.t_n = ho.t_n; L.t_ptr = ho.t_ptr; } }");
-            ret_switch(B_H1);
-        }
-        if (!rets[B_H2].empty()) {
-            E.line("  G_H2: { const HelperOut ho = helper_update(kp, L, r1, r2, r3); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0; }");
-            ret_switch(B_H2);
-        }
-        if (!rets[B_H3].empty()) {
-            E.line("  G_H3: { const HelperOut ho = helper_delete(kp, L, r1, r2); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0; }");
-            ret_switch(B_H3);
-        }
-        if (!rets[B_H12].empty()) {
-            E.line("  G_H12: { const HelperOut ho = helper_tailcall(kp, L, r2, r3); if (ho.st) TERM(ho.st, gpc_); if (ho.set_r0) r0 = ho.r0;");
-            E.line("    if (ho.tail) {");
-            E.line("      L.tailcalls++;");
-            E.line("      switch (ho.new_prog) {");
-            for (auto &q : P) {
-                if (q.n == 0) E.line("      case %u: TERM(MIMIC_ERR_PC_OOB, gpc_);", q.id);
-                else E.line("      case %u: goto P%u_0;", q.id, q.id);
-            }
-            E.line("      default: TERM(MIMIC_ERR_PC_OOB, gpc_);");
-            E.line("      }");
-            E.line("    } }");
-            ret_switch(B_H12);
-        }
-    }
-
     // fast-path conditions and values for an access of n bytes at address ga_ (see hint())
     struct Fast {
         std::string cond, val, store;
@@ -438,6 +388,11 @@ class Gen {
             f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord("ld_n(L.pkt + " + o + ", " + N + ")", n),
                          "{ st_n(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
                              (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
+            // the map value region the last lookup returned (translation cache, resolve()):
+            // [t_lo, t_lo + t_n - 1] with GetEntry's inclusive end, t_n = 0 when empty
+            f.push_back({"(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n",
+                         "ld_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), " + N + ")",
+                         "st_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), " + N + ", " + v + ")"});
             break;
         }
         }
@@ -457,14 +412,8 @@ class Gen {
                    " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
             pre = "    else ";
         }
-        if (share) {
-            E.line("%s{", pre.c_str());
-            to_blk(B_LD, i, "gn_ = " + std::to_string(n) + "u;");
-            E.line("      %s = gv_; }", dst.c_str());
-        } else {
-            E.line("%s{ uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, ga_), %uu, v_); if (s_) TERM(s_, %u); %s = v_; }",
-                   pre.c_str(), n, i, dst.c_str());
-        }
+        // generic GetEntry + Load (cold, out of line)
+        E.line("%s{ COLD_CALL(cold_load(kp, sp_, ga_, %uu), %u); %s = sp_.v; }", pre.c_str(), n, i, dst.c_str());
     }
 
     void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val) {
@@ -481,18 +430,11 @@ class Gen {
                    " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
             pre = "    else ";
         }
-        if (share) {
-            E.line("%s{", pre.c_str());
-            to_blk(B_ST, i, "gn_ = " + std::to_string(n) + "u; gv_ = " + val + ";");
-            E.line("    }");
-        } else {
-            E.line("%s{ const Ref R_ = resolve(kp, L, ga_); const int s_ = mem_store(kp, L, R_, %uu, %s); if (s_) TERM(s_, %u);",
-                   pre.c_str(), n, val.c_str(), i);
-            if (stage)
-                E.line("      if (R_.ptr == L.pkt && (R_.rk == RK_GLOBAL || R_.rk == RK_BEPKT)) win_store_rel(pwin_, tl_, W_, R_.off, %uu, %uu, %s); }",
-                       wb(), n, ord(val, n).c_str());
-            else E.line("    }");
-        }
+        // generic GetEntry + Store (cold); the stack / xdp_md state it may change comes back
+        E.line("%s{ COLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u);", pre.c_str(), n, val.c_str(), i);
+        if (stage)  // a store that reached the packet updates the window too
+            E.line("      if (sp_.po) win_store_rel(pwin_, tl_, W_, sp_.po - 1u, %uu, %uu, %s); }", wb(), n, ord(val, n).c_str());
+        else E.line("    }");
     }
 
     void insn(const ProgView &p, uint32_t i) {
@@ -583,34 +525,48 @@ class Gen {
         }
     }
 
+    // the LD_IMM64 slot whose constant R1 still holds at slot i (same basic block, R1 not
+    // written in between; helpers keep R1, Q8), or -1
+    int64_t r1_def(const ProgView &p, uint32_t i) const {
+        for (int64_t j = (int64_t)i - 1; j >= (int64_t)blk_start; j--) {
+            const DInsn &x = p.ins[j];
+            const uint32_t h = AUX_H(x.aux), d = insn_dst(x);
+            if (h == H_LDIMM && d == 1) return j;
+            if ((h == H_ALU64 || h == H_ALU32 || h == H_LDX || h == H_SLOW || h == H_LDIMM) && d == 1) return -1;
+            if (h == H_LDABS || h == H_CALL_LOCAL) return -1;
+        }
+        return -1;
+    }
+
     void helper(const ProgView &p, uint32_t i) {  // emulator_linux_.go:125-194
         const DInsn &x = p.ins[i];
         const uint32_t h = (uint32_t)x.k;
-        if (share && (h == 1 || h == 2 || h == 3 || h == 12)) {
-            E.line("    {");
-            to_blk(h == 1 ? B_H1 : h == 2 ? B_H2 : h == 3 ? B_H3 : B_H12, i, "");
-            E.line("    }");
-            return;
-        }
         switch (h) {
-        case 1:
-            E.line("    { const HelperOut ho = helper_lookup(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0;", i);
-            E.line("      if (ho.t_n) { L.t_lo = ho.t_lo; L.t_n = ho.t_n; L.t_ptr = ho.t_ptr; } }");
+        case 1: {
+            const int64_t j = fast_paths ? r1_def(p, i) : -1;
+            if (j >= 0) {  // inline array lookup when R1 is the map object the LD_IMM64 hint names
+                E.line("    { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", p.base + (uint32_t)j);
+                E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) COLD_CALL(cold_lookup(kp, sp_), %u); }", i);
+            } else {
+                E.line("    COLD_CALL(cold_lookup(kp, sp_), %u);", i);
+            }
             break;
+        }
         case 2:
-            E.line("    { const HelperOut ho = helper_update(kp, L, r1, r2, r3); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
+            E.line("    COLD_CALL(cold_update(kp, sp_), %u);", i);
             break;
         case 3:
-            E.line("    { const HelperOut ho = helper_delete(kp, L, r1, r2); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0; }", i);
+            E.line("    COLD_CALL(cold_delete(kp, sp_), %u);", i);
             break;
         case 8:
             E.line("    r0 = (uint64_t)(int64_t)L.cpu;");
             break;
         case 12:
-            E.line("    { const HelperOut ho = helper_tailcall(kp, L, r2, r3); if (ho.st) TERM(ho.st, %u); if (ho.set_r0) r0 = ho.r0;", i);
-            E.line("      if (ho.tail) {");
+            E.line("    COLD_CALL(cold_tailcall(kp, sp_), %u);", i);
+            E.line("    {");
+            E.line("      if (sp_.tail) {");
             E.line("        L.tailcalls++;");
-            E.line("        switch (ho.new_prog) {");
+            E.line("        switch (sp_.new_prog) {");
             for (auto &q : P) {
                 if (q.n == 0) E.line("        case %u: TERM(MIMIC_ERR_PC_OOB, %u);", q.id, i);
                 else E.line("        case %u: goto P%u_0;", q.id, q.id);
@@ -621,9 +577,7 @@ class Gen {
             E.line("    }");
             break;
         default:  // 65: bpf_xdp_adjust_tail (emulator_linux_helpers.go:842-864)
-            E.line("    { const Ref R_ = resolve(kp, L, (uint32_t)r1);");
-            E.line("      if ((R_.rk == RK_GLOBAL || R_.rk == RK_STACK) && R_.map < 0 && R_.limit == 20) TERM(MIMIC_ERR_ENGINE_HELPER, %u);", i);
-            E.line("      r0 = (uint64_t)(int64_t)-22; }");
+            E.line("    COLD_CALL(cold_adjust_tail(kp, sp_), %u);", i);
             break;
         }
     }
@@ -636,7 +590,7 @@ class Gen {
         const uint32_t n = AUX_SZ(x.aux), s = insn_src(x);
         const bool ind = (x.aux & AUX_X) != 0;
         if (ind && s > 10) {  // Registers.Get panics (after the R6 check)
-            E.line("    { uint64_t v_ = 0; const int s_ = ld_abs(kp, L, r6, 0u, %uu, true, v_); TERM(s_ ? s_ : MIMIC_PANIC_BADREG, %u); }", n, i);
+            E.line("    { SPILL(); cold_ldabs(kp, sp_, 0u, %uu, true); FILL(); TERM(sp_.st ? sp_.st : MIMIC_PANIC_BADREG, %u); }", n, i);
             return;
         }
         const std::string N = std::to_string(n) + "u";
@@ -653,14 +607,7 @@ class Gen {
             E.line("    }");
             pre = "    else ";
         }
-        if (share) {
-            E.line("%s{", pre.c_str());
-            to_blk(B_ABS, i, "gn_ = " + N + ";");
-            E.line("      r0 = gv_; }");
-        } else {
-            E.line("%s{ uint64_t v_ = 0; const int s_ = ld_abs(kp, L, r6, ga_, %s, false, v_); if (s_) TERM(s_, %u); r0 = v_; }",
-                   pre.c_str(), N.c_str(), i);
-        }
+        E.line("%sCOLD_CALL(cold_ldabs(kp, sp_, ga_, %s, false), %u);", pre.c_str(), N.c_str(), i);
         E.line("    r1 = 0; r2 = 0; r3 = 0; r4 = 0; r5 = 0;");
     }
 
@@ -673,8 +620,7 @@ class Gen {
         const int32_t off = insn_off(x);
         if (cls == 1) {  // LDX with dst >= 10: the memory error comes first, inst.go:298-318
             static const uint32_t szs[4] = {4, 2, 1, 8};
-            E.line("    { uint64_t v_ = 0; const int s_ = mem_load(kp, L, resolve(kp, L, %s), %uu, v_); if (s_) TERM(s_, %u); }",
-                   addr(s, off).c_str(), szs[(op >> 3) & 3], i);
+            E.line("    COLD_CALL(cold_load(kp, sp_, %s, %uu), %u);", addr(s, off).c_str(), szs[(op >> 3) & 3], i);
             E.line("    TERM(%s, %u);", d > 10 ? "MIMIC_PANIC_BADREG" : "MIMIC_ERR_R10_WRITE", i);
             return;
         }
@@ -803,7 +749,6 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->checks_budget = g.careful_copies;
         info->max_n = g.max_n;
         info->tail_calls = g.has_tail();
-        info->kp_by_value = g.kp_by_value;
     }
     return src;
 }
@@ -839,6 +784,10 @@ int mimic_jit_compile(int device, const std::string &src, hipFunction_t *fn, std
     return 0;
 }
 
+int mimic_jit_build_code(const std::string &src, std::vector<char> &code, std::string *log) {
+    return build_code(src, code, log);
+}
+
 // compile into the disk cache only (no device): prewarming for later processes
 int mimic_jit_prebuild_source(const std::string &src, std::string *log) {
     std::vector<char> code;
@@ -848,9 +797,9 @@ int mimic_jit_prebuild_source(const std::string &src, std::string *log) {
 int mimic_jit_launch(hipFunction_t fn, const JitInfo &info, const KParams *kp, const KParams *d_kp, hipStream_t st) {
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
+    (void)info;
     const KParams *p = d_kp;
-    KParams v = *kp;
-    void *args[] = {info.kp_by_value ? (void *)&v : (void *)&p};
+    void *args[] = {(void *)&p};
     return hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
 }
 

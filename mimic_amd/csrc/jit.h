@@ -12,7 +12,6 @@ struct JitInfo {
     bool checks_budget;  // the kernel has the per-block budget checks (loops / BPF-to-BPF calls)
     uint32_t max_n;      // longest program
     bool tail_calls;     // some program calls bpf_tail_call
-    bool kp_by_value;    // the kernel takes KParams by value (else a pointer to a device copy)
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
@@ -26,5 +25,7 @@ int mimic_jit_compile(int device, const std::string &src, hipFunction_t *fn, std
 int mimic_jit_launch(hipFunction_t fn, const JitInfo &info, const KParams *kp, const KParams *d_kp, hipStream_t st);
 // hipRTC compile only, no device needed
 int mimic_jit_check_source(const std::string &src, std::string *log, size_t *code_size);
+// source -> gfx950 code object (through the MIMIC_JIT_CACHE directory when set), no device
+int mimic_jit_build_code(const std::string &src, std::vector<char> &code, std::string *log);
 // compile into the MIMIC_JIT_CACHE directory without a device (prewarming)
 int mimic_jit_prebuild_source(const std::string &src, std::string *log);

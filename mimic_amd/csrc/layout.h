@@ -115,6 +115,10 @@ enum Handler : uint32_t {
 #define AUX_X (1u << 12)         // register source
 #define AUX_ARG(a) (((a) >> 16) & 0xffu)
 #define AUX_SZ(a) ((a) >> 24)
+// H_LDIMM only: 1 + the id of the array / per-CPU array map whose object address the constant
+// is (set at upload, engine.cpp); the JIT's inline lookup reads it at run time, so the kernel
+// source does not depend on it
+#define AUX_MAPHINT(a) ((a) >> 16)
 struct DInsn {
     uint32_t w;
     uint32_t aux;
@@ -148,7 +152,9 @@ struct KParams {
     uint32_t priv_xdp_q;        // qword index of the xdp_md overlay
     uint32_t priv_frame_q;      // qword index of the saved-frame area
     uint32_t priv_key_q;        // qword index of the hash-key scratch (ceil(K/8) words, max over hash maps)
-    uint32_t pad_k;
+    uint32_t cpu_lanes;         // lanes [0, cpu_lanes) are vCPUs vcpu_begin + g; lane cpu_lanes runs the
+                                // processes whose CPU ID was never set (-1), lane cpu_lanes + 1 those
+                                // with ID == V (SetCPUID accepts it, vm.go:214, 268-283)
     uint64_t budget;
     // batch
     uint32_t n;

@@ -81,6 +81,12 @@ struct Lane {
 
 static constexpr int EXIT_SIG = -1;
 
+// the CPU ID of the processes lane g runs (KParams::cpu_lanes)
+DEV int32_t lane_cpu(const KParams &kp, uint32_t g) {
+    if (g < kp.cpu_lanes) return (int32_t)(kp.vcpu_begin + g);
+    return g == kp.cpu_lanes ? -1 : (int32_t)kp.total_vcpus;
+}
+
 // ---------------------------------------------------------------------------------------
 // raw loads / stores (unaligned accesses are legal on gfx950 global memory)
 // ---------------------------------------------------------------------------------------
@@ -717,6 +723,117 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1) {
     for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
     r1 = kp.static_next + kp.stack_size + 1;
     return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Cold paths of the JIT kernels: real (non-inlined) functions, so that a kernel holds one
+// copy of the generic memory controller / helpers instead of one per instruction (hipRTC
+// time, instruction cache).  A call site spills the whole process state (lane state and
+// r0..r10) into the kernel's Spill record, calls, and reloads all of it: nothing of the
+// process is live across the call, so the call's ABI (callee-saved VGPR ranges) does not
+// widen the hot path's register allocation.  Results come back through the record.
+// ---------------------------------------------------------------------------------------
+struct Spill {
+    Lane L;
+    uint64_t r[11];
+    uint64_t v;          // loaded value
+    int32_t st;          // 0 or a status
+    uint32_t po;         // store: 1 + packet-memory offset when it wrote the packet (window mirror)
+    uint32_t tail;       // tail call taken
+    uint32_t new_prog;
+};
+#if defined(MIMIC_COLD_INLINE) && MIMIC_COLD_INLINE
+#define COLD DEV
+#define COLD_OPAQUE() do { } while (0)
+#else
+#define COLD static __device__ __attribute__((noinline, cold))
+// the callee is opaque to the caller's alias analysis: the record is always re-read
+#define COLD_OPAQUE() asm volatile("" ::: "memory")
+#endif
+// GetEntry + VMMem.Load (inst.go:298-318)
+COLD void cold_load(const KParams &kp, Spill &S, uint32_t a, uint32_t n) {
+    COLD_OPAQUE();
+    S.v = 0;
+    S.st = mem_load(kp, S.L, resolve(kp, S.L, a), n, S.v);
+}
+// GetEntry + VMMem.Store (inst.go:320-363); may set S.L.sm0 / sm1 / xdp_dirty
+COLD void cold_store(const KParams &kp, Spill &S, uint32_t a, uint32_t n, uint64_t v) {
+    COLD_OPAQUE();
+    const Ref R = resolve(kp, S.L, a);
+    S.st = mem_store(kp, S.L, R, n, v);
+    S.po = (!S.st && R.ptr == S.L.pkt && (R.rk == RK_GLOBAL || R.rk == RK_BEPKT)) ? R.off + 1 : 0;
+}
+DEV void cold_take(Spill &S, const HelperOut &ho) {
+    S.st = ho.st;
+    if (!ho.st && ho.set_r0) S.r[0] = ho.r0;
+}
+COLD void cold_lookup(const KParams &kp, Spill &S) {
+    COLD_OPAQUE();
+    const HelperOut ho = helper_lookup(kp, S.L, S.r[1], S.r[2]);
+    cold_take(S, ho);
+    if (!ho.st && ho.t_n) {
+        S.L.t_lo = ho.t_lo;
+        S.L.t_n = ho.t_n;
+        S.L.t_ptr = ho.t_ptr;
+    }
+}
+COLD void cold_update(const KParams &kp, Spill &S) {
+    COLD_OPAQUE();
+    cold_take(S, helper_update(kp, S.L, S.r[1], S.r[2], S.r[3]));
+}
+COLD void cold_delete(const KParams &kp, Spill &S) {
+    COLD_OPAQUE();
+    cold_take(S, helper_delete(kp, S.L, S.r[1], S.r[2]));
+}
+COLD void cold_tailcall(const KParams &kp, Spill &S) {
+    COLD_OPAQUE();
+    const HelperOut ho = helper_tailcall(kp, S.L, S.r[2], S.r[3]);
+    cold_take(S, ho);
+    S.tail = !ho.st && ho.tail;
+    S.new_prog = ho.new_prog;
+}
+// LD_ABS / LD_IND through the generic path (emulator_linux_.go:198-288): R0, then R1-R5 = 0
+COLD void cold_ldabs(const KParams &kp, Spill &S, uint32_t x, uint32_t n, bool bad_src) {
+    COLD_OPAQUE();
+    uint64_t v = 0;
+    S.st = ld_abs(kp, S.L, S.r[6], x, n, bad_src, v);
+    if (!S.st) {
+        S.r[0] = v;
+        for (int q = 1; q <= 5; q++) S.r[q] = 0;
+    }
+}
+// bpf_xdp_adjust_tail (emulator_linux_helpers.go:842-864): R0 = -EINVAL, or a status
+COLD void cold_adjust_tail(const KParams &kp, Spill &S) {
+    COLD_OPAQUE();
+    const Ref R = resolve(kp, S.L, (uint32_t)S.r[1]);
+    S.st = ((R.rk == RK_GLOBAL || R.rk == RK_STACK) && R.map < 0 && R.limit == 20) ? MIMIC_ERR_ENGINE_HELPER : 0;
+    if (!S.st) S.r[0] = (uint64_t)(int64_t)-22;
+}
+
+// Inline form of helper 1 (map_lookup_elem, emulator_linux_helpers.go:477-504) for the usual
+// case: R1 is exactly the object of array / per-CPU array map `mid` (a hint from the LD_IMM64
+// slot that set R1; checked here, so a wrong hint only costs the slow path) and the 4-byte
+// key lies on the stack.  Then regToMap, derefMapKey and LinuxArrayMap.Lookup reduce to the
+// lines below.  Returns false when the case does not apply (the caller runs cold_lookup).
+DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint64_t r2, uint64_t &r0) {
+    const DMap m = cget(kp.maps, mid);
+    if ((uint32_t)r1 != m.obj_addr || m.key_size != 4) return false;
+    if (m.family != FAM_ARRAY && m.family != FAM_PERCPU_ARRAY) return false;
+    const uint32_t ko = (uint32_t)r2 - kp.static_next;
+    if ((uint64_t)ko + 4 > kp.stack_size) return false;
+    int32_t which = -1;
+    if (m.family == FAM_PERCPU_ARRAY) {
+        if (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu) return false;   // error path: cold
+        which = L.cpu;
+    }
+    const uint32_t k = (uint32_t)stack_load(kp, L, ko, 4);
+    r0 = array_value_addr(m, which, k);
+    if (r0) {
+        L.t_lo = m.backing_addr + (which > 0 ? (uint32_t)which * m.addr_period : 0u);
+        L.t_n = m.max_entries * m.value_size + 1;
+        L.t_ptr = array_value_ptr(kp, m, which, 0);
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1,0 +1,162 @@
+"""JIT tooling around the engine's per-program-set kernels (csrc/jit.cpp), host only.
+
+* ``kernel_source(raws, ctx)`` -- the HIP source the engine generates for a set of loaded
+  programs (raw 8-byte slots, in AddProgram order).  It depends only on the instructions and
+  the batch context, never on map relocations, so it is also the code-object cache key.
+* ``code_object(src)`` / ``kernel_resources(code)`` -- the hipRTC gfx950 code object and the
+  register / scratch / LDS usage its AMDGPU metadata note declares (occupancy checks).
+* ``prewarm(kernels)`` -- compile many kernels into ``MIMIC_JIT_CACHE`` in parallel worker
+  PROCESSES before any device is used (hipRTC serialises compiles inside one process).  The
+  workers only load the library and call hipRTC; they never touch a GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+import tempfile
+from typing import Dict, Iterable, List, Sequence, Tuple
+
+from . import _lib
+
+CTX_XDP, CTX_SKB = 0, 1
+
+
+def _progs_args(raws: Sequence[bytes]):
+    bufs = [C.create_string_buffer(bytes(r), max(len(r), 1)) for r in raws]
+    arr = (C.c_void_p * max(len(raws), 1))(*[C.cast(b, C.c_void_p) for b in bufs])
+    ns = (C.c_uint32 * max(len(raws), 1))(*[len(r) // 8 for r in raws])
+    return bufs, arr, ns
+
+
+def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP) -> str:
+    lib = _lib.load()
+    keep, arr, ns = _progs_args(raws)
+    n = lib.mimic_jit_source_for_ctx(arr, ns, len(raws), ctx, None, 0)
+    if n < 0:
+        raise ValueError(f"cannot decode programs ({n})")
+    buf = C.create_string_buffer(n + 1)
+    lib.mimic_jit_source_for_ctx(arr, ns, len(raws), ctx, buf, n + 1)
+    return buf.value.decode()
+
+
+def code_object(src: str) -> bytes:
+    lib = _lib.load()
+    size = C.c_size_t()
+    if lib.mimic_jit_code(src.encode(), None, 0, C.byref(size)) != 0:
+        raise RuntimeError("hipRTC compile failed")
+    buf = C.create_string_buffer(size.value)
+    lib.mimic_jit_code(src.encode(), buf, size.value, C.byref(size))
+    return buf.raw[:size.value]
+
+
+def _notes(elf: bytes):
+    """(name, type, desc) of every note in the ELF's SHT_NOTE sections (64-bit little endian)."""
+    import struct
+
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", elf, 0x3A)
+    for i in range(shnum):
+        sh = shoff + i * shentsize
+        stype, = struct.unpack_from("<I", elf, sh + 4)
+        if stype != 7:  # SHT_NOTE
+            continue
+        off, size = struct.unpack_from("<QQ", elf, sh + 0x18)
+        p, end = off, off + size
+        while p + 12 <= end:
+            nsz, dsz, typ = struct.unpack_from("<III", elf, p)
+            name = elf[p + 12:p + 12 + nsz].rstrip(b"\0").decode()
+            d0 = p + 12 + ((nsz + 3) & ~3)
+            yield name, typ, elf[d0:d0 + dsz]
+            p = d0 + ((dsz + 3) & ~3)
+
+
+def kernel_resources(code: bytes, kernel: str = "mimic_jit_kernel") -> Dict[str, int]:
+    """VGPR / AGPR / SGPR counts, spills, scratch and LDS bytes of a kernel, and the waves per
+    SIMD its registers allow on gfx950 (512 unified VGPRs per SIMD lane, granule 8, max 8)."""
+    import msgpack
+
+    for name, typ, desc in _notes(code):
+        if name != "AMDGPU" or typ != 32:  # NT_AMDGPU_METADATA
+            continue
+        md = msgpack.unpackb(desc, raw=False)
+        for k in md.get("amdhsa.kernels", []):
+            if k.get(".name") != kernel:
+                continue
+            # gfx950: .vgpr_count is the unified total (arch VGPRs, aligned, + AGPRs)
+            total, a = int(k.get(".vgpr_count", 0)), int(k.get(".agpr_count", 0))
+            alloc = max(8, (total + 7) & ~7)
+            return {"vgpr": total - a, "agpr": a, "vgpr_total": total, "sgpr": int(k.get(".sgpr_count", 0)),
+                    "vgpr_spill": int(k.get(".vgpr_spill_count", 0)), "sgpr_spill": int(k.get(".sgpr_spill_count", 0)),
+                    "scratch": int(k.get(".private_segment_fixed_size", 0)),
+                    "lds": int(k.get(".group_segment_fixed_size", 0)), "waves_per_simd": min(8, 512 // alloc)}
+    raise KeyError(f"kernel {kernel} not in the code object's metadata")
+
+
+def _cache_dir() -> str:
+    d = os.environ.get("MIMIC_JIT_CACHE", "")
+    if not d:
+        raise RuntimeError("MIMIC_JIT_CACHE is not set: prewarming needs an on-disk kernel cache")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def prewarm(kernels: Iterable[Tuple[Sequence[bytes], int]], workers: int = 0) -> Dict[str, float]:
+    """Compile the kernels of (raws, ctx) program sets into MIMIC_JIT_CACHE using `workers`
+    parallel processes (0: min(16, cpus) - 1).  Returns {"kernels": n, "seconds": t}."""
+    import time
+
+    t0 = time.time()
+    _cache_dir()
+    srcs: Dict[str, None] = {}
+    for raws, ctx in kernels:
+        srcs[kernel_source(list(raws), ctx)] = None
+    todo = sorted(srcs, key=len, reverse=True)        # longest first: better packing
+    if not todo:
+        return {"kernels": 0, "seconds": 0.0}
+    if workers <= 0:
+        workers = max(1, min(16, os.cpu_count() or 1) - 1)
+    workers = min(workers, len(todo))
+    with tempfile.TemporaryDirectory(prefix="mimic_jitwarm_") as tmp:
+        lists = [[] for _ in range(workers)]
+        for k, s in enumerate(todo):                  # round-robin over the sorted list
+            path = os.path.join(tmp, f"k{k}.hip")
+            with open(path, "w") as f:
+                f.write(s)
+            lists[k % workers].append(path)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+        def launch(w):
+            env = dict(os.environ)
+            env["TMPDIR"] = os.path.join(tmp, f"t{w}")    # compiler temp files: one directory per worker
+            os.makedirs(env["TMPDIR"], exist_ok=True)
+            return subprocess.Popen([sys.executable, "-m", "mimic_amd.jit", os.path.join(tmp, f"w{w}.txt")],
+                                    env=env, cwd=root)
+
+        for w, paths in enumerate(lists):
+            with open(os.path.join(tmp, f"w{w}.txt"), "w") as f:
+                f.write("\n".join(paths))
+        rcs = [p.wait() for p in [launch(w) for w in range(workers)]]
+        # a worker that died retries its list once (finished kernels are cache hits); kernels still
+        # missing after that are compiled by the engine when first used
+        retry = [w for w, rc in enumerate(rcs) if rc]
+        rcs2 = [p.wait() for p in [launch(w) for w in retry]]
+    return {"kernels": len(todo), "seconds": time.time() - t0, "worker_failures": len(retry),
+            "failed_after_retry": sum(1 for rc in rcs2 if rc)}
+
+
+def _worker(list_file: str) -> int:
+    lib = _lib.load()
+    rc = 0
+    with open(list_file) as f:
+        for path in f.read().split():
+            with open(path) as g:
+                if lib.mimic_jit_cache_source(g.read().encode()) != 0:
+                    print(f"mimic_amd.jit: compile failed: {path}", file=sys.stderr)
+                    rc = 1
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(_worker(sys.argv[1]))

@@ -336,6 +336,12 @@ def VMOptDevice(d: int):
     return ("device", d)
 
 
+def VMOptExecMode(mode: str):
+    """'jit' (per-program-set kernels, the default), 'interp' (the batch interpreter) or
+    'default' (the MIMIC_EXEC environment variable decides)."""
+    return ("exec", {"default": 0, "interp": 1, "jit": 2}[mode])
+
+
 def VMOptShard(begin: int, count: int):
     """Execute only vCPUs [begin, begin+count) on this engine (multi-GPU sharding)."""
     return ("shard", (begin, count))
@@ -349,6 +355,7 @@ class VMSettings:
     device: int = 0
     vcpu_begin: int = 0
     vcpu_count: int = 0
+    exec_mode: int = 0
 
 
 class MemoryControllerView:
@@ -375,7 +382,8 @@ class VM:
         self.lib = L.load()
         self.settings = settings
         s = L.VMSettings(settings.vcpus, settings.stack_frame_size, settings.stack_frame_count,
-                         emulator.MaxTailCalls, settings.device, settings.vcpu_begin, settings.vcpu_count, 0)
+                         emulator.MaxTailCalls, settings.device, settings.vcpu_begin, settings.vcpu_count,
+                         settings.exec_mode)
         h = C.c_void_p()
         rc = self.lib.mimic_vm_create(C.byref(s), C.byref(h))
         if rc != 0:
@@ -530,6 +538,8 @@ def NewVM(*opts) -> VM:  # vm.go:54-76
             s.device = v
         elif k == "shard":
             s.vcpu_begin, s.vcpu_count = v
+        elif k == "exec":
+            s.exec_mode = v
     return VM(emu, s)
 
 
@@ -566,9 +576,10 @@ class Process:
     def Run(self, step_budget: int = 0) -> None:  # vm.go:343-360
         import torch
 
+        # cpuID stays -1 when SetCPUID was never called (vm.go:214) and may equal V (vm.go:273):
+        # the reference runs such processes; only per-CPU map operations fail in them
+        # (emulator_linux_map_array.go:236-238) and bpf_get_smp_processor_id returns the ID as set
         ctx = self.Context or LinuxContextXDP()
-        if self.cpuID < 0 or self.cpuID >= self.VM.settings.vcpus:
-            raise MimicError("process has no valid CPU ID (SetCPUID first)")
         dev = f"cuda:{self.VM.settings.device}"
         if isinstance(ctx, LinuxContextSKBuff):
             batch = SKBBatch.from_packets([ctx.Packet], device=dev, ifindex=ctx.Dev.IFIndex if ctx.Dev else 0,

@@ -1432,7 +1432,9 @@ int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_resul
         uint32_t steps = 0;
         int32_t epc = -1;
         int st;
-        if (orc_proc_set_cpu(p, cpu)) {
+        /* cpu -1: SetCPUID was never called, the process keeps cpuID -1 (vm.go:214); only the
+         * per-CPU map operations fail then (emulator_linux_map_array.go:236-238) */
+        if (cpu != -1 && orc_proc_set_cpu(p, cpu)) {
             st = ORC_ERR_NO_CPU;
         } else {
             st = run(p, budget, &steps, &epc);
@@ -1902,7 +1904,8 @@ int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_resul
         int32_t epc = -1;
         int st = skb_load(p, mem + 32, L, b->ifindex);
         if (!st) {
-            if (orc_proc_set_cpu(p, b->cpu ? b->cpu[i] : 0)) st = ORC_ERR_NO_CPU;
+            const int cpu = b->cpu ? b->cpu[i] : 0;
+            if (cpu != -1 && orc_proc_set_cpu(p, cpu)) st = ORC_ERR_NO_CPU;   /* -1: never set */
             else st = run(p, budget, &steps, &epc);
         }
         if (out->r0) out->r0[i] = p->R.r[0];

@@ -1,5 +1,6 @@
 import os
 import sys
+import time
 
 import pytest
 
@@ -11,12 +12,11 @@ if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 
 
-# JIT kernels compiled by earlier processes (or prewarmed on a CPU host with
-# MIMIC_JIT_PREWARM=1 python -m pytest tests -m gpu -n 8) are reused from here
+# JIT code objects live here for the session (and across sessions on the same machine); a fresh
+# GPU box starts empty and the `gpu` fixture fills it in parallel before the first GPU test
 JIT_CACHE = os.path.join(ROOT, ".jitcache")
 os.makedirs(JIT_CACHE, exist_ok=True)
 os.environ.setdefault("MIMIC_JIT_CACHE", JIT_CACHE)
-PREWARM = bool(os.environ.get("MIMIC_JIT_PREWARM"))
 
 
 def pytest_configure(config):
@@ -24,12 +24,34 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+def _session_kernels(session):
+    """Every JIT kernel the selected GPU tests will run: the jit_kernels() of their modules."""
+    kernels, seen = [], set()
+    for item in session.items:
+        if item.get_closest_marker("gpu") is None:
+            continue
+        mod = getattr(item, "module", None)
+        if mod is None or mod.__name__ in seen:
+            continue
+        seen.add(mod.__name__)
+        fn = getattr(mod, "jit_kernels", None)
+        if fn is not None:
+            kernels.extend(fn())
+    return kernels
+
+
 @pytest.fixture(scope="session")
-def gpu():
+def gpu(request):
+    """The GPU session: first compiles the session's JIT kernels in parallel worker processes
+    (hipRTC only, no device), then checks that a GPU is visible."""
+    from mimic_amd import jit as J
+
+    t0 = time.time()
+    kernels = _session_kernels(request.session)
+    info = J.prewarm(kernels)
+    sys.stderr.write(f"\n[jit prewarm] {info['kernels']} kernels in {time.time() - t0:.1f}s\n")
     import torch
 
-    if PREWARM:
-        return 0
     if not torch.cuda.is_available():
         pytest.fail("GPU test run without a visible GPU")
     return 0

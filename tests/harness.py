@@ -57,32 +57,21 @@ def build_oracle(sc: Scenario):
     return vm, mids, pids
 
 
-def jit_prewarm(raws, ctx: int = 0) -> None:
-    """MIMIC_JIT_PREWARM=1 (CPU host): compile the scenario's JIT kernel into the cache, skip."""
-    import ctypes as C
-
-    import pytest
-
-    from mimic_amd import _lib
-
-    lib = _lib.load()
-    bufs = [C.create_string_buffer(bytes(r), max(len(r), 1)) for r in raws]
-    arr = (C.c_void_p * max(len(raws), 1))(*[C.cast(b, C.c_void_p) for b in bufs])
-    ns = (C.c_uint32 * max(len(raws), 1))(*[len(r) // 8 for r in raws])
-    lib.mimic_jit_prebuild_ctx(arr, ns, len(raws), ctx)
-    pytest.skip("JIT prewarm")
+def kernel_of(sc: Scenario, ctx: int = 0):
+    """The JIT kernel a scenario's VM runs: (raw programs in load order, batch context) -- what
+    a test module's jit_kernels() lists for the session prewarm (conftest.py)."""
+    return [raw for _, raw, _ in sc.progs], ctx
 
 
-def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0):
+def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0, exec_mode: Optional[str] = None):
     import mimic_amd as M
-
-    if os.environ.get("MIMIC_JIT_PREWARM"):
-        jit_prewarm([raw for _, raw, _ in sc.progs], ctx)
 
     emu = M.NewLinuxEmulator(M.OptMaxTailCalls(sc.max_tail_calls))
     opts = [M.VMOptEmulator(emu), M.VMOptSetvCPUs(sc.vcpus), M.VMOptDevice(device)]
     if shard is not None:
         opts.append(M.VMOptShard(*shard))
+    if exec_mode is not None:
+        opts.append(M.VMOptExecMode(exec_mode))
     vm = M.NewVM(*opts)
     maps = {}
     for m in sc.maps:
@@ -129,10 +118,10 @@ def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, ta
 
 
 def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=0, tailroom=0, ingress=0, rxq=0,
-               egress=0, step_budget=0, schedule=None, device: int = 0):
+               egress=0, step_budget=0, schedule=None, device: int = 0, exec_mode: Optional[str] = None):
     import mimic_amd as M
 
-    vm, maps, pids = build_engine(sc, device)
+    vm, maps, pids = build_engine(sc, device, exec_mode=exec_mode)
     if schedule is None:
         schedule = M.SCHED_EXPLICIT
     batch = M.XDPBatch.from_numpy(buf, off, lens, device=f"cuda:{device}", headroom=headroom, tailroom=tailroom,
@@ -235,12 +224,12 @@ def run_oracle_skb(sc: Scenario, buf, off, lens, cpu, entry: int = 0, ifindex: i
 
 
 def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
-                   schedule=None, splits=None, device: int = 0):
+                   schedule=None, splits=None, device: int = 0, exec_mode: Optional[str] = None):
     import torch
 
     import mimic_amd as M
 
-    vm, maps, pids = build_engine(sc, device, ctx=1)
+    vm, maps, pids = build_engine(sc, device, ctx=1, exec_mode=exec_mode)
     if schedule is None:
         schedule = M.SCHED_EXPLICIT
     dev = f"cuda:{device}"
@@ -259,3 +248,84 @@ def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifind
     out["last_exec"] = vm.LastExec()
     vm.close()
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# sequences: many single batches, each with its own entry program, on ONE VM (one JIT kernel
+# for all its programs).  The oracle runs the same sequence on the same layout.
+# ---------------------------------------------------------------------------------------------
+def _maps_out(sc, read_values, read_hash):
+    maps, hashes = {}, {}
+    for m in sc.maps:
+        vals = [read_values(m["name"], c) for c in range(ncpus(sc, m))]
+        maps[m["name"]] = vals
+        if is_hash(m):
+            hashes[m["name"]] = read_hash(m, vals)
+    return maps, hashes
+
+
+def run_sequence_oracle(sc: Scenario, runs):
+    vm, mids, pids = build_oracle(sc)
+    outs = []
+    for r in runs:
+        if r.get("skb"):
+            b = np.array(r["buf"], dtype=np.uint8, copy=True)
+            o = vm.run_skb_batch(pids[r["entry"]], b, r["off"], r["lens"], r["cpu"], r.get("ifindex", 0),
+                                 r.get("step_budget", 0))
+            o["pkt"] = b
+            outs.append(o)
+            continue
+        o = vm.run_xdp_batch(pids[r["entry"]], r["buf"].copy(), r["off"], r["lens"], r["cpu"], r.get("headroom", 0),
+                             r.get("tailroom", 0), r.get("ingress"), r.get("rxq"), r.get("egress"),
+                             r.get("step_budget", 0))
+        outs.append(o)
+
+    def hread(m, vals):
+        S = m["value_size"]
+        return {k: [v[s * S:(s + 1) * S] for v in vals] for k, s in vm.map_entries(mids[m["name"]])}
+
+    maps, hashes = _maps_out(sc, lambda name, c: vm.map_values(mids[name], c), hread)
+    vm.close()
+    return outs, maps, hashes
+
+
+def run_sequence_engine(sc: Scenario, runs, exec_mode: Optional[str] = None, device: int = 0):
+    import mimic_amd as M
+
+    vm, maps, pids = build_engine(sc, device, ctx=1 if runs and runs[0].get("skb") else 0, exec_mode=exec_mode)
+    outs = []
+    for r in runs:
+        if r.get("skb"):
+            sb = M.SKBBatch.from_numpy(r["buf"], r["off"], r["lens"], f"cuda:{device}", r.get("ifindex", 0),
+                                       M.SCHED_EXPLICIT, r["cpu"], r.get("step_budget", 0))
+            o = vm.RunSKBBatch(pids[r["entry"]], sb).numpy(len(r["lens"]))
+            o["pkt"] = sb.pkt_data.cpu().numpy()
+            o["last_exec"] = vm.LastExec()
+            outs.append(o)
+            continue
+        zero = np.zeros(len(r["lens"]), np.int32)
+        batch = M.XDPBatch.from_numpy(r["buf"], r["off"], r["lens"], device=f"cuda:{device}",
+                                      headroom=r.get("headroom", 0), tailroom=r.get("tailroom", 0),
+                                      ingress=r.get("ingress", zero), rxq=r.get("rxq", zero),
+                                      egress=r.get("egress", zero), schedule=M.SCHED_EXPLICIT, cpu=r["cpu"],
+                                      step_budget=r.get("step_budget", 0))
+        o = vm.RunXDPBatch(pids[r["entry"]], batch).numpy(len(r["lens"]))
+        o["pkt"] = batch.pkt_data.cpu().numpy()
+        o["last_exec"] = vm.LastExec()
+        outs.append(o)
+    mp, hs = _maps_out(sc, lambda name, c: maps[name].Values(c), lambda m, vals: maps[m["name"]].Contents())
+    vm.close()
+    return outs, mp, hs
+
+
+def assert_same_sequence(o, e, tag=""):
+    oo, om, oh = o
+    eo, em, eh = e
+    assert len(oo) == len(eo)
+    for k, (a, b) in enumerate(zip(oo, eo)):
+        try:
+            assert_same(dict(a, maps={}, hash={}), dict(b, maps={}, hash={}))
+        except AssertionError as ex:
+            raise AssertionError(f"{tag} run {k}: {ex}") from None
+    if oo:  # final map contents
+        assert_same(dict(oo[-1], maps=om, hash=oh), dict(eo[-1], maps=em, hash=eh), check_pkt=False)

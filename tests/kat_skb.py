@@ -29,3 +29,19 @@ def check(c, out):
                "r0": int(out["r0"][i]) & ((1 << 64) - 1), "steps": int(out["steps"][i])}
         for k, v in ex.items():
             assert got[k] == v, f"{c['name']} ({c['ref']}) packet {i}: {k} = {got[k]:#x} expected {v:#x} (got {got})"
+
+
+def jit_groups(cases, max_progs: int = 40):
+    """All vectors share one setup (1 vCPU, no maps): chunks of max_progs programs per VM, each
+    case a batch of its own (sk_buff leaks carry over between the batches, as in the oracle)."""
+    out = []
+    for a in range(0, len(cases), max_progs):
+        chunk = cases[a:a + max_progs]
+        progs, runs = [], []
+        for k, c in enumerate(chunk):
+            progs.append((f"k{k}", bytes.fromhex(c["raw"]), []))
+            i = inputs(c)
+            runs.append(dict(skb=True, entry=k, buf=i["buf"], off=i["off"], lens=i["lens"], cpu=i["cpu"],
+                             ifindex=i["ifindex"]))
+        out.append((Scenario(vcpus=1, progs=progs), runs, chunk))
+    return out

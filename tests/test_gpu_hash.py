@@ -8,7 +8,8 @@ verdicts and the map contents per key (programs whose results do not depend on t
 import numpy as np
 import pytest
 
-from harness import Scenario, assert_same, build_engine, build_oracle, packets_to_buffer, run_engine, run_oracle
+from harness import (Scenario, assert_same, build_engine, build_oracle, kernel_of, packets_to_buffer, run_engine,
+                     run_oracle)
 from mimic_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
@@ -16,6 +17,21 @@ pytestmark = pytest.mark.gpu
 
 def _sc(p: W.Program, vcpus: int) -> Scenario:
     return Scenario(vcpus=vcpus, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+
+
+def _fuzz(seed):
+    from fuzz import random_program
+
+    rng = np.random.default_rng(7000 + seed)
+    raw, rel = random_program(rng, n_body=int(rng.integers(20, 70)), map_name="m")
+    mt = 5 if seed % 2 else 1
+    return Scenario(vcpus=4, maps=[dict(name="m", type=mt, key_size=4, value_size=8, max_entries=3)],
+                    progs=[("fz", raw, rel)]), rng
+
+
+def jit_kernels():
+    ps = [W.prog_flowtrack(), W.prog_flowcount(), W.prog_flowcount(delete_every=3), W.prog_flowcount(delete_every=1)]
+    return [kernel_of(_sc(p, 1)) for p in ps] + [kernel_of(_fuzz(s)[0]) for s in range(12)]
 
 
 @pytest.mark.parametrize("mtype", [1, 5])
@@ -125,14 +141,8 @@ def test_tombstone_rebuild_between_batches(gpu):
 @pytest.mark.parametrize("seed", range(12))
 def test_hash_helpers_random_programs(gpu, seed):
     """The fuzz generator's map calls against a per-CPU hash map with 4-byte keys, one vCPU."""
-    from fuzz import random_program
-
     if True:
-        rng = np.random.default_rng(7000 + seed)
-        raw, rel = random_program(rng, n_body=int(rng.integers(20, 70)), map_name="m")
-        mt = 5 if seed % 2 else 1
-        sc = Scenario(vcpus=4, maps=[dict(name="m", type=mt, key_size=4, value_size=8, max_entries=3)],
-                      progs=[("fz", raw, rel)])
+        sc, rng = _fuzz(seed)
         pk = [bytes(rng.integers(0, 256, int(rng.choice([0, 14, 64])), dtype=np.uint8)) for _ in range(48)]
         b, off, lens = packets_to_buffer(pk)
         cpu = np.zeros(len(pk), dtype=np.int32)

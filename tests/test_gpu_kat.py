@@ -1,25 +1,58 @@
 """The GPU engine against the hand-derived KATs and the reference's own tests (through the
-Python mirror of the reference API)."""
+Python mirror of the reference API).
+
+* Every KAT runs on the batch interpreter in a VM of its own (the KAT's exact address layout)
+  and must give the expected R0 / status / steps / err_pc.
+* The JIT runs the same single-program KATs in chunks: one VM (one generated kernel) holds a
+  chunk's programs, each case runs as its own batch with its program as the entry, and every
+  batch plus the final maps must equal the oracle running the same sequence on the same
+  layout (the oracle is pinned to the KATs by tests/test_oracle_golden.py).  The multi-program
+  KATs (tail calls) run on the JIT in VMs of their own against the expected values.
+"""
 import numpy as np
 import pytest
 
 import mimic_amd as M
-from harness import run_engine
-from kat import check, inputs, load_cases, scenario
+from harness import (assert_same_sequence, kernel_of, run_engine, run_sequence_engine, run_sequence_oracle)
+from kat import check, inputs, jit_groups, load_cases, multi_cases, scenario
 
 pytestmark = pytest.mark.gpu
 
 CASES = load_cases()
+GROUPS = jit_groups(CASES)
+MULTI = multi_cases(CASES)
+
+
+def jit_kernels():
+    """The JIT kernels this module runs (compiled in parallel before the session, conftest.py)."""
+    return [kernel_of(sc) for sc, _, _ in GROUPS] + [kernel_of(scenario(c)) for c in MULTI]
+
+
+def _run_kat(c, exec_mode):
+    i = inputs(c)
+    return run_engine(scenario(c), i["buf"], i["off"], i["lens"], i["cpu"], headroom=i["headroom"],
+                      tailroom=i["tailroom"], ingress=np.array([c["ingress"]], np.int32),
+                      rxq=np.array([c["rxq"]], np.int32), egress=np.array([c["egress"]], np.int32),
+                      step_budget=i["step_budget"], exec_mode=exec_mode)
 
 
 @pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
-def test_engine_kat(gpu, c):
-    i = inputs(c)
-    out = run_engine(scenario(c), i["buf"], i["off"], i["lens"], i["cpu"], headroom=i["headroom"],
-                     tailroom=i["tailroom"], ingress=np.array([c["ingress"]], np.int32),
-                     rxq=np.array([c["rxq"]], np.int32), egress=np.array([c["egress"]], np.int32),
-                     step_budget=i["step_budget"])
-    check(c, out)
+def test_engine_kat_interp(gpu, c):
+    check(c, _run_kat(c, "interp"))
+
+
+@pytest.mark.parametrize("g", range(len(GROUPS)), ids=[f"chunk{k}_{len(g[2])}" for k, g in enumerate(GROUPS)])
+def test_engine_kat_jit_chunk(gpu, g):
+    sc, runs, chunk = GROUPS[g]
+    o = run_sequence_oracle(sc, runs)
+    e = run_sequence_engine(sc, runs, exec_mode="jit")
+    assert_same_sequence(o, e, tag=f"chunk {g}")
+    assert any(r["last_exec"] == "jit" for r in e[0]), "no batch of the chunk ran on the JIT kernel"
+
+
+@pytest.mark.parametrize("c", MULTI, ids=[c["name"] for c in MULTI])
+def test_engine_kat_jit_multi(gpu, c):
+    check(c, _run_kat(c, "jit"))
 
 
 def _k(v):

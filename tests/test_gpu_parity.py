@@ -2,8 +2,9 @@
 import numpy as np
 import pytest
 
-from harness import Scenario, assert_same, packets_to_buffer, run_engine, run_oracle, single
-from mimic_amd import asm as A  # noqa: F401
+from harness import Scenario, assert_same, kernel_of, packets_to_buffer, run_engine, run_oracle, single
+import mimic_amd as M
+from mimic_amd import asm as A
 from mimic_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
@@ -11,6 +12,12 @@ pytestmark = pytest.mark.gpu
 
 def _prog_scenario(p: W.Program, vcpus: int) -> Scenario:
     return Scenario(vcpus=vcpus, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+
+
+def jit_kernels():
+    ks = [kernel_of(_prog_scenario(p, 1)) for p in (W.prog_pass8(), W.prog_classifier(), W.prog_parse5())]
+    ks += [kernel_of(_fuzz(s)[0]) for s in range(40)]
+    return ks + [kernel_of(_tailcall_sc()), kernel_of(_rewrite_sc()), kernel_of(_cpuid_sc())]
 
 
 def test_pass8(gpu):
@@ -34,12 +41,16 @@ def test_classifier_small(gpu, mode):
     assert set(np.unique(o["r0"])) <= {1, 2}
 
 
-@pytest.mark.parametrize("seed", range(40))
-def test_fuzz_programs(gpu, seed):
+def _fuzz(seed):
     rng = np.random.default_rng(1000 + seed)
     raw, rel = __import__("fuzz").random_program(rng, n_body=int(rng.integers(10, 80)), map_name="m")
-    sc = Scenario(vcpus=8, maps=[dict(name="m", type=6, key_size=4, value_size=8, max_entries=4)],
-                  progs=[("fz", raw, rel)])
+    return Scenario(vcpus=8, maps=[dict(name="m", type=6, key_size=4, value_size=8, max_entries=4)],
+                    progs=[("fz", raw, rel)]), rng
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_fuzz_programs(gpu, seed):
+    sc, rng = _fuzz(seed)
     pk = [bytes(rng.integers(0, 256, int(rng.choice([0, 14, 60, 64, 100])), dtype=np.uint8)) for _ in range(64)]
     buf, off, lens = packets_to_buffer(pk)
     cpu = rng.integers(0, 8, 64).astype(np.int32)
@@ -96,9 +107,7 @@ def test_schedules(gpu, sched):
     assert_same(o, e)
 
 
-def test_tailcall_divergence(gpu):
-    """Lanes of one wave tail-call into different programs (and some do not) -- the wave
-    runs several programs at once (min-key scheduling over global instruction indices)."""
+def _tailcall_sc():
     PA = dict(name="progs", type=3, key_size=4, value_size=4, max_entries=4)
     CNT = dict(name="cnt", type=6, key_size=4, value_size=8, max_entries=4)
     main = [A.mov64_reg(6, 1), A.ldx(4, 2, 6, 0), A.ldx(4, 3, 6, 4), A.mov64_reg(4, 2), A.alu64("add", 4, 1),
@@ -111,8 +120,14 @@ def test_tailcall_divergence(gpu):
                 A.mov64_imm(0, v), A.exit_()]
 
     progs = [("main", *A.assemble(main))] + [(f"l{v}", *A.assemble(leaf(v))) for v in range(3)]
-    sc = Scenario(vcpus=32, maps=[PA, CNT], progs=progs, prog_array=[("progs", 0, 1), ("progs", 1, 2),
-                                                                      ("progs", 2, 3)])
+    return Scenario(vcpus=32, maps=[PA, CNT], progs=progs, prog_array=[("progs", 0, 1), ("progs", 1, 2),
+                                                                        ("progs", 2, 3)])
+
+
+def test_tailcall_divergence(gpu):
+    """Lanes of one wave tail-call into different programs (and some do not) -- the wave
+    runs several programs at once (min-key scheduling over global instruction indices)."""
+    sc = _tailcall_sc()
     rng = np.random.default_rng(11)
     pk = [bytes(rng.integers(0, 256, int(rng.choice([0, 8, 64])), dtype=np.uint8)) for _ in range(3000)]
     buf, off, lens = packets_to_buffer(pk)
@@ -120,8 +135,7 @@ def test_tailcall_divergence(gpu):
     assert_same(run_oracle(sc, buf, off, lens, cpu), run_engine(sc, buf, off, lens, cpu))
 
 
-def test_packet_rewrite_and_room(gpu):
-    """XDP_TX-style MAC swap written in place, per-packet headroom/tailroom arrays."""
+def _rewrite_sc():
     items = [A.ldx(4, 2, 1, 0), A.ldx(4, 3, 1, 4), A.mov64_reg(4, 2), A.alu64("add", 4, 12),
              A.jmp("jgt", 4, 3, "out", reg=True),
              A.ldx(4, 5, 2, 0), A.ldx(2, 6, 2, 4), A.ldx(4, 7, 2, 6), A.ldx(2, 8, 2, 10),
@@ -129,7 +143,12 @@ def test_packet_rewrite_and_room(gpu):
              A.ldx(1, 9, 2, -1), A.mov64_imm(0, A.XDP_TX), A.alu64("add", 0, 9, reg=True), A.exit_(),
              "out", A.mov64_imm(0, A.XDP_DROP), A.exit_()]
     raw, rel = A.assemble(items)
-    sc = Scenario(vcpus=8, progs=[("tx", raw, rel)])
+    return Scenario(vcpus=8, progs=[("tx", raw, rel)])
+
+
+def test_packet_rewrite_and_room(gpu):
+    """XDP_TX-style MAC swap written in place, per-packet headroom/tailroom arrays."""
+    sc = _rewrite_sc()
     rng = np.random.default_rng(5)
     n = 700
     pk = [bytes(rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8)) for _ in range(n)]
@@ -146,3 +165,59 @@ def test_packet_rewrite_and_room(gpu):
         a, m = int(off[i]), int(H[i] + lens[i] + T[i])
         assert bytes(o["pkt"][a:a + m]) == bytes(e["pkt"][a:a + m]), i
     assert_same(o, e, check_pkt=False)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_programs_interp(gpu, seed):
+    """The same random programs on the batch interpreter."""
+    sc, rng = _fuzz(seed)
+    pk = [bytes(rng.integers(0, 256, int(rng.choice([0, 14, 60, 64, 100])), dtype=np.uint8)) for _ in range(64)]
+    buf, off, lens = packets_to_buffer(pk)
+    cpu = rng.integers(0, 8, 64).astype(np.int32)
+    assert_same(run_oracle(sc, buf, off, lens, cpu, step_budget=5000),
+                run_engine(sc, buf, off, lens, cpu, step_budget=5000, exec_mode="interp"))
+
+
+def _cpuid_sc():
+    """r6 = get_smp_processor_id(); then a per-CPU array lookup (fails for CPU IDs -1 and V,
+    emulator_linux_map_array.go:236-238) unless the packet is empty."""
+    items = [A.call(8), A.mov64_reg(6, 0), A.ldx(4, 2, 1, 0), A.ldx(4, 3, 1, 4), A.jmp("jeq", 2, 3, "out", reg=True),
+             A.st(4, 10, -4, 0), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, "pc"), A.call(1),
+             "out", A.mov64_reg(0, 6), A.exit_()]
+    raw, rel = A.assemble(items)
+    return Scenario(vcpus=4, maps=[dict(name="pc", type=6, key_size=4, value_size=8, max_entries=2)],
+                    progs=[("cpuid", raw, rel)])
+
+
+@pytest.mark.parametrize("exec_mode", ["jit", "interp"])
+def test_unset_and_V_cpu_ids(gpu, exec_mode):
+    """Processes whose CPU ID was never set (-1, vm.go:214) or equals V (SetCPUID accepts it,
+    vm.go:273) run: helper 8 returns the ID as set, per-CPU map operations fail."""
+    sc = _cpuid_sc()
+    pk = [b"", bytes(64), b"", bytes(64), b"", bytes(64)]
+    buf, off, lens = packets_to_buffer(pk)
+    cpu = np.array([-1, -1, 4, 4, 1, 1], np.int32)
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu, exec_mode=exec_mode)
+    assert_same(o, e)
+    assert [int(x) for x in e["r0"][:3]] == [2 ** 64 - 1, 2 ** 64 - 1, 4]
+    st = [M.STATUS_NAMES[int(x)] for x in e["status"]]
+    assert st == ["OK", "ERR_HELPER_MAP_OP", "OK", "ERR_HELPER_MAP_OP", "OK", "OK"], st
+
+
+def test_process_run_cpu_unset_and_V(gpu):
+    """The Process.Run drop-in without SetCPUID, and with SetCPUID(V)."""
+    emu = M.NewLinuxEmulator()
+    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(3))
+    raw, _ = A.assemble([A.call(8), A.exit_()])
+    pid = vm.AddProgram(M.ProgramSpec("smp", raw))
+    p = vm.NewProcess(pid, M.LinuxContextXDP(Packet=bytes(64)))
+    p.Run()
+    assert p.Registers.R0 == 2 ** 64 - 1
+    p = vm.NewProcess(pid, M.LinuxContextXDP(Packet=bytes(64)))
+    p.SetCPUID(3)
+    p.Run()
+    assert p.Registers.R0 == 3
+    with pytest.raises(M.MimicError):
+        p.SetCPUID(4)
+    vm.close()

@@ -7,29 +7,57 @@ import pytest
 
 import kat_skb
 from fuzz_skb import random_skb_program
-from harness import Scenario, assert_same, run_engine_skb, run_oracle_skb
+from harness import (Scenario, assert_same, assert_same_sequence, kernel_of, run_engine_skb, run_oracle_skb,
+                     run_sequence_engine, run_sequence_oracle)
 from mimic_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
 
 CASES = kat_skb.load_cases()
+GROUPS = kat_skb.jit_groups(CASES)
 
 
-@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
-def test_skb_kat(gpu, c):
+def _fuzz(seed):
+    rng = np.random.default_rng(7000 + seed)
+    raw, rel = random_skb_program(rng, n_ops=int(rng.integers(3, 16)))
+    return Scenario(vcpus=8, progs=[("fz", raw, rel)]), rng
+
+
+def jit_kernels():
+    ks = [kernel_of(sc, 1) for sc, _, _ in GROUPS] + [kernel_of(_fuzz(s)[0], 1) for s in range(24)]
+    progs, _, _ = W.skb_programs()
+    from mimic_amd import asm as A
+    return ks + [([p.raw for p in progs], 1), ([A.assemble([A.ldx(4, 0, 1, A.SKB["data"]), A.exit_()])[0]], 1),
+                 ([A.assemble([A.ldx(4, 0, 1, A.SKB["sk"]), A.exit_()])[0]], 1)]
+
+
+def _skb_kat(c, exec_mode):
     sc = kat_skb.scenario(c)
     inp = kat_skb.inputs(c)
-    e = run_engine_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"])
+    e = run_engine_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"], exec_mode=exec_mode)
     kat_skb.check(c, e)
     o = run_oracle_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"])
     assert_same(o, e)
 
 
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_skb_kat_interp(gpu, c):
+    _skb_kat(c, "interp")
+
+
+@pytest.mark.parametrize("g", range(len(GROUPS)))
+def test_skb_kat_jit_chunk(gpu, g):
+    """The vectors' programs in chunks, one JIT kernel per chunk, against the oracle running the
+    same batch sequence on the same VM layout."""
+    sc, runs, _ = GROUPS[g]
+    e = run_sequence_engine(sc, runs, exec_mode="jit")
+    assert_same_sequence(run_sequence_oracle(sc, runs), e, tag=f"skb chunk {g}")
+    assert any(r["last_exec"] == "jit" for r in e[0])
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_skb_fuzz(gpu, seed):
-    rng = np.random.default_rng(7000 + seed)
-    raw, rel = random_skb_program(rng, n_ops=int(rng.integers(3, 16)))
-    sc = Scenario(vcpus=8, progs=[("fz", raw, rel)])
+    sc, rng = _fuzz(seed)
     buf, off, lens = W.make_skb_packets(96, sizes=(14, 40, 64, 128, 576), weights=(1, 1, 3, 2, 1), seed=seed,
                                         variety=0.6)
     cpu = rng.integers(0, 8, len(lens)).astype(np.int32)

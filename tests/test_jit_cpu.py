@@ -74,7 +74,7 @@ def test_skb_chain_kernel_compiles():
     progs, _, _ = W.skb_programs()
     src = _source([p.raw for p in progs], _lib.CTX_SKB)
     assert "#define MIMIC_CTX_FIXED 1" in src and "skb_load(kp, L, i, r1)" in src
-    assert "ld_abs(kp, L, r6" in src and "bswap_n(" in src
+    assert "cold_ldabs(kp, sp_" in src and "bswap_n(" in src
     assert _compiles(src) > 0
 
 
@@ -83,3 +83,26 @@ def test_skb_and_xdp_kernels_differ_only_in_context():
     x, s = _source([p.raw]), _source([p.raw], _lib.CTX_SKB)
     assert "#define MIMIC_CTX_FIXED 0" in x and "#define MIMIC_CTX_FIXED 1" in s
     _compiles(s)
+
+
+# ---------------------------------------------------------------------------------------------
+# register budget of the generated kernels (code-object metadata of the hipRTC build): the
+# kernels are latency-bound, so occupancy is what hides the per-packet HBM round trips
+# ---------------------------------------------------------------------------------------------
+def _resources(raws, ctx=_lib.CTX_XDP):
+    from mimic_amd import jit as J
+
+    return J.kernel_resources(J.code_object(J.kernel_source(raws, ctx)))
+
+
+@pytest.mark.parametrize("fn", ["prog_classifier", "prog_parse5"])
+def test_hot_kernels_fit_five_waves(fn):
+    """cfg 2 / cfg 3 kernels: <= 96 unified VGPRs (5 waves per SIMD), no spills, no scratch."""
+    r = _resources([getattr(W, fn)().raw])
+    assert r["vgpr_total"] <= 96 and r["waves_per_simd"] >= 5, r
+    assert r["vgpr_spill"] == 0 and r["sgpr_spill"] == 0 and r["scratch"] == 0, r
+
+
+def test_small_kernel_resources():
+    r = _resources([W.prog_pass8().raw])
+    assert r["waves_per_simd"] == 8 and r["lds"] == 0 and r["scratch"] == 0, r

@@ -92,3 +92,19 @@ def test_prog_load_rejects_truncated_ld_imm64():
     bad2 = A.encode(0x18, 1, 0, 0, 5) + A.encode(0x07, 0, 0, 0, 1)
     with pytest.raises(oracle.OracleError):
         vm.prog_load("bad2", bad2)
+
+
+def test_oracle_cpu_unset_and_V():
+    """vm.go:214 (cpuID -1 until SetCPUID) and vm.go:273 (id == V accepted): the process runs,
+    helper 8 returns the ID, a per-CPU array lookup is a fatal map error."""
+    from harness import Scenario, packets_to_buffer, run_oracle
+
+    raw, rel = A.assemble([A.call(8), A.mov64_reg(6, 0), A.st(4, 10, -4, 0), A.mov64_reg(2, 10),
+                           A.alu64("add", 2, -4), A.ld_map_fd(1, "pc"), A.call(1), A.mov64_reg(0, 6), A.exit_()])
+    sc = Scenario(vcpus=2, maps=[dict(name="pc", type=6, key_size=4, value_size=8, max_entries=2)],
+                  progs=[("p", raw, rel)])
+    buf, off, lens = packets_to_buffer([bytes(8)] * 4)
+    o = run_oracle(sc, buf, off, lens, np.array([-1, 2, 1, 3], np.int32))
+    from mimic_amd import STATUS_NAMES
+    assert [STATUS_NAMES[int(s)] for s in o["status"]] == ["ERR_HELPER_MAP_OP", "ERR_HELPER_MAP_OP", "OK", "ERR_NO_CPU"]
+    assert [int(x) for x in o["r0"][:3]] == [2 ** 64 - 1, 2, 1]
