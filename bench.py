@@ -2,22 +2,28 @@
 """bench.py -- Mpkts/s (and eBPF insns/s) of the MI355X batch-eBPF engine, device-resident.
 
 A *step* is one pass of the hot path over one batch: for every packet of the batch,
-NewProcess + SetCPUID + Run + read R0 + Cleanup (vm.go:198-374), i.e. one mimic_run_xdp launch.
-Default workload = BASELINE.json configs[1]: 1 048 576 x 64 B xdp_md packets, the ~36-slot
-parse+hash DROP/PASS classifier, per-CPU array map (E=4, S=8), one MI355X.
+NewProcess + SetCPUID + Run + read R0 + Cleanup (vm.go:198-374), i.e. one mimic_run_xdp (or
+mimic_run_skb) launch.  Default workload = BASELINE.json configs[1]: 1 048 576 x 64 B xdp_md
+packets, the ~36-slot parse+hash DROP/PASS classifier, per-CPU array map (E=4, S=8), one MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config classifier|pass8|parse5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config classifier|pass8|parse5|flowtrack|skb]
 
 With N > 1 run under torch.distributed.run: every rank owns its own vCPUs and its own packet
 shard (weak scaling, no data-path collective); RCCL broadcasts the program bytes at setup and
 all-reduces the per-CPU verdict counters after the timed region (the sum-over-CPUs readout).
+
+roofline.traffic / valu_busy come from a committed rocprofv3 summary (profiles/*_pmc_*.json,
+written by tools/pmc_summary.py) whose kernel-source hash, workload and vCPU count match this
+run exactly; with no such profile they are null.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -39,6 +45,9 @@ CONFIGS = {
     "flowtrack": dict(prog="prog_flowtrack", packets=1 << 21, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 18,
                       workload="cfg4 per-GPU shard: 2M IMIX xdp_md (16M over 8 GPUs), 5-tuple parse + "
                                "insert-if-absent into a shared hash map K=16 S=8 E=131072"),
+    "skb": dict(kind="skb", packets=1 << 20, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 16,
+                workload="cfg5: 1M IMIX sk_buff contexts, 5-program tail-call chain (~230 slots): __sk_buff "
+                         "fields, LD_ABS/IND parse, hash flow lookups, per-CPU counters"),
 }
 
 
@@ -51,7 +60,7 @@ def dist_env():
 
 def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps) -> int:
     """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU array
-    state, 2*E*(K+S) of hash-map state (K + V*S for a per-CPU hash).
+    state, 2*E*(K+S) of hash-map state (K + V*S for a per-CPU hash), 2*E*S of plain arrays.
     (The engine's actual descriptor is 12 B and it also writes a 1-B status; not counted.)"""
     b = int(lens.astype(np.int64).sum()) + 16 * len(lens)
     for m in maps:
@@ -64,60 +73,160 @@ def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps) -> int:
     return b
 
 
-def cpu_baseline(cfg_name: str, min_seconds: float, vcpus_cpu: int = 8):
-    """The oracle (C restatement of the reference algorithm, 1 thread) on a bounded sample."""
-    import oracle
+# ---------------------------------------------------------------------------------------------
+# workloads
+# ---------------------------------------------------------------------------------------------
+class Workload:
+    """The programs, maps and input batch of one config (host side)."""
+
+    def __init__(self, cfg_name: str, n: int, seed: int):
+        from mimic_amd import workloads as W
+
+        self.cfg = CONFIGS[cfg_name]
+        self.name = cfg_name
+        self.skb = self.cfg.get("kind") == "skb"
+        if self.skb:
+            self.progs, self.maps, self.prog_array = W.skb_programs()
+            self.buf, self.off, self.lens = W.make_skb_packets(n, self.cfg["sizes"], self.cfg["weights"], seed=seed,
+                                                               variety=0.05)
+            m = min(n, 1 << 16)
+            self.map_init = [("flows", k, v) for k, v in W.skb_flow_keys(self.buf, self.off[:m], self.lens[:m])]
+        else:
+            p = getattr(W, self.cfg["prog"])()
+            self.progs, self.maps, self.prog_array = [p], p.maps, []
+            self.buf, self.off, self.lens = W.make_packets(n, self.cfg["sizes"], self.cfg["weights"], seed=seed)
+            self.map_init = []
+        self.ctx = 1 if self.skb else 0
+
+    def kernel_src_hash(self) -> str:
+        return kernel_src_hash_of(self.name)
+
+    def build_vm(self, M, V, device, shard, raws):
+        emu = M.NewLinuxEmulator()
+        vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(V), M.VMOptDevice(device), M.VMOptShard(*shard))
+        maps = {}
+        for m in self.maps:
+            mm = M.MapSpecToLinuxMap(M.MapSpec(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"]))
+            emu.AddMap(m["name"], mm)
+            maps[m["name"]] = mm
+        pids = [vm.AddProgram(M.ProgramSpec(p.name, raw, p.relocs)) for p, raw in zip(self.progs, raws)]
+        for mname, key, pi in self.prog_array:
+            assert maps[mname].UpdateProgram(key.to_bytes(4, "little"), pids[pi]) == 0
+        for mname, key, val in self.map_init:
+            assert maps[mname].Update(key, val, 0, 0) == 0
+        return vm, maps, pids
+
+
+def kernel_src_hash_of(cfg_name: str) -> str:
+    """sha256 (16 hex) of the JIT kernel source the config's programs generate: the key that ties
+    a committed rocprofv3 summary to the exact kernel it measured."""
+    from mimic_amd import jit as J
     from mimic_amd import workloads as W
 
     cfg = CONFIGS[cfg_name]
-    prog = getattr(W, cfg["prog"])()
-    n = min(cfg["packets"], 1 << 18)
-    buf, off, lens = W.make_packets(n, cfg["sizes"], cfg["weights"], seed=W.SEED)
-    vm = oracle.OracleVM(vcpus_cpu)
-    mids = {m["name"]: vm.map_create(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"])
-            for m in prog.maps}
-    pid = vm.prog_load(prog.name, prog.raw, [(s, mids[nm]) for s, nm in prog.relocs])
-    cpu = W.schedule_cpu(n, vcpus_cpu, "chunked")
-    done = 0
-    steps = 0
+    if cfg.get("kind") == "skb":
+        progs, ctx = W.skb_programs()[0], 1
+    else:
+        progs, ctx = [getattr(W, cfg["prog"])()], 0
+    h = hashlib.sha256(J.kernel_source([p.raw for p in progs], ctx).encode())
+    for f in ("mimic_amd/csrc/layout.h", "mimic_amd/csrc/hashmap.h", "mimic_amd/csrc/skb.h", "mimic_amd/csrc/runtime.h",
+              "include/mimic_amd.h"):   # the headers embedded into every JIT kernel
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def cpu_baseline(wl: Workload, min_seconds: float, threads: int = 1):
+    """The oracle (C restatement of the reference algorithm) on a bounded sample of the same
+    workload: `threads` host threads, each one vCPU of a V = threads VM running its own chunk of
+    the sample in order (processPool's one-worker-per-vCPU shape, vm.go:521-573); ctypes releases
+    the GIL for every batch call, so the threads run the C code in parallel."""
+    import oracle
+
+    n = min(len(wl.lens), 1 << 18)
+    chunk = (n + threads - 1) // threads
+    done = [0] * threads
+    steps = [0] * threads
+    stop = threading.Event()
+
+    def make_vm():
+        vm = oracle.OracleVM(threads)
+        mids = {m["name"]: vm.map_create(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"])
+                for m in wl.maps}
+        pids = [vm.prog_load(p.name, p.raw, [(s, mids[nm]) for s, nm in p.relocs]) for p in wl.progs]
+        for mname, key, pi in wl.prog_array:
+            vm.map_update(mids[mname], key.to_bytes(4, "little"), vm.prog_addr(pids[pi]).to_bytes(4, "little"))
+        for mname, key, val in wl.map_init:
+            vm.map_update(mids[mname], key, val, 0, 0)
+        return vm, pids[0]
+
+    def worker(t):
+        a, b = t * chunk, min(n, (t + 1) * chunk)
+        off, lens = wl.off[a:b], wl.lens[a:b]
+        cpu = np.full(b - a, t, np.int32)
+        vm, pid = make_vm()
+        while not stop.is_set():
+            if wl.skb:
+                o = vm.run_skb_batch(pid, wl.buf, off, lens, cpu, 1, 0, write_back=False)
+                # sk_buff processes leak their entries (context_sk_buff.go:110-119): a fresh VM per
+                # pass keeps the 32-bit address space from running out
+                vm.close()
+                vm, pid = make_vm()
+            else:
+                o = vm.run_xdp_batch(pid, wl.buf, off, lens, cpu, write_back=False)
+            done[t] += b - a
+            steps[t] += int(o["steps"].astype(np.int64).sum())
+        vm.close()
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
     t0 = time.perf_counter()
-    while True:
-        o = vm.run_xdp_batch(pid, buf, off, lens, cpu, write_back=False)
-        done += n
-        steps += int(o["steps"].astype(np.int64).sum())
-        if time.perf_counter() - t0 >= min_seconds:
-            break
+    for th in ths:
+        th.start()
+    time.sleep(min_seconds)
+    stop.set()
+    for th in ths:
+        th.join()
     dt = time.perf_counter() - t0
-    vm.close()
-    return dict(value=done / dt / 1e6, unit="Mpkts/s", cores=1, kind="port",
-                insns_per_s=steps / dt,
-                sample=f"{done} packets ({done // n} passes over the first {n} packets of the {cfg_name} workload, "
-                       f"{vcpus_cpu} vCPUs, chunked), C oracle single-threaded, {dt:.1f} s")
+    tot = sum(done)
+    return dict(value=tot / dt / 1e6, unit="Mpkts/s", cores=threads, kind="port",
+                insns_per_s=sum(steps) / dt,
+                sample=f"{tot} packets of the first {n} packets of the {wl.name} workload, {threads} thread(s) x "
+                       f"1 vCPU chunk each (V = {threads}), C oracle, {dt:.1f} s")
 
 
-def read_pmc_traffic(cfg_name: str, kernel: str):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/*pmc*.json) of the
-    same workload and kernel (mimic_jit_kernel / mimic_xdp_kernel)."""
+def host_threads() -> int:
+    """Host threads this job may use: the affinity mask, capped at the 16-CPU share of one GPU."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+
+
+def read_profile(cfg_name: str, kernel: str, src_hash: str, n: int, vcpus: int):
+    """The committed rocprofv3 summary of exactly this kernel (source hash) on this workload."""
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_*.json"))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("config") == cfg_name and d.get("kernel") == kernel and d.get("bytes_per_launch"):
-            best = d
+        if (d.get("config") == cfg_name and d.get("kernel") == kernel and d.get("kernel_src_hash") == src_hash
+                and d.get("packets") == n and d.get("vcpus") == vcpus):
+            best = dict(d, file=os.path.relpath(f, ROOT))
     return best
 
 
-def host_resident_rate(vm, M, pid, buf, off, lens, sched, dev, chunks: int = 0, reps: int = 5):
+def host_resident_rate(vm, pid, wl, sched, chunks: int = 0, reps: int = 5):
     """Packets start and end in host memory: mimic_run_xdp_host pipelines sub-batches (H2D of
     packet bytes + descriptors, the kernel, D2H of r0 + status) on separate streams.  The host
     arrays are pinned once (hipHostRegister) like NIC / capture buffers would be."""
-    n = len(lens)
-    off = np.ascontiguousarray(off, dtype=np.uint64)
-    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    buf = wl.buf
+    n = len(wl.lens)
+    off = np.ascontiguousarray(wl.off, dtype=np.uint64)
+    lens = np.ascontiguousarray(wl.lens, dtype=np.uint32)
     r0 = np.empty(n, np.uint64)
     st = np.empty(n, np.uint8)
     arrs = (buf, off, lens, r0, st)
@@ -145,14 +254,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="classifier", choices=sorted(CONFIGS))
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
-    ap.add_argument("--vcpus", type=int, default=0, help="vCPUs per GPU (default: packets/4)")
+    ap.add_argument("--vcpus", type=int, default=0, help="vCPUs per GPU (default: the config's, else packets/4)")
     ap.add_argument("--sched", default="interleaved", choices=["chunked", "interleaved"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-resident", action="store_true", help="skip the PCIe-inclusive rate")
     args = ap.parse_args()
-    # compiled JIT kernels persist here across runs (tools/jit_prewarm.py fills it on a CPU host)
-    os.environ.setdefault("MIMIC_JIT_CACHE", os.path.join(os.path.dirname(os.path.abspath(__file__)), ".jitcache"))
+    # compiled JIT kernels persist here across runs
+    os.environ.setdefault("MIMIC_JIT_CACHE", os.path.join(ROOT, ".jitcache"))
     os.makedirs(os.environ["MIMIC_JIT_CACHE"], exist_ok=True)
 
     import torch
@@ -174,34 +283,35 @@ def main():
     n = args.packets or cfg["packets"]
     vpg = args.vcpus or cfg.get("vcpus") or max(64, n // 4)
     V = vpg * ws
+    wl = Workload(args.config, n, W.SEED + rank)
 
     # program bytes: built on rank 0, broadcast over RCCL (the setup-time exchange)
-    prog = getattr(W, cfg["prog"])()
-    raw_bytes = D.broadcast_bytes(prog.raw if rank == 0 else None, dev) if ws > 1 else prog.raw
+    raws = [D.broadcast_bytes(p.raw if rank == 0 else None, dev) if ws > 1 else p.raw for p in wl.progs]
+    vm, maps, pids = wl.build_vm(M, V, local, D.shard(vpg, rank), raws)
+    pid = pids[0]
 
-    emu = M.NewLinuxEmulator()
-    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(V), M.VMOptDevice(local), M.VMOptShard(*D.shard(vpg, rank)))
-    maps = {}
-    for m in prog.maps:
-        mm = M.MapSpecToLinuxMap(M.MapSpec(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"]))
-        emu.AddMap(m["name"], mm)
-        maps[m["name"]] = mm
-    pid = vm.AddProgram(M.ProgramSpec(prog.name, raw_bytes, prog.relocs))
-
-    buf, off, lens = W.make_packets(n, cfg["sizes"], cfg["weights"], seed=W.SEED + rank)
     sched = M.SCHED_INTERLEAVED if args.sched == "interleaved" else M.SCHED_CHUNKED
-    batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, ingress=1, schedule=sched)
+    if wl.skb:
+        batch = M.SKBBatch.from_numpy(wl.buf, wl.off, wl.lens, device=dev, ifindex=1, schedule=sched)
+    else:
+        batch = M.XDPBatch.from_numpy(wl.buf, wl.off, wl.lens, device=dev, ingress=1, schedule=sched)
     res = M.XDPResults.empty(n, dev, full=False)  # R0 + status per packet; steps via per-lane counters
     stream = torch.cuda.Stream(device=dev)
 
-    def step():
-        vm.RunXDPBatch(pid, batch, res, stream=stream, sync=False)
+    if wl.skb:
+        def step():
+            vm.RunSKBBatch(pid, batch, res, stream=stream, sync=False)
+            vm.SKBRelease()   # the batch's leaked sk_buff entries: a long run would exhaust 32-bit addresses
+    else:
+        def step():
+            vm.RunXDPBatch(pid, batch, res, stream=stream, sync=False)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
+    # per-launch device time: HIP events on the stream the kernel runs on
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -223,27 +333,31 @@ def main():
     else:
         steps_total_batch = float(steps_per_batch)
 
-    # sum-over-CPUs readout of the verdict counters (RCCL all-reduce across ranks)
+    # sum-over-CPUs readout of the per-CPU counters (RCCL all-reduce across ranks); shared hash
+    # maps: one replica per GPU, (key, value) records merged
     counters = None
     hash_keys = None
-    if prog.maps:
-        m0 = prog.maps[0]
-        if m0["type"] == 1:  # shared hash map: one replica per GPU, (key, value) records merged
-            mine = {k: v[0] for k, v in maps[m0["name"]].Contents().items()}
-            merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], dev) if ws > 1 else mine
-            hash_keys = len(merged)
-        else:
-            b0, cnt = D.shard(vpg, rank)
-            local_sum = maps[m0["name"]].SumU64(b0, b0 + cnt)
-            counters = D.allreduce_sum_u64(local_sum, dev) if ws > 1 else local_sum
+    pcm = [m for m in wl.maps if m["type"] == 6 and m["value_size"] == 8]
+    hm = [m for m in wl.maps if m["type"] == 1]
+    if hm and not wl.skb:
+        m0 = hm[0]
+        mine = {k: v[0] for k, v in maps[m0["name"]].Contents().items()}
+        merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], dev, m0["max_entries"]) if ws > 1 else mine
+        hash_keys = len(merged)
+    if pcm:
+        b0, cnt = D.shard(vpg, rank)
+        local_sum = maps[pcm[0]["name"]].SumU64(b0, b0 + cnt)
+        counters = D.allreduce_sum_u64(local_sum, dev) if ws > 1 else local_sum
 
     if rank == 0:
         total_pkts = n * ws * args.steps
         value = total_pkts / elapsed / 1e6
         avg_launch_s = float(np.mean(kern_ms)) / 1e3
-        alg = algorithmic_bytes(lens, vpg, prog.maps)
+        alg = algorithmic_bytes(wl.lens, vpg, wl.maps)
         achieved = alg / avg_launch_s
-        pmc = read_pmc_traffic(args.config, "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel")
+        kernel = "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel"
+        src_hash = wl.kernel_src_hash()
+        prof = read_profile(args.config, kernel, src_hash, n, vpg)
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",
             "value": round(value, 3),
@@ -258,22 +372,29 @@ def main():
             "dtype": "u64",
             "data": "synthetic (seeded PCG64 packet mix, SURVEY.md 8(d))",
             "config": {"workload": cfg["workload"], "packets_per_gpu": n, "vcpus_per_gpu": vpg,
-                       "schedule": args.sched, "parallelism": f"dp{ws}", "program_slots": len(prog.raw) // 8,
-                       "engine": vm.LastExec()},
+                       "schedule": args.sched, "parallelism": f"dp{ws}",
+                       "program_slots": sum(len(p.raw) // 8 for p in wl.progs), "engine": vm.LastExec(),
+                       "kernel_src_hash": src_hash},
             "insns_per_s": round(steps_total_batch * args.steps / elapsed, 1),
             "mean_insns_per_packet": round(steps_total_batch / (n * ws), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
-                         "traffic": pmc["bytes_per_launch"] if pmc else None,
+                         "traffic": prof["bytes_per_launch"] if prof else None,
+                         "traffic_over_algorithmic": round(prof["bytes_per_launch"] / alg, 3) if prof else None,
+                         "valu_busy": prof.get("valu_busy") if prof else None,
+                         "profile": prof["file"] if prof else None,
                          "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
             "status_ok_frac": float((st == 0).mean()),
             "counters_sum": counters,
             "hash_keys": hash_keys,
         }
-        if not args.no_host_resident and ws == 1:
-            out["host_resident"] = host_resident_rate(vm, M, pid, buf, off, lens, sched, dev)
+        if not args.no_host_resident and ws == 1 and not wl.skb:
+            out["host_resident"] = host_resident_rate(vm, pid, wl, sched)
         if not args.no_cpu_baseline and ws == 1:
-            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+            one = cpu_baseline(wl, args.cpu_seconds, 1)
+            T = host_threads()
+            allc = cpu_baseline(wl, args.cpu_seconds, T) if T > 1 else one
+            out["cpu_baseline"] = dict(one, all_cores=allc)
         print(json.dumps(out), flush=True)
     if ws > 1:
         dist.destroy_process_group()

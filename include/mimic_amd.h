@@ -223,6 +223,39 @@ int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *batch,
  * frees them).  Needed before adding maps / programs or running xdp_md batches again. */
 int mimic_skb_release(mimic_vm *vm);
 
+/* ---- single processes: the NewProcess / SetCPUID / Step / Run / Cleanup surface ---------------
+ * A process holds its own packet memory, private memory (stack, frames) and register state on
+ * the device, so it can be advanced instruction by instruction (the edb debugger's use of
+ * Process.Step, Readme.md:8).  Steps run on the batch interpreter with one lane.  xdp_md
+ * contexts only (LinuxContextXDP). */
+typedef struct mimic_process mimic_process;
+typedef struct {
+    uint64_t r[11];             /* Registers.R0 .. R10 */
+    int32_t pc;                 /* Registers.PC: next instruction; the offending one after an error */
+    uint32_t prog_id;           /* the program PC indexes (tail calls switch it) */
+    uint64_t steps;             /* Step() calls that executed an instruction so far */
+    int32_t status;             /* MIMIC_OK, or the fatal status once the process terminated */
+    uint32_t exited;            /* Step's `exited`: the program exited or hit a fatal error */
+} mimic_process_regs;
+/* VM.NewProcess(prog, &LinuxContextXDP{Packet, Headroom, Tailroom, ...}). vm.go:198-235,
+ * context_xdp_md.go:47-115.  packet = host bytes. */
+int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
+                      uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
+                      mimic_process **out);
+/* Process.SetCPUID: id < 0 or id > V is an error (vm.go:268-283); never called = -1 (vm.go:214). */
+int mimic_process_set_cpu(mimic_process *p, int32_t id);
+/* n x Process.Step (vm.go:291-340), stopping early when the process exits or fails; the
+ * registers after the last step in *out.  Stepping a process that hit a fatal error returns
+ * MIMIC_EINVAL ("process has been terminated"); after a clean exit Step reports exited again. */
+int mimic_process_step(mimic_process *p, uint32_t n, mimic_process_regs *out);
+/* Process.Run (vm.go:343-360): Step until exit / fatal error, or `budget` more steps (0 = the
+ * default budget; a suspended process can be run or stepped again). */
+int mimic_process_run(mimic_process *p, uint64_t budget, mimic_process_regs *out);
+/* The process's packet memory (headroom + packet + tailroom) as the program left it. */
+int mimic_process_packet(mimic_process *p, void *buf, size_t cap);
+/* Process.Cleanup (vm.go:363-374): frees the process. */
+void mimic_process_free(mimic_process *p);
+
 /* Wait for all work the vm enqueued on `hip_stream` (NULL = own stream). */
 int mimic_sync(mimic_vm *vm, void *hip_stream);
 /* Executed Step() count of the last completed mimic_run_xdp (sum over packets). */

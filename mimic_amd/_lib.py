@@ -40,6 +40,11 @@ class MapSpecC(C.Structure):
                 ("value_size", C.c_uint32), ("max_entries", C.c_uint32), ("flags", C.c_uint32)]
 
 
+class ProcessRegs(C.Structure):
+    _fields_ = [("r", C.c_uint64 * 11), ("pc", C.c_int32), ("prog_id", C.c_uint32), ("steps", C.c_uint64),
+                ("status", C.c_int32), ("exited", C.c_uint32)]
+
+
 class Reloc(C.Structure):
     _fields_ = [("slot", C.c_uint32), ("map_id", C.c_uint32)]
 
@@ -114,6 +119,13 @@ EXPORTS = {
                                              C.c_char_p, C.c_size_t]),
     "mimic_jit_prebuild_ctx": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32]),
     "mimic_jit_cache_source": (C.c_int, [C.c_char_p]),
+    "mimic_process_new": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "mimic_process_set_cpu": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mimic_process_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "mimic_process_run": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p]),
+    "mimic_process_packet": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "mimic_process_free": (None, [C.c_void_p]),
     "mimic_jit_code": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "mimic_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mimic_last_steps": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
@@ -129,6 +141,14 @@ def load() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    # torch's wheel bundles its own ROCm runtime (libamdhip64 / libhiprtc / comgr).  torch links it
+    # by a name the engine's NEEDED entry does not match, so loading the engine first would put two
+    # HIP runtimes in the process; loading torch first lets the engine bind to torch's copy by
+    # soname: one runtime, one device context, shared by the engine's kernels and torch's tensors.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)

@@ -1010,9 +1010,15 @@ int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out) {
 struct SkbRun {     // the sk_buff part of a batch (mimic_run_skb)
     uint32_t ifindex;
 };
+struct StepRun {    // a stepped single process (mimic_process_*): its state, private memory and budget
+    StepState *state;
+    uint8_t *priv;
+    uint64_t priv_bytes;
+    uint64_t budget;
+};
 
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
-                        hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr);
+                        hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr, const StepRun *step = nullptr);
 
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                   void *hip_stream) {
@@ -1079,8 +1085,25 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st) {
     return 0;
 }
 
+// the private-memory plan of a VM: qwords per lane and the qword offsets of its areas
+struct PrivPlan {
+    uint32_t xdp_q, frame_q, key_q, q_per_lane;
+};
+static PrivPlan priv_plan(const mimic_vm *vm) {
+    PrivPlan p;
+    const uint32_t stack_q = stack_size(vm) / 8;   // stack | xdp_md overlay | saved frames | hash key
+    p.xdp_q = stack_q;
+    p.frame_q = p.xdp_q + 3;
+    p.key_q = p.frame_q + MIMIC_MAX_FRAMES * MIMIC_FRAME_QWORDS;
+    uint32_t key_words = 0;  // hash helpers copy the key here once (derefMapKey)
+    for (auto &m : vm->maps)
+        if (is_hash(m)) key_words = std::max(key_words, (m.key_size + 7) / 8);
+    p.q_per_lane = p.key_q + key_words;
+    return p;
+}
+
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
-                        hipStream_t st_in, uint64_t first_index, const SkbRun *skb) {
+                        hipStream_t st_in, uint64_t first_index, const SkbRun *skb, const StepRun *step) {
     if (!vm || !b || !res) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
@@ -1091,25 +1114,21 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     int rc = upload_tables(vm);
     if (rc) return rc;
     hipStream_t st = st_in ? st_in : vm->stream;
-    const uint32_t cpu_lanes = (uint32_t)vm->s.vcpu_count;
+    const uint32_t cpu_lanes = step ? 1u : (uint32_t)vm->s.vcpu_count;
     // EXPLICIT batches may hold processes whose CPU ID is unset (-1) or V: two extra lanes
     bool extra = false;
-    if (b->schedule == MIMIC_SCHED_EXPLICIT && b->cpu)
+    if (!step && b->schedule == MIMIC_SCHED_EXPLICIT && b->cpu)
         for (uint32_t i = 0; i < b->n && !extra; i++) extra = b->cpu[i] == -1 || b->cpu[i] == vm->s.vcpus;
     const uint32_t lanes = cpu_lanes + (extra ? 2u : 0u);
     const uint32_t S = stack_size(vm);
-    // private memory: stack | xdp_md overlay | saved frames, qword-interleaved over lanes
-    const uint32_t stack_q = S / 8;
-    const uint32_t xdp_q = stack_q;
-    const uint32_t frame_q = xdp_q + 3;
-    const uint32_t key_q = frame_q + MIMIC_MAX_FRAMES * MIMIC_FRAME_QWORDS;
-    uint32_t key_words = 0;  // hash helpers copy the key here once (derefMapKey)
-    for (auto &m : vm->maps)
-        if (is_hash(m)) key_words = std::max(key_words, (m.key_size + 7) / 8);
-    const uint32_t q_per_lane = key_q + key_words;
+    // private memory: stack | xdp_md overlay | saved frames | hash key, qword-interleaved over lanes
+    const PrivPlan pp = priv_plan(vm);
+    const uint32_t xdp_q = pp.xdp_q, frame_q = pp.frame_q, key_q = pp.key_q, q_per_lane = pp.q_per_lane;
     const uint32_t plan = (lanes + 255) & ~255u;
     const uint64_t need = (uint64_t)q_per_lane * plan * 8;
-    if (need > vm->priv_bytes || plan != vm->priv_lanes) {
+    if (step) {
+        if (step->priv_bytes < (uint64_t)q_per_lane * 8) return fail(vm, MIMIC_EINVAL, "process private memory too small");
+    } else if (need > vm->priv_bytes || plan != vm->priv_lanes) {
         hipStreamSynchronize(st);
         hipFree(vm->priv);
         vm->priv = nullptr;
@@ -1145,12 +1164,13 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.vcpu_begin = (uint32_t)vm->s.vcpu_begin;
     kp.lanes = lanes;
     kp.cpu_lanes = cpu_lanes;
-    kp.priv_lanes = vm->priv_lanes;
-    kp.priv = vm->priv;
+    kp.priv_lanes = step ? 1u : vm->priv_lanes;
+    kp.priv = step ? step->priv : vm->priv;
     kp.priv_xdp_q = xdp_q;
     kp.priv_frame_q = frame_q;
     kp.priv_key_q = key_q;
-    kp.budget = b->step_budget ? b->step_budget : MIMIC_DEFAULT_BUDGET;
+    kp.budget = step ? step->budget : (b->step_budget ? b->step_budget : MIMIC_DEFAULT_BUDGET);
+    kp.step = step ? step->state : nullptr;
     kp.n = b->n;
     kp.sched = b->schedule;
     kp.pkt_data = b->pkt_data;
@@ -1240,7 +1260,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
-    bool jit = vm->exec_mode == MIMIC_EXEC_JIT;
+    bool jit = vm->exec_mode == MIMIC_EXEC_JIT && !step;   // stepping runs on the interpreter
     if (jit && !vm->jit_fn[ctx]) {
         std::string log;
         if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx]),
@@ -1265,6 +1285,183 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     vm->last_lanes = lanes;
     vm->last_stream = st;
     return 0;
+}
+
+}  // extern "C"
+
+struct mimic_process {
+    mimic_vm *vm = nullptr;
+    uint32_t prog = 0;
+    uint32_t H = 0, T = 0, len = 0;
+    int32_t ingress = 0, rxq = 0, egress = 0;
+    uint8_t *d_pkt = nullptr;         // packet memory H + len + T
+    uint64_t *d_off = nullptr;        // descriptor of the one-packet batch
+    uint32_t *d_len = nullptr;
+    uint64_t *d_r0 = nullptr;
+    uint8_t *d_st = nullptr;
+    uint32_t *d_steps = nullptr;
+    int32_t *d_epc = nullptr;
+    StepState *d_state = nullptr;
+    uint8_t *d_priv = nullptr;
+    uint64_t priv_bytes = 0;
+    StepState h;                      // host copy after the last launch
+    int32_t cpu = -1;
+};
+
+static void process_release(mimic_process *p) {
+    hipFree(p->d_pkt);
+    hipFree(p->d_off);
+    hipFree(p->d_len);
+    hipFree(p->d_r0);
+    hipFree(p->d_st);
+    hipFree(p->d_steps);
+    hipFree(p->d_epc);
+    hipFree(p->d_state);
+    hipFree(p->d_priv);
+}
+
+static void process_regs(const mimic_process *p, mimic_process_regs *out) {
+    if (!out) return;
+    memset(out, 0, sizeof *out);
+    for (int q = 0; q < 11; q++) out->r[q] = p->h.r[q];
+    out->pc = p->h.pc;
+    out->prog_id = p->h.started ? p->h.prog : p->prog;
+    out->steps = p->h.steps;
+    out->status = p->h.finished ? p->h.status : MIMIC_OK;
+    out->exited = p->h.finished;
+}
+
+// one launch: run the process until `budget` total steps (or exit / error), then sync its state
+static int process_advance(mimic_process *p, uint64_t budget) {
+    mimic_vm *vm = p->vm;
+    hipSetDevice(vm->s.device);
+    // the VM may have grown (maps / programs) since the process was made: its private plan too
+    const PrivPlan pp = priv_plan(vm);
+    if ((uint64_t)pp.q_per_lane * 8 > p->priv_bytes && p->h.started)
+        return fail(vm, MIMIC_ENOTSUP, "the VM's process layout changed under a started process");
+    if ((uint64_t)pp.q_per_lane * 8 > p->priv_bytes) {
+        hipFree(p->d_priv);
+        p->d_priv = nullptr;
+        p->priv_bytes = (uint64_t)pp.q_per_lane * 8;
+        HIP_OK(vm, hipMalloc(&p->d_priv, p->priv_bytes));
+    }
+    StepState st = p->h;
+    st.cpu = p->cpu;
+    HIP_OK(vm, hipMemcpy(p->d_state, &st, sizeof st, hipMemcpyHostToDevice));
+    mimic_xdp_batch b{};
+    b.n = 1;
+    b.schedule = MIMIC_SCHED_CHUNKED;
+    b.pkt_data = p->d_pkt;
+    b.pkt_off = p->d_off;
+    b.pkt_len = p->d_len;
+    b.headroom_all = p->H;
+    b.tailroom_all = p->T;
+    b.ingress_all = p->ingress;
+    b.rxq_all = p->rxq;
+    b.egress_all = p->egress;
+    mimic_xdp_results r{};
+    r.r0 = p->d_r0;
+    r.status = p->d_st;
+    r.steps = p->d_steps;
+    r.err_pc = p->d_epc;
+    const StepRun sr{p->d_state, p->d_priv, p->priv_bytes, budget};
+    int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, nullptr, &sr);
+    if (rc) return rc;
+    HIP_OK(vm, hipMemcpyAsync(&p->h, p->d_state, sizeof p->h, hipMemcpyDeviceToHost, vm->stream));
+    HIP_OK(vm, hipStreamSynchronize(vm->stream));
+    return 0;
+}
+
+extern "C" {
+
+int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
+                      uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
+                      mimic_process **out) {
+    if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
+    if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
+    if (vm->skb_leaked) return fail(vm, MIMIC_ENOTSUP, "xdp_md processes after sk_buff batches are not supported");
+    hipSetDevice(vm->s.device);
+    mimic_process *p = new mimic_process();
+    p->vm = vm;
+    p->prog = prog_id;
+    p->H = headroom;
+    p->T = tailroom;
+    p->len = len;
+    p->ingress = ingress_ifindex;
+    p->rxq = rx_queue_index;
+    p->egress = egress_ifindex;
+    memset(&p->h, 0, sizeof p->h);
+    const uint64_t M = (uint64_t)headroom + len + tailroom;
+    const uint64_t zero = 0;
+    hipError_t e = hipMalloc(&p->d_pkt, std::max<uint64_t>(M, 1));
+    if (e == hipSuccess) e = hipMemset(p->d_pkt, 0, std::max<uint64_t>(M, 1));
+    if (e == hipSuccess && len) e = hipMemcpy(p->d_pkt + headroom, packet, len, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_off, 8);
+    if (e == hipSuccess) e = hipMemcpy(p->d_off, &zero, 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_len, 4);
+    if (e == hipSuccess) e = hipMemcpy(p->d_len, &len, 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_r0, 8);
+    if (e == hipSuccess) e = hipMalloc(&p->d_st, 1);
+    if (e == hipSuccess) e = hipMalloc(&p->d_steps, 4);
+    if (e == hipSuccess) e = hipMalloc(&p->d_epc, 4);
+    if (e == hipSuccess) e = hipMalloc(&p->d_state, sizeof(StepState));
+    if (e != hipSuccess) {
+        process_release(p);
+        delete p;
+        return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
+    }
+    *out = p;
+    return 0;
+}
+
+int mimic_process_set_cpu(mimic_process *p, int32_t id) {
+    if (!p) return MIMIC_EINVAL;
+    if (id < 0) return fail(p->vm, MIMIC_EINVAL, "not a valid CPU ID");
+    if (id > p->vm->s.vcpus)
+        return fail(p->vm, MIMIC_EINVAL, "vm only has %d vCPUs, max CPU ID is %d", p->vm->s.vcpus, p->vm->s.vcpus - 1);
+    p->cpu = id;
+    return 0;
+}
+
+int mimic_process_step(mimic_process *p, uint32_t n, mimic_process_regs *out) {
+    if (!p) return MIMIC_EINVAL;
+    if (p->h.finished) {
+        process_regs(p, out);
+        // a clean exit leaves PC on the exit instruction: stepping it again exits again
+        return p->h.status == MIMIC_OK ? 0 : fail(p->vm, MIMIC_EINVAL, "process has been terminated");
+    }
+    if (n) {
+        const int rc = process_advance(p, (uint64_t)p->h.steps + n);
+        if (rc) return rc;
+    }
+    process_regs(p, out);
+    return 0;
+}
+
+int mimic_process_run(mimic_process *p, uint64_t budget, mimic_process_regs *out) {
+    if (!p) return MIMIC_EINVAL;
+    if (p->h.finished) return mimic_process_step(p, 0, out);
+    const int rc = process_advance(p, (uint64_t)p->h.steps + (budget ? budget : MIMIC_DEFAULT_BUDGET));
+    if (rc) return rc;
+    process_regs(p, out);
+    return 0;
+}
+
+int mimic_process_packet(mimic_process *p, void *buf, size_t cap) {
+    if (!p || !buf) return MIMIC_EINVAL;
+    const uint64_t M = (uint64_t)p->H + p->len + p->T;
+    if (cap < M) return fail(p->vm, MIMIC_EINVAL, "buffer too small");
+    hipSetDevice(p->vm->s.device);
+    HIP_OK(p->vm, hipMemcpy(buf, p->d_pkt, M, hipMemcpyDeviceToHost));
+    return (int)M;
+}
+
+void mimic_process_free(mimic_process *p) {
+    if (!p) return;
+    hipSetDevice(p->vm->s.device);
+    hipStreamSynchronize(p->vm->stream);
+    process_release(p);
+    delete p;
 }
 
 int mimic_sync(mimic_vm *vm, void *hip_stream) {

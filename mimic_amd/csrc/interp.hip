@@ -33,6 +33,21 @@
 // ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
+// Process.Step: save the process at the end of a launch (suspended by the step budget, or done)
+static_assert(sizeof(Lane) <= sizeof(((StepState *)0)->lane), "StepState::lane too small");
+static __device__ void step_save(const KParams &kp, const Lane &L, const uint64_t *RB, int st, int32_t pc, uint32_t steps,
+                                 uint32_t prog) {
+    StepState *S = kp.step;
+    for (int q = 0; q < 11; q++) S->r[q] = RB[q * 64];
+    __builtin_memcpy(S->lane, &L, sizeof(Lane));
+    S->pc = pc;
+    S->prog = prog;
+    S->steps = steps;
+    S->status = st;
+    S->started = 1;
+    S->finished = st != MIMIC_ERR_STEP_LIMIT;
+}
+
 #define WAVES_PER_BLOCK 4
 #define NREGS 11
 #define KEY_DONE 0xffffffffu
@@ -50,7 +65,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
     const bool lane_valid = g < kp.lanes;
     Lane L;
     L.lane = g;
-    L.cpu = lane_cpu(kp, g);
+    L.cpu = kp.step ? kp.step->cpu : lane_cpu(kp, g);
 
     uint32_t ex_begin = 0, ex_count = 0;
     if (lane_valid && kp.sched == SCHED_EXPLICIT) {
@@ -80,6 +95,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
 #pragma unroll
         for (int q = 0; q < NREGS; q++) REG(q) = 0;
         uint32_t pn = entry.n, pbase = entry.base;
+        uint32_t cur_prog = kp.entry_prog;
         uint32_t key = KEY_DONE;   // global instruction index = pbase + PC; KEY_DONE = not running
         uint32_t steps = 0;
         L.sm0 = 0;
@@ -104,8 +120,31 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
             if (kp.err_pc) kp.err_pc[i] = (int32_t)(epc_);             \
             lane_steps += steps;                                       \
             key = KEY_DONE;                                            \
+            if (kp.step) step_save(kp, L, RB, (st_), (epc_), steps, cur_prog); \
         } while (0)
-        if (i != 0xffffffffu && kp.ctx_kind == CTX_SKB) {   // LinuxContextSKBuff.Load (skb.h)
+        // Process.Step: a stepped process resumes where its last launch suspended it
+        bool resumed = false;
+        if (i != 0xffffffffu && kp.step && kp.step->started) {
+            const StepState *S = kp.step;
+#pragma unroll
+            for (int q = 0; q < NREGS; q++) REG(q) = S->r[q];
+            __builtin_memcpy(&L, S->lane, sizeof(Lane));
+            L.cpu = S->cpu;           // SetCPUID may have moved the process between steps
+            steps = S->steps;
+            cur_prog = S->prog;
+            const DProg cp = kp.progs[cur_prog];
+            pn = cp.n;
+            pbase = cp.base;
+            resumed = true;
+            if (S->pc < 0) {          // a jump left PC negative: this Step panics on the fetch (vm.go:300)
+                steps++;
+                TERM(MIMIC_PANIC_PC, S->pc);
+            } else {
+                key = pbase + (uint32_t)S->pc;
+            }
+        }
+        if (resumed) {
+        } else if (i != 0xffffffffu && kp.ctx_kind == CTX_SKB) {   // LinuxContextSKBuff.Load (skb.h)
             uint64_t r1 = 0;
             const int ls = skb_load(kp, L, i, r1);
             REG(10) = kp.static_next + kp.frame_size;
@@ -142,7 +181,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
         }
 
         // ---- Process.Run ------------------------------------------------------------------
-        uint64_t wsteps = 0;          // wave-steps since the packets started: bounds every lane's steps
+        uint64_t wsteps = resumed ? steps : 0;   // wave-steps since the packets started: bounds every lane's steps
         uint32_t cand = KEY_DONE;     // speculated next key (where the first executing lane went)
         for (;;) {
             const uint64_t live = __ballot(key != KEY_DONE);
@@ -261,6 +300,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
                             if (ho.tail) {  // PC = -1, then Step's bounds check on the new program
                                 const DProg np = kp.progs[ho.new_prog];
                                 L.tailcalls++;
+                                cur_prog = ho.new_prog;
                                 if (np.n == 0) st = MIMIC_ERR_PC_OOB;
                                 else {
                                     pn = np.n;
@@ -326,7 +366,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
                     }
 
                     if (st == EXIT_SIG) {
-                        TERM(MIMIC_OK, -1);
+                        TERM(MIMIC_OK, kp.step ? (int32_t)pc : -1);   // a stepped process keeps PC at the exit
                     } else if (st) {
                         TERM(st, pc);
                     } else if (jmp == 0) {                 // PC+1 (vm.go:328-337)

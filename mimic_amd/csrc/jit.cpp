@@ -186,6 +186,9 @@ class Gen {
         E.line("  uint32_t ga_ = 0;   // the address of the current memory access");
         E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
         E.line("    uint32_t i;");
+        // fields used once per packet are read through an opaque copy of the parameter pointer:
+        // loaded where used instead of hoisted out of the packet loop into SGPRs
+        E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         // The lane's private-memory and LDS addresses are loop-invariant; hoisted out of the packet
         // loop they would stay live (one VGPR pair per stack slot) through every packet.  An opaque
         // per-iteration copy of the lane index keeps each address next to its use.
@@ -203,10 +206,10 @@ class Gen {
                 E.line("    const uint32_t W_ = ls_ ? 0u : win_stage(pwin_, tl_, L.pkt + SKB_HEADROOM, L.M - SKB_HEADROOM);");
         } else {
             // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
-            E.line("    const uint32_t H = kp.headroom_arr ? kp.headroom_arr[i] : kp.headroom;");
-            E.line("    const uint32_t T = kp.tailroom_arr ? kp.tailroom_arr[i] : kp.tailroom;");
-            E.line("    const uint32_t len = kp.pkt_len[i];");
-            E.line("    L.pkt = kp.pkt_data + kp.pkt_off[i];");
+            E.line("    const uint32_t H = kq_.headroom_arr ? kq_.headroom_arr[i] : kq_.headroom;");
+            E.line("    const uint32_t T = kq_.tailroom_arr ? kq_.tailroom_arr[i] : kq_.tailroom;");
+            E.line("    const uint32_t len = kq_.pkt_len[i];");
+            E.line("    L.pkt = kq_.pkt_data + kq_.pkt_off[i];");
             E.line("    L.M = H + len + T;");
             E.line("    L.pa = P;");
             E.line("    L.rec = nullptr;");
@@ -214,9 +217,9 @@ class Gen {
             E.line("    for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;");
             E.line("    L.data = P + H;");
             E.line("    L.data_end = P + H + len;");
-            E.line("    L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);");
-            E.line("    L.rxq = (uint32_t)(kp.rxq_arr ? kp.rxq_arr[i] : kp.rxq);");
-            E.line("    L.egress = (uint32_t)(kp.egress_arr ? kp.egress_arr[i] : kp.egress);");
+            E.line("    L.ingress = (uint32_t)(kq_.ingress_arr ? kq_.ingress_arr[i] : kq_.ingress);");
+            E.line("    L.rxq = (uint32_t)(kq_.rxq_arr ? kq_.rxq_arr[i] : kq_.rxq);");
+            E.line("    L.egress = (uint32_t)(kq_.egress_arr ? kq_.egress_arr[i] : kq_.egress);");
             if (stage && fast_paths) E.line("    const uint32_t W_ = win_stage(pwin_, tl_, L.pkt, L.M);");
             E.line("    uint64_t r1 = P + L.M + 1;");
         }
@@ -237,10 +240,10 @@ class Gen {
         for (auto &p : P) program(p);
         E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
         E.line("  L_term:");
-        E.line("    if (kp.r0) kp.r0[i] = r0;");
-        E.line("    if (kp.status) kp.status[i] = (uint8_t)st_;");
-        E.line("    if (kp.steps) kp.steps[i] = steps;");
-        E.line("    if (kp.err_pc) kp.err_pc[i] = epc_;");
+        E.line("    if (kq_.r0) kq_.r0[i] = r0;");
+        E.line("    if (kq_.status) kq_.status[i] = (uint8_t)st_;");
+        E.line("    if (kq_.steps) kq_.steps[i] = steps;");
+        E.line("    if (kq_.err_pc) kq_.err_pc[i] = epc_;");
         E.line("    lane_steps += steps;");
         E.line("  }");
         E.line("  if (kp.lane_steps) kp.lane_steps[g] = lane_steps;");
@@ -658,6 +661,8 @@ std::string cache_name(const std::string &src, const char *const *opts, int nopt
     };
     mix(src.data(), src.size());
     for (int i = 0; i < nopts; i++) mix(opts[i], strlen(opts[i]) + 1);
+    // the embedded runtime headers are part of every kernel: a changed header is a new kernel
+    for (int i = 0; i < kJitHeaderCount; i++) mix(kJitHeaderSrc[i], strlen(kJitHeaderSrc[i]));
     int maj = 0, min = 0;
     hiprtcVersion(&maj, &min);
     char v[32];
@@ -704,6 +709,9 @@ const int kNOpts = (int)(sizeof kOpts / sizeof *kOpts);
 int build_code(const std::string &src, std::vector<char> &code, std::string *log) {
     const std::string path = cache_path(cache_name(src, kOpts, kNOpts));
     if (!path.empty() && read_file(path, code)) return 0;
+    // comgr's own compile cache does not see the embedded headers change; ours (keyed on the
+    // source, the options and the headers) is the only one in use
+    setenv("AMD_COMGR_CACHE", "0", 0);
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "mimic_jit.hip", kJitHeaderCount, kJitHeaderSrc, kJitHeaderNames) !=
         HIPRTC_SUCCESS) {
@@ -805,6 +813,7 @@ int mimic_jit_launch(hipFunction_t fn, const JitInfo &info, const KParams *kp, c
 
 // compile only (no device needed): the hipRTC log, for build checks and tests
 int mimic_jit_check_source(const std::string &src, std::string *log, size_t *code_size) {
+    setenv("AMD_COMGR_CACHE", "0", 0);
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "mimic_jit.hip", kJitHeaderCount, kJitHeaderSrc, kJitHeaderNames) !=
         HIPRTC_SUCCESS)

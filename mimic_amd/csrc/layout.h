@@ -187,4 +187,25 @@ struct KParams {
     SkbRec *skb_rec;
     const uint64_t *skb_prefix;
     const uint64_t *skb_base;
+    // single-process stepping (Process.Step, vm.go:291-340): one lane, one packet, interpreter
+    // only.  The process state is restored from / saved to *step around the launch, and the
+    // step budget suspends the process instead of ending it.
+    struct StepState *step;
+};
+
+// The state of one stepped process between launches (engine.cpp mimic_process_*): the
+// reference's Registers (PC, R0-R10), the current program, the step count, and the lane
+// state (stack validity, xdp_md overlay, frames, tail calls, translation cache) -- the stack,
+// frames and xdp_md overlay themselves stay in the process's own private memory.
+struct StepState {
+    uint64_t r[11];
+    int32_t pc;           // Registers.PC: the next instruction (or the offending / exit one)
+    uint32_t prog;        // current program (tail calls change it)
+    uint32_t steps;       // Step() calls executed so far
+    int32_t status;       // final MIMIC status (finished only)
+    uint32_t started;     // NewProcess + Load done
+    uint32_t finished;    // exited (status OK) or terminated by a fatal error
+    int32_t cpu;          // Process.cpuID (-1 until SetCPUID)
+    uint32_t pad;
+    uint8_t lane[256];    // the kernel's Lane record (runtime.h), opaque to the host
 };

@@ -68,15 +68,35 @@ def allgather_records(records: bytes, rec_size: int, device) -> List[bytes]:
     return [bytes(o[:int(s.item())].cpu().numpy().tobytes()) for o, s in zip(outs, sizes)]
 
 
-def merge_hash_replicas(contents: Dict[bytes, bytes], key_size: int, value_size: int, device) -> Dict[bytes, bytes]:
+class ReplicaOverflow(RuntimeError):
+    """The replicas together hold more keys than the map's MaxEntries: the reference's one shared
+    table would have answered E2BIG to some of these inserts, so the sharded run is not exact."""
+
+
+def merge_records(blobs: Sequence[bytes], key_size: int, value_size: int,
+                  max_entries: Optional[int] = None) -> Dict[bytes, bytes]:
+    """Merge per-replica (key, value) record blobs in rank order; the first rank's value wins.
+    With max_entries, more distinct keys than the map holds raise ReplicaOverflow."""
+    rs = key_size + value_size
+    merged: Dict[bytes, bytes] = {}
+    for blob in blobs:
+        for o in range(0, len(blob), rs):
+            merged.setdefault(blob[o:o + key_size], blob[o + key_size:o + rs])
+    if max_entries is not None and len(merged) > max_entries:
+        raise ReplicaOverflow(f"{len(merged)} keys over the replicas, MaxEntries {max_entries}")
+    return merged
+
+
+def replica_blob(contents: Dict[bytes, bytes]) -> bytes:
+    return b"".join(k + v for k, v in sorted(contents.items()))
+
+
+def merge_hash_replicas(contents: Dict[bytes, bytes], key_size: int, value_size: int, device,
+                        max_entries: Optional[int] = None) -> Dict[bytes, bytes]:
     """Shared hash map over N GPUs kept as one replica per GPU (SURVEY 8(e) option 1): gather
     every replica's (key, value) records and keep the first rank's value for each key.  Exact
-    for insert-if-absent programs whose values are a function of the key (cfg 4)."""
-    rs = key_size + value_size
-    mine = b"".join(k + v for k, v in sorted(contents.items()))
-    merged: Dict[bytes, bytes] = {}
-    for blob in allgather_records(mine, rs, device):
-        for o in range(0, len(blob), rs):
-            k, v = blob[o:o + key_size], blob[o + key_size:o + rs]
-            merged.setdefault(k, v)
-    return merged
+    for insert-if-absent programs whose values are a function of the key (cfg 4) as long as the
+    replicas together stay within MaxEntries (checked when max_entries is given).  A rank does
+    not see the keys other ranks inserted during the batch."""
+    blobs = allgather_records(replica_blob(contents), key_size + value_size, device)
+    return merge_records(blobs, key_size, value_size, max_entries)

@@ -544,13 +544,21 @@ def NewVM(*opts) -> VM:  # vm.go:54-76
 
 
 class Registers:
+    """Process.Registers (vm.go:378-405): PC and R0..R10."""
+
     def __init__(self):
         self.PC = 0
-        self.R0 = 0
+        for q in range(11):
+            setattr(self, f"R{q}", 0)
+
+    def Get(self, r: int) -> int:
+        return getattr(self, f"R{r}")
 
 
 class Process:
-    """Single process = a one-packet batch on the GPU (the Process.Run drop-in)."""
+    """A process of the VM (vm.go:238-374).  Run() alone is a one-packet batch on the JIT kernel;
+    Step() advances the process one instruction at a time on the device (a single-lane
+    interpreter launch per call, mimic_process_step) and a Run() after Step() continues it."""
 
     def __init__(self, vm: VM, prog_id: int, ctx=None):
         self.VM = vm
@@ -562,6 +570,9 @@ class Process:
         self.Status = None
         self.ErrPC = -1
         self.PacketAfter: Optional[bytes] = None
+        self._native = None
+        self._exited = False
+        self.Registers.R10 = vm.StackAddress() + vm.settings.stack_frame_size   # vm.go:224
 
     def CPUID(self) -> int:
         return self.cpuID
@@ -570,15 +581,63 @@ class Process:
         if i < 0:
             raise MimicError("not a valid CPU ID")
         if i > self.VM.settings.vcpus:
-            raise MimicError(f"vm only has {self.VM.settings.vcpus} vCPUs")
+            raise MimicError(f"vm only has {self.VM.settings.vcpus} vCPUs, max CPU ID is {self.VM.settings.vcpus - 1}")
         self.cpuID = i
+        if self._native is not None:
+            _check(self.VM.h, self.VM.lib.mimic_process_set_cpu(self._native, i), "SetCPUID")
+
+    # ---- stepping (device-resident single process) -----------------------------------------
+    def _ensure_native(self):
+        if self._native is not None:
+            return
+        ctx = self.Context or LinuxContextXDP()
+        if isinstance(ctx, LinuxContextSKBuff):
+            raise MimicError("Step on sk_buff contexts is not supported (Run is)")
+        h = C.c_void_p()
+        pkt = bytes(ctx.Packet)
+        _check(self.VM.h, self.VM.lib.mimic_process_new(self.VM.h, self.prog_id, pkt, len(pkt), ctx.Headroom,
+                                                         ctx.Tailroom, ctx.IngessIfIndex, ctx.RxQueueIndex,
+                                                         ctx.EgressIfIndex, C.byref(h)), "NewProcess")
+        self._native = h
+        if self.cpuID >= 0:
+            _check(self.VM.h, self.VM.lib.mimic_process_set_cpu(h, self.cpuID), "SetCPUID")
+
+    def _take(self, regs) -> None:
+        for q in range(11):
+            setattr(self.Registers, f"R{q}", int(regs.r[q]))
+        self.Registers.PC = int(regs.pc)
+        self.ProgramID = int(regs.prog_id)
+        self.Steps = int(regs.steps)
+        self.Status = int(regs.status)
+        self._exited = bool(regs.exited)
+
+    def Step(self) -> bool:
+        """Process.Step (vm.go:291-340): execute one instruction; True once the program exited.
+        A fatal error raises MimicError (the reference returns it), after which the process is
+        terminated."""
+        self._ensure_native()
+        regs = L.ProcessRegs()
+        rc = self.VM.lib.mimic_process_step(self._native, 1, C.byref(regs))
+        if rc < 0:
+            _check(self.VM.h, rc, "Step")
+        self._take(regs)
+        if self.Status:
+            self.ErrPC = self.Registers.PC
+            raise MimicError(f"inst at PC({self.Registers.PC}): {L.STATUS_NAMES[self.Status]}")
+        return self._exited
 
     def Run(self, step_budget: int = 0) -> None:  # vm.go:343-360
-        import torch
-
         # cpuID stays -1 when SetCPUID was never called (vm.go:214) and may equal V (vm.go:273):
         # the reference runs such processes; only per-CPU map operations fail in them
         # (emulator_linux_map_array.go:236-238) and bpf_get_smp_processor_id returns the ID as set
+        if self._native is not None:
+            regs = L.ProcessRegs()
+            _check(self.VM.h, self.VM.lib.mimic_process_run(self._native, step_budget, C.byref(regs)), "Run")
+            self._take(regs)
+            self.ErrPC = self.Registers.PC if self.Status else -1
+            if self.Status:
+                raise MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[self.Status]} at PC({self.ErrPC})")
+            return
         ctx = self.Context or LinuxContextXDP()
         dev = f"cuda:{self.VM.settings.device}"
         if isinstance(ctx, LinuxContextSKBuff):
@@ -598,8 +657,26 @@ class Process:
         if self.Status != 0:
             raise MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[self.Status]} at PC({self.ErrPC})")
 
-    def Cleanup(self) -> None:
-        pass
+    def Packet(self) -> bytes:
+        """Packet memory (headroom + packet + tailroom) of a stepped process, as it is now."""
+        if self._native is None:
+            return self.PacketAfter or b""
+        ctx = self.Context or LinuxContextXDP()
+        n = ctx.Headroom + len(ctx.Packet) + ctx.Tailroom
+        buf = C.create_string_buffer(max(n, 1))
+        _check(self.VM.h, self.VM.lib.mimic_process_packet(self._native, buf, max(n, 1)), "packet")
+        return buf.raw[:n]
+
+    def Cleanup(self) -> None:  # vm.go:363-374
+        if self._native is not None and getattr(self.VM, "h", None):   # (a closed VM freed its device state)
+            self.VM.lib.mimic_process_free(self._native)
+        self._native = None
+
+    def __del__(self):
+        try:
+            self.Cleanup()
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------------------------

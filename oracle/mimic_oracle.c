@@ -1414,6 +1414,31 @@ static void xdp_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t H, ui
     p->R.r[1] = xa;
 }
 
+/* NewProcess(prog, &LinuxContextXDP{...}) for single-process stepping (vm.go:198-235) */
+orc_proc *orc_proc_new_xdp(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t H, uint32_t T,
+                           int32_t ingress, int32_t rxq, int32_t egress) {
+    if (prog_id < 0 || prog_id >= vm->nprogs) return NULL;
+    orc_proc *p = proc_new(vm, prog_id);
+    xdp_load(p, pkt, L, H, T, ingress, rxq, egress);
+    return p;
+}
+
+/* Process.Step (vm.go:291-340): 0 = continue, -1 = exited, > 0 = fatal status */
+int orc_proc_step(orc_proc *p, int32_t *err_pc) {
+    int32_t e = -1;
+    const int rc = step(p, &e);
+    if (err_pc) *err_pc = e;
+    return rc;
+}
+
+int64_t orc_proc_get_pc(orc_proc *p) { return p->R.pc; }
+
+int orc_proc_get_prog(orc_proc *p) {
+    for (int i = 0; i < p->vm->nprogs; i++)
+        if (p->vm->progs[i] == p->prog) return i;
+    return -1;
+}
+
 int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_results *out) {
     if (prog_id < 0 || prog_id >= vm->nprogs) {
         set_err(vm, "no program with id '%d' is loaded", prog_id);

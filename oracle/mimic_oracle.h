@@ -120,6 +120,13 @@ void orc_proc_free(orc_proc *p);                   /* Cleanup */
 int orc_proc_set_cpu(orc_proc *p, int cpu);        /* SetCPUID */
 uint64_t orc_proc_get_reg(orc_proc *p, int r);
 void orc_proc_set_reg(orc_proc *p, int r, uint64_t v);
+/* Single-process stepping: NewProcess with an xdp_md context, Process.Step (0 continue, -1
+ * exited, > 0 fatal status), Registers.PC and the current program. */
+orc_proc *orc_proc_new_xdp(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t H, uint32_t T,
+                           int32_t ingress, int32_t rxq, int32_t egress);
+int orc_proc_step(orc_proc *p, int32_t *err_pc);
+int64_t orc_proc_get_pc(orc_proc *p);
+int orc_proc_get_prog(orc_proc *p);
 /* emulator.CallHelperFunction directly (as the reference tests call linuxHelper* directly). */
 int orc_proc_call_helper(orc_proc *p, int32_t helper);
 

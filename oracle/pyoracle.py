@@ -73,6 +73,11 @@ def load(build: bool = True) -> C.CDLL:
         "orc_proc_get_reg": (C.c_uint64, [C.c_void_p, C.c_int]),
         "orc_proc_set_reg": (None, [C.c_void_p, C.c_int, C.c_uint64]),
         "orc_proc_call_helper": (C.c_int, [C.c_void_p, C.c_int32]),
+        "orc_proc_new_xdp": (C.c_void_p, [C.c_void_p, C.c_int, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_int32, C.c_int32, C.c_int32]),
+        "orc_proc_step": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+        "orc_proc_get_pc": (C.c_int64, [C.c_void_p]),
+        "orc_proc_get_prog": (C.c_int, [C.c_void_p]),
         "orc_run_xdp_batch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(_Batch), C.POINTER(_Results)]),
         "orc_run_skb_batch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(_SkbBatch), C.POINTER(_Results)]),
     }
@@ -85,11 +90,28 @@ def load(build: bool = True) -> C.CDLL:
 
 
 class OracleProcess:
-    def __init__(self, vm: "OracleVM", prog_id: int):
+    def __init__(self, vm: "OracleVM", prog_id: int, xdp=None):
+        """xdp = (packet bytes, headroom, tailroom, ingress, rxq, egress): an xdp_md context."""
         self.vm = vm
-        self.p = vm.lib.orc_proc_new(vm.h, prog_id)
+        if xdp is None:
+            self.p = vm.lib.orc_proc_new(vm.h, prog_id)
+        else:
+            pkt, H, T, ing, rxq, eg = xdp
+            self.p = vm.lib.orc_proc_new_xdp(vm.h, prog_id, bytes(pkt), len(pkt), H, T, ing, rxq, eg)
         if not self.p:
             raise OracleError("no such program")
+
+    def step(self):
+        """Process.Step: (0 continue | -1 exited | status, err_pc)."""
+        e = C.c_int32(-1)
+        rc = self.vm.lib.orc_proc_step(self.p, C.byref(e))
+        return rc, e.value
+
+    def pc(self) -> int:
+        return self.vm.lib.orc_proc_get_pc(self.p)
+
+    def prog(self) -> int:
+        return self.vm.lib.orc_proc_get_prog(self.p)
 
     def set_cpu(self, c: int) -> int:
         return self.vm.lib.orc_proc_set_cpu(self.p, c)

@@ -12,6 +12,7 @@ if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 
 
+
 # JIT code objects live here for the session (and across sessions on the same machine); a fresh
 # GPU box starts empty and the `gpu` fixture fills it in parallel before the first GPU test
 JIT_CACHE = os.path.join(ROOT, ".jitcache")

@@ -133,3 +133,13 @@ def test_two_rank_hash_replicas_merge_to_single_process():
     assert len(want) > 1000
     for rank, got in res:
         assert got == want, rank
+
+
+def test_replica_overflow_is_detected():
+    import pytest
+
+    blobs = [D.replica_blob({bytes([i]) * 4: bytes(8) for i in range(3)}),
+             D.replica_blob({bytes([i]) * 4: bytes(8) for i in range(2, 6)})]
+    assert len(D.merge_records(blobs, 4, 8, max_entries=6)) == 6
+    with pytest.raises(D.ReplicaOverflow):
+        D.merge_records(blobs, 4, 8, max_entries=5)

@@ -1,0 +1,125 @@
+"""Process.Step (vm.go:291-340) on the device, instruction by instruction, against the oracle's
+Step: after every step the registers (PC, R0..R10), the current program and the exit / fatal
+state must be identical -- for the cfg-2 classifier, a BPF-to-BPF + tail-call program, and the
+error paths (fatal error, stepping a terminated process, Run after Step)."""
+import numpy as np
+import pytest
+
+import mimic_amd as M
+from harness import Scenario, build_engine, build_oracle, kernel_of
+from mimic_amd import asm as A
+from mimic_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def jit_kernels():
+    return []   # stepping runs on the interpreter
+
+
+def _trace(sc, entry, pkt, cpu, H=0, T=0, max_steps=500):
+    ovm, omids, opids = build_oracle(sc)
+    evm, emaps, epids = build_engine(sc)
+    from oracle.pyoracle import OracleProcess
+
+    o = OracleProcess(ovm, opids[entry], xdp=(pkt, H, T, 1, 0, 0))
+    if cpu >= 0:
+        assert o.set_cpu(cpu) == 0
+    e = evm.NewProcess(epids[entry], M.LinuxContextXDP(Packet=pkt, Headroom=H, Tailroom=T, IngessIfIndex=1))
+    if cpu >= 0:
+        e.SetCPUID(cpu)
+    n = 0
+    while True:
+        n += 1
+        rc, epc = o.step()
+        try:
+            exited = e.Step()
+            err = None
+        except M.MimicError as ex:
+            exited, err = True, ex
+        regs_o = [o.reg(r) for r in range(11)]
+        regs_e = [e.Registers.Get(r) for r in range(11)]
+        assert regs_e == regs_o, (n, regs_e, regs_o)
+        if rc > 0:
+            assert err is not None and M.STATUS_NAMES[e.Status] == M.STATUS_NAMES[rc], (n, e.Status, rc)
+            assert e.Registers.PC == epc, (n, e.Registers.PC, epc)
+            break
+        assert err is None, (n, err)
+        assert e.Registers.PC == o.pc(), (n, e.Registers.PC, o.pc())
+        assert e.ProgramID == o.prog(), n
+        if rc == -1:
+            assert exited
+            break
+        assert not exited, n
+        assert n < max_steps
+    pk = e.Packet()
+    o.cleanup()
+    e.Cleanup()
+    ovm.close()
+    evm.close()
+    return n, pk
+
+
+def test_step_trace_classifier(gpu):
+    p = W.prog_classifier()
+    sc = Scenario(vcpus=4, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    buf, off, lens = W.make_packets(8, seed=5)
+    for i in range(4):
+        pkt = bytes(buf[int(off[i]):int(off[i]) + int(lens[i])])
+        n, _ = _trace(sc, 0, pkt, cpu=i % 4)
+        assert n > 20
+
+
+def _calls_sc():
+    PA = dict(name="progs", type=3, key_size=4, value_size=4, max_entries=2)
+    main = [A.mov64_reg(6, 1), A.mov64_imm(1, 5), A.call_local("f"), A.mov64_reg(7, 0), A.mov64_reg(1, 6),
+            A.ld_map_fd(2, "progs"), A.mov64_imm(3, 0), A.call(A.FN_TAIL_CALL), A.mov64_imm(0, 99), A.exit_(),
+            "f", A.mov64_reg(0, 1), A.alu64("mul", 0, 3), A.st(8, 10, -8, 7), A.ldx(8, 2, 10, -8),
+            A.alu64("add", 0, 2, reg=True), A.exit_()]
+    leaf = [A.ldx(4, 2, 1, 0), A.ldx(1, 0, 2, 0), A.alu64("add", 0, 7, reg=True), A.exit_()]
+    return Scenario(vcpus=2, maps=[PA], progs=[("main", *A.assemble(main)), ("leaf", *A.assemble(leaf))],
+                    prog_array=[("progs", 0, 1)])
+
+
+def test_step_trace_bpf2bpf_and_tailcall(gpu):
+    n, _ = _trace(_calls_sc(), 0, bytes(range(1, 65)), cpu=1)
+    assert n > 15
+
+
+def test_step_fatal_error_then_terminated(gpu):
+    raw, _ = A.assemble([A.mov64_imm(0, 1), A.mov64_imm(2, 0), A.alu64("div", 0, 2, reg=True), A.exit_()])
+    sc = Scenario(vcpus=1, progs=[("d", raw, [])])
+    _trace(sc, 0, bytes(16), cpu=0)
+    evm, _, pids = build_engine(sc)
+    p = evm.NewProcess(pids[0], M.LinuxContextXDP(Packet=bytes(16)))
+    p.SetCPUID(0)
+    assert p.Step() is False and p.Step() is False
+    with pytest.raises(M.MimicError, match="PANIC_DIV0"):
+        p.Step()
+    assert p.Registers.PC == 2
+    with pytest.raises(M.MimicError, match="terminated"):
+        p.Step()
+    evm.close()
+
+
+def test_step_then_run_and_exit_again(gpu):
+    """A few Steps, then Run to the end: the same R0 and packet as one Run; stepping after a clean
+    exit reports exited again (the exit leaves PC on the EXIT instruction, vm.go:318-325)."""
+    p = W.prog_classifier()
+    sc = Scenario(vcpus=2, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    buf, off, lens = W.make_packets(2, seed=11)
+    pkt = bytes(buf[int(off[0]):int(off[0]) + int(lens[0])])
+    evm, maps, pids = build_engine(sc)
+    a = evm.NewProcess(pids[0], M.LinuxContextXDP(Packet=pkt))
+    a.SetCPUID(1)
+    for _ in range(5):
+        assert a.Step() is False
+    a.Run()
+    b = evm.NewProcess(pids[0], M.LinuxContextXDP(Packet=pkt))
+    b.SetCPUID(0)
+    b.Run()
+    assert a.Registers.R0 == b.Registers.R0 and a.Registers.R0 in (1, 2)
+    pc = a.Registers.PC
+    assert a.Step() is True and a.Registers.PC == pc
+    assert a.Packet() == pkt
+    evm.close()

@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 runs of one bench config into profiles/<tag>_pmc_<config>.json.
+
+Input (tools/profile.sh): under DIR, one rocprofv3 output directory per pass:
+  kt_<cfg>     --kernel-trace --stats            (kernel time)
+  fetch_<cfg>  --pmc FETCH_SIZE                  (HBM read bytes, KiB per dispatch)
+  write_<cfg>  --pmc WRITE_SIZE                  (HBM write bytes, KiB per dispatch)
+  sq_<cfg>     --pmc SQ_* + GRBM_GUI_ACTIVE      (instruction mix, VALU busy)
+Per-dispatch values are averaged over the dispatches of the engine's kernel.  FETCH_SIZE is
+also reported doubled (MI355X_MICROARCH.md: on gfx950 it counts 1/2 of wide streaming reads);
+`bytes_per_launch` = doubled FETCH + WRITE, an upper estimate for this kernel's mixed-width
+loads.  The summary is keyed to the kernel source hash, packets and vCPUs of the run, which is
+how bench.py finds it.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def col(r, *names):
+    for n in names:
+        if n in r:
+            return r[n]
+    raise KeyError(names)
+
+
+def counters(d, kernel):
+    """counter name -> mean over the kernel's dispatches of the per-dispatch value"""
+    per = {}
+    for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
+        if kernel not in col(r, "Kernel_Name", "Kernel-Name", "KernelName"):
+            continue
+        disp = col(r, "Dispatch_Id", "Dispatch-Id", "Correlation_Id")
+        name = col(r, "Counter_Name", "Counter-Name")
+        per.setdefault(name, {}).setdefault(disp, 0.0)
+        per[name][disp] += float(col(r, "Counter_Value", "Counter-Value"))
+    return {k: sum(v.values()) / len(v) for k, v in per.items() if v}
+
+
+def kernel_stats(d, kernel):
+    for r in rows(os.path.join(d, "**", "*kernel_stats.csv")):
+        if r.get("Name") == kernel:
+            return {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                    "max_ns": float(r["MaxNs"])}
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--dir", required=True)
+    ap.add_argument("--tag", default="r02")
+    ap.add_argument("--kernel", default="mimic_jit_kernel")
+    ap.add_argument("--packets", type=int, default=0)
+    ap.add_argument("--vcpus", type=int, default=0)
+    ap.add_argument("--out", default="")
+    ap.add_argument("--command", default="")
+    a = ap.parse_args()
+    import bench
+
+    cfg = bench.CONFIGS[a.config]
+    n = a.packets or cfg["packets"]
+    vcpus = a.vcpus or cfg.get("vcpus") or max(64, n // 4)
+    c = a.config
+    ks = kernel_stats(os.path.join(a.dir, f"kt_{c}"), a.kernel)
+    fetch = counters(os.path.join(a.dir, f"fetch_{c}"), a.kernel).get("FETCH_SIZE")
+    write = counters(os.path.join(a.dir, f"write_{c}"), a.kernel).get("WRITE_SIZE")
+    sq = counters(os.path.join(a.dir, f"sq_{c}"), a.kernel)
+    out = {"config": c, "round": a.tag, "kernel": a.kernel, "kernel_src_hash": bench.kernel_src_hash_of(c),
+           "packets": n, "vcpus": vcpus, "kernel_stats": ks}
+    if fetch is not None and write is not None:
+        out["fetch_size_kib_per_launch"] = fetch
+        out["write_size_kib_per_launch"] = write
+        out["raw_bytes_per_launch"] = int((fetch + write) * 1024)
+        out["bytes_per_launch"] = int((2 * fetch + write) * 1024)
+        out["correction"] = ("FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 FETCH_SIZE counts 1/2 of wide "
+                             "streaming reads); this kernel mixes 8-B and narrower loads, so true read bytes lie "
+                             "between the raw and the doubled value")
+    if sq:
+        out["sq_per_launch"] = sq
+        waves = sq.get("SQ_WAVES") or 0
+        if waves:
+            out["sq_per_wave"] = {k: v / waves for k, v in sq.items() if k.startswith("SQ_") and k != "SQ_WAVES"}
+        grbm = sq.get("GRBM_GUI_ACTIVE")
+        if grbm and "SQ_ACTIVE_INST_VALU" in sq:
+            # gfx94x VALUBusy formula (no gfx950 section in ROCm 7.2): SQ_ACTIVE_INST_VALU counts
+            # quad-cycles; 1024 SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs
+            out["valu_busy"] = round(sq["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (grbm / 8), 4)
+        if sq.get("SQ_WAVE_CYCLES"):
+            out["active_inst_frac_of_wave_cycles"] = round(sq.get("SQ_ACTIVE_INST_ANY", 0) / sq["SQ_WAVE_CYCLES"], 4)
+    if a.command:
+        out["command"] = a.command
+    path = a.out or os.path.join(ROOT, "profiles", f"{a.tag}_pmc_{c}.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out)[:600])
+
+
+if __name__ == "__main__":
+    main()
