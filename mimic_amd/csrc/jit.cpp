@@ -89,12 +89,20 @@ class Gen {
         // packet's result stores costs more than the couple of SGPRs spilled into VGPR lanes.
         const char *kq = getenv("MIMIC_JIT_KQ");
         kq_mode = kq ? atoi(kq) : 0;
+        // MIMIC_JIT_NT=1: non-temporal packet / descriptor / result accesses.  Measured slower on
+        // MI355X (cfg 2: 48 us vs 37 us per launch): a packet is read by several small loads, and
+        // evict-first lines make the later ones miss.
+        const char *ntv = getenv("MIMIC_JIT_NT");
+        nt = ntv && ntv[0] == '1';
         const char *ol = getenv("MIMIC_JIT_OPAQUE_LANE");
         opaque_lane = ol && ol[0] == '1';
         const char *cm = getenv("MIMIC_JIT_COLD");   // call | inline (default: by kernel size)
         cold_mode = !cm ? 0 : !strcmp(cm, "call") ? 1 : !strcmp(cm, "inline") ? 2 : 0;
+        // MIMIC_JIT_STAGE=1: stage each packet's first 64 bytes in LDS.  Measured slower on MI355X
+        // for every config (cfg 2: 74 us vs 37 us, cfg 3: 2.6 ms vs 1.2 ms per launch): the staging
+        // waits for all eight qwords before the first use, while direct loads hit L1 / L2 anyway.
         const char *sg = getenv("MIMIC_JIT_STAGE");
-        stage = !(sg && sg[0] == '0');
+        stage = sg && sg[0] == '1';
         for (auto &p : P)
             for (uint32_t i = 0; i < p.n; i++) {
                 const DInsn &x = p.ins[i];
@@ -127,10 +135,11 @@ class Gen {
     int cold_mode = 0;         // MIMIC_JIT_COLD: 0 auto, 1 call, 2 inline
     int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
+    bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
     bool cold_inline = true;   // the cold paths are inlined at every site (else called)
     uint32_t cold_sites = 0;
     static constexpr uint32_t kColdInlineSites = 48;
-    bool stage = true;         // MIMIC_JIT_STAGE=0: no LDS packet window
+    bool stage = false;        // MIMIC_JIT_STAGE=1: LDS packet window
     bool has_tail() const { return any_tail; }
     uint32_t ctx = CTX_XDP;    // the batch context this kernel is generated for
 
@@ -189,7 +198,7 @@ class Gen {
         E.line("  L.lane = g;");
         E.line("  L.cpu = lane_cpu(kp, g);");
         E.line("  uint32_t ex_begin = 0, ex_count = 0;");
-        E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = kp.sched_start[g]; ex_count = kp.sched_start[g + 1] - ex_begin; }");
+        E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = *gp(kp.sched_start + g); ex_count = *gp(kp.sched_start + g + 1) - ex_begin; }");
         E.line("  uint64_t lane_steps = 0;");
         E.line("  const uint32_t P = kp.static_next + kp.stack_size + 1;");
         if (ctx == CTX_SKB) E.line("  const uint32_t SK_ = P;   // the sk_buff entry (skb.h)");
@@ -211,7 +220,7 @@ class Gen {
         }
         E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
-        E.line("    else { if (j >= ex_count) break; i = kp.sched_pkts[ex_begin + j]; }");
+        E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
         if (ctx == CTX_SKB) {
             // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107, skb.h)
             E.line("    uint64_t r1 = 0;");
@@ -221,20 +230,25 @@ class Gen {
                 E.line("    const uint32_t W_ = ls_ ? 0u : win_stage(pwin_, tl_, L.pkt + SKB_HEADROOM, L.M - SKB_HEADROOM);");
         } else {
             // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
-            E.line("    const uint32_t H = kq_.headroom_arr ? kq_.headroom_arr[i] : kq_.headroom;");
-            E.line("    const uint32_t T = kq_.tailroom_arr ? kq_.tailroom_arr[i] : kq_.tailroom;");
-            E.line("    const uint32_t len = kq_.pkt_len[i];");
-            E.line("    L.pkt = kq_.pkt_data + kq_.pkt_off[i];");
+            E.line("    const uint32_t H = kq_.headroom_arr ? ld_nt(kq_.headroom_arr + i) : kq_.headroom;");
+            E.line("    const uint32_t T = kq_.tailroom_arr ? ld_nt(kq_.tailroom_arr + i) : kq_.tailroom;");
+            if (nt) {
+                E.line("    const uint32_t len = ld_nt(kq_.pkt_len + i);");
+                E.line("    L.pkt = kq_.pkt_data + ld_nt(kq_.pkt_off + i);");
+            } else {
+                E.line("    const uint32_t len = kq_.pkt_len[i];");
+                E.line("    L.pkt = kq_.pkt_data + kq_.pkt_off[i];");
+            }
             E.line("    L.M = H + len + T;");
             E.line("    L.pa = P;");
             E.line("    L.rec = nullptr;");
-            E.line("    for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;");
-            E.line("    for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;");
+            E.line("    for (uint32_t b = 0; b < H; b++) *gp(L.pkt + b) = 0;");
+            E.line("    for (uint32_t b = 0; b < T; b++) *gp(L.pkt + H + len + b) = 0;");
             E.line("    L.data = P + H;");
             E.line("    L.data_end = P + H + len;");
-            E.line("    L.ingress = (uint32_t)(kq_.ingress_arr ? kq_.ingress_arr[i] : kq_.ingress);");
-            E.line("    L.rxq = (uint32_t)(kq_.rxq_arr ? kq_.rxq_arr[i] : kq_.rxq);");
-            E.line("    L.egress = (uint32_t)(kq_.egress_arr ? kq_.egress_arr[i] : kq_.egress);");
+            E.line("    L.ingress = (uint32_t)(kq_.ingress_arr ? ld_nt(kq_.ingress_arr + i) : kq_.ingress);");
+            E.line("    L.rxq = (uint32_t)(kq_.rxq_arr ? ld_nt(kq_.rxq_arr + i) : kq_.rxq);");
+            E.line("    L.egress = (uint32_t)(kq_.egress_arr ? ld_nt(kq_.egress_arr + i) : kq_.egress);");
             if (stage && fast_paths) E.line("    const uint32_t W_ = win_stage(pwin_, tl_, L.pkt, L.M);");
             E.line("    uint64_t r1 = P + L.M + 1;");
         }
@@ -259,14 +273,19 @@ class Gen {
             E.line("    { const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else
             E.line("    {");
-        E.line("    if (kq_.r0) kq_.r0[i] = r0;");
-        E.line("    if (kq_.status) kq_.status[i] = (uint8_t)st_;");
-        E.line("    if (kq_.steps) kq_.steps[i] = steps;");
-        E.line("    if (kq_.err_pc) kq_.err_pc[i] = epc_;");
+        if (nt) {
+            E.line("    if (kq_.r0) st_nt(kq_.r0 + i, r0);");
+            E.line("    if (kq_.status) st_nt(kq_.status + i, (uint8_t)st_);");
+        } else {
+            E.line("    if (kq_.r0) kq_.r0[i] = r0;");
+            E.line("    if (kq_.status) kq_.status[i] = (uint8_t)st_;");
+        }
+        E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
+        E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
         E.line("    }");
         E.line("    lane_steps += steps;");
         E.line("  }");
-        E.line("  if (kp.lane_steps) kp.lane_steps[g] = lane_steps;");
+        E.line("  if (kp.lane_steps) st_nt(kp.lane_steps + g, lane_steps);");
         E.line("}");
         return E.s;
     }
@@ -408,7 +427,7 @@ class Gen {
                 const std::string wo = "(uint32_t)(ga_ - " + std::string(pa()) + " - " + std::to_string(wb()) + "u)";
                 f.push_back({"(uint64_t)" + wo + " + " + N + " <= W_", ord("win_load(pwin_, tl_, " + wo + ", " + N + ")", n), ""});
             }
-            f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord("ld_n(L.pkt + " + o + ", " + N + ")", n),
+            f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord(std::string(nt ? "ld_n_nt" : "ld_n") + "(L.pkt + " + o + ", " + N + ")", n),
                          "{ st_n(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
                              (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
             // the map value region the last lookup returned (translation cache, resolve()):

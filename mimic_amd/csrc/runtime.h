@@ -88,31 +88,61 @@ DEV int32_t lane_cpu(const KParams &kp, uint32_t g) {
 }
 
 // ---------------------------------------------------------------------------------------
-// raw loads / stores (unaligned accesses are legal on gfx950 global memory)
+// raw loads / stores (unaligned accesses are legal on gfx950 global memory).  Every engine
+// pointer (packets, arena, private memory, results) is global memory: the accesses are made
+// through the global address space so they compile to global_* instructions -- FLAT ones would
+// also count against lgkmcnt and make every LDS / scalar-load wait drain them too.
 // ---------------------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GAS __attribute__((address_space(1)))
+#else
+#define GAS
+#endif
+template <typename T>
+DEV GAS T *gp(T *p) { return (GAS T *)p; }
+template <typename T>
+DEV const GAS T *gp(const T *p) { return (const GAS T *)p; }
+
 DEV uint64_t ld_n(const uint8_t *p, uint32_t n) {
     switch (n) {
-    case 1: return *p;
-    case 2: return *(const u16u *)p;
-    case 4: return *(const u32u *)p;
-    case 8: return *(const u64u *)p;
+    case 1: return *gp(p);
+    case 2: return *(const GAS u16u *)p;
+    case 4: return *(const GAS u32u *)p;
+    case 8: return *(const GAS u64u *)p;
     default: {
         uint64_t v = 0;
-        for (uint32_t i = n; i-- > 0;) v = (v << 8) | p[i];
+        for (uint32_t i = n; i-- > 0;) v = (v << 8) | *gp(p + i);
         return v;
     }
     }
 }
 DEV void st_n(uint8_t *p, uint32_t n, uint64_t v) {
     switch (n) {
-    case 1: *p = (uint8_t)v; return;
-    case 2: *(u16u *)p = (uint16_t)v; return;
-    case 4: *(u32u *)p = (uint32_t)v; return;
-    case 8: *(u64u *)p = v; return;
+    case 1: *gp(p) = (uint8_t)v; return;
+    case 2: *(GAS u16u *)p = (uint16_t)v; return;
+    case 4: *(GAS u32u *)p = (uint32_t)v; return;
+    case 8: *(GAS u64u *)p = v; return;
     default:
-        for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * i));
+        for (uint32_t i = 0; i < n; i++) *gp(p + i) = (uint8_t)(v >> (8 * i));
     }
 }
+
+// Streaming accesses (packet bytes, descriptors, per-packet results) are each touched by one
+// process: non-temporal loads / stores keep them from evicting the lane-resident lines (per-CPU
+// map values, stack words) that later packets of the same vCPU reuse from L2.
+DEV uint64_t ld_n_nt(const uint8_t *p, uint32_t n) {
+    switch (n) {
+    case 1: return __builtin_nontemporal_load(gp(p));
+    case 2: return __builtin_nontemporal_load((const GAS u16u *)p);
+    case 4: return __builtin_nontemporal_load((const GAS u32u *)p);
+    case 8: return __builtin_nontemporal_load((const GAS u64u *)p);
+    default: return ld_n(p, n);
+    }
+}
+template <typename T>
+DEV T ld_nt(const T *p) { return __builtin_nontemporal_load(gp(p)); }
+template <typename T>
+DEV void st_nt(T *p, T v) { __builtin_nontemporal_store(v, gp(p)); }
 
 // private memory: byte offset o of lane l lives at priv + ((o>>3)*priv_lanes + l)*8 + (o&7)
 DEV uint8_t *priv_b(const KParams &kp, uint32_t lane, uint32_t o) {
@@ -121,7 +151,7 @@ DEV uint8_t *priv_b(const KParams &kp, uint32_t lane, uint32_t o) {
 DEV uint64_t priv_load(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n) {
     if ((o & 7) + n <= 8) return ld_n(priv_b(kp, lane, o), n);
     uint64_t v = 0;
-    for (uint32_t i = 0; i < n; i++) v |= (uint64_t)*priv_b(kp, lane, o + i) << (8 * i);
+    for (uint32_t i = 0; i < n; i++) v |= (uint64_t)*gp(priv_b(kp, lane, o + i)) << (8 * i);
     return v;
 }
 DEV void priv_store(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n, uint64_t v) {
@@ -129,7 +159,7 @@ DEV void priv_store(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n, ui
         st_n(priv_b(kp, lane, o), n, v);
         return;
     }
-    for (uint32_t i = 0; i < n; i++) *priv_b(kp, lane, o + i) = (uint8_t)(v >> (8 * i));
+    for (uint32_t i = 0; i < n; i++) *gp(priv_b(kp, lane, o + i)) = (uint8_t)(v >> (8 * i));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -149,14 +179,14 @@ DEV void stk_touch(const KParams &kp, Lane &L, uint32_t o) {
     if (o < STK_FINE) {
         const uint32_t q = o >> 3;
         if (!((L.sm0 >> q) & 1)) {
-            *(uint64_t *)priv_b(kp, L.lane, q << 3) = 0;
+            *gp((uint64_t *)priv_b(kp, L.lane, q << 3)) = 0;
             L.sm0 |= 1ull << q;
         }
     } else {
         const uint32_t c = (o - STK_FINE) >> kp.chunk_shift;
         if (!((L.sm1 >> c) & 1)) {
             const uint32_t q0 = (STK_FINE + (c << kp.chunk_shift)) >> 3, nq = (1u << kp.chunk_shift) >> 3;
-            for (uint32_t q = 0; q < nq; q++) *(uint64_t *)priv_b(kp, L.lane, (q0 + q) << 3) = 0;
+            for (uint32_t q = 0; q < nq; q++) *gp((uint64_t *)priv_b(kp, L.lane, (q0 + q) << 3)) = 0;
             L.sm1 |= 1ull << c;
         }
     }
@@ -169,7 +199,7 @@ DEV uint64_t stack_load(const KParams &kp, const Lane &L, uint32_t o, uint32_t n
     uint64_t v = 0;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t oo = o + i;
-        if (stk_valid(kp, L, oo)) v |= (uint64_t)*priv_b(kp, L.lane, oo) << (8 * i);
+        if (stk_valid(kp, L, oo)) v |= (uint64_t)*gp(priv_b(kp, L.lane, oo)) << (8 * i);
     }
     return v;
 }
@@ -178,7 +208,7 @@ DEV void stack_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_
         if (o < STK_FINE && !((L.sm0 >> (o >> 3)) & 1)) {
             // first write to this word: store the whole word, zero-extended around the value
             const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
-            *(uint64_t *)priv_b(kp, L.lane, o & ~7u) = (v & m) << (8 * (o & 7));
+            *gp((uint64_t *)priv_b(kp, L.lane, o & ~7u)) = (v & m) << (8 * (o & 7));
             L.sm0 |= 1ull << (o >> 3);
             return;
         }
@@ -189,7 +219,7 @@ DEV void stack_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t oo = o + i;
         stk_touch(kp, L, oo);
-        *priv_b(kp, L.lane, oo) = (uint8_t)(v >> (8 * i));
+        *gp(priv_b(kp, L.lane, oo)) = (uint8_t)(v >> (8 * i));
     }
 }
 
@@ -218,7 +248,7 @@ DEV void xdp_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t 
     if (!L.xdp_dirty) {
         for (uint32_t w = 0; w < 3; w++) {
             uint64_t q = (uint64_t)xdp_word(L, 2 * w) | ((uint64_t)xdp_word(L, 2 * w + 1) << 32);
-            *(uint64_t *)priv_b(kp, L.lane, (kp.priv_xdp_q + w) * 8) = q;
+            *gp((uint64_t *)priv_b(kp, L.lane, (kp.priv_xdp_q + w) * 8)) = q;
         }
         L.xdp_dirty = 1;
     }
@@ -979,7 +1009,7 @@ DEV uint32_t win_stage(PWin &w, uint32_t tl, const uint8_t *pkt, uint32_t M) {
     const uint32_t W = M >= PWIN_Q * 8 ? PWIN_Q * 8 : (M & ~7u);
 #pragma unroll
     for (uint32_t q = 0; q < PWIN_Q; q++)
-        if (q * 8 < W) w[q][tl] = *(const u64u *)(pkt + q * 8);
+        if (q * 8 < W) w[q][tl] = *(const GAS u64u *)(pkt + q * 8);
     return W;
 }
 // n bytes at offset o, o + n <= W
