@@ -317,20 +317,21 @@ def main():
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
-    # per-launch device time: HIP events on the stream the kernel runs on
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # device time of the timed region: two HIP events on the stream the kernels run on, around the
+    # K back-to-back launches (an event pair per launch would itself sit between the kernels)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.steps):
-        ev[k][0].record(stream)
         step()
-        ev[k][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    region_ms = ev0.elapsed_time(ev1)
     steps_per_batch = vm.LastSteps()
     st = res.status[:n].cpu().numpy()
     if ws > 1:
@@ -358,7 +359,7 @@ def main():
     if rank == 0:
         total_pkts = n * ws * args.steps
         value = total_pkts / elapsed / 1e6
-        avg_launch_s = float(np.mean(kern_ms)) / 1e3
+        avg_launch_s = region_ms / args.steps / 1e3   # per launch, gaps between launches included
         alg = algorithmic_bytes(wl.lens, vpg, wl.maps)
         achieved = alg / avg_launch_s
         kernel = "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel"

@@ -393,17 +393,41 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
 }
 
 // Sum of a per-CPU u64 array over cpus: out[k] = sum_c base[c*stride + 8k] (the "sum over CPUs"
-// readout of a per-CPU counter map).  Threads are laid out so that each owns one key k.
-extern "C" __global__ void mimic_sum_u64_kernel(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus,
-                                                uint64_t *out) {
-    const uint32_t T = gridDim.x * blockDim.x;
-    const uint32_t m = T / nvals;  // threads per key
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m * nvals) return;
-    const uint32_t k = t % nvals;
-    uint64_t s = 0;
-    for (uint32_t c = t / nvals; c < cpus; c += m) s += *(const uint64_t *)(base + (uint64_t)c * stride + 8ull * k);
-    atomicAdd((unsigned long long *)&out[k], (unsigned long long)s);
+// readout of a per-CPU counter map).  The per-CPU backings are contiguous ([cpu][key], stride =
+// E*8), so the values form one flat u64 array: for E <= 256 every thread walks it with a stride
+// that is a multiple of E, so it always adds the same key; the block reduces per key in LDS and
+// adds one partial per key to out (out is zeroed first).  For larger E a thread owns a key and
+// walks the cpus (consecutive threads read consecutive keys of a cpu).  No contended
+// per-element atomics: at most one atomic per (block, key).
+#define SUM_THREADS 256
+extern "C" __global__ __launch_bounds__(SUM_THREADS) void mimic_sum_u64_kernel(const uint64_t *base, uint64_t stride_q,
+                                                                              uint32_t nvals, uint32_t cpus,
+                                                                              uint64_t *out) {
+    __shared__ uint64_t part[SUM_THREADS];
+    const uint32_t t = threadIdx.x;
+    if (nvals <= SUM_THREADS && stride_q == nvals) {
+        const uint32_t per = SUM_THREADS / nvals * nvals;          // threads of a block that take part
+        const uint64_t total = (uint64_t)cpus * nvals;
+        const uint64_t step = (uint64_t)gridDim.x * per;
+        uint64_t acc = 0;
+        if (t < per)
+            for (uint64_t i = (uint64_t)blockIdx.x * per + t; i < total; i += step) acc += *gp(base + i);
+        part[t] = acc;
+        __syncthreads();
+        if (t < nvals) {
+            uint64_t s = 0;
+            for (uint32_t j = t; j < per; j += nvals) s += part[j];
+            atomicAdd((unsigned long long *)&out[t], (unsigned long long)s);
+        }
+        return;
+    }
+    // one thread per key, cpus walked in groups (blockIdx.y): strided backings, large E
+    const uint32_t k = blockIdx.x * SUM_THREADS + t;
+    if (k >= nvals) return;
+    const uint32_t groups = gridDim.y;
+    uint64_t acc = 0;
+    for (uint32_t c = blockIdx.y; c < cpus; c += groups) acc += *gp(base + (uint64_t)c * stride_q + k);
+    atomicAdd((unsigned long long *)&out[k], (unsigned long long)acc);
 }
 
 // One host-side hash-map operation (mimic_map_update/lookup/delete), run by the same device code
@@ -495,10 +519,21 @@ extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStrea
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st) {
     if (hipMemsetAsync(out, 0, (size_t)nvals * 8, st) != hipSuccess) return -1;
-    uint32_t threads = nvals * std::max(1u, std::min(cpus, 65536u / std::max(1u, nvals)));
-    threads = std::max(threads, nvals);
-    threads = (threads / nvals) * nvals;
-    const uint32_t blocks = (threads + 255) / 256;
-    hipLaunchKernelGGL(mimic_sum_u64_kernel, dim3(blocks), dim3(256), 0, st, base, stride, nvals, cpus, out);
+    if (!nvals || !cpus) return 0;
+    if ((stride & 7) || ((uintptr_t)base & 7)) return -1;
+    const uint64_t sq = stride / 8;
+    if (nvals <= SUM_THREADS && sq == nvals) {
+        const uint64_t total = (uint64_t)cpus * nvals;
+        // about 16 values per thread; at most 1024 blocks (= 1024 atomics per key)
+        const uint64_t per_block = (uint64_t)(SUM_THREADS / nvals * nvals) * 16;
+        const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (total + per_block - 1) / per_block));
+        hipLaunchKernelGGL(mimic_sum_u64_kernel, dim3(blocks), dim3(SUM_THREADS), 0, st, (const uint64_t *)base, sq, nvals,
+                           cpus, out);
+    } else {
+        const uint32_t kb = (nvals + SUM_THREADS - 1) / SUM_THREADS;
+        const uint32_t groups = std::max<uint32_t>(1, std::min<uint32_t>(cpus, std::max<uint32_t>(1, 2048 / kb)));
+        hipLaunchKernelGGL(mimic_sum_u64_kernel, dim3(kb, groups), dim3(SUM_THREADS), 0, st, (const uint64_t *)base, sq,
+                           nvals, cpus, out);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -424,6 +424,11 @@ class VM:
         self.programs.append(prog)
         return pid.value
 
+    def GetProcessPool(self) -> "ProcessPool":  # vm.go:79-81
+        if getattr(self, "_pool", None) is None:
+            self._pool = ProcessPool(self)
+        return self._pool
+
     def GetPrograms(self) -> List[ProgramSpec]:
         return list(self.programs)
 
@@ -894,3 +899,171 @@ class XDPResults:
         n = self.r0.numel() if n is None else n
         return {"r0": self.r0[:n].cpu().numpy().view(np.uint64), "status": self.status[:n].cpu().numpy(),
                 "steps": self.steps[:n].cpu().numpy().view(np.uint32), "err_pc": self.err_pc[:n].cpu().numpy()}
+
+
+# ---------------------------------------------------------------------------------------------
+# ProcessPool (vm.go:468-583) on the device
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class Context:
+    """The part of context.Context a job uses: cancellation and a deadline (time.monotonic())."""
+    Deadline: Optional[float] = None
+    Cancelled: bool = False
+
+    def Err(self) -> Optional[str]:
+        import time
+
+        if self.Cancelled:
+            return "context canceled"
+        if self.Deadline is not None and time.monotonic() >= self.Deadline:
+            return "context deadline exceeded"
+        return None
+
+
+@dataclass
+class ProcessPoolJob:  # vm.go:485-496
+    Process: "Process"
+    Context: Optional[Context] = None
+    Handoff: Optional[object] = None   # callable(process, err: Optional[Exception])
+
+
+class ProcessPool:
+    """processPool (vm.go:468-583) the GPU way.  The reference runs V worker goroutines, worker c
+    being vCPU c, each taking the next job off one channel and running it to completion.  Here one
+    dispatcher thread drains the backlog in micro-batches: it gives the jobs vCPUs round-robin (a
+    vCPU's jobs keep their enqueue order, so per-CPU map state is touched in order, the property
+    the reference's pool guarantees) and runs each batch as ONE device launch with the EXPLICIT
+    schedule -- thousands of vCPUs' processes at once instead of V goroutines.  Handoff callbacks
+    run on their own threads (the reference starts a goroutine per handoff); without one the
+    process is cleaned up."""
+
+    def __init__(self, vm: VM, max_batch: int = 1 << 16):
+        self.vm = vm
+        self.max_batch = max_batch
+        self._q = None
+        self._thread = None
+        self._next_cpu = 0
+
+    def Start(self, backlog: int) -> None:
+        import queue
+        import threading
+
+        if self._thread is not None:
+            raise MimicError("pool is already running")
+        if backlog < 1:
+            raise MimicError("backlog must be at least 1")
+        self._q = queue.Queue(maxsize=backlog)
+        self._thread = threading.Thread(target=self._dispatch, name="mimic-process-pool", daemon=True)
+        self._thread.start()
+
+    def Enqueue(self, job: ProcessPoolJob, noblock: bool = False) -> None:
+        import queue
+
+        if self._thread is None:
+            raise MimicError("pool is not yet running")
+        if noblock:
+            try:
+                self._q.put_nowait(job)
+            except queue.Full:
+                raise MimicError("backlog is full") from None
+        else:
+            self._q.put(job)
+
+    def Stop(self) -> None:
+        """All pending jobs complete; returns when the dispatcher has exited."""
+        if self._thread is None:
+            return
+        self._q.put(None)
+        self._thread.join()
+        self._thread = None
+        self._q = None
+
+    # ---- dispatcher ---------------------------------------------------------------------------
+    def _handoff(self, job: ProcessPoolJob, err: Optional[Exception]) -> None:
+        import threading
+
+        if job.Handoff is not None:
+            threading.Thread(target=job.Handoff, args=(job.Process, err), daemon=True).start()
+        else:
+            job.Process.Cleanup()
+
+    def _dispatch(self) -> None:
+        import queue
+
+        done = False
+        while not done:
+            first = self._q.get()
+            if first is None:
+                break
+            jobs = [first]
+            while len(jobs) < self.max_batch:
+                try:
+                    j = self._q.get_nowait()
+                except queue.Empty:
+                    break
+                if j is None:
+                    done = True
+                    break
+                jobs.append(j)
+            self._run(jobs)
+
+    def _run(self, jobs) -> None:
+        V = self.vm.settings.vcpus
+        groups: Dict[Tuple[int, bool], list] = {}
+        for job in jobs:
+            err = job.Context.Err() if job.Context is not None else None
+            if err is not None:
+                self._handoff(job, MimicError(err))
+                continue
+            job.Process.SetCPUID(self._next_cpu)
+            self._next_cpu = (self._next_cpu + 1) % V
+            skb = isinstance(job.Process.Context, LinuxContextSKBuff)
+            groups.setdefault((job.Process.prog_id, skb), []).append(job)
+        for (pid, skb), js in groups.items():
+            try:
+                self._launch(pid, skb, js)
+            except MimicError as ex:
+                for job in js:
+                    self._handoff(job, ex)
+                continue
+            for job in js:
+                p = job.Process
+                err = None
+                if p.Status:
+                    err = MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[p.Status]} at PC({p.ErrPC})")
+                self._handoff(job, err)
+
+    def _launch(self, pid: int, skb: bool, js) -> None:
+        dev = f"cuda:{self.vm.settings.device}"
+        ctxs = [j.Process.Context or LinuxContextXDP() for j in js]
+        cpus = [j.Process.cpuID for j in js]
+        if skb:
+            batch = SKBBatch.from_packets([c.Packet for c in ctxs], device=dev,
+                                          ifindex=ctxs[0].Dev.IFIndex if ctxs[0].Dev else 0,
+                                          schedule=L.SCHED_EXPLICIT, cpu=cpus)
+            res = self.vm.RunSKBBatch(pid, batch).numpy(len(js))
+            self.vm.SKBRelease()
+            hr = [SKBBatch.HEADROOM] * len(js)
+        else:
+            import numpy as np
+
+            hr = [c.Headroom for c in ctxs]
+            batch = XDPBatch.from_packets([c.Packet for c in ctxs], device=dev, headroom=np.array(hr, np.uint32),
+                                          tailroom=np.array([c.Tailroom for c in ctxs], np.uint32),
+                                          ingress=np.array([c.IngessIfIndex for c in ctxs], np.int32),
+                                          rxq=np.array([c.RxQueueIndex for c in ctxs], np.int32),
+                                          egress=np.array([c.EgressIfIndex for c in ctxs], np.int32),
+                                          schedule=L.SCHED_EXPLICIT, cpu=cpus)
+            res = self.vm.RunXDPBatch(pid, batch).numpy(len(js))
+        mem = batch.pkt_data.cpu().numpy()
+        offs = batch.pkt_off.cpu().numpy()
+        for k, j in enumerate(js):
+            p = j.Process
+            p.Registers.R0 = int(res["r0"][k]) & 0xFFFFFFFFFFFFFFFF
+            p.Steps = int(res["steps"][k])
+            p.Status = int(res["status"][k])
+            p.ErrPC = int(res["err_pc"][k])
+            c = ctxs[k]
+            tail = SKBBatch.TAILROOM if skb else c.Tailroom
+            o = int(offs[k])
+            p.PacketAfter = bytes(mem[o:o + hr[k] + len(c.Packet) + tail].tobytes())

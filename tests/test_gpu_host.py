@@ -61,3 +61,25 @@ def test_host_pipeline_packet_writeback(gpu):
         a, m = int(off[i]), 4 + int(lens[i]) + 2
         assert bytes(out[a:a + m]) == bytes(o["pkt"][a:a + m]), i
     vm.close()
+
+
+def test_pcap_to_host_pipeline(gpu):
+    """A captured pcap (mimic_amd.pcap) straight into mimic_run_xdp_host: the cfg-3 parser's
+    verdicts and per-CPU counters equal the oracle's over the same frames."""
+    import mimic_amd as M
+    from mimic_amd import pcap
+
+    b0, o0, l0 = W.make_packets(3000, **W.IMIX, seed=21)
+    data = pcap.write_pcap(pcap.batch_to_frames(b0, o0, l0))
+    buf, off, lens, _, _ = pcap.read_pcap(data)
+    p = W.prog_parse5()
+    V = 64
+    sc = Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    cpu = W.schedule_cpu(len(lens), V, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    vm, maps, pids = build_engine(sc)
+    r0, st = vm.RunXDPHost(pids[0], buf, off, lens, schedule=M.SCHED_INTERLEAVED, chunks=3)
+    assert np.array_equal(r0, o["r0"].astype(np.uint64)) and np.array_equal(st, o["status"].astype(np.uint8))
+    for c in range(V):
+        assert maps["flows"].Values(c) == o["maps"]["flows"][c]
+    vm.close()

@@ -17,7 +17,7 @@ def _prog_scenario(p: W.Program, vcpus: int) -> Scenario:
 def jit_kernels():
     ks = [kernel_of(_prog_scenario(p, 1)) for p in (W.prog_pass8(), W.prog_classifier(), W.prog_parse5())]
     ks += [kernel_of(_fuzz(s)[0]) for s in range(40)]
-    return ks + [kernel_of(_tailcall_sc()), kernel_of(_rewrite_sc()), kernel_of(_cpuid_sc())]
+    return ks + [kernel_of(_tailcall_sc()), kernel_of(_rewrite_sc()), kernel_of(_cpuid_sc()), kernel_of(_elf_sc())]
 
 
 def test_pass8(gpu):
@@ -220,4 +220,53 @@ def test_process_run_cpu_unset_and_V(gpu):
     assert p.Registers.R0 == 3
     with pytest.raises(M.MimicError):
         p.SetCPUID(4)
+    vm.close()
+
+
+def _elf_sc():
+    import os
+    import sys
+
+    from mimic_amd import elf
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from test_elf import OBJ, scenario_of
+
+    spec = elf.LoadCollectionSpec(OBJ)
+    return scenario_of(spec, ["xdp_count", "xdp_pass"])
+
+
+@pytest.mark.parametrize("exec_mode", ["jit", "interp"])
+def test_elf_object_on_the_engine(gpu, exec_mode):
+    """The committed ELF object (tests/golden/xdp_count.o) loaded through mimic_amd.elf runs on
+    the engine exactly like the oracle: BPF-to-BPF calls (with Q12), per-CPU map, .data datasec."""
+    sc = _elf_sc()
+    pk = [bytes([i % 256]) * (1 + i % 70) for i in range(300)] + [b""]
+    buf, off, lens = packets_to_buffer(pk)
+    cpu = (np.arange(len(pk)) % 4).astype(np.int32)
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu, exec_mode=exec_mode)
+    assert_same(o, e)
+    assert int(e["r0"][1]) == 0x1122334455667788 + 1
+
+
+@pytest.mark.parametrize("V,E", [(1000, 4), (64, 300), (7, 1)])
+def test_sum_u64_readout(gpu, V, E):
+    """mimic_map_sum_u64 (the sum-over-CPUs readout the multi-GPU all-reduce starts from) equals
+    the per-cpu Values summed on the host, for flat (E <= 256) and per-key (E > 256) layouts."""
+    emu = M.NewLinuxEmulator()
+    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(V))
+    m = M.LinuxPerCPUArrayMap(M.MapSpec("c", M.MapType.PerCPUArray, 4, 8, E))
+    emu.AddMap("c", m)
+    rng = np.random.default_rng(V * 7 + E)
+    want = np.zeros(E, np.uint64)
+    for _ in range(min(400, V * E)):
+        k, c = int(rng.integers(0, E)), int(rng.integers(0, V))
+        v = int(rng.integers(0, 1 << 62))
+        assert m.Update(k.to_bytes(4, "little"), v.to_bytes(8, "little"), 0, c) == 0
+    for c in range(V):
+        want += np.frombuffer(m.Values(c), np.uint64)
+    assert m.SumU64() == [int(x) for x in want]
+    assert m.SumU64(1, V) == [int(x) for x in want - np.frombuffer(m.Values(0), np.uint64)]
     vm.close()

@@ -1,0 +1,91 @@
+"""ProcessPool (vm.go:468-583) on the device: jobs enqueued from the host run in micro-batches,
+each a single launch; every job's R0 and status, and the per-CPU map state, equal the oracle
+running the jobs in enqueue order on the vCPUs the pool gave them."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import mimic_amd as M
+from harness import Scenario, build_engine, kernel_of, packets_to_buffer, run_oracle
+from mimic_amd import asm as A
+from mimic_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _sc(V):
+    p = W.prog_classifier()
+    return Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+
+
+def jit_kernels():
+    return [kernel_of(_sc(1))]
+
+
+@pytest.mark.parametrize("backlog", [16, 4096])
+def test_pool_runs_jobs_like_the_oracle(gpu, backlog):
+    V = 8
+    sc = _sc(V)
+    buf, off, lens = W.make_packets(1500, seed=17)
+    pk = [bytes(buf[int(o):int(o) + int(n)]) for o, n in zip(off, lens)]
+    vm, maps, pids = build_engine(sc)
+    pool = vm.GetProcessPool()
+    pool.Start(backlog)
+    got = {}
+    mu = threading.Lock()
+
+    def handoff(proc, err):
+        with mu:
+            got[proc.idx] = (proc.Registers.R0, proc.CPUID(), proc.Status, err)
+        proc.Cleanup()
+
+    for i, p in enumerate(pk):
+        proc = vm.NewProcess(pids[0], M.LinuxContextXDP(Packet=p))
+        proc.idx = i
+        pool.Enqueue(M.ProcessPoolJob(proc, None, handoff))
+    pool.Stop()
+    t0 = time.time()
+    while len(got) < len(pk) and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert len(got) == len(pk)
+    cpu = np.array([got[i][1] for i in range(len(pk))], np.int32)
+    assert set(cpu.tolist()) == set(range(V))
+    o = run_oracle(sc, *packets_to_buffer(pk), cpu)
+    assert [got[i][0] for i in range(len(pk))] == [int(x) for x in o["r0"]]
+    assert all(got[i][2] == 0 and got[i][3] is None for i in range(len(pk)))
+    for c in range(V):
+        assert maps["verdicts"].Values(c) == o["maps"]["verdicts"][c]
+    vm.close()
+
+
+def test_pool_api_rules_and_errors(gpu):
+    emu = M.NewLinuxEmulator()
+    vm = M.NewVM(M.VMOptEmulator(emu), M.VMOptSetvCPUs(2))
+    raw, _ = A.assemble([A.mov64_imm(0, 1), A.mov64_imm(2, 0), A.alu64("div", 0, 2, reg=True), A.exit_()])
+    pid = vm.AddProgram(M.ProgramSpec("div0", raw))
+    pool = vm.GetProcessPool()
+    with pytest.raises(M.MimicError, match="not yet running"):
+        pool.Enqueue(M.ProcessPoolJob(vm.NewProcess(pid, M.LinuxContextXDP(Packet=bytes(8)))))
+    with pytest.raises(M.MimicError, match="backlog"):
+        pool.Start(0)
+    pool.Start(2)
+    with pytest.raises(M.MimicError, match="already running"):
+        pool.Start(2)
+    errs = []
+    ev = threading.Event()
+
+    def handoff(proc, err):
+        errs.append(err)
+        if len(errs) == 2:
+            ev.set()
+
+    pool.Enqueue(M.ProcessPoolJob(vm.NewProcess(pid, M.LinuxContextXDP(Packet=bytes(8))), None, handoff))
+    pool.Enqueue(M.ProcessPoolJob(vm.NewProcess(pid, M.LinuxContextXDP(Packet=bytes(8))), M.Context(Cancelled=True),
+                                  handoff))
+    pool.Stop()
+    assert ev.wait(10)
+    msgs = sorted(str(e) for e in errs)
+    assert "context canceled" in msgs[0] and "PANIC_DIV0" in msgs[1]
+    vm.close()
