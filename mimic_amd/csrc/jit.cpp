@@ -94,6 +94,12 @@ class Gen {
         // evict-first lines make the later ones miss.
         const char *ntv = getenv("MIMIC_JIT_NT");
         nt = ntv && ntv[0] == '1';
+        const char *pfv = getenv("MIMIC_JIT_PREFETCH");   // 0: no descriptor prefetch
+        prefetch = !(pfv && pfv[0] == '0');
+        const char *fw = getenv("MIMIC_JIT_FWD");   // 0: no stack-store -> lookup key forwarding
+        forward = !(fw && fw[0] == '0');
+        const char *wv = getenv("MIMIC_JIT_WAVES");   // minimum waves per SIMD the register budget targets
+        if (wv) waves = atoi(wv);
         const char *ol = getenv("MIMIC_JIT_OPAQUE_LANE");
         opaque_lane = ol && ol[0] == '1';
         const char *cm = getenv("MIMIC_JIT_COLD");   // call | inline (default: by kernel size)
@@ -136,6 +142,9 @@ class Gen {
     int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
+    bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
+    int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
+    bool prefetch = true;      // MIMIC_JIT_PREFETCH=0: no next-packet descriptor prefetch
     bool cold_inline = true;   // the cold paths are inlined at every site (else called)
     uint32_t cold_sites = 0;
     static constexpr uint32_t kColdInlineSites = 48;
@@ -185,7 +194,11 @@ class Gen {
         // KParams is read through a pointer to a device copy: fields are loaded (scalar) where
         // they are used instead of all being preloaded into SGPRs from the kernarg segment
         // (which spills SGPRs and costs VGPRs / occupancy)
-        E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");
+        if (waves > 0)
+            E.line((std::string("extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(") + std::to_string(waves) +
+                   "))) void mimic_jit_kernel(const KParams *__restrict__ kpp) {").c_str());
+        else
+            E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");
         E.line("  const KParams &kp = *kpp;");
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
         E.line("  if (g >= kp.lanes) return;");
@@ -203,8 +216,26 @@ class Gen {
         E.line("  const uint32_t P = kp.static_next + kp.stack_size + 1;");
         if (ctx == CTX_SKB) E.line("  const uint32_t SK_ = P;   // the sk_buff entry (skb.h)");
         E.line("  uint32_t ga_ = 0;   // the address of the current memory access");
+        if (forward)
+            for (auto &p : P) analyze_fwd(p);
+        for (auto &f : fwd_store) E.line("  uint32_t fwd%u_%u_ = 0;   // value of the stack store at P%u slot %u", f.first, f.second, f.first, f.second);
+        // The packet loop is software-pipelined by one descriptor: packet j+1's index, offset and
+        // length are loaded while packet j runs (they travel with packet j's first loads), which
+        // takes one dependent HBM round trip off every packet after the first.
+        const bool pf = ctx == CTX_XDP && prefetch;
+        if (pf) {
+            E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
+            E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+        }
         E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
         E.line("    uint32_t i;");
+        E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
+        E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
+        E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
+        if (pf) {
+            E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
+            E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+        }
         // fields used once per packet are read through an opaque copy of the parameter pointer:
         // loaded where used instead of hoisted out of the packet loop into SGPRs
         if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
@@ -218,9 +249,6 @@ class Gen {
         } else if (stage && fast_paths) {
             E.line("    const uint32_t tl_ = tl0_;");
         }
-        E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
-        E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
-        E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
         if (ctx == CTX_SKB) {
             // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107, skb.h)
             E.line("    uint64_t r1 = 0;");
@@ -232,12 +260,15 @@ class Gen {
             // NewProcess + LinuxContextXDP.Load (vm.go:198-235, context_xdp_md.go:47-115)
             E.line("    const uint32_t H = kq_.headroom_arr ? ld_nt(kq_.headroom_arr + i) : kq_.headroom;");
             E.line("    const uint32_t T = kq_.tailroom_arr ? ld_nt(kq_.tailroom_arr + i) : kq_.tailroom;");
-            if (nt) {
+            if (pf) {
+                E.line("    const uint32_t len = plen_;");
+                E.line("    L.pkt = kq_.pkt_data + poff_;");
+            } else if (nt) {
                 E.line("    const uint32_t len = ld_nt(kq_.pkt_len + i);");
                 E.line("    L.pkt = kq_.pkt_data + ld_nt(kq_.pkt_off + i);");
             } else {
-                E.line("    const uint32_t len = kq_.pkt_len[i];");
-                E.line("    L.pkt = kq_.pkt_data + kq_.pkt_off[i];");
+                E.line("    const uint32_t len = *gp(kq_.pkt_len + i);");
+                E.line("    L.pkt = kq_.pkt_data + *gp(kq_.pkt_off + i);");
             }
             E.line("    L.M = H + len + T;");
             E.line("    L.pa = P;");
@@ -303,10 +334,9 @@ class Gen {
     static constexpr uint32_t SKB_HEADROOM_J = 32;
     bool any_tail = false, any_local = false, all_leaders = false;
     uint32_t blk_start = 0;   // first slot of the basic block being emitted
+    uint32_t cur_prog = 0;    // program being emitted
 
-    void program(const ProgView &p) {
-        if (p.n == 0) return;
-        ctx_hints(p);
+    std::vector<uint32_t> leaders(const ProgView &p) const {
         std::set<uint32_t> lead = {0};
         for (uint32_t i = 0; i < p.n; i++) {
             const DInsn &x = p.ins[i];
@@ -316,7 +346,65 @@ class Gen {
             if (ends_block(x) && i + 1 < p.n) lead.insert(i + 1);
             if (all_leaders) lead.insert(i);
         }
-        std::vector<uint32_t> L(lead.begin(), lead.end());
+        return std::vector<uint32_t>(lead.begin(), lead.end());
+    }
+
+    // Stack-store forwarding into helper 1's key (per basic block): which 4-byte store to
+    // R10 + c the key at R2 = R10 + c was written by, with no possibly-aliasing store between.
+    // Registers are tracked only as "R10 + constant"; a store through any other base clears it.
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> fwd_call;   // (prog, call slot) -> store slot
+    std::set<std::pair<uint32_t, uint32_t>> fwd_store;            // (prog, store slot) to capture
+    void analyze_fwd(const ProgView &p) {
+        if (!fast_paths || p.n == 0) return;
+        const std::vector<uint32_t> Lb = leaders(p);
+        for (size_t b = 0; b < Lb.size(); b++) {
+            const uint32_t s0 = Lb[b], e = b + 1 < Lb.size() ? Lb[b + 1] : p.n;
+            bool known[11] = {};
+            int64_t rel[11] = {};
+            known[10] = true;
+            std::map<int64_t, std::pair<uint32_t, uint32_t>> recs;   // offset -> (size, slot)
+            for (uint32_t i = s0; i < e; i++) {
+                const DInsn &x = p.ins[i];
+                const uint32_t h = AUX_H(x.aux), op = insn_op(x), d = insn_dst(x), sr = insn_src(x);
+                if (h == H_CALL && (uint32_t)x.k == 1 && known[2]) {
+                    auto it = recs.find(rel[2]);
+                    if (it != recs.end() && it->second.first == 4) {
+                        fwd_call[{p.id, i}] = it->second.second;
+                        fwd_store.insert({p.id, it->second.second});
+                    }
+                }
+                if (h == H_ST || h == H_STX) {
+                    const uint32_t n = AUX_SZ(x.aux);
+                    if (d <= 10 && known[d]) {
+                        const int64_t o = rel[d] + insn_off(x);
+                        for (auto it = recs.begin(); it != recs.end();) {
+                            if (it->first < o + (int64_t)n && o < it->first + (int64_t)it->second.first) it = recs.erase(it);
+                            else ++it;
+                        }
+                        recs[o] = {n, i};
+                    } else {
+                        recs.clear();
+                    }
+                }
+                if (h == H_ALU64 && op == 0xbf && sr <= 10 && known[sr]) {           // mov rD, (R10 + c)
+                    known[d] = true;
+                    rel[d] = rel[sr];
+                } else if (h == H_ALU64 && op == 0x07 && d <= 10 && known[d]) {      // add rD, imm
+                    rel[d] += (int64_t)(int32_t)(uint32_t)x.k;
+                } else if ((h == H_ALU64 || h == H_ALU32 || h == H_LDIMM || h == H_LDX || h == H_SLOW) && d <= 10) {
+                    known[d] = d == 10;
+                }
+                if (h == H_CALL) known[0] = false;
+                if (h == H_LDABS) for (int r = 0; r <= 5; r++) known[r] = false;
+            }
+        }
+    }
+
+    void program(const ProgView &p) {
+        if (p.n == 0) return;
+        ctx_hints(p);
+        cur_prog = p.id;
+        std::vector<uint32_t> L = leaders(p);
         for (int careful = 0; careful < (careful_copies ? 2 : 1); careful++) {
             for (size_t b = 0; b < L.size(); b++) {
                 const uint32_t s = L[b], e = b + 1 < L.size() ? L[b + 1] : p.n;
@@ -459,6 +547,7 @@ class Gen {
     }
 
     void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val) {
+        if (fwd_store.count({cur_prog, i})) E.line("    fwd%u_%u_ = (uint32_t)(%s);", cur_prog, i, val.c_str());
         E.line("    ga_ = %s;", addr(base, off).c_str());
         std::string pre = "    ";
         for (auto &f : fast_forms(base, n, val)) {
@@ -588,7 +677,12 @@ class Gen {
             const int64_t j = fast_paths ? r1_def(p, i) : -1;
             if (j >= 0) {  // inline array lookup when R1 is the map object the LD_IMM64 hint names
                 E.line("    { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", p.base + (uint32_t)j);
-                E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) COLD_CALL(cold_lookup(kp, sp_), %u); }", i);
+                auto f = fwd_call.find({p.id, i});
+                if (f != fwd_call.end())
+                    E.line("      if (!(mh_ && lookup_fast_k(kp, L, mh_ - 1u, r1, r2, r0, true, fwd%u_%u_))) COLD_CALL(cold_lookup(kp, sp_), %u); }",
+                           p.id, f->second, i);
+                else
+                    E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) COLD_CALL(cold_lookup(kp, sp_), %u); }", i);
             } else {
                 E.line("    COLD_CALL(cold_lookup(kp, sp_), %u);", i);
             }

@@ -103,6 +103,30 @@ DEV GAS T *gp(T *p) { return (GAS T *)p; }
 template <typename T>
 DEV const GAS T *gp(const T *p) { return (const GAS T *)p; }
 
+// index of the j-th packet lane g runs under the batch's schedule, or NO_PKT
+#define NO_PKT 0xffffffffu
+DEV uint32_t pkt_index(const KParams &kp, uint32_t g, uint32_t j, uint32_t ex_begin, uint32_t ex_count) {
+    if (j >= kp.per_lane) return NO_PKT;
+    if (kp.sched == SCHED_CHUNKED) {
+        const uint64_t ii = (uint64_t)g * kp.per_lane + j;
+        return ii < kp.n ? (uint32_t)ii : NO_PKT;
+    }
+    if (kp.sched == SCHED_INTERLEAVED) {
+        const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift);
+        return ii < kp.n ? (uint32_t)ii : NO_PKT;
+    }
+    return j < ex_count ? *(const GAS uint32_t *)(kp.sched_pkts + ex_begin + j) : NO_PKT;
+}
+
+// the packet after packet i (the j-th of lane g) under the schedule: the chunked and
+// interleaved schedules step by 1 and by the lane count
+DEV uint32_t pkt_next(const KParams &kp, uint32_t i, uint32_t j, uint32_t ex_begin, uint32_t ex_count) {
+    if (j >= kp.per_lane) return NO_PKT;
+    if (kp.sched == SCHED_EXPLICIT) return j < ex_count ? *(const GAS uint32_t *)(kp.sched_pkts + ex_begin + j) : NO_PKT;
+    const uint64_t ii = (uint64_t)i + (kp.sched == SCHED_CHUNKED ? 1u : kp.lanes);
+    return ii < kp.n ? (uint32_t)ii : NO_PKT;
+}
+
 DEV uint64_t ld_n(const uint8_t *p, uint32_t n) {
     switch (n) {
     case 1: return *gp(p);
@@ -845,7 +869,10 @@ COLD void cold_adjust_tail(const KParams &kp, Spill &S) {
 // slot that set R1; checked here, so a wrong hint only costs the slow path) and the 4-byte
 // key lies on the stack.  Then regToMap, derefMapKey and LinuxArrayMap.Lookup reduce to the
 // lines below.  Returns false when the case does not apply (the caller runs cold_lookup).
-DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint64_t r2, uint64_t &r0) {
+// fwd_key: the key's 4 bytes when the JIT knows them from a store earlier in the basic block
+// (the stack store itself is still made; the lookup just does not wait for it to read it back)
+DEV bool lookup_fast_k(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint64_t r2, uint64_t &r0, bool fwd,
+                       uint32_t fwd_key) {
     const DMap m = cget(kp.maps, mid);
     if ((uint32_t)r1 != m.obj_addr || m.key_size != 4) return false;
     if (m.family != FAM_ARRAY && m.family != FAM_PERCPU_ARRAY) return false;
@@ -856,7 +883,7 @@ DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint
         if (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu) return false;   // error path: cold
         which = L.cpu;
     }
-    const uint32_t k = (uint32_t)stack_load(kp, L, ko, 4);
+    const uint32_t k = fwd ? fwd_key : (uint32_t)stack_load(kp, L, ko, 4);
     r0 = array_value_addr(m, which, k);
     if (r0) {
         L.t_lo = m.backing_addr + (which > 0 ? (uint32_t)which * m.addr_period : 0u);
@@ -864,6 +891,9 @@ DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint
         L.t_ptr = array_value_ptr(kp, m, which, 0);
     }
     return true;
+}
+DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint64_t r2, uint64_t &r0) {
+    return lookup_fast_k(kp, L, mid, r1, r2, r0, false, 0);
 }
 
 // ---------------------------------------------------------------------------------------
