@@ -262,9 +262,10 @@ int mimic_sync(mimic_vm *vm, void *hip_stream);
 int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out);
 
 /* Host-resident batches: packets start and end in host memory (captured pcap, ctx JSON, NIC
- * buffers).  The engine pipelines the batch in sub-batches: H2D of packet bytes + descriptors,
- * the kernel, D2H of r0/status (and of the packet memory when pkt_out is set), on separate
- * streams so that copies overlap kernels.  vCPU assignment is that of the whole batch.
+ * buffers).  The engine pipelines the batch in sub-batches: H2D of the sub-batch's descriptors,
+ * packet window and launch parameters, the kernel, D2H of r0/status (and of the packet memory
+ * when pkt_out is set), on separate streams so that copies overlap kernels.  vCPU assignment is
+ * that of the whole batch.  pkt_out needs each sub-batch's packets ascending and non-overlapping.
  * Host memory should be pinned (mimic_host_register) for the copies to run asynchronously. */
 typedef struct {
     uint32_t n;
@@ -281,7 +282,7 @@ typedef struct {
     uint64_t *r0;                 /* host, [n] */
     uint8_t *status;              /* host, [n] */
 } mimic_xdp_host_batch;
-/* chunks = number of sub-batches (0: about 16 MiB of packet memory each) */
+/* chunks = number of sub-batches (0: about 8 MiB of packet memory each) */
 int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks);
 /* Pin / unpin host memory for DMA (hipHostRegister / hipHostUnregister). */
 int mimic_host_register(void *p, size_t bytes);

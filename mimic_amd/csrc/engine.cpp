@@ -101,18 +101,22 @@ struct mimic_vm {
     int kp_next = 0, kp_last = -1;
     hipStream_t kp_last_stream = nullptr;
     // host-resident pipeline (mimic_run_xdp_host): NB rotating device staging slots
-    static constexpr int NB = 3;
+    // (packet window, its descriptors, its results); launch parameters are copied on the H2D
+    // stream too (kp_copy_stream), so no copy ever queues on the compute stream
+    static constexpr int NB = 4;
     struct Slot {
         uint8_t *buf = nullptr;
+        uint64_t *off = nullptr;
+        uint32_t *len = nullptr;
         uint64_t *r0 = nullptr;
         uint8_t *st = nullptr;
+        size_t cap_bytes = 0, cap_n = 0;
         hipEvent_t e_in = nullptr, e_k = nullptr, e_out = nullptr;
         bool used = false;
     } slot[NB];
-    size_t hp_cap_bytes = 0, hp_cap_n = 0, hp_cap_desc = 0;
-    uint64_t *hp_off = nullptr;   // whole-batch descriptors (one copy each per batch)
-    uint32_t *hp_len = nullptr;
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    hipStream_t kp_copy_stream = nullptr;
+    hipEvent_t kp_copy_ev = nullptr;
     // sk_buff batches (skb.h): per-packet records, footprints, their prefix, scan scratch, and
     // the device word pair {next leak address, this batch's leak base}
     SkbRec *d_skb_rec = nullptr;
@@ -155,7 +159,13 @@ static int kp_slot(mimic_vm *vm, const KParams &kp, hipStream_t st, const KParam
         vm->kp_next = (slot + 1) % mimic_vm::KP_SLOTS;
         if (vm->kp_used[slot]) HIP_OK(vm, hipEventSynchronize(vm->kp_ev[slot]));  // its last kernel is done
         vm->h_kp[slot] = kp;
-        HIP_OK(vm, hipMemcpyAsync(vm->d_kp + slot, vm->h_kp + slot, sizeof kp, hipMemcpyHostToDevice, st));
+        if (vm->kp_copy_stream) {   // the host pipeline: behind the sub-batch's own copies
+            HIP_OK(vm, hipMemcpyAsync(vm->d_kp + slot, vm->h_kp + slot, sizeof kp, hipMemcpyHostToDevice, vm->kp_copy_stream));
+            HIP_OK(vm, hipEventRecord(vm->kp_copy_ev, vm->kp_copy_stream));
+            HIP_OK(vm, hipStreamWaitEvent(st, vm->kp_copy_ev, 0));
+        } else {
+            HIP_OK(vm, hipMemcpyAsync(vm->d_kp + slot, vm->h_kp + slot, sizeof kp, hipMemcpyHostToDevice, st));
+        }
         vm->kp_last = slot;
         vm->kp_last_stream = st;
     }
@@ -532,13 +542,14 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (vm->h_kp) hipHostFree(vm->h_kp);
     for (auto &sl : vm->slot) {
         hipFree(sl.buf);
+        hipFree(sl.off);
+        hipFree(sl.len);
         hipFree(sl.r0);
         hipFree(sl.st);
         for (hipEvent_t e : {sl.e_in, sl.e_k, sl.e_out})
             if (e) hipEventDestroy(e);
     }
-    hipFree(vm->hp_off);
-    hipFree(vm->hp_len);
+    if (vm->kp_copy_ev) hipEventDestroy(vm->kp_copy_ev);
     hipFree(vm->d_skb_rec);
     hipFree(vm->d_skb_foot);
     hipFree(vm->d_skb_prefix);
@@ -1571,6 +1582,53 @@ int mimic_host_unregister(void *p) {
     return hipHostUnregister(p) == hipSuccess ? 0 : MIMIC_EDEVICE;
 }
 
+// Sub-batch c: its host byte window [lo, hi) (packets need not be in order) and whether its
+// packets are ascending and non-overlapping (pkt_out copies the window back as one block).
+struct HostWindow {
+    uint64_t lo = ~0ull, hi = 0;
+    bool ascending = true;
+};
+static HostWindow host_window(const mimic_xdp_host_batch *hb, uint32_t a, uint32_t m, uint64_t room) {
+    HostWindow w;
+    uint64_t prev_end = 0;
+    for (uint32_t i = a; i < a + m; i++) {
+        const uint64_t o = hb->pkt_off[i], e = o + hb->pkt_len[i] + room;
+        w.lo = std::min(w.lo, o);
+        w.hi = std::max(w.hi, e);
+        if (i > a && o < prev_end) w.ascending = false;
+        prev_end = e;
+    }
+    return w;
+}
+
+static int slot_reserve(mimic_vm *vm, mimic_vm::Slot &sl, size_t bytes, size_t n) {
+    if (bytes <= sl.cap_bytes && n <= sl.cap_n) return 0;
+    if (sl.used) HIP_OK(vm, hipEventSynchronize(sl.e_out));   // its last sub-batch is done
+    if (bytes > sl.cap_bytes) {
+        hipFree(sl.buf);
+        sl.buf = nullptr;
+        sl.cap_bytes = std::max(bytes, sl.cap_bytes + sl.cap_bytes / 2);
+        HIP_OK(vm, hipMalloc(&sl.buf, sl.cap_bytes));
+    }
+    if (n > sl.cap_n) {
+        for (void *q : {(void *)sl.off, (void *)sl.len, (void *)sl.r0, (void *)sl.st}) hipFree(q);
+        sl.off = nullptr;
+        sl.len = nullptr;
+        sl.r0 = nullptr;
+        sl.st = nullptr;
+        sl.cap_n = std::max(n, sl.cap_n + sl.cap_n / 2);
+        HIP_OK(vm, hipMalloc(&sl.off, 8 * sl.cap_n));
+        HIP_OK(vm, hipMalloc(&sl.len, 4 * sl.cap_n));
+        HIP_OK(vm, hipMalloc(&sl.r0, 8 * sl.cap_n));
+        HIP_OK(vm, hipMalloc(&sl.st, sl.cap_n));
+    }
+    return 0;
+}
+
+// Sub-batch pipeline over NB staging slots.  Per sub-batch, on the H2D stream: its descriptors,
+// its packet window and its launch parameters; the kernel on the VM stream after them; its r0 /
+// status (and packet bytes) on the D2H stream after the kernel.  The host-side scan of sub-batch
+// c + 1 runs while sub-batch c's copies are in flight, so no O(n) pass precedes the first copy.
 int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks) {
     if (!vm || !hb) return MIMIC_EINVAL;
     const uint32_t n = hb->n;
@@ -1579,28 +1637,12 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
         return fail(vm, MIMIC_EINVAL, "missing host arrays");
     hipSetDevice(vm->s.device);
     const uint64_t room = (uint64_t)hb->headroom_all + hb->tailroom_all;
-    if (chunks == 0) {  // auto: ~16 MiB of packet memory per sub-batch (copies of that size run at link rate)
-        uint64_t bytes = 0;
-        for (uint32_t i = 0; i < n; i++) bytes += hb->pkt_len[i] + room;
-        chunks = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(2, bytes >> 24));
+    if (chunks == 0) {  // auto: ~8 MiB of packet memory per sub-batch, estimated from the batch's ends
+        const uint64_t first = hb->pkt_off[0], last = hb->pkt_off[n - 1] + hb->pkt_len[n - 1] + room;
+        const uint64_t bytes = last > first ? last - first : (uint64_t)n * (room + 1500);
+        chunks = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(2, bytes >> 23));
     }
     chunks = std::max<uint32_t>(1, std::min(chunks, n));
-    // per sub-batch: the host byte window [lo, hi) holding its packets
-    std::vector<uint32_t> bnd(chunks + 1);
-    for (uint32_t c = 0; c <= chunks; c++) bnd[c] = (uint32_t)((uint64_t)n * c / chunks);
-    std::vector<uint64_t> lo(chunks, ~0ull), hi(chunks, 0);
-    size_t max_bytes = 0, max_n = 0;
-    bool ascending = true;
-    for (uint32_t c = 0; c < chunks; c++) {
-        for (uint32_t i = bnd[c]; i < bnd[c + 1]; i++) {
-            lo[c] = std::min<uint64_t>(lo[c], hb->pkt_off[i]);
-            hi[c] = std::max<uint64_t>(hi[c], hb->pkt_off[i] + hb->pkt_len[i] + room);
-            if (i && hb->pkt_off[i] < hb->pkt_off[i - 1] + hb->pkt_len[i - 1] + room) ascending = false;
-        }
-        max_bytes = std::max<size_t>(max_bytes, hi[c] - lo[c]);
-        max_n = std::max<size_t>(max_n, bnd[c + 1] - bnd[c]);
-    }
-    if (hb->pkt_out && !ascending) return fail(vm, MIMIC_EINVAL, "pkt_out needs ascending, non-overlapping packets");
     // CHUNKED over the whole batch = EXPLICIT with cpu(i) = vcpu_begin + i / ceil(n / lanes)
     std::vector<int32_t> cpu_chunked;
     uint32_t sched = hb->schedule;
@@ -1617,53 +1659,37 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
     if (!vm->s_h2d) {
         HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_h2d, hipStreamNonBlocking));
         HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_d2h, hipStreamNonBlocking));
+        HIP_OK(vm, hipEventCreateWithFlags(&vm->kp_copy_ev, hipEventDisableTiming));
         for (auto &sl : vm->slot)
             for (hipEvent_t *e : {&sl.e_in, &sl.e_k, &sl.e_out}) HIP_OK(vm, hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
-    if (n > vm->hp_cap_desc) {
-        HIP_OK(vm, hipDeviceSynchronize());
-        hipFree(vm->hp_off);
-        hipFree(vm->hp_len);
-        vm->hp_off = nullptr;
-        vm->hp_len = nullptr;
-        HIP_OK(vm, hipMalloc(&vm->hp_off, 8ull * n));
-        HIP_OK(vm, hipMalloc(&vm->hp_len, 4ull * n));
-        vm->hp_cap_desc = n;
-    }
-    if (max_bytes > vm->hp_cap_bytes || max_n > vm->hp_cap_n) {
-        HIP_OK(vm, hipDeviceSynchronize());
-        for (auto &sl : vm->slot) {
-            hipFree(sl.buf);
-            hipFree(sl.r0);
-            hipFree(sl.st);
-            HIP_OK(vm, hipMalloc(&sl.buf, std::max<size_t>(max_bytes, 1)));
-            HIP_OK(vm, hipMalloc(&sl.r0, max_n * 8));
-            HIP_OK(vm, hipMalloc(&sl.st, max_n));
-            sl.used = false;
-        }
-        vm->hp_cap_bytes = max_bytes;
-        vm->hp_cap_n = max_n;
-    }
-    // descriptors of the whole batch first (two copies), then one packet-bytes copy per sub-batch;
-    // the previous batch's kernels may still read hp_off / hp_len
-    for (auto &sl : vm->slot)
-        if (sl.used) HIP_OK(vm, hipStreamWaitEvent(vm->s_h2d, sl.e_k, 0));
-    HIP_OK(vm, hipMemcpyAsync(vm->hp_off, hb->pkt_off, 8ull * n, hipMemcpyHostToDevice, vm->s_h2d));
-    HIP_OK(vm, hipMemcpyAsync(vm->hp_len, hb->pkt_len, 4ull * n, hipMemcpyHostToDevice, vm->s_h2d));
+    struct CopyStreamScope {   // launch parameters go on the H2D stream for this call only
+        mimic_vm *vm;
+        ~CopyStreamScope() { vm->kp_copy_stream = nullptr; }
+    } scope{vm};
     for (uint32_t c = 0; c < chunks; c++) {
         auto &sl = vm->slot[c % mimic_vm::NB];
-        const uint32_t a = bnd[c], m = bnd[c + 1] - bnd[c];
+        const uint32_t a = (uint32_t)((uint64_t)n * c / chunks), m = (uint32_t)((uint64_t)n * (c + 1) / chunks) - a;
         if (m == 0) continue;
+        const HostWindow w = host_window(hb, a, m, room);
+        if (hb->pkt_out && !w.ascending) {
+            hipStreamSynchronize(vm->s_d2h);
+            return fail(vm, MIMIC_EINVAL, "pkt_out needs ascending, non-overlapping packets (sub-batch %u)", c);
+        }
+        int rc = slot_reserve(vm, sl, std::max<uint64_t>(w.hi - w.lo, 1), m);
+        if (rc) return rc;
         if (sl.used) HIP_OK(vm, hipStreamWaitEvent(vm->s_h2d, sl.e_out, 0));  // the slot's last D2H is done
-        HIP_OK(vm, hipMemcpyAsync(sl.buf, hb->pkt_data + lo[c], hi[c] - lo[c], hipMemcpyHostToDevice, vm->s_h2d));
+        HIP_OK(vm, hipMemcpyAsync(sl.off, hb->pkt_off + a, 8ull * m, hipMemcpyHostToDevice, vm->s_h2d));
+        HIP_OK(vm, hipMemcpyAsync(sl.len, hb->pkt_len + a, 4ull * m, hipMemcpyHostToDevice, vm->s_h2d));
+        HIP_OK(vm, hipMemcpyAsync(sl.buf, hb->pkt_data + w.lo, w.hi - w.lo, hipMemcpyHostToDevice, vm->s_h2d));
         HIP_OK(vm, hipEventRecord(sl.e_in, vm->s_h2d));
         HIP_OK(vm, hipStreamWaitEvent(vm->stream, sl.e_in, 0));
         mimic_xdp_batch b{};
         b.n = m;
         b.schedule = sched;
-        b.pkt_data = sl.buf - lo[c];  // offsets stay those of the host batch
-        b.pkt_off = vm->hp_off + a;
-        b.pkt_len = vm->hp_len + a;
+        b.pkt_data = sl.buf - w.lo;  // offsets stay those of the host batch
+        b.pkt_off = sl.off;
+        b.pkt_len = sl.len;
         b.headroom_all = hb->headroom_all;
         b.tailroom_all = hb->tailroom_all;
         b.ingress_all = hb->ingress_all;
@@ -1674,16 +1700,15 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
         mimic_xdp_results r{};
         r.r0 = sl.r0;
         r.status = sl.st;
-        int rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a);
+        vm->kp_copy_stream = vm->s_h2d;
+        rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a);
+        vm->kp_copy_stream = nullptr;
         if (rc) return rc;
         HIP_OK(vm, hipEventRecord(sl.e_k, vm->stream));
         HIP_OK(vm, hipStreamWaitEvent(vm->s_d2h, sl.e_k, 0));
         HIP_OK(vm, hipMemcpyAsync(hb->r0 + a, sl.r0, 8ull * m, hipMemcpyDeviceToHost, vm->s_d2h));
         HIP_OK(vm, hipMemcpyAsync(hb->status + a, sl.st, m, hipMemcpyDeviceToHost, vm->s_d2h));
-        if (hb->pkt_out) {
-            const uint64_t plo = hb->pkt_off[a], phi = hb->pkt_off[a + m - 1] + hb->pkt_len[a + m - 1] + room;
-            HIP_OK(vm, hipMemcpyAsync(hb->pkt_out + plo, sl.buf + (plo - lo[c]), phi - plo, hipMemcpyDeviceToHost, vm->s_d2h));
-        }
+        if (hb->pkt_out) HIP_OK(vm, hipMemcpyAsync(hb->pkt_out + w.lo, sl.buf, w.hi - w.lo, hipMemcpyDeviceToHost, vm->s_d2h));
         HIP_OK(vm, hipEventRecord(sl.e_out, vm->s_d2h));
         sl.used = true;
     }

@@ -98,6 +98,10 @@ class Gen {
         prefetch = !(pfv && pfv[0] == '0');
         const char *fw = getenv("MIMIC_JIT_FWD");   // 0: no stack-store -> lookup key forwarding
         forward = !(fw && fw[0] == '0');
+        const char *nr = getenv("MIMIC_JIT_NTRES");   // 1: per-packet results stored non-temporal
+        ntres = nr && nr[0] == '1';
+        const char *spv = getenv("MIMIC_JIT_SPEC");   // 0: no early packet loads
+        if (spv) speculate = atoi(spv);
         const char *wv = getenv("MIMIC_JIT_WAVES");   // minimum waves per SIMD the register budget targets
         if (wv) waves = atoi(wv);
         const char *ol = getenv("MIMIC_JIT_OPAQUE_LANE");
@@ -142,6 +146,8 @@ class Gen {
     int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
+    int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
+    bool ntres = false;        // MIMIC_JIT_NTRES=1: r0 / status stores non-temporal
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
     bool prefetch = true;      // MIMIC_JIT_PREFETCH=0: no next-packet descriptor prefetch
@@ -219,6 +225,11 @@ class Gen {
         if (forward)
             for (auto &p : P) analyze_fwd(p);
         for (auto &f : fwd_store) E.line("  uint32_t fwd%u_%u_ = 0;   // value of the stack store at P%u slot %u", f.first, f.second, f.first, f.second);
+        if (speculate && fast_paths && !stage && ctx == CTX_XDP && !all_leaders)
+            for (auto &p : P) analyze_spec(p);
+        for (auto &u : spec_use)
+            E.line("  %s sp%u_%u_ = 0;   // packet load of P%u slot %u, issued early", u.second == 8 ? "uint64_t" : "uint32_t",
+                   u.first.first, u.first.second, u.first.first, u.first.second);
         // The packet loop is software-pipelined by one descriptor: packet j+1's index, offset and
         // length are loaded while packet j runs (they travel with packet j's first loads), which
         // takes one dependent HBM round trip off every packet after the first.
@@ -304,12 +315,12 @@ class Gen {
             E.line("    { const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else
             E.line("    {");
-        if (nt) {
+        if (nt || ntres) {
             E.line("    if (kq_.r0) st_nt(kq_.r0 + i, r0);");
             E.line("    if (kq_.status) st_nt(kq_.status + i, (uint8_t)st_);");
         } else {
-            E.line("    if (kq_.r0) kq_.r0[i] = r0;");
-            E.line("    if (kq_.status) kq_.status[i] = (uint8_t)st_;");
+            E.line("    if (kq_.r0) *gp(kq_.r0 + i) = r0;");
+            E.line("    if (kq_.status) *gp(kq_.status + i) = (uint8_t)st_;");
         }
         E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
         E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
@@ -400,6 +411,98 @@ class Gen {
         }
     }
 
+    // Early packet loads.  A "region" is a run of basic blocks entered only at its first block:
+    // every later block's only predecessor is the fall-through from the block before it.  A
+    // packet load in a region whose base register is not written, and with no store, call or
+    // other memory-changing slot, between an earlier point of the region and the load is issued
+    // at that point (into sp<prog>_<slot>_), ahead of the branches in between: the loads of
+    // several headers then travel together instead of one round trip per basic block.  The
+    // early load reads only the packet memory [P, P + M) of the lane (the same bounds test as
+    // the fast path); the load itself still runs its full test and uses the early value only
+    // when that test passes, so results never change.
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> spec_use;                  // (prog, load slot) -> size
+    std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> spec_at;     // (prog, slot) -> loads issued before it
+    void analyze_spec(const ProgView &p) {
+        if (p.n == 0) return;
+        ctx_hints(p);
+        const std::vector<uint32_t> Lb = leaders(p);
+        std::vector<uint32_t> preds(p.n + 1, 0);
+        std::vector<bool> special(p.n + 1, false);
+        special[0] = true;
+        for (uint32_t i = 0; i < p.n; i++) {
+            const DInsn &x = p.ins[i];
+            const uint32_t h = AUX_H(x.aux);
+            if ((h == H_JA || h == H_JCC || h == H_CALL_LOCAL) && (x.aux & AUX_JT_OK)) {
+                const int64_t t = jump_target(x, i);
+                if (t >= 0 && t <= (int64_t)p.n) {
+                    preds[t]++;
+                    if (h == H_CALL_LOCAL) special[t] = true;
+                }
+            }
+            if (h == H_CALL_LOCAL) special[i + 1] = true;   // return site
+            if ((!ends_block(x) || h == H_JCC || (h == H_CALL && (uint32_t)x.k == 12)) && (x.aux & AUX_FALL_OK)) preds[i + 1]++;
+        }
+        uint32_t def[11] = {}, kill = 0, start = 0, live = 0;
+        bool mapv[11] = {};   // holds a helper's result (a map value, not a packet address)
+        int last_jcc = -1;
+        for (size_t b = 0; b < Lb.size(); b++) {
+            const uint32_t s0 = Lb[b], e = b + 1 < Lb.size() ? Lb[b + 1] : p.n;
+            const DInsn &prev = p.ins[s0 ? s0 - 1 : 0];
+            const bool cont = s0 > 0 && !special[s0] && preds[s0] == 1 && (AUX_H(prev.aux) == H_JCC || !ends_block(prev)) &&
+                              (prev.aux & AUX_FALL_OK);
+            if (!cont) {   // a new region
+                start = s0;
+                kill = s0;
+                for (auto &d : def) d = s0;
+                for (auto &m : mapv) m = false;
+                live = 0;
+                last_jcc = -1;
+            }
+            for (uint32_t i = s0; i < e; i++) {
+                const DInsn &x = p.ins[i];
+                const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x);
+                if (h == H_LDX && sr <= 10 && hint(sr) == HINT_PKT && !mapv[sr] && live < (uint32_t)speculate) {
+                    const uint32_t hp = std::max(std::max(def[sr], kill), start);
+                    if (last_jcc >= (int)hp) {   // a branch lies between the issue point and the load
+                        spec_use[{p.id, i}] = AUX_SZ(x.aux);
+                        spec_at[{p.id, hp}].push_back(i);
+                        live++;
+                    }
+                }
+                switch (h) {
+                case H_ALU64: case H_ALU32: case H_LDIMM: case H_LDX:
+                    if (d <= 10) {
+                        def[d] = i + 1;
+                        mapv[d] = h == H_ALU64 && insn_op(x) == 0xbf && insn_src(x) <= 10 && mapv[insn_src(x)];
+                    }
+                    break;
+                case H_JCC: case H_JA:
+                    last_jcc = (int)i;
+                    break;
+                case H_NOP:
+                    break;
+                default:   // stores, calls, LD_ABS, anything generic: nothing moves above it
+                    kill = i + 1;
+                    for (auto &r : def) r = i + 1;
+                    for (auto &m : mapv) m = false;
+                    if (h == H_CALL) mapv[0] = true;
+                    break;
+                }
+            }
+        }
+    }
+    void emit_spec(const ProgView &p, uint32_t i) {
+        auto it = spec_at.find({p.id, i});
+        if (it == spec_at.end()) return;
+        for (uint32_t j : it->second) {
+            const DInsn &x = p.ins[j];
+            const uint32_t n = AUX_SZ(x.aux);
+            E.line("    ga_ = %s;   // early load for slot %u", addr(insn_src(x), insn_off(x)).c_str(), j);
+            E.line("    if ((uint64_t)(uint32_t)(ga_ - P) + %uu <= L.M) sp%u_%u_ = (%s)ld_n(L.pkt + (uint32_t)(ga_ - P), %uu);", n, p.id, j,
+                   n == 8 ? "uint64_t" : "uint32_t", n);
+        }
+    }
+
     void program(const ProgView &p) {
         if (p.n == 0) return;
         ctx_hints(p);
@@ -417,6 +520,7 @@ class Gen {
                 }
                 for (uint32_t i = s; i < e; i++) {
                     if (careful) E.line("    if (steps == kp.budget) TERM(MIMIC_ERR_STEP_LIMIT, %u);", i);
+                    emit_spec(p, i);
                     insn(p, i);
                 }
                 // falling off the end of the block
@@ -532,8 +636,10 @@ class Gen {
     void load(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &dst) {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         std::string pre = "    ";
-        for (auto &f : fast_forms(base, n, "")) {
-            E.line("%sif (%s) %s = %s;", pre.c_str(), f.cond.c_str(), dst.c_str(), f.val.c_str());
+        bool sp = spec_use.count({cur_prog, i}) > 0;
+        for (auto &f : fast_forms(base, n, "")) {   // the first form of a packet access is the packet
+            if (sp) sp = false, E.line("%sif (%s) %s = sp%u_%u_;", pre.c_str(), f.cond.c_str(), dst.c_str(), cur_prog, i);
+            else E.line("%sif (%s) %s = %s;", pre.c_str(), f.cond.c_str(), dst.c_str(), f.val.c_str());
             pre = "    else ";
         }
         if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {  // __sk_buff field: convertAccess directly
