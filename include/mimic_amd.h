@@ -282,7 +282,7 @@ typedef struct {
     uint64_t *r0;                 /* host, [n] */
     uint8_t *status;              /* host, [n] */
 } mimic_xdp_host_batch;
-/* chunks = number of sub-batches (0: about 8 MiB of packet memory each) */
+/* chunks = number of sub-batches (0: about 16 MiB of packet memory each) */
 int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks);
 /* Pin / unpin host memory for DMA (hipHostRegister / hipHostUnregister). */
 int mimic_host_register(void *p, size_t bytes);

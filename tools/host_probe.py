@@ -1,4 +1,5 @@
-"""Host-resident pipeline probe: mimic_run_xdp_host with registered vs hipHostMalloc'd host memory."""
+"""Host-resident pipeline probe: mimic_run_xdp_host with registered vs hipHostMalloc'd host memory.
+    python tools/host_probe.py [modes] [chunk counts]     e.g.  registered,pinned 0,4,8,16"""
 import sys
 import time
 
@@ -9,6 +10,9 @@ sys.path.insert(0, ".")
 import mimic_amd as M  # noqa: E402
 from mimic_amd import workloads as W  # noqa: E402
 
+modes = sys.argv[1].split(",") if len(sys.argv) > 1 else ["pinned", "registered"]
+chunk_list = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 4, 8, 16, 32]
+reps = 5
 p = W.prog_classifier()
 n = 1 << 20
 emu = M.NewLinuxEmulator()
@@ -17,7 +21,7 @@ for m in p.maps:
     emu.AddMap(m["name"], M.MapSpecToLinuxMap(M.MapSpec(m["name"], m["type"], m["key_size"], m["value_size"], m["max_entries"])))
 pid = vm.AddProgram(M.ProgramSpec(p.name, p.raw, p.relocs))
 buf, off, lens = W.make_packets(n)
-for mode in ("pinned", "registered"):
+for mode in modes:
     if mode == "pinned":
         tb = torch.from_numpy(buf).pin_memory(); b = tb.numpy()
         to = torch.from_numpy(off.view(np.int64)).pin_memory(); o = to.numpy().view(np.uint64)
@@ -29,11 +33,14 @@ for mode in ("pinned", "registered"):
         r0, st = np.empty(n, np.uint64), np.empty(n, np.uint8)
         for a in (b, o, l_, r0, st):
             vm.HostRegister(a)
-    for chunks in (0, 2, 4, 8, 16):
+    for chunks in chunk_list:
         vm.RunXDPHost(pid, b, o, l_, schedule=M.SCHED_INTERLEAVED, ingress=1, chunks=chunks, r0=r0, status=st)
-        t = time.perf_counter()
-        for _ in range(5):
+        ts_ = []
+        for _ in range(reps):
+            t = time.perf_counter()
             vm.RunXDPHost(pid, b, o, l_, schedule=M.SCHED_INTERLEAVED, ingress=1, chunks=chunks, r0=r0, status=st)
-        dt = (time.perf_counter() - t) / 5
-        print(mode, chunks, f"{n / dt / 1e6:.1f} Mpkts/s  {(buf.nbytes + 21 * n) / dt / 1e9:.1f} GB/s", flush=True)
+            ts_.append(time.perf_counter() - t)
+        dt = float(np.median(ts_))
+        print(mode, chunks, f"median {n / dt / 1e6:.1f} Mpkts/s  {(buf.nbytes + 21 * n) / dt / 1e9:.1f} GB/s  "
+              f"(per call ms: {' '.join(f'{x * 1e3:.2f}' for x in ts_)})", flush=True)
 vm.close()
