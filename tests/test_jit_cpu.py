@@ -95,13 +95,15 @@ def _resources(raws, ctx=_lib.CTX_XDP):
     return J.kernel_resources(J.code_object(J.kernel_source(raws, ctx)))
 
 
-@pytest.mark.parametrize("fn", ["prog_classifier", "prog_parse5"])
-def test_hot_kernels_fit_five_waves(fn):
-    """cfg 2 / cfg 3 kernels: <= 96 unified VGPRs (5 waves per SIMD), no VGPR spills, no scratch.
-    At most a few SGPRs may spill (into VGPR lanes): keeping the per-packet result pointers in
-    SGPRs measured faster than reloading them (jit.cpp, MIMIC_JIT_KQ)."""
+@pytest.mark.parametrize("fn,vgprs,waves", [("prog_classifier", 96, 5), ("prog_parse5", 112, 4)])
+def test_hot_kernels_register_budget(fn, vgprs, waves):
+    """cfg 2 / cfg 3 kernels: unified VGPRs within budget, no VGPR spills, no scratch.  At most a
+    few SGPRs may spill (into VGPR lanes): keeping the per-packet result pointers in SGPRs measured
+    faster than reloading them (jit.cpp, MIMIC_JIT_KQ).  parse5's early packet loads (jit.cpp,
+    analyze_spec) cost it the fifth wave and measured faster anyway: 1.155 vs 1.193 ms per launch;
+    forcing 5 waves (MIMIC_JIT_WAVES=5) measured 1.47 ms."""
     r = _resources([getattr(W, fn)().raw])
-    assert r["vgpr_total"] <= 96 and r["waves_per_simd"] >= 5, r
+    assert r["vgpr_total"] <= vgprs and r["waves_per_simd"] >= waves, r
     assert r["vgpr_spill"] == 0 and r["sgpr_spill"] <= 4 and r["scratch"] == 0, r
 
 
