@@ -98,8 +98,10 @@ class Gen {
         prefetch = !(pfv && pfv[0] == '0');
         const char *fw = getenv("MIMIC_JIT_FWD");   // 0: no stack-store -> lookup key forwarding
         forward = !(fw && fw[0] == '0');
-        const char *nr = getenv("MIMIC_JIT_NTRES");   // 1: per-packet results stored non-temporal
-        ntres = nr && nr[0] == '1';
+        const char *nr = getenv("MIMIC_JIT_NTRES");   // 0: per-packet results stored as plain stores
+        ntres = !(nr && nr[0] == '0');
+        const char *el = getenv("MIMIC_JIT_ELIDE");   // 0: forwarded key stores are always made
+        elide = !(el && el[0] == '0');
         const char *spv = getenv("MIMIC_JIT_SPEC");   // 0: no early packet loads
         if (spv) speculate = atoi(spv);
         const char *wv = getenv("MIMIC_JIT_WAVES");   // minimum waves per SIMD the register budget targets
@@ -146,8 +148,9 @@ class Gen {
     int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
+    bool elide = true;         // MIMIC_JIT_ELIDE=0: no deferred stack stores
     int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
-    bool ntres = false;        // MIMIC_JIT_NTRES=1: r0 / status stores non-temporal
+    bool ntres = true;         // MIMIC_JIT_NTRES=0: r0 / status stores not non-temporal (measured 1-3 % slower)
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
     bool prefetch = true;      // MIMIC_JIT_PREFETCH=0: no next-packet descriptor prefetch
@@ -224,6 +227,8 @@ class Gen {
         E.line("  uint32_t ga_ = 0;   // the address of the current memory access");
         if (forward)
             for (auto &p : P) analyze_fwd(p);
+        if (forward && elide)
+            for (auto &p : P) analyze_elide(p);
         for (auto &f : fwd_store) E.line("  uint32_t fwd%u_%u_ = 0;   // value of the stack store at P%u slot %u", f.first, f.second, f.first, f.second);
         if (speculate && fast_paths && !stage && ctx == CTX_XDP && !all_leaders)
             for (auto &p : P) analyze_spec(p);
@@ -245,7 +250,8 @@ class Gen {
         E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
         if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
-            E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+            if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
+            else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
         // fields used once per packet are read through an opaque copy of the parameter pointer:
         // loaded where used instead of hoisted out of the packet loop into SGPRs
@@ -365,6 +371,70 @@ class Gen {
     // Registers are tracked only as "R10 + constant"; a store through any other base clears it.
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> fwd_call;   // (prog, call slot) -> store slot
     std::set<std::pair<uint32_t, uint32_t>> fwd_store;            // (prog, store slot) to capture
+    // Forwarded stores whose memory write is deferred into the lookup's cold path: in a program
+    // that never reads the stack other than through forwarded lookup keys (no load through R10
+    // or a register derived from it, no other helper call, no BPF-to-BPF call, no tail call in
+    // the set), the stack is dead at exit and nothing else observes the word, so the store is
+    // only made when the generic lookup (which reads the key from memory) runs.
+    std::set<std::pair<uint32_t, uint32_t>> elided;
+    void analyze_elide(const ProgView &p) {
+        if (any_tail || any_local) return;
+        // forward may-analysis over the CFG: which registers may hold a stack address
+        const std::vector<uint32_t> Lb = leaders(p);
+        std::map<uint32_t, size_t> blk;
+        for (size_t b = 0; b < Lb.size(); b++) blk[Lb[b]] = b;
+        std::vector<uint32_t> in(Lb.size(), 0);
+        std::vector<bool> seen(Lb.size(), false);
+        in[0] = 1u << 10;
+        seen[0] = true;
+        auto transfer = [&](uint32_t t, const DInsn &x) {
+            const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x), op = insn_op(x);
+            if (d > 10) return t;
+            if (h == H_ALU64 || h == H_ALU32) {
+                const bool mov = (op & 0xf0) == 0xb0;
+                const bool src_t = (x.aux & AUX_X) && sr <= 10 && ((t >> sr) & 1);
+                const bool res = mov ? src_t : (((t >> d) & 1) || src_t);
+                return res ? (t | (1u << d)) : (t & ~(1u << d));
+            }
+            if (h == H_LDX || h == H_LDIMM) return t & ~(1u << d);
+            if (h == H_CALL) return t & ~1u;
+            return t;
+        };
+        for (bool changed = true; changed;) {
+            changed = false;
+            for (size_t b = 0; b < Lb.size(); b++) {
+                if (!seen[b]) continue;
+                const uint32_t s0 = Lb[b], e = b + 1 < Lb.size() ? Lb[b + 1] : p.n;
+                uint32_t t = in[b];
+                for (uint32_t i = s0; i < e; i++) {
+                    const DInsn &x = p.ins[i];
+                    const uint32_t h = AUX_H(x.aux), sr = insn_src(x);
+                    if (h == H_LDX && sr <= 10 && ((t >> sr) & 1)) return;   // reads the stack
+                    if (h == H_STX && sr <= 10 && ((t >> sr) & 1)) return;   // a stack address escapes to memory
+                    if (h == H_SLOW || h == H_LDABS || h == H_CALL_LOCAL) return;
+                    if (h == H_CALL && !((uint32_t)x.k == 1 && fwd_call.count({p.id, i})) && (uint32_t)x.k != 8) return;
+                    t = transfer(t, x);
+                }
+                const DInsn &last = p.ins[e - 1];
+                const uint32_t h = AUX_H(last.aux);
+                std::vector<int64_t> succ;
+                if ((!ends_block(last) || h == H_JCC) && (last.aux & AUX_FALL_OK)) succ.push_back(e);
+                if ((h == H_JA || h == H_JCC) && (last.aux & AUX_JT_OK)) succ.push_back(jump_target(last, e - 1));
+                for (int64_t sx : succ) {
+                    auto it = blk.find((uint32_t)sx);
+                    if (it == blk.end()) continue;
+                    const uint32_t nin = in[it->second] | t;
+                    if (!seen[it->second] || nin != in[it->second]) {
+                        in[it->second] = nin;
+                        seen[it->second] = true;
+                        changed = true;
+                    }
+                }
+            }
+        }
+        for (auto &f : fwd_store)
+            if (f.first == p.id && AUX_H(p.ins[f.second].aux) == H_STX && insn_dst(p.ins[f.second]) == 10) elided.insert(f);
+    }
     void analyze_fwd(const ProgView &p) {
         if (!fast_paths || p.n == 0) return;
         const std::vector<uint32_t> Lb = leaders(p);
@@ -498,8 +568,8 @@ class Gen {
             const DInsn &x = p.ins[j];
             const uint32_t n = AUX_SZ(x.aux);
             E.line("    ga_ = %s;   // early load for slot %u", addr(insn_src(x), insn_off(x)).c_str(), j);
-            E.line("    if ((uint64_t)(uint32_t)(ga_ - P) + %uu <= L.M) sp%u_%u_ = (%s)ld_n(L.pkt + (uint32_t)(ga_ - P), %uu);", n, p.id, j,
-                   n == 8 ? "uint64_t" : "uint32_t", n);
+            E.line("    if ((uint64_t)(uint32_t)(ga_ - P) + %uu <= L.M) sp%u_%u_ = (%s)%s(L.pkt + (uint32_t)(ga_ - P), %uu);", n, p.id, j,
+                   n == 8 ? "uint64_t" : "uint32_t", nt ? "ld_n_nt" : "ld_n", n);
         }
     }
 
@@ -652,9 +722,14 @@ class Gen {
         E.line("%s{ COLD_CALL(cold_load(kp, sp_, ga_, %uu), %u); %s = sp_.v; }", pre.c_str(), n, i, dst.c_str());
     }
 
-    void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val) {
-        if (fwd_store.count({cur_prog, i})) E.line("    fwd%u_%u_ = (uint32_t)(%s);", cur_prog, i, val.c_str());
+    void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val, bool deferred = false) {
+        if (!deferred && fwd_store.count({cur_prog, i})) E.line("    fwd%u_%u_ = (uint32_t)(%s);", cur_prog, i, val.c_str());
         E.line("    ga_ = %s;", addr(base, off).c_str());
+        if (!deferred && elided.count({cur_prog, i})) {   // the write happens in the lookup's cold path
+            const auto f = fast_forms(base, n, val);
+            E.line("    if (!(%s)) { COLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u); }", f.at(0).cond.c_str(), n, val.c_str(), i);
+            return;
+        }
         std::string pre = "    ";
         for (auto &f : fast_forms(base, n, val)) {
             if (f.store.empty()) continue;
@@ -784,7 +859,12 @@ class Gen {
             if (j >= 0) {  // inline array lookup when R1 is the map object the LD_IMM64 hint names
                 E.line("    { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", p.base + (uint32_t)j);
                 auto f = fwd_call.find({p.id, i});
-                if (f != fwd_call.end())
+                if (f != fwd_call.end() && elided.count({p.id, f->second})) {
+                    E.line("      if (!(mh_ && lookup_fast_k(kp, L, mh_ - 1u, r1, r2, r0, true, fwd%u_%u_))) {", p.id, f->second);
+                    const DInsn &sx = p.ins[f->second];   // the deferred stack store, then the generic lookup
+                    store(f->second, insn_dst(sx), insn_off(sx), AUX_SZ(sx.aux), "fwd" + std::to_string(p.id) + "_" + std::to_string(f->second) + "_", true);
+                    E.line("      COLD_CALL(cold_lookup(kp, sp_), %u); } }", i);
+                } else if (f != fwd_call.end())
                     E.line("      if (!(mh_ && lookup_fast_k(kp, L, mh_ - 1u, r1, r2, r0, true, fwd%u_%u_))) COLD_CALL(cold_lookup(kp, sp_), %u); }",
                            p.id, f->second, i);
                 else

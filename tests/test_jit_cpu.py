@@ -95,13 +95,15 @@ def _resources(raws, ctx=_lib.CTX_XDP):
     return J.kernel_resources(J.code_object(J.kernel_source(raws, ctx)))
 
 
-@pytest.mark.parametrize("fn,vgprs,waves", [("prog_classifier", 96, 5), ("prog_parse5", 112, 4)])
+@pytest.mark.parametrize("fn,vgprs,waves", [("prog_classifier", 104, 4), ("prog_parse5", 120, 4)])
 def test_hot_kernels_register_budget(fn, vgprs, waves):
     """cfg 2 / cfg 3 kernels: unified VGPRs within budget, no VGPR spills, no scratch.  At most a
     few SGPRs may spill (into VGPR lanes): keeping the per-packet result pointers in SGPRs measured
     faster than reloading them (jit.cpp, MIMIC_JIT_KQ).  parse5's early packet loads (jit.cpp,
     analyze_spec) cost it the fifth wave and measured faster anyway: 1.155 vs 1.193 ms per launch;
-    forcing 5 waves (MIMIC_JIT_WAVES=5) measured 1.47 ms."""
+    forcing 5 waves (MIMIC_JIT_WAVES=5) measured 1.47 ms.  The classifier's deferred key store
+    (analyze_elide) costs it the fifth wave too and measured 29.1 vs 32.4 us per launch; forced to
+    5 waves (8 VGPRs spilled) 29.6 us."""
     r = _resources([getattr(W, fn)().raw])
     assert r["vgpr_total"] <= vgprs and r["waves_per_simd"] >= waves, r
     assert r["vgpr_spill"] == 0 and r["sgpr_spill"] <= 4 and r["scratch"] == 0, r
