@@ -378,7 +378,7 @@ class Gen {
     // only made when the generic lookup (which reads the key from memory) runs.
     std::set<std::pair<uint32_t, uint32_t>> elided;
     void analyze_elide(const ProgView &p) {
-        if (any_tail || any_local) return;
+        if (any_tail || any_local || p.n == 0) return;
         // forward may-analysis over the CFG: which registers may hold a stack address
         const std::vector<uint32_t> Lb = leaders(p);
         std::map<uint32_t, size_t> blk;

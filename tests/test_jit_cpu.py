@@ -118,3 +118,19 @@ def test_cfg4_cfg5_kernels_have_no_vgpr_scratch_spill():
     """cfg 4 (hash insert) and cfg 5 (sk_buff tail-call chain) kernels: no VGPR spills to scratch."""
     r = _resources([W.prog_flowtrack().raw])
     assert r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 3, r
+
+
+def test_every_gpu_test_kernel_generates():
+    """Kernel source generation (host C++: leaders, forwarding, early loads, deferred stores) for
+    every program set the GPU suite compiles, so a crash in the generator shows up on the CPU."""
+    import importlib
+
+    from mimic_amd import jit as J
+
+    count = 0
+    for name in ("test_gpu_kat", "test_gpu_skb", "test_gpu_parity", "test_gpu_hash"):
+        mod = importlib.import_module(name)
+        for raws, ctx in mod.jit_kernels():
+            assert "mimic_jit_kernel" in J.kernel_source(raws, ctx)
+            count += 1
+    assert count > 20
