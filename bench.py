@@ -34,8 +34,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table
 
 CONFIGS = {
-    "pass8": dict(prog="prog_pass8", packets=1 << 20, sizes=(64,), weights=(1,),
-                  workload="cfg1-shape: 8-insn XDP_PASS over 1M x 64B xdp_md"),
+    "pass8": dict(prog="prog_pass8", packets=1 << 20, sizes=(64,), weights=(1,), reads_packet=False,
+                  workload="cfg1-shape: 8-insn XDP_PASS over 1M x 64B xdp_md (reads ctx fields, no packet bytes)"),
     "classifier": dict(prog="prog_classifier", packets=1 << 20, sizes=(64,), weights=(1,),
                        workload="cfg2: 1M x 64B xdp_md, 36-slot parse+hash DROP/PASS classifier, "
                                 "per-CPU array E=4 S=8"),
@@ -58,11 +58,12 @@ def dist_env():
     return ws, rank, local
 
 
-def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps) -> int:
+def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps, reads_packet: bool = True) -> int:
     """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU array
     state, 2*E*(K+S) of hash-map state (K + V*S for a per-CPU hash), 2*E*S of plain arrays.
+    A program that never reads packet bytes (pass8) is charged only its 16 B per packet.
     (The engine's actual descriptor is 12 B and it also writes a 1-B status; not counted.)"""
-    b = int(lens.astype(np.int64).sum()) + 16 * len(lens)
+    b = (int(lens.astype(np.int64).sum()) if reads_packet else 0) + 16 * len(lens)
     for m in maps:
         if m["type"] in (1, 5):
             ncpu = vcpus if m["type"] == 5 else 1
@@ -360,7 +361,7 @@ def main():
         total_pkts = n * ws * args.steps
         value = total_pkts / elapsed / 1e6
         avg_launch_s = region_ms / args.steps / 1e3   # per launch, gaps between launches included
-        alg = algorithmic_bytes(wl.lens, vpg, wl.maps)
+        alg = algorithmic_bytes(wl.lens, vpg, wl.maps, wl.cfg.get("reads_packet", True))
         achieved = alg / avg_launch_s
         kernel = "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel"
         src_hash = wl.kernel_src_hash()
