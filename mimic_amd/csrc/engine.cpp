@@ -394,7 +394,8 @@ static int upload_tables(mimic_vm *vm) {
     for (auto &m : vm->maps) dm.push_back(to_dmap(m));
     if (dm.empty()) dm.push_back(DMap{});
     if (dp.empty()) dp.push_back(DProg{});
-    std::vector<Seg> sg = vm->segs;
+    std::vector<Seg> sg = vm->segs;   // sorted by address: resolve() binary-searches them
+    std::sort(sg.begin(), sg.end(), [](const Seg &x, const Seg &y) { return x.lo < y.lo; });
     if (sg.empty()) sg.push_back(Seg{});
     hipFree(vm->d_insns);
     hipFree(vm->d_progs);

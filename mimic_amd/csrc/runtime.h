@@ -344,11 +344,17 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
         R.limit = L.t_n - 1;
         return R;
     }
-    bool found = false;
-    for (uint32_t s = 0; s < kp.nsegs; s++) {
-        const Seg g = cget(kp.segs, s);
-        if (!found && a >= g.lo && a <= g.hi) {
-            found = true;
+    // static entries are disjoint and sorted by address (upload_tables): binary search for the
+    // last entry starting at or below a
+    uint32_t sl = 0, sr = kp.nsegs;
+    while (sl < sr) {
+        const uint32_t sm = (sl + sr) >> 1;
+        if (cget(kp.segs, sm).lo <= a) sl = sm + 1;
+        else sr = sm;
+    }
+    if (sl > 0) {
+        const Seg g = cget(kp.segs, sl - 1);
+        if (a <= g.hi) {
             uint32_t off = a - g.lo;
             switch (g.kind) {
             case SEG_PLAIN:
