@@ -100,8 +100,14 @@ class Gen {
         forward = !(fw && fw[0] == '0');
         const char *nr = getenv("MIMIC_JIT_NTRES");   // 0: per-packet results stored as plain stores
         ntres = !(nr && nr[0] == '0');
+        const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
+        skb_fields = !(sf && sf[0] == '0');
+        const char *ti = getenv("MIMIC_JIT_TAIL");   // 0: tail calls always through the generic helper
+        tail_inline = !(ti && ti[0] == '0');
         const char *el = getenv("MIMIC_JIT_ELIDE");   // 0: forwarded key stores are always made
         elide = !(el && el[0] == '0');
+        const char *wnd = getenv("MIMIC_JIT_WINDOW");   // 0: early loads one by one
+        window = !(wnd && wnd[0] == '0');
         const char *spv = getenv("MIMIC_JIT_SPEC");   // 0: no early packet loads
         if (spv) speculate = atoi(spv);
         const char *wv = getenv("MIMIC_JIT_WAVES");   // minimum waves per SIMD the register budget targets
@@ -148,7 +154,10 @@ class Gen {
     int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
+    bool skb_fields = true;    // MIMIC_JIT_SKBFIELD=0: no per-field sk_buff access code
+    bool tail_inline = true;   // MIMIC_JIT_TAIL=0: no inline tail calls
     bool elide = true;         // MIMIC_JIT_ELIDE=0: no deferred stack stores
+    bool window = true;        // MIMIC_JIT_WINDOW=0: no windowed early loads
     int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
     bool ntres = true;         // MIMIC_JIT_NTRES=0: r0 / status stores not non-temporal (measured 1-3 % slower)
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
@@ -199,7 +208,10 @@ class Gen {
         E.line("#define FILL() do { r0 = sp_.r[0]; r1 = sp_.r[1]; r2 = sp_.r[2]; r3 = sp_.r[3]; r4 = sp_.r[4]; r5 = sp_.r[5]; "
                "L.sm0 = sp_.L.sm0; L.sm1 = sp_.L.sm1; L.xdp_dirty = sp_.L.xdp_dirty; L.t_lo = sp_.L.t_lo; L.t_n = sp_.L.t_n; "
                "L.t_ptr = sp_.L.t_ptr; } while (0)");
-        E.line("#define COLD_CALL(call_, pc_) do { SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
+        if (getenv("MIMIC_JIT_NOCOLD") && getenv("MIMIC_JIT_NOCOLD")[0] == '1')   // measurement only: no slow paths
+            E.line("#define COLD_CALL(call_, pc_) TERM(MIMIC_ERR_ENGINE_HELPER, pc_)");
+        else
+            E.line("#define COLD_CALL(call_, pc_) do { SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
         // KParams is read through a pointer to a device copy: fields are loaded (scalar) where
         // they are used instead of all being preloaded into SGPRs from the kernarg segment
         // (which spills SGPRs and costs VGPRs / occupancy)
@@ -561,15 +573,47 @@ class Gen {
             }
         }
     }
+    void emit_spec_one(const ProgView &p, uint32_t j, const char *pre) {
+        const DInsn &x = p.ins[j];
+        const uint32_t n = AUX_SZ(x.aux);
+        E.line("%sga_ = %s;   // early load for slot %u", pre, addr(insn_src(x), insn_off(x)).c_str(), j);
+        E.line("%sif ((uint64_t)(uint32_t)(ga_ - P) + %uu <= L.M) sp%u_%u_ = (%s)%s(L.pkt + (uint32_t)(ga_ - P), %uu);", pre, n, p.id, j,
+               n == 8 ? "uint64_t" : "uint32_t", nt ? "ld_n_nt" : "ld_n", n);
+    }
+    // Early loads from one base register that fall in a 32-byte span are made as one window of
+    // 8-byte loads (fewer memory instructions per packet); the fields are cut out of the window
+    // with constant shifts.  A packet too short for the whole window takes the loads one by one.
     void emit_spec(const ProgView &p, uint32_t i) {
         auto it = spec_at.find({p.id, i});
         if (it == spec_at.end()) return;
-        for (uint32_t j : it->second) {
-            const DInsn &x = p.ins[j];
-            const uint32_t n = AUX_SZ(x.aux);
-            E.line("    ga_ = %s;   // early load for slot %u", addr(insn_src(x), insn_off(x)).c_str(), j);
-            E.line("    if ((uint64_t)(uint32_t)(ga_ - P) + %uu <= L.M) sp%u_%u_ = (%s)%s(L.pkt + (uint32_t)(ga_ - P), %uu);", n, p.id, j,
-                   n == 8 ? "uint64_t" : "uint32_t", nt ? "ld_n_nt" : "ld_n", n);
+        std::map<uint32_t, std::vector<uint32_t>> by_base;
+        for (uint32_t j : it->second) by_base[insn_src(p.ins[j])].push_back(j);
+        for (auto &bb : by_base) {
+            const std::vector<uint32_t> &js = bb.second;
+            int64_t lo = INT64_MAX, hi = INT64_MIN;
+            for (uint32_t j : js) {
+                lo = std::min<int64_t>(lo, insn_off(p.ins[j]));
+                hi = std::max<int64_t>(hi, (int64_t)insn_off(p.ins[j]) + AUX_SZ(p.ins[j].aux));
+            }
+            if (!window || js.size() < 2 || hi - lo > 32) {
+                for (uint32_t j : js) emit_spec_one(p, j, "    ");
+                continue;
+            }
+            const uint32_t words = (uint32_t)((hi - lo + 7) / 8);
+            E.line("    { const uint32_t wo_ = %s - P;   // window of %u bytes for slots", addr(bb.first, (int32_t)lo).c_str(), 8 * words);
+            E.line("      if ((uint64_t)wo_ + %uu <= L.M) {", 8 * words);
+            for (uint32_t q = 0; q < words; q++)
+                E.line("        const uint64_t w%u_ = %s(L.pkt + wo_ + %uu, 8u);", q, nt ? "ld_n_nt" : "ld_n", 8 * q);
+            for (uint32_t j : js) {
+                const uint32_t o = (uint32_t)(insn_off(p.ins[j]) - lo), n = AUX_SZ(p.ins[j].aux), q = o / 8, r = o % 8;
+                std::string v = r == 0 ? "w" + std::to_string(q) + "_" : "(w" + std::to_string(q) + "_ >> " + std::to_string(8 * r) + ")";
+                if (r + n > 8) v = "(" + v + " | (w" + std::to_string(q + 1) + "_ << " + std::to_string(64 - 8 * r) + "))";
+                if (n < 8) v = "(" + v + " & 0x" + (n == 1 ? std::string("ffull") : n == 2 ? std::string("ffffull") : std::string("ffffffffull")) + ")";
+                E.line("        sp%u_%u_ = (%s)%s;", p.id, j, n == 8 ? "uint64_t" : "uint32_t", v.c_str());
+            }
+            E.line("      } else {");
+            for (uint32_t j : js) emit_spec_one(p, j, "        ");
+            E.line("      } }");
         }
     }
 
@@ -703,6 +747,12 @@ class Gen {
         return f;
     }
 
+    // an sk_buff field access at a constant offset: convertAccess with the offset, size and
+    // direction known, which the compiler folds to the one field's code
+    bool skb_field_ok(int32_t off, uint32_t n) const {
+        return skb_fields && off >= 0 && (uint32_t)off < 192 && (n == 1 || n == 2 || n == 4 || n == 8);
+    }
+
     void load(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &dst) {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         std::string pre = "    ";
@@ -713,6 +763,12 @@ class Gen {
             pre = "    else ";
         }
         if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {  // __sk_buff field: convertAccess directly
+            if (skb_field_ok(off, n)) {   // the field the instruction names, when base is the sk_buff
+                E.line("%sif (ga_ == SK_ + %uu) { uint64_t v_ = 0; const int s_ = skb_convert_(*L.rec, kp.skb_ifindex, L.pa + SKB_HEADROOM, "
+                       "L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, %uu, %uu, v_, true); if (s_) TERM(s_, %u); %s = v_; }",
+                       pre.c_str(), (uint32_t)off, (uint32_t)off, n, i, dst.c_str());
+                pre = "    else ";
+            }
             E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
                    "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, 0, true);"
                    " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
@@ -737,6 +793,12 @@ class Gen {
             pre = "    else ";
         }
         if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {
+            if (skb_field_ok(off, n)) {
+                E.line("%sif (ga_ == SK_ + %uu) { uint64_t v_ = %s; const int s_ = skb_convert_(*L.rec, kp.skb_ifindex, L.pa + SKB_HEADROOM, "
+                       "L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, %uu, %uu, v_, false); if (s_) TERM(s_, %u); }",
+                       pre.c_str(), (uint32_t)off, val.c_str(), (uint32_t)off, n, i);
+                pre = "    else ";
+            }
             E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
                    "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, %s, false);"
                    " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
@@ -839,13 +901,17 @@ class Gen {
 
     // the LD_IMM64 slot whose constant R1 still holds at slot i (same basic block, R1 not
     // written in between; helpers keep R1, Q8), or -1
-    int64_t r1_def(const ProgView &p, uint32_t i) const {
+    int64_t r1_def(const ProgView &p, uint32_t i) const { return reg_def(p, i, 1); }
+    // the LD_IMM64 slot whose constant register r still holds at slot i (same basic block, r not
+    // written in between; helpers keep R1, Q8, any other register is taken as clobbered), or -1
+    int64_t reg_def(const ProgView &p, uint32_t i, uint32_t r) const {
         for (int64_t j = (int64_t)i - 1; j >= (int64_t)blk_start; j--) {
             const DInsn &x = p.ins[j];
             const uint32_t h = AUX_H(x.aux), d = insn_dst(x);
-            if (h == H_LDIMM && d == 1) return j;
-            if ((h == H_ALU64 || h == H_ALU32 || h == H_LDX || h == H_SLOW || h == H_LDIMM) && d == 1) return -1;
+            if (h == H_LDIMM && d == r) return j;
+            if ((h == H_ALU64 || h == H_ALU32 || h == H_LDX || h == H_SLOW || h == H_LDIMM) && d == r) return -1;
             if (h == H_LDABS || h == H_CALL_LOCAL) return -1;
+            if (h == H_CALL && r != 1) return -1;
         }
         return -1;
     }
@@ -883,21 +949,39 @@ class Gen {
         case 8:
             E.line("    r0 = (uint64_t)(int64_t)L.cpu;");
             break;
-        case 12:
-            E.line("    COLD_CALL(cold_tailcall(kp, sp_), %u);", i);
-            E.line("    {");
-            E.line("      if (sp_.tail) {");
-            E.line("        L.tailcalls++;");
-            E.line("        switch (sp_.new_prog) {");
-            for (auto &q : P) {
-                if (q.n == 0) E.line("        case %u: TERM(MIMIC_ERR_PC_OOB, %u);", q.id, i);
-                else E.line("        case %u: goto P%u_0;", q.id, q.id);
+        case 12: {
+            // inline when R2 is a prog-array object named by an LD_IMM64 in this block
+            const int64_t j = fast_paths && tail_inline ? reg_def(p, i, 2) : -1;
+            auto jump_table = [&](const char *var) {
+                E.line("        L.tailcalls++;");
+                E.line("        switch (%s) {", var);
+                for (auto &q : P) {
+                    if (q.n == 0) E.line("        case %u: TERM(MIMIC_ERR_PC_OOB, %u);", q.id, i);
+                    else E.line("        case %u: goto P%u_0;", q.id, q.id);
+                }
+                E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);
+                E.line("        }");
+            };
+            if (j >= 0) {
+                E.line("    { const uint32_t th_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", p.base + (uint32_t)j);
+                E.line("      const int np_ = th_ ? tail_fast(kp, L, th_ - 1u, r2, r3, r0) : -2;");
+                E.line("      if (np_ >= 0) {");
+                jump_table("np_");
+                E.line("      } else if (np_ == -2) {");
+                E.line("      COLD_CALL(cold_tailcall(kp, sp_), %u);", i);
+                E.line("      if (sp_.tail) {");
+                jump_table("sp_.new_prog");
+                E.line("      } } }");
+            } else {
+                E.line("    COLD_CALL(cold_tailcall(kp, sp_), %u);", i);
+                E.line("    {");
+                E.line("      if (sp_.tail) {");
+                jump_table("sp_.new_prog");
+                E.line("      }");
+                E.line("    }");
             }
-            E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);
-            E.line("        }");
-            E.line("      }");
-            E.line("    }");
             break;
+        }
         default:  // 65: bpf_xdp_adjust_tail (emulator_linux_helpers.go:842-864)
             E.line("    COLD_CALL(cold_adjust_tail(kp, sp_), %u);", i);
             break;

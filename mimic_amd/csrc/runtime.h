@@ -282,6 +282,18 @@ DEV void xdp_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t 
 // ---------------------------------------------------------------------------------------
 // MemoryController.GetEntry (memory_controller.go:117-145) over the lane's address space
 // ---------------------------------------------------------------------------------------
+// the static entry holding address a, or -1: the entries are disjoint and sorted by address
+// (upload_tables), so a binary search for the last one starting at or below a
+DEV int32_t seg_find(const KParams &kp, uint32_t a) {
+    uint32_t sl = 0, sr = kp.nsegs;
+    while (sl < sr) {
+        const uint32_t sm = (sl + sr) >> 1;
+        if (cget(kp.segs, sm).lo <= a) sl = sm + 1;
+        else sr = sm;
+    }
+    return sl > 0 && a <= cget(kp.segs, sl - 1).hi ? (int32_t)(sl - 1) : -1;
+}
+
 DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
     Ref R;
     R.rk = RK_UNRES;
@@ -344,17 +356,10 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
         R.limit = L.t_n - 1;
         return R;
     }
-    // static entries are disjoint and sorted by address (upload_tables): binary search for the
-    // last entry starting at or below a
-    uint32_t sl = 0, sr = kp.nsegs;
-    while (sl < sr) {
-        const uint32_t sm = (sl + sr) >> 1;
-        if (cget(kp.segs, sm).lo <= a) sl = sm + 1;
-        else sr = sm;
-    }
-    if (sl > 0) {
-        const Seg g = cget(kp.segs, sl - 1);
-        if (a <= g.hi) {
+    const int32_t si = seg_find(kp, a);
+    if (si >= 0) {
+        const Seg g = cget(kp.segs, (uint32_t)si);
+        {
             uint32_t off = a - g.lo;
             switch (g.kind) {
             case SEG_PLAIN:
@@ -900,6 +905,31 @@ DEV bool lookup_fast_k(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, ui
 }
 DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint64_t r2, uint64_t &r0) {
     return lookup_fast_k(kp, L, mid, r1, r2, r0, false, 0);
+}
+
+// Inline form of helper 12 (tail_call, emulator_linux_helpers.go:649-738) for the usual case: R2
+// is exactly the object of prog-array map `mid` (the LD_IMM64 hint, checked here) and R3 indexes
+// one of its slots.  Returns the program to continue in; -1 when the call fails (R0 set as the
+// helper sets it: the tail-call budget is spent, or the slot holds no program); -2 when the
+// generic path has to decide (cold_tailcall).  helper_tailcall's steps reduce to these for
+// that case: regToMap finds the map object, the slot's first 4 bytes are the program address,
+// and resolving it finds a program entry or not.
+DEV int tail_fast(const KParams &kp, const Lane &L, uint32_t mid, uint64_t r2, uint64_t r3, uint64_t &r0) {
+    if (L.tailcalls >= kp.max_tail_calls) {
+        r0 = (uint64_t)(int64_t)-1;   // -EPERM
+        return -1;
+    }
+    const DMap m = cget(kp.maps, mid);
+    if (r2 != (uint64_t)m.obj_addr || m.type != MIMIC_MAP_PROG_ARRAY || m.key_size != 4 || m.family != FAM_ARRAY ||
+        m.value_size < 4 || (uint32_t)r3 >= m.max_entries)
+        return -2;
+    const uint32_t pa = *(const GAS u32u *)array_value_ptr(kp, m, -1, (uint32_t)r3);
+    const int32_t si = seg_find(kp, pa);
+    if (si < 0 || cget(kp.segs, (uint32_t)si).kind != SEG_PROG) {
+        r0 = (uint64_t)(int64_t)-22;  // -EINVAL
+        return -1;
+    }
+    return (int)cget(kp.segs, (uint32_t)si).id;
 }
 
 // ---------------------------------------------------------------------------------------
