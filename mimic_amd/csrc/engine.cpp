@@ -375,12 +375,13 @@ static void build_host_tables(const std::vector<HostProg> &progs, std::vector<DI
 static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     build_host_tables(vm->progs, vm->h_all, vm->h_dp);
-    // map hints of LD_IMM64 constants that are array-family map objects (AUX_MAPHINT)
+    // map hints of LD_IMM64 constants that are map objects (AUX_MAPHINT): the JIT's inline
+    // helpers check the map at run time, so a hint only selects a fast path
     for (auto &x : vm->h_all) {
         if (AUX_H(x.aux) != H_LDIMM || x.k > 0xffffffffull) continue;
         for (size_t m = 0; m < vm->maps.size() && m < 0xfffe; m++) {
             const HostMap &hm = vm->maps[m];
-            if (hm.obj_addr == (uint32_t)x.k && (hm.family == FAM_ARRAY || hm.family == FAM_PERCPU_ARRAY)) {
+            if (hm.obj_addr == (uint32_t)x.k) {
                 x.aux = (x.aux & 0xffffu) | ((uint32_t)(m + 1) << 16);
                 break;
             }

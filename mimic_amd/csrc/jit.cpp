@@ -102,8 +102,12 @@ class Gen {
         ntres = !(nr && nr[0] == '0');
         const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
         skb_fields = !(sf && sf[0] == '0');
+        const char *hf = getenv("MIMIC_JIT_HASH");   // 0: hash-map lookups always through the generic helper
+        hash_fast = !(hf && hf[0] == '0');
         const char *ti = getenv("MIMIC_JIT_TAIL");   // 0: tail calls always through the generic helper
         tail_inline = !(ti && ti[0] == '0');
+        const char *ce = getenv("MIMIC_JIT_CENSUS");   // 1: per-packet slow-path call counts in place of steps
+        census = ce && ce[0] == '1';
         const char *el = getenv("MIMIC_JIT_ELIDE");   // 0: forwarded key stores are always made
         elide = !(el && el[0] == '0');
         const char *wnd = getenv("MIMIC_JIT_WINDOW");   // 0: early loads one by one
@@ -155,7 +159,9 @@ class Gen {
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
     bool skb_fields = true;    // MIMIC_JIT_SKBFIELD=0: no per-field sk_buff access code
+    bool hash_fast = true;     // MIMIC_JIT_HASH=0: no inline hash-map lookups
     bool tail_inline = true;   // MIMIC_JIT_TAIL=0: no inline tail calls
+    bool census = false;       // MIMIC_JIT_CENSUS=1: diagnostics (tools/cold_census.py)
     bool elide = true;         // MIMIC_JIT_ELIDE=0: no deferred stack stores
     bool window = true;        // MIMIC_JIT_WINDOW=0: no windowed early loads
     int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
@@ -229,6 +235,10 @@ class Gen {
         }
         E.line("  Lane L;");
         E.line("  Spill sp_;");
+        if (census) {
+            E.line("  uint32_t coldn_ = 0;");
+            E.line("#define COLD_CALL_K(k_, call_, pc_) do { coldn_ += 1u << (k_); COLD_CALL(call_, pc_); } while (0)");
+        }
         E.line("  L.lane = g;");
         E.line("  L.cpu = lane_cpu(kp, g);");
         E.line("  uint32_t ex_begin = 0, ex_count = 0;");
@@ -316,6 +326,7 @@ class Gen {
         E.line("    uint64_t r0 = 0, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0, r9 = 0;");
         E.line("    uint64_t r10 = kp.static_next + kp.frame_size;");
         E.line("    uint32_t steps = 0;");
+        if (census) E.line("    coldn_ = 0;");
         E.line("    int st_ = 0;");
         E.line("    int32_t epc_ = -1;");
         if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
@@ -340,13 +351,22 @@ class Gen {
             E.line("    if (kq_.r0) *gp(kq_.r0 + i) = r0;");
             E.line("    if (kq_.status) *gp(kq_.status + i) = (uint8_t)st_;");
         }
-        E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
+        if (census) E.line("    if (kq_.steps) st_nt(kq_.steps + i, coldn_);   // census: slow-path calls, not steps");
+        else E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
         E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
         E.line("    }");
         E.line("    lane_steps += steps;");
         E.line("  }");
         E.line("  if (kp.lane_steps) st_nt(kp.lane_steps + g, lane_steps);");
         E.line("}");
+        if (census) {   // diagnostics: each slow-path call adds 1 to its kind's 4-bit field of coldn_
+            static const char *kinds[] = {"cold_load(", "cold_store(", "cold_lookup(", "cold_update(", "cold_delete(",
+                                          "cold_tailcall(", "cold_ldabs(", "cold_adjust_tail("};
+            for (int k = 0; k < 8; k++) {
+                const std::string from = std::string("COLD_CALL(") + kinds[k], to = "COLD_CALL_K(" + std::to_string(4 * k) + ", " + kinds[k];
+                for (size_t q = E.s.find(from); q != std::string::npos; q = E.s.find(from, q + to.size())) E.s.replace(q, from.size(), to);
+            }
+        }
         return E.s;
     }
 
@@ -753,6 +773,41 @@ class Gen {
         return skb_fields && off >= 0 && (uint32_t)off < 192 && (n == 1 || n == 2 || n == 4 || n == 8);
     }
 
+    // sk_buff programs: does `base` hold the bpf_flow_keys (1) or bpf_sock (2) pointer, read from
+    // the context earlier in this basic block (LDX from flow_keys / sk)?  0 otherwise.  The
+    // generated code still compares the address, so a wrong guess only costs the fast path.
+    int skb_ptr_kind(uint32_t i, uint32_t base) const {
+        if (ctx != CTX_SKB || !skb_fields || base > 10) return 0;
+        const ProgView *pv = nullptr;
+        for (auto &q : P) if (q.id == cur_prog) pv = &q;
+        if (!pv) return 0;
+        for (int64_t j = (int64_t)i - 1; j >= (int64_t)blk_start; j--) {
+            const DInsn &x = pv->ins[j];
+            const uint32_t h = AUX_H(x.aux), d = insn_dst(x);
+            if (h == H_CALL || h == H_LDABS || h == H_CALL_LOCAL) return 0;
+            if ((h == H_ALU64 || h == H_ALU32 || h == H_LDIMM || h == H_SLOW || h == H_LDX) && d == base) {
+                if (h != H_LDX || insn_src(x) > 10 || hint(insn_src(x)) != HINT_CTX) return 0;
+                const int32_t o = insn_off(x);
+                return (o == 144 || o == 148) ? 1 : (o == 168 || o == 172) ? 2 : 0;
+            }
+        }
+        return 0;
+    }
+    // the inline bpf_flow_keys / bpf_sock field access for a base skb_ptr_kind() recognised
+    void skb_ptr_fast(uint32_t i, uint32_t base, int32_t off, uint32_t n, bool load, const std::string &v, std::string &pre) {
+        const int k = fast_paths ? skb_ptr_kind(i, base) : 0;
+        if (!k || off < 0 || off > (k == 1 ? 40 : 80) || !(n == 1 || n == 2 || n == 4 || n == 8)) return;
+        const char *fn = k == 1 ? "fk_convert_" : "sk_convert_";
+        const char *at = k == 1 ? "L.ka + SKB_SK_SIZE + 1u + " : "L.ka + ";
+        if (load)
+            E.line("%sif (L.rec && ga_ == %s%uu) { uint64_t v_ = 0; const int s_ = %s(*L.rec, %uu, %uu, v_, true); if (s_) TERM(s_, %u); %s = v_; }",
+                   pre.c_str(), at, (uint32_t)off, fn, (uint32_t)off, n, i, v.c_str());
+        else
+            E.line("%sif (L.rec && ga_ == %s%uu) { uint64_t v_ = %s; const int s_ = %s(*L.rec, %uu, %uu, v_, false); if (s_) TERM(s_, %u); }",
+                   pre.c_str(), at, (uint32_t)off, v.c_str(), fn, (uint32_t)off, n, i);
+        pre = "    else ";
+    }
+
     void load(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &dst) {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         std::string pre = "    ";
@@ -774,6 +829,7 @@ class Gen {
                    " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
             pre = "    else ";
         }
+        skb_ptr_fast(i, base, off, n, true, dst, pre);
         // generic GetEntry + Load (cold, out of line)
         E.line("%s{ COLD_CALL(cold_load(kp, sp_, ga_, %uu), %u); %s = sp_.v; }", pre.c_str(), n, i, dst.c_str());
     }
@@ -804,6 +860,7 @@ class Gen {
                    " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
             pre = "    else ";
         }
+        skb_ptr_fast(i, base, off, n, false, val, pre);
         // generic GetEntry + Store (cold); the stack / xdp_md state it may change comes back
         E.line("%s{ COLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u);", pre.c_str(), n, val.c_str(), i);
         if (stage)  // a store that reached the packet updates the window too
@@ -925,16 +982,19 @@ class Gen {
             if (j >= 0) {  // inline array lookup when R1 is the map object the LD_IMM64 hint names
                 E.line("    { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", p.base + (uint32_t)j);
                 auto f = fwd_call.find({p.id, i});
-                if (f != fwd_call.end() && elided.count({p.id, f->second})) {
+                // array maps inline (with the key forwarded from its stack store when known); then
+                // hash maps inline (the key read from the stack); then the generic helper
+                const std::string hfast = hash_fast ? "mh_ && hash_lookup_fast(kp, L, mh_ - 1u, r1, r2, r0)" : "false";
+                if (f != fwd_call.end()) {
                     E.line("      if (!(mh_ && lookup_fast_k(kp, L, mh_ - 1u, r1, r2, r0, true, fwd%u_%u_))) {", p.id, f->second);
-                    const DInsn &sx = p.ins[f->second];   // the deferred stack store, then the generic lookup
-                    store(f->second, insn_dst(sx), insn_off(sx), AUX_SZ(sx.aux), "fwd" + std::to_string(p.id) + "_" + std::to_string(f->second) + "_", true);
-                    E.line("      COLD_CALL(cold_lookup(kp, sp_), %u); } }", i);
-                } else if (f != fwd_call.end())
-                    E.line("      if (!(mh_ && lookup_fast_k(kp, L, mh_ - 1u, r1, r2, r0, true, fwd%u_%u_))) COLD_CALL(cold_lookup(kp, sp_), %u); }",
-                           p.id, f->second, i);
-                else
-                    E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) COLD_CALL(cold_lookup(kp, sp_), %u); }", i);
+                    if (elided.count({p.id, f->second})) {   // the deferred stack store first: the others read the key
+                        const DInsn &sx = p.ins[f->second];
+                        store(f->second, insn_dst(sx), insn_off(sx), AUX_SZ(sx.aux), "fwd" + std::to_string(p.id) + "_" + std::to_string(f->second) + "_", true);
+                    }
+                } else {
+                    E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) {");
+                }
+                E.line("      if (!(%s)) COLD_CALL(cold_lookup(kp, sp_), %u); } }", hfast.c_str(), i);
             } else {
                 E.line("    COLD_CALL(cold_lookup(kp, sp_), %u);", i);
             }

@@ -907,6 +907,39 @@ DEV bool lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint
     return lookup_fast_k(kp, L, mid, r1, r2, r0, false, 0);
 }
 
+// key words of a hash-map key held in registers (h_hash / h_key_eq read them repeatedly)
+struct KeyRegs {
+    uint64_t w0, w1, w2, w3;
+    __device__ uint64_t word(uint32_t q) const { return q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3; }
+};
+// Inline form of helper 1 for hash / per-CPU hash maps (LinuxHashMap.Lookup :134-155,
+// LinuxPerCPUHashMap.Lookup :537-561): R1 is exactly the map object `mid` hints, the key (at
+// most 32 bytes) lies on the stack.  Then regToMap and derefMapKey reduce to reading the key
+// words off the stack (unwritten bytes read as zero, as stack_load does), and the lookup is the
+// lock-free probe of hashmap.h.  Returns false when the case does not apply (cold_lookup).
+DEV bool hash_lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1, uint64_t r2, uint64_t &r0) {
+    const DMap m = cget(kp.maps, mid);
+    if ((uint32_t)r1 != m.obj_addr || (m.family != FAM_HASH && m.family != FAM_PERCPU_HASH) || m.key_size == 0 ||
+        m.key_size > 32)
+        return false;
+    if (m.family == FAM_PERCPU_HASH && (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu)) return false;   // error path: cold
+    const uint32_t K = m.key_size, ko = (uint32_t)r2 - kp.static_next;
+    if ((uint64_t)ko + K > kp.stack_size) return false;
+    KeyRegs ks;
+    ks.w0 = stack_load(kp, L, ko, K < 8 ? K : 8);
+    ks.w1 = K > 8 ? stack_load(kp, L, ko + 8, K - 8 < 8 ? K - 8 : 8) : 0;
+    ks.w2 = K > 16 ? stack_load(kp, L, ko + 16, K - 16 < 8 ? K - 16 : 8) : 0;
+    ks.w3 = K > 24 ? stack_load(kp, L, ko + 24, K - 24) : 0;
+    const int32_t idx = h_find(h_table(kp.arena, m), ks, h_hash(ks, K), nullptr);
+    r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
+    if (idx >= 0) {
+        L.t_lo = hash_value_addr(m, L.cpu, 0);
+        L.t_n = m.max_entries * m.value_size + 1;
+        L.t_ptr = hash_value_ptr(kp, m, L.cpu, 0);
+    }
+    return true;
+}
+
 // Inline form of helper 12 (tail_call, emulator_linux_helpers.go:649-738) for the usual case: R2
 // is exactly the object of prog-array map `mid` (the LD_IMM64 hint, checked here) and R3 indexes
 // one of its slots.  Returns the program to continue in; -1 when the call fails (R0 set as the
