@@ -102,6 +102,8 @@ class Gen {
         ntres = !(nr && nr[0] == '0');
         const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
         skb_fields = !(sf && sf[0] == '0');
+        const char *sl = getenv("MIMIC_JIT_SKBLDS");   // 0: sk_buff records read from global memory
+        skb_lds_knob = !(sl && sl[0] == '0');
         const char *hf = getenv("MIMIC_JIT_HASH");   // 0: hash-map lookups always through the generic helper
         hash_fast = !(hf && hf[0] == '0');
         const char *ti = getenv("MIMIC_JIT_TAIL");   // 0: tail calls always through the generic helper
@@ -159,6 +161,9 @@ class Gen {
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
     bool skb_fields = true;    // MIMIC_JIT_SKBFIELD=0: no per-field sk_buff access code
+    bool skb_lds_knob = true;  // MIMIC_JIT_SKBLDS=0: no LDS copy of the sk_buff record
+    bool skb_lds = false;
+    static constexpr uint32_t kSrecQ = 21;   // 8-byte words per LDS record slot (SkbRec is 20)
     bool hash_fast = true;     // MIMIC_JIT_HASH=0: no inline hash-map lookups
     bool tail_inline = true;   // MIMIC_JIT_TAIL=0: no inline tail calls
     bool census = false;       // MIMIC_JIT_CENSUS=1: diagnostics (tools/cold_census.py)
@@ -233,6 +238,10 @@ class Gen {
             E.line("  __shared__ PWin pwin_;");
             E.line("  const uint32_t tl0_ = threadIdx.x;");
         }
+        skb_lds = ctx == CTX_SKB && fast_paths && skb_fields && skb_lds_knob;
+        // the sk_buff records of the block's lanes, 168 bytes apart (an odd number of 8-byte
+        // words: lanes reading the same field hit different banks); nothing reads them back
+        if (skb_lds) E.line("  __shared__ uint64_t srec_[%uu * 256u];", kSrecQ);
         E.line("  Lane L;");
         E.line("  Spill sp_;");
         if (census) {
@@ -292,6 +301,11 @@ class Gen {
             // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107, skb.h)
             E.line("    uint64_t r1 = 0;");
             E.line("    const int ls_ = skb_load(kp, L, i, r1);");
+            if (skb_lds) {   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
+                E.line("    if (!ls_) { const GAS uint64_t *s_ = (const GAS uint64_t *)L.rec; uint64_t *d_ = srec_ + %uu * threadIdx.x;", kSrecQ);
+                E.line("      for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) d_[q] = s_[q];");
+                E.line("      L.rec = (SkbRec *)d_; }");
+            }
             // the window starts at the packet (skb.data = packet memory + 32)
             if (stage && fast_paths)
                 E.line("    const uint32_t W_ = ls_ ? 0u : win_stage(pwin_, tl_, L.pkt + SKB_HEADROOM, L.M - SKB_HEADROOM);");

@@ -81,7 +81,13 @@ struct SkbRes {
     int st;   // 0 or a status
 };
 
-SKB_DEV uint16_t skb_rd16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+// packet bytes for the header walk: b[k] is byte k of the packet; here plain memory
+struct SkbBytes {
+    const uint8_t *p;
+    __device__ uint8_t operator[](uint32_t k) const { return p[k]; }
+};
+template <class B>
+SKB_DEV uint16_t skb_rd16(const B &b, uint32_t k) { return (uint16_t)((b[k] << 8) | b[k + 1]); }
 
 // ---------------------------------------------------------------------------------------
 // SKBuffFromBytes (emulator_linux_sk_buff.go:108-265) over gopacket v1.1.19's eager decode
@@ -95,7 +101,8 @@ SKB_DEV uint16_t skb_rd16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[
 // ---------------------------------------------------------------------------------------
 enum { SW_DONE, SW_ETH, SW_ETYPE, SW_LLC, SW_DOT1Q, SW_IP, SW_PROTO };
 
-SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
+template <class B>
+SKB_DEV int skb_walk(const B &pkt, uint32_t L, SkbRec &r) {
     uint32_t st = SW_ETH, o = 0, len = L, t = 0;
     uint32_t link = 0, net = 0, trans = 0;
     for (uint32_t guard = 0; guard < L + 64; guard++) {  // each Dot1Q step consumes 4 bytes
@@ -103,7 +110,7 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
         case SW_ETH: {
             if (len < 14) return 0;      // "Ethernet packet too small": no layer
             if (link++) return 1;
-            t = skb_rd16(pkt + o + 12);
+            t = skb_rd16(pkt, o + 12);
             uint32_t pl = len - 14;
             if (t < 0x0600) {            // 802.3 length field: EthernetTypeLLC, payload trimmed
                 if (pl > t) pl = t;
@@ -127,15 +134,15 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
             break;
         case SW_LLC: {   // LLC + SNAP (llc.go)
             if (len < 3) return 0;
-            const uint8_t *d = pkt + o;
+            const uint32_t d = o;
             uint32_t hl = 3;
-            if (!(d[2] & 1) || (d[2] & 3) == 1) {   // I- or S-format: 2-byte control
+            if (!(pkt[d + 2] & 1) || (pkt[d + 2] & 3) == 1) {   // I- or S-format: 2-byte control
                 if (len < 4) return 0;
                 hl = 4;
             }
-            if ((d[0] & 0xfe) != 0xaa || (d[1] & 0xfe) != 0xaa) return 0;
+            if ((pkt[d] & 0xfe) != 0xaa || (pkt[d + 1] & 0xfe) != 0xaa) return 0;
             if (len - hl < 5) return 0;
-            t = skb_rd16(d + hl + 3);
+            t = skb_rd16(pkt, d + hl + 3);
             o += hl + 5;
             len -= hl + 5;
             st = SW_ETYPE;
@@ -143,11 +150,10 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
         }
         case SW_DOT1Q: {
             if (len < 4) return 0;
-            const uint8_t *d = pkt + o;
-            r.vlan_proto = skb_rd16(d + 2);   // Dot1Q.Type (:182)
-            r.vlan_tci = skb_rd16(d);
+            r.vlan_proto = skb_rd16(pkt, o + 2);   // Dot1Q.Type (:182)
+            r.vlan_tci = skb_rd16(pkt, o);
             r.vlan_present = 1;
-            t = skb_rd16(d + 2);
+            t = skb_rd16(pkt, o + 2);
             o += 4;
             len -= 4;
             st = SW_ETYPE;
@@ -156,7 +162,7 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
         case SW_IP: {    // decodeIPv4orIPv6
             if (len == 0) return 0;
             const uint32_t v = pkt[o] >> 4;
-            const uint8_t *d = pkt + o;
+            const uint32_t d = o;
             if (v == 4) {
                 if (net++) return 1;
                 r.family = 2;
@@ -167,25 +173,25 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
                 }
                 r.ip[0].kind = 2; r.ip[0].off = o + 12;
                 r.ip[1].kind = 2; r.ip[1].off = o + 16;
-                const uint32_t ihl = d[0] & 0x0f, ff = skb_rd16(d + 6);
-                uint32_t tl = skb_rd16(d + 2);
+                const uint32_t ihl = pkt[d] & 0x0f, ff = skb_rd16(pkt, d + 6);
+                uint32_t tl = skb_rd16(pkt, d + 2);
                 if (tl == 0) tl = len;   // TSO
                 if (tl < 20 || ihl < 5 || ihl * 4 > tl) return 0;
                 uint32_t dl = len;
                 if (len > tl) dl = tl;
                 else if (len < tl && ihl * 4 > len) return 0;
                 for (uint32_t q = 20; q < ihl * 4;) {   // options: a malformed one ends the decode
-                    const uint8_t ot = d[q];
+                    const uint8_t ot = pkt[d + q];
                     if (ot == 0) break;
                     if (ot == 1) { q++; continue; }
                     if (ihl * 4 - q < 2) return 0;
-                    const uint8_t ol = d[q + 1];
+                    const uint8_t ol = pkt[d + q + 1];
                     if (ihl * 4 - q < ol) return 0;
                     if (ol <= 2) return 0;
                     q += ol;
                 }
                 if ((ff & 0x2000) || (ff & 0x1fff)) return 0;   // a fragment
-                t = d[9];
+                t = pkt[d + 9];
                 o += ihl * 4;
                 len = dl - ihl * 4;
                 st = SW_PROTO;
@@ -199,8 +205,8 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
                 }
                 r.ip[2].kind = 2; r.ip[2].off = o + 8;
                 r.ip[3].kind = 2; r.ip[3].off = o + 24;
-                uint32_t next = d[6];
-                const uint32_t plen = skb_rd16(d + 4);
+                uint32_t next = pkt[d + 6];
+                const uint32_t plen = skb_rd16(pkt, d + 4);
                 if (next == 0) return 0;   // Hop-by-Hop / jumbograms: not restated
                 if (plen == 0) return 0;
                 uint32_t po = o + 40, pl = len - 40;
@@ -232,8 +238,8 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
             if (t == 6) {            // TCP: the layer is added even when its decode fails
                 if (trans++) return 1;
                 if (len >= 20) {
-                    r.sport = skb_rd16(pkt + o);
-                    r.dport = skb_rd16(pkt + o + 2);
+                    r.sport = skb_rd16(pkt, o);
+                    r.dport = skb_rd16(pkt, o + 2);
                 }
                 return 0;
             }
@@ -242,10 +248,9 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
             {                        // UDP (udp.go) and the tunnels behind it
                 if (trans++) return 1;
                 if (len < 8) return 0;
-                const uint8_t *d = pkt + o;
-                r.sport = skb_rd16(d);
-                r.dport = skb_rd16(d + 2);
-                const uint32_t ulen = skb_rd16(d + 4);
+                r.sport = skb_rd16(pkt, o);
+                r.dport = skb_rd16(pkt, o + 2);
+                const uint32_t ulen = skb_rd16(pkt, o + 4);
                 uint32_t plen;
                 if (ulen >= 8) plen = (ulen > len ? len : ulen) - 8;
                 else if (ulen == 0) plen = len - 8;
@@ -263,7 +268,6 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
                     break;
                 }
                 const uint32_t po = o + 8;
-                const uint8_t *q = pkt + po;
                 if (port == 4789) {          // VXLAN, then Ethernet
                     if (plen < 8) return 0;
                     o = po + 8;
@@ -271,16 +275,16 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
                     st = SW_ETH;
                 } else if (port == 6081) {   // Geneve: 8 + options, then the protocol type
                     if (plen < 8) return 0;
-                    const uint32_t hl = 8 + (q[0] & 0x3f) * 4u;
+                    const uint32_t hl = 8 + (pkt[po] & 0x3f) * 4u;
                     if (plen < hl) return 0;
-                    t = skb_rd16(q + 2);
+                    t = skb_rd16(pkt, po + 2);
                     o = po + hl;
                     len = plen - hl;
                     st = SW_ETYPE;
                 } else if (port == 2152) {   // GTPv1-U, then IPv4 / IPv6
                     if (plen < 8) return 0;
-                    const uint32_t hl = (q[0] & 0x07) ? 12 : 8;
-                    if ((q[0] & 0x04) || plen <= hl) return 0;
+                    const uint32_t hl = (pkt[po] & 0x07) ? 12 : 8;
+                    if ((pkt[po] & 0x04) || plen <= hl) return 0;
                     o = po + hl;
                     len = plen - hl;
                     st = SW_IP;
@@ -297,7 +301,8 @@ SKB_DEV int skb_walk(const uint8_t *pkt, uint32_t L, SkbRec &r) {
 }
 
 // SKBuffFromBytes + the parts of LinuxContextSKBuff.Load that do not depend on addresses
-SKB_DEV void skb_init(const uint8_t *pkt, uint32_t L, SkbRec &r) {
+template <class B>
+SKB_DEV void skb_init(const B &pkt, uint32_t L, SkbRec &r) {
     uint64_t *w = (uint64_t *)&r;
     for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) w[q] = 0;
     r.ip[0].n = 4; r.ip[1].n = 4; r.ip[2].n = 16; r.ip[3].n = 16;   // make(net.IP, 4/16)

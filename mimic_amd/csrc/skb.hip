@@ -15,17 +15,43 @@
 
 #include "runtime.h"
 
+// The header walk reads single bytes at data-dependent offsets.  As global byte loads each one is
+// a memory instruction touching 64 scattered lines per wave; instead each thread first copies the
+// first PREP_W bytes of its packet into LDS with 8-byte loads, and the walk reads bytes from there
+// (bytes past the window, deep tunnels only, come from global memory).  LDS layout
+// [dword][thread]: the threads of a wave reading the same header offset hit consecutive dwords.
+#define PREP_W 128u
+#define PREP_T 256u
+struct SkbLdsBytes {
+    const uint32_t *w;   // this block's window words; thread t's dword q at w[q * PREP_T + t]
+    const uint8_t *p;    // the packet in global memory
+    uint32_t t;
+    __device__ uint8_t operator[](uint32_t k) const {
+        if (k < PREP_W) return (uint8_t)(w[(k >> 2) * PREP_T + t] >> (8 * (k & 3)));
+        return p[k];
+    }
+};
+
 // packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them
-extern "C" __global__ __launch_bounds__(256) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
-                                                                       const uint64_t *__restrict__ pkt_off,
-                                                                       const uint32_t *__restrict__ pkt_len,
-                                                                       uint32_t n, SkbRec *__restrict__ rec,
-                                                                       uint64_t *__restrict__ foot) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
+                                                                          const uint64_t *__restrict__ pkt_off,
+                                                                          const uint32_t *__restrict__ pkt_len,
+                                                                          uint32_t n, SkbRec *__restrict__ rec,
+                                                                          uint64_t *__restrict__ foot) {
+    __shared__ uint32_t win[(PREP_W / 4) * PREP_T];
+    const uint32_t t = threadIdx.x, i = blockIdx.x * blockDim.x + t;
+    if (i >= n) return;   // no block-wide barrier below: each thread reads only its own window
     const uint32_t L = pkt_len[i];
+    const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
+    // 8-byte chunks that start inside the packet (a chunk may run into the 64-byte tailroom)
+    for (uint32_t c = 0; c < PREP_W / 8; c++) {
+        if (8 * c >= L) break;
+        const uint64_t v = *(const u64u *)(pkt + 8 * c);
+        win[(2 * c) * PREP_T + t] = (uint32_t)v;
+        win[(2 * c + 1) * PREP_T + t] = (uint32_t)(v >> 32);
+    }
     SkbRec r;
-    skb_init(pkt_data + pkt_off[i] + SKB_HEADROOM, L, r);
+    skb_init(SkbLdsBytes{win, pkt, t}, L, r);
     rec[i] = r;
     foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
 }
@@ -52,7 +78,7 @@ extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pk
                                      size_t scan_bytes, uint64_t *state, uint64_t init_base, uint32_t use_init,
                                      hipStream_t st) {
     if (n) {
-        hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pkt_data, pkt_off, pkt_len, n,
+        hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
                            rec, foot);
         if (hipGetLastError() != hipSuccess) return -1;
         size_t bytes = scan_bytes;
