@@ -261,11 +261,12 @@ class Gen {
         if (forward && elide)
             for (auto &p : P) analyze_elide(p);
         for (auto &f : fwd_store) E.line("  uint32_t fwd%u_%u_ = 0;   // value of the stack store at P%u slot %u", f.first, f.second, f.first, f.second);
-        if (speculate && fast_paths && !stage && ctx == CTX_XDP && !all_leaders)
+        if (speculate && fast_paths && !stage && !all_leaders)
             for (auto &p : P) analyze_spec(p);
         for (auto &u : spec_use)
             E.line("  %s sp%u_%u_ = 0;   // packet load of P%u slot %u, issued early", u.second == 8 ? "uint64_t" : "uint32_t",
                    u.first.first, u.first.second, u.first.first, u.first.second);
+        if (!spec_use.empty()) E.line("  uint32_t spv_ = 1;   // 0 once a store through R10 left the stack: early values void");
         // The packet loop is software-pipelined by one descriptor: packet j+1's index, offset and
         // length are loaded while packet j runs (they travel with packet j's first loads), which
         // takes one dependent HBM round trip off every packet after the first.
@@ -341,6 +342,7 @@ class Gen {
         E.line("    uint64_t r10 = kp.static_next + kp.frame_size;");
         E.line("    uint32_t steps = 0;");
         if (census) E.line("    coldn_ = 0;");
+        if (!spec_use.empty()) E.line("    spv_ = 1;");
         E.line("    int st_ = 0;");
         E.line("    int32_t epc_ = -1;");
         if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
@@ -577,8 +579,12 @@ class Gen {
             for (uint32_t i = s0; i < e; i++) {
                 const DInsn &x = p.ins[i];
                 const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x);
-                if (h == H_LDX && sr <= 10 && hint(sr) == HINT_PKT && !mapv[sr] && live < (uint32_t)speculate) {
-                    const uint32_t hp = std::max(std::max(def[sr], kill), start);
+                // xdp_md: packet loads through a packet pointer; sk_buff: LD_ABS / LD_IND
+                const bool xdp_ld = ctx == CTX_XDP && h == H_LDX && sr <= 10 && hint(sr) == HINT_PKT && !mapv[sr];
+                const bool ind = (x.aux & AUX_X) != 0;
+                const bool skb_abs = ctx == CTX_SKB && h == H_LDABS && (!ind || sr <= 10);
+                if ((xdp_ld || skb_abs) && live < (uint32_t)speculate) {
+                    const uint32_t hp = skb_abs && !ind ? std::max(kill, start) : std::max(std::max(def[sr], kill), start);
                     if (last_jcc >= (int)hp) {   // a branch lies between the issue point and the load
                         spec_use[{p.id, i}] = AUX_SZ(x.aux);
                         spec_at[{p.id, hp}].push_back(i);
@@ -597,7 +603,21 @@ class Gen {
                     break;
                 case H_NOP:
                     break;
-                default:   // stores, calls, LD_ABS, anything generic: nothing moves above it
+                case H_ST: case H_STX:
+                    // a store through R10 stays in the stack on its fast path; its slow path (an
+                    // address outside the stack) clears spv_, which voids every early value
+                    if (d == 10) break;
+                    kill = i + 1;
+                    for (auto &r : def) r = i + 1;
+                    for (auto &m : mapv) m = false;
+                    break;
+                case H_LDABS:   // writes R0-R5, no memory
+                    for (int r = 0; r <= 5; r++) {
+                        def[r] = i + 1;
+                        mapv[r] = false;
+                    }
+                    break;
+                default:   // stores, calls, anything generic: nothing moves above it
                     kill = i + 1;
                     for (auto &r : def) r = i + 1;
                     for (auto &m : mapv) m = false;
@@ -610,6 +630,13 @@ class Gen {
     void emit_spec_one(const ProgView &p, uint32_t j, const char *pre) {
         const DInsn &x = p.ins[j];
         const uint32_t n = AUX_SZ(x.aux);
+        if (AUX_H(x.aux) == H_LDABS) {   // packet bytes at 32 + imm (+ index register), BigEndian applied at the use
+            const bool ind = (x.aux & AUX_X) != 0;
+            E.line("%sga_ = (uint32_t)%s%s;   // early LD_ABS for slot %u", pre, imm(x.k).c_str(), ind ? (" + (uint32_t)" + reg(insn_src(x))).c_str() : "", j);
+            E.line("%sif ((uint64_t)(uint32_t)(%uu + ga_) + %uu <= L.M) sp%u_%u_ = (%s)ld_n(L.pkt + (uint32_t)(%uu + ga_), %uu);", pre,
+                   SKB_HEADROOM_J, n, p.id, j, n == 8 ? "uint64_t" : "uint32_t", SKB_HEADROOM_J, n);
+            return;
+        }
         E.line("%sga_ = %s;   // early load for slot %u", pre, addr(insn_src(x), insn_off(x)).c_str(), j);
         E.line("%sif ((uint64_t)(uint32_t)(ga_ - P) + %uu <= L.M) sp%u_%u_ = (%s)%s(L.pkt + (uint32_t)(ga_ - P), %uu);", pre, n, p.id, j,
                n == 8 ? "uint64_t" : "uint32_t", nt ? "ld_n_nt" : "ld_n", n);
@@ -621,7 +648,10 @@ class Gen {
         auto it = spec_at.find({p.id, i});
         if (it == spec_at.end()) return;
         std::map<uint32_t, std::vector<uint32_t>> by_base;
-        for (uint32_t j : it->second) by_base[insn_src(p.ins[j])].push_back(j);
+        for (uint32_t j : it->second) {
+            if (AUX_H(p.ins[j].aux) == H_LDABS) emit_spec_one(p, j, "    ");
+            else by_base[insn_src(p.ins[j])].push_back(j);
+        }
         for (auto &bb : by_base) {
             const std::vector<uint32_t> &js = bb.second;
             int64_t lo = INT64_MAX, hi = INT64_MIN;
@@ -827,7 +857,7 @@ class Gen {
         std::string pre = "    ";
         bool sp = spec_use.count({cur_prog, i}) > 0;
         for (auto &f : fast_forms(base, n, "")) {   // the first form of a packet access is the packet
-            if (sp) sp = false, E.line("%sif (%s) %s = sp%u_%u_;", pre.c_str(), f.cond.c_str(), dst.c_str(), cur_prog, i);
+            if (sp) sp = false, E.line("%sif (spv_ && %s) %s = sp%u_%u_;", pre.c_str(), f.cond.c_str(), dst.c_str(), cur_prog, i);
             else E.line("%sif (%s) %s = %s;", pre.c_str(), f.cond.c_str(), dst.c_str(), f.val.c_str());
             pre = "    else ";
         }
@@ -853,7 +883,8 @@ class Gen {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         if (!deferred && elided.count({cur_prog, i})) {   // the write happens in the lookup's cold path
             const auto f = fast_forms(base, n, val);
-            E.line("    if (!(%s)) { COLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u); }", f.at(0).cond.c_str(), n, val.c_str(), i);
+            E.line("    if (!(%s)) { %sCOLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u); }", f.at(0).cond.c_str(),
+                   base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "", n, val.c_str(), i);
             return;
         }
         std::string pre = "    ";
@@ -876,7 +907,8 @@ class Gen {
         }
         skb_ptr_fast(i, base, off, n, false, val, pre);
         // generic GetEntry + Store (cold); the stack / xdp_md state it may change comes back
-        E.line("%s{ COLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u);", pre.c_str(), n, val.c_str(), i);
+        E.line("%s{ %sCOLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u);", pre.c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
+               n, val.c_str(), i);
         if (stage)  // a store that reached the packet updates the window too
             E.line("      if (sp_.po) win_store_rel(pwin_, tl_, W_, sp_.po - 1u, %uu, %uu, %s); }", wb(), n, ord(val, n).c_str());
         else E.line("    }");
@@ -1081,6 +1113,9 @@ class Gen {
             if (stage)
                 E.line("      if ((uint64_t)ga_ + %s <= W_) r0 = %s; else r0 = %s;", N.c_str(),
                        ord("win_load(pwin_, tl_, ga_, " + N + ")", n).c_str(),
+                       ord("ld_n(L.pkt + (uint32_t)(" + std::to_string(SKB_HEADROOM_J) + "u + ga_), " + N + ")", n).c_str());
+            else if (spec_use.count({cur_prog, i}))
+                E.line("      r0 = spv_ ? %s : %s;", ord("sp" + std::to_string(cur_prog) + "_" + std::to_string(i) + "_", n).c_str(),
                        ord("ld_n(L.pkt + (uint32_t)(" + std::to_string(SKB_HEADROOM_J) + "u + ga_), " + N + ")", n).c_str());
             else
                 E.line("      r0 = %s;", ord("ld_n(L.pkt + (uint32_t)(" + std::to_string(SKB_HEADROOM_J) + "u + ga_), " + N + ")", n).c_str());

@@ -957,6 +957,12 @@ DEV int tail_fast(const KParams &kp, const Lane &L, uint32_t mid, uint64_t r2, u
         m.value_size < 4 || (uint32_t)r3 >= m.max_entries)
         return -2;
     const uint32_t pa = *(const GAS u32u *)array_value_ptr(kp, m, -1, (uint32_t)r3);
+    if (kp.nprogs <= 16) {   // program entries [addr, addr + 8]: compare against each (uniform loads)
+        for (uint32_t k = 0; k < kp.nprogs; k++)
+            if (pa - cget(kp.progs, k).addr <= 8u) return (int)k;
+        r0 = (uint64_t)(int64_t)-22;  // -EINVAL
+        return -1;
+    }
     const int32_t si = seg_find(kp, pa);
     if (si < 0 || cget(kp.segs, (uint32_t)si).kind != SEG_PROG) {
         r0 = (uint64_t)(int64_t)-22;  // -EINVAL
