@@ -137,6 +137,7 @@ def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=
         if is_hash(m):
             out["hash"][m["name"]] = maps[m["name"]].Contents()
     out["steps_total"] = vm.LastSteps()
+    out["last_exec"] = vm.LastExec()
     vm.close()
     return out
 

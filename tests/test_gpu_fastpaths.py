@@ -1,0 +1,317 @@
+"""The JIT's inline fast paths against the oracle, each driven into its edge cases and fallbacks
+(jit.cpp: early loads and their void flag, inline hash lookups, inline tail calls, flow-keys /
+sock pointer accesses, early LD_ABS / LD_IND).  Every run compares per-packet R0 / status / steps
+/ err_pc, the packet memory and every map with the oracle, bit for bit."""
+import numpy as np
+import pytest
+
+from harness import (Scenario, assert_same, kernel_of, run_engine, run_engine_skb, run_oracle, run_oracle_skb,
+                     run_sequence_engine, run_sequence_oracle, assert_same_sequence)
+from mimic_amd import asm as A
+from mimic_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+S, FK, SK = A.SKB, A.FLOW_KEYS, A.SOCK
+
+
+def _prog(name, items, maps=()):
+    raw, rel = A.assemble(items)
+    return (name, raw, rel)
+
+
+# ---------------------------------------------------------------------------------------------
+# early packet loads (analyze_spec): a store through R10 that leaves the stack lands in the packet
+# between the early load's issue point and its use -- the void flag must force the reload
+# ---------------------------------------------------------------------------------------------
+def _escape_prog(off, size=1, through_stack=False):
+    # R10 = St + 256; packet data = St + 2048 + 1 (headroom 0): R10 + 1805 = data + 12 (the
+    # store leaves the stack and lands on the loaded bytes); R10 - 8 stays in the stack
+    r10_off = -8 if through_stack else 1805
+    return _prog("esc", [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),
+        A.ldx(4, 3, 6, 4),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 34),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.st(size, 10, r10_off, 0xAB),
+        A.jmp("jeq", 2, 0, "out"),
+        A.ldx(size, 0, 2, off),
+        A.ldx(1, 5, 2, off + 1),
+        A.alu64("lsh", 0, 8),
+        A.alu64("or", 0, 5, reg=True),
+        A.exit_(),
+        "out",
+        A.mov64_imm(0, 2),
+        A.exit_(),
+    ])
+
+
+def _escape_scenarios():
+    return [Scenario(vcpus=4, progs=[_escape_prog(12, s, st)]) for s in (1, 2, 4) for st in (False, True)]
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_early_load_voided_by_stack_escape(gpu, k):
+    sc = _escape_scenarios()[k]
+    n = 2048
+    buf, off, lens = W.make_packets(n, sizes=(64, 128), weights=(1, 1))
+    cpu = W.schedule_cpu(n, 4, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
+
+
+# ---------------------------------------------------------------------------------------------
+# inline hash-map lookups: key sizes around the 8-byte words and the 32-byte limit, keys at odd
+# stack offsets, partly unwritten keys (unwritten stack bytes read as zero), per-CPU hash maps
+# ---------------------------------------------------------------------------------------------
+HASH_CASES = [(1, 1, 4), (1, 3, 5), (1, 4, 8), (1, 8, 9), (1, 12, 16), (1, 16, 21), (1, 20, 24), (1, 32, 40),
+              (1, 33, 40), (1, 40, 48), (5, 4, 8), (5, 16, 19)]
+
+
+def _hash_prog(K, ko):
+    items = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),
+        A.ldx(4, 3, 6, 4),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 8),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(4, 7, 2, 0),
+        A.alu64("and", 7, 0x3F),               # 64 distinct keys
+        A.stx(1, 10, -ko, 7),                  # key byte 0 ...
+    ]
+    if K >= 4:
+        items.append(A.stx(2, 10, -ko + 2, 7))  # ... bytes 2-3; byte 1 stays unwritten (zero)
+    if K >= 12:
+        items += [A.mov64_reg(8, 7), A.alu64("xor", 8, 0x55), A.stx(4, 10, -ko + 8, 8)]
+    items += [
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -ko),
+        A.ld_map_fd(1, "h"),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jeq", 0, 0, "miss"),
+        A.ldx(8, 0, 0, 0),
+        A.exit_(),
+        "miss",
+        A.mov64_imm(0, 0xFFFF),
+        A.exit_(),
+        "out",
+        A.mov64_imm(0, 2),
+        A.exit_(),
+    ]
+    return _prog("hl", items)
+
+
+def _key_of(v, K):
+    b = bytearray(K)
+    b[0] = v & 0xFF
+    if K >= 4:
+        b[2] = v & 0xFF
+        b[3] = 0
+    if K >= 12:
+        w = (v ^ 0x55).to_bytes(4, "little")
+        b[8:12] = w
+    return bytes(b)
+
+
+def _hash_scenario(mtype, K, ko):
+    m = dict(name="h", type=mtype, key_size=K, value_size=8, max_entries=64)
+    init = []
+    for v in range(0, 64, 2):          # every other key present: hits and misses
+        cpus = range(4) if mtype == 5 else [0]
+        for c in cpus:
+            init.append(("h", _key_of(v, K), (v * 1000 + c + 7).to_bytes(8, "little"), c))
+    return Scenario(vcpus=4, maps=[m], progs=[_hash_prog(K, ko)], map_init=init)
+
+
+@pytest.mark.parametrize("mtype,K,ko", HASH_CASES)
+def test_inline_hash_lookup(gpu, mtype, K, ko):
+    sc = _hash_scenario(mtype, K, ko)
+    n = 4096
+    buf, off, lens = W.make_packets(n)
+    cpu = W.schedule_cpu(n, 4, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    assert_same(o, e)
+    hits = (o["r0"] != 0xFFFF) & (o["r0"] != 2)
+    assert hits.any() and (~hits).any()
+
+
+def test_inline_hash_lookup_unset_cpu(gpu):
+    """Per-CPU hash lookups from a process whose CPU ID is unset (-1) fail in the helper: the
+    inline form must leave them to the generic path."""
+    sc = _hash_scenario(5, 8, 9)
+    n = 512
+    buf, off, lens = W.make_packets(n)
+    cpu = np.where(np.arange(n) % 3 == 0, -1, np.arange(n) % 4).astype(np.int32)
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    assert_same(o, e)
+    assert (o["status"] != 0).any()
+
+
+# ---------------------------------------------------------------------------------------------
+# inline tail calls: a program slot, an empty slot, an index past max_entries, a self-call loop
+# that runs out of the tail-call budget, and a prog-array pointer that is not the exact object
+# ---------------------------------------------------------------------------------------------
+def _tail_progs(r2_bump):
+    entry = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 7, 6, 0),
+        A.ldx(4, 8, 6, 4),
+        A.mov64_reg(4, 7),
+        A.alu64("add", 4, 1),
+        A.jmp("jgt", 4, 8, "out", reg=True),
+        A.ldx(1, 9, 7, 0),
+        A.alu64("and", 9, 7),
+        A.mov64_reg(1, 6),
+        A.ld_map_fd(2, "progs"),
+    ]
+    if r2_bump:
+        entry.append(A.alu64("add", 2, r2_bump))
+    entry += [
+        A.mov64_reg(3, 9),
+        A.call(A.FN_TAIL_CALL),
+        A.mov64_reg(0, 9),
+        A.alu64("add", 0, 100),
+        A.exit_(),
+        "out",
+        A.mov64_imm(0, 2),
+        A.exit_(),
+    ]
+    other = [A.mov64_imm(0, 7), A.alu64("add", 0, 9, reg=True), A.exit_()]
+    return [_prog("entry", entry), _prog("other", other)]
+
+
+def _tail_scenario(bump):
+    # slots: 0 -> other, 1 empty, 2 -> entry (loops until the budget is spent), 3 -> other;
+    # indexes 4..7 lie past max_entries
+    return Scenario(vcpus=4, maps=[dict(name="progs", type=3, key_size=4, value_size=4, max_entries=4)],
+                    progs=_tail_progs(bump), prog_array=[("progs", 0, 1), ("progs", 2, 0), ("progs", 3, 1)],
+                    max_tail_calls=9)
+
+
+@pytest.mark.parametrize("bump", [0, 3])
+def test_inline_tail_calls(gpu, bump):
+    sc = _tail_scenario(bump)
+    n = 2048
+    buf, off, lens = W.make_packets(n)
+    cpu = W.schedule_cpu(n, 4, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    assert_same(o, e)
+    assert len(set(o["r0"].tolist())) >= 5
+
+
+# ---------------------------------------------------------------------------------------------
+# sk_buff: flow-keys and sock pointer accesses at every offset and size (including read-only
+# fields, slices that panic and offsets past the object, which take the generic path)
+# ---------------------------------------------------------------------------------------------
+def _ptr_cases():
+    cases = []
+    for o in list(range(0, 44, 1)):
+        for n in (1, 2, 4, 8):
+            cases.append(("fk", o, n, True))
+            cases.append(("fk", o, n, False))
+    for o in list(range(0, 84, 2)):
+        for n in (1, 4):
+            cases.append(("sk", o, n, True))
+    for o in (0, 16, 20, 3):
+        cases.append(("sk", o, 4, False))
+    return cases
+
+
+def _ptr_prog(kind, o, n, load):
+    field = S["flow_keys"] if kind == "fk" else S["sk"]
+    items = [A.mov64_reg(6, 1), A.ldx(4, 1, 6, field)]
+    if load:
+        items += [A.ldx(n, 0, 1, o)]
+    else:
+        items += [A.mov64_imm(3, 0x1234567), A.stx(n, 1, o, 3), A.ldx(n, 0, 1, o & ~(n - 1))]
+    items += [A.exit_()]
+    return _prog(f"{kind}_{o}_{n}_{int(load)}", items)
+
+
+def _ptr_groups(per=40):
+    cs = _ptr_cases()
+    return [cs[a:a + per] for a in range(0, len(cs), per)]
+
+
+def _ptr_scenario(group):
+    return Scenario(vcpus=2, progs=[_ptr_prog(*c) for c in group])
+
+
+@pytest.mark.parametrize("g", range(len(_ptr_groups())))
+def test_flow_keys_and_sock_accesses(gpu, g):
+    sc = _ptr_scenario(_ptr_groups()[g])
+    buf, off, lens = W.make_skb_packets(8, sizes=(64, 90), weights=(1, 1))
+    cpu = np.zeros(8, np.int32)
+    runs = [dict(skb=True, buf=buf, off=off, lens=lens, cpu=cpu, entry=k, ifindex=1) for k in range(len(sc.progs))]
+    o = run_sequence_oracle(sc, runs)
+    e = run_sequence_engine(sc, runs)
+    assert_same_sequence(o, e, tag=f"group {g}")
+
+
+# ---------------------------------------------------------------------------------------------
+# sk_buff: early LD_ABS / LD_IND -- the index register changes, and a packet store sits between
+# ---------------------------------------------------------------------------------------------
+def _ldabs_prog(store):
+    items = [
+        A.mov64_reg(6, 1),
+        A.ld_abs(1, 14),
+        A.mov64_reg(7, 0),
+        A.alu64("and", 7, 0x0F),
+        A.alu64("lsh", 7, 2),
+        A.jmp("jlt", 7, 20, "bad"),
+        A.ld_abs(1, 23),
+        A.mov64_reg(9, 0),
+        A.stx(4, 10, -4, 0),
+    ]
+    if store:   # rewrite packet byte 23 (the protocol) through skb->data, BigEndian memory
+        items += [A.ldx(4, 2, 6, S["data"]), A.ldx(4, 3, 6, S["data_end"]), A.mov64_reg(4, 2), A.alu64("add", 4, 24),
+                  A.jmp("jgt", 4, 3, "bad", reg=True), A.st(1, 2, 23, 0x5A)]
+    items += [
+        A.ld_ind(2, 7, 14),
+        A.mov64_reg(8, 0),
+        A.alu64("add", 7, 2),
+        A.jmp("jeq", 8, 0, "skip"),
+        A.ld_ind(2, 7, 14),
+        A.alu64("xor", 8, 0, reg=True),
+        "skip",
+        A.ld_abs(1, 23),
+        A.alu64("lsh", 8, 8),
+        A.alu64("or", 8, 0, reg=True),
+        A.alu64("lsh", 8, 8),
+        A.alu64("or", 8, 9, reg=True),
+        A.mov64_reg(0, 8),
+        A.exit_(),
+        "bad",
+        A.mov64_imm(0, 2),
+        A.exit_(),
+    ]
+    return _prog("ldabs", items)
+
+
+@pytest.mark.parametrize("store", [False, True])
+def test_early_ld_abs(gpu, store):
+    sc = Scenario(vcpus=4, progs=[_ldabs_prog(store)])
+    n = 4096
+    buf, off, lens = W.make_skb_packets(n, **W.IMIX, variety=0.3)
+    cpu = W.schedule_cpu(n, 4, "interleaved")
+    o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=1)
+    e = run_engine_skb(sc, buf, off, lens, cpu, ifindex=1)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
+
+
+def jit_kernels():
+    ks = [kernel_of(sc) for sc in _escape_scenarios()]
+    ks += [kernel_of(_hash_scenario(*c)) for c in HASH_CASES]
+    ks += [kernel_of(_tail_scenario(b)) for b in (0, 3)]
+    ks += [kernel_of(_ptr_scenario(g), ctx=1) for g in _ptr_groups()]
+    ks += [kernel_of(Scenario(vcpus=4, progs=[_ldabs_prog(s)]), ctx=1) for s in (False, True)]
+    return ks

@@ -128,7 +128,7 @@ def test_every_gpu_test_kernel_generates():
     from mimic_amd import jit as J
 
     count = 0
-    for name in ("test_gpu_kat", "test_gpu_skb", "test_gpu_parity", "test_gpu_hash"):
+    for name in ("test_gpu_kat", "test_gpu_skb", "test_gpu_parity", "test_gpu_hash", "test_gpu_fastpaths"):
         mod = importlib.import_module(name)
         for raws, ctx in mod.jit_kernels():
             assert "mimic_jit_kernel" in J.kernel_source(raws, ctx)
