@@ -117,6 +117,8 @@ EXPORTS = {
     "mimic_skb_release": (C.c_int, [C.c_void_p]),
     "mimic_jit_source_for_ctx": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32,
                                              C.c_char_p, C.c_size_t]),
+    "mimic_jit_source_vc": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32,
+                                       C.POINTER(C.c_uint32), C.c_uint32, C.c_char_p, C.c_size_t]),
     "mimic_jit_prebuild_ctx": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32]),
     "mimic_jit_cache_source": (C.c_int, [C.c_char_p]),
     "mimic_process_new": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,

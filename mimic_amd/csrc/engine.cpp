@@ -53,6 +53,12 @@ struct HostMap {
     uint32_t keys_addr, ht_cap, rec_q, nlocks, fl_cap;
 };
 
+// can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
+bool vc_row_ok(uint32_t family, uint32_t max_entries, uint32_t value_size) {
+    const uint64_t rb = (uint64_t)max_entries * value_size;
+    return family == FAM_PERCPU_ARRAY && rb > 0 && rb <= 32 && (rb & 7) == 0;
+}
+
 struct HostProg {
     std::string name;
     std::vector<DInsn> ins;
@@ -1278,7 +1284,15 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     bool jit = vm->exec_mode == MIMIC_EXEC_JIT && !step;   // stepping runs on the interpreter
     if (jit && !vm->jit_fn[ctx]) {
         std::string log;
-        if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx]),
+        std::vector<uint32_t> vc;   // LD_IMM64 slots naming a per-CPU array whose row the lane value cache can hold
+        for (size_t s = 0; s < vm->h_all.size(); s++) {
+            const DInsn &x = vm->h_all[s];
+            const uint32_t mh = AUX_MAPHINT(x.aux);
+            if (AUX_H(x.aux) != H_LDIMM || !mh || mh > vm->maps.size()) continue;
+            const HostMap &hm = vm->maps[mh - 1];
+            if (vc_row_ok(hm.family, hm.max_entries, hm.value_size)) vc.push_back((uint32_t)s);
+        }
+        if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx], &vc),
                               &vm->jit_fn[ctx], &log))
             return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
     }
@@ -1513,6 +1527,11 @@ long mimic_jit_source_for(const void *const *progs, const uint32_t *n_slots, uin
 
 long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
                               char *buf, size_t cap) {
+    return mimic_jit_source_vc(progs, n_slots, n_progs, ctx_kind, nullptr, 0, buf, cap);
+}
+
+long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
+                         const uint32_t *vc_slots, uint32_t n_vc, char *buf, size_t cap) {
     if (ctx_kind != MIMIC_CTX_XDP && ctx_kind != MIMIC_CTX_SKB) return MIMIC_EINVAL;
     std::vector<HostProg> hp(n_progs);
     for (uint32_t p = 0; p < n_progs; p++) {
@@ -1522,7 +1541,13 @@ long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots,
     std::vector<DInsn> all;
     std::vector<DProg> dp;
     build_host_tables(hp, all, dp);
-    const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr);
+    std::vector<uint32_t> vc;
+    for (uint32_t q = 0; q < n_vc; q++) {
+        const uint32_t p = vc_slots[2 * q], s = vc_slots[2 * q + 1];
+        if (p >= dp.size() || s >= dp[p].n) return MIMIC_EINVAL;
+        vc.push_back(dp[p].base + s);
+    }
+    const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr, &vc);
     if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);
     return (long)src.size();
 }

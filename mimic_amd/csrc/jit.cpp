@@ -96,6 +96,10 @@ class Gen {
         nt = ntv && ntv[0] == '1';
         const char *pfv = getenv("MIMIC_JIT_PREFETCH");   // 0: no descriptor prefetch
         prefetch = !(pfv && pfv[0] == '0');
+        const char *xv = getenv("MIMIC_JIT_XPF");   // 1: next-packet header window prefetch
+        xpf_knob = xv && xv[0] == '1';
+        const char *vcv = getenv("MIMIC_JIT_VC");   // 0: no lane value cache
+        vc_knob = !(vcv && vcv[0] == '0');
         const char *fw = getenv("MIMIC_JIT_FWD");   // 0: no stack-store -> lookup key forwarding
         forward = !(fw && fw[0] == '0');
         const char *nr = getenv("MIMIC_JIT_NTRES");   // 0: per-packet results stored as plain stores
@@ -174,6 +178,19 @@ class Gen {
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
     bool prefetch = true;      // MIMIC_JIT_PREFETCH=0: no next-packet descriptor prefetch
+    bool xpf_knob = false;     // MIMIC_JIT_XPF=1: next-packet header window prefetch (measured slower)
+    bool vc_knob = true;       // MIMIC_JIT_VC=0: no lane value cache (analyze_vc)
+    bool vc_on = false;
+    std::set<uint32_t> vc_ok;  // LD_IMM64 slots (kernel-wide) naming a per-CPU array whose row can be cached
+    uint32_t vc_slot = 0;      // the LD_IMM64 slot (kernel-wide index) whose map hint names the cached map
+    // The cross-packet window prefetch (analyze_xpf): the entry program `prog` makes its first
+    // window of early loads at slot `hp` from register `base` = data + `off` - lo; the window's
+    // bytes lie at data offset `off` .. off + 8 * words of the packet.
+    struct Xpf {
+        bool on = false;
+        uint32_t prog = 0, hp = 0, base = 0, words = 0;
+        int64_t off = 0;
+    } xpf;
     bool cold_inline = true;   // the cold paths are inlined at every site (else called)
     uint32_t cold_sites = 0;
     static constexpr uint32_t kColdInlineSites = 48;
@@ -208,6 +225,7 @@ class Gen {
         if (careful_copies) sites *= 2;
         cold_sites = sites;
         cold_inline = cold_mode == 2 || (cold_mode == 0 && sites <= kColdInlineSites);
+        analyze_vc();
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         E.line("#include \"runtime.h\"");
@@ -222,7 +240,12 @@ class Gen {
         if (getenv("MIMIC_JIT_NOCOLD") && getenv("MIMIC_JIT_NOCOLD")[0] == '1')   // measurement only: no slow paths
             E.line("#define COLD_CALL(call_, pc_) TERM(MIMIC_ERR_ENGINE_HELPER, pc_)");
         else
-            E.line("#define COLD_CALL(call_, pc_) do { SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
+            E.line("#define COLD_CALL(call_, pc_) do { VC_FLUSH(); SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
+        // a cold path may read or write the cached row in memory: write it back and stop caching
+        if (vc_on)
+            E.line("#define VC_FLUSH() do { if (vcd_) { vc_writeback(vcp_, vcb_, vc0_, vc1_, vc2_, vc3_); vcd_ = 0u; } vcv_ = 0u; } while (0)");
+        else
+            E.line("#define VC_FLUSH() do { } while (0)");
         // KParams is read through a pointer to a device copy: fields are loaded (scalar) where
         // they are used instead of all being preloaded into SGPRs from the kernarg segment
         // (which spills SGPRs and costs VGPRs / occupancy)
@@ -250,6 +273,12 @@ class Gen {
         }
         E.line("  L.lane = g;");
         E.line("  L.cpu = lane_cpu(kp, g);");
+        if (vc_on) {
+            // the lane's own row of the per-CPU array the hint names (analyze_vc)
+            E.line("  uint64_t vc0_ = 0, vc1_ = 0, vc2_ = 0, vc3_ = 0; uint32_t vcv_ = 0u, vcd_ = 0u, vclo_ = 0u, vcb_ = 0u; uint8_t *vcp_ = nullptr;");
+            E.line("  { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", vc_slot);
+            E.line("    if (mh_) vc_open(kp, cget(kp.maps, mh_ - 1u), L.cpu, vcp_, vclo_, vcb_, vcv_, vc0_, vc1_, vc2_, vc3_); }");
+        }
         E.line("  uint32_t ex_begin = 0, ex_count = 0;");
         E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = *gp(kp.sched_start + g); ex_count = *gp(kp.sched_start + g + 1) - ex_begin; }");
         E.line("  uint64_t lane_steps = 0;");
@@ -271,7 +300,19 @@ class Gen {
         // length are loaded while packet j runs (they travel with packet j's first loads), which
         // takes one dependent HBM round trip off every packet after the first.
         const bool pf = ctx == CTX_XDP && prefetch;
-        if (pf) {
+        if (!spec_use.empty()) analyze_xpf();
+        if (pf && xpf.on) {
+            // descriptors two packets ahead, the window one packet ahead (analyze_xpf)
+            E.line("  const bool xpf_on_ = kp.entry_prog == %uu && !kp.headroom_arr;   // P%u slot %u window, data + %u, %u words",
+                   xpf.prog, xpf.prog, xpf.hp, (uint32_t)xpf.off, xpf.words);
+            E.line("  uint64_t noff_ = 0, noff2_ = 0; uint32_t nlen_ = 0, nlen2_ = 0, nidx_ = NO_PKT, nidx2_ = NO_PKT, xn_ok_ = 0u, xc_ok_ = 0u;");
+            for (uint32_t q = 0; q < xpf.words; q++) E.line("  uint64_t xn%u_ = 0;", q);
+            E.line("  nidx_ = pkt_index(kp, g, 0u, ex_begin, ex_count);");
+            E.line("  if (nidx_ != NO_PKT) { noff_ = *gp(kp.pkt_off + nidx_); nlen_ = *gp(kp.pkt_len + nidx_); }");
+            emit_xpf_issue("  ");
+            E.line("  nidx2_ = nidx_ != NO_PKT ? pkt_next(kp, nidx_, 1u, ex_begin, ex_count) : NO_PKT;");
+            E.line("  if (nidx2_ != NO_PKT) { noff2_ = *gp(kp.pkt_off + nidx2_); nlen2_ = *gp(kp.pkt_len + nidx2_); }");
+        } else if (pf) {
             E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
             E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
@@ -280,7 +321,15 @@ class Gen {
         E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
         E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
-        if (pf) {
+        if (pf && xpf.on) {
+            E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
+            E.line("    xc_ok_ = xn_ok_;");
+            for (uint32_t q = 0; q < xpf.words; q++) E.line("    const uint64_t xc%u_ = xn%u_;", q, q);
+            E.line("    noff_ = noff2_; nlen_ = nlen2_; nidx_ = nidx2_;");
+            emit_xpf_issue("    ");
+            E.line("    nidx2_ = nidx_ != NO_PKT ? pkt_next(kp, nidx_, j + 2u, ex_begin, ex_count) : NO_PKT;");
+            E.line("    if (nidx2_ != NO_PKT) { noff2_ = *gp(kp.pkt_off + nidx2_); nlen2_ = *gp(kp.pkt_len + nidx2_); }");
+        } else if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
@@ -373,6 +422,7 @@ class Gen {
         E.line("    }");
         E.line("    lane_steps += steps;");
         E.line("  }");
+        if (vc_on) E.line("  VC_FLUSH();");
         E.line("  if (kp.lane_steps) st_nt(kp.lane_steps + g, lane_steps);");
         E.line("}");
         if (census) {   // diagnostics: each slow-path call adds 1 to its kind's 4-bit field of coldn_
@@ -627,6 +677,142 @@ class Gen {
             }
         }
     }
+    // Cross-packet window prefetch.  When the entry program's first early-load window is made in
+    // its first region from a register that provably holds `data + c` (traced from slot 0: r1 is
+    // the xdp_md, a 4-byte load of its offset 0 is `data` while nothing has been stored, moves and
+    // constant adds keep the form) and no slot before the window writes memory or calls, the
+    // window's bytes depend only on the packet: packet j + 1's window is loaded while packet j
+    // runs (its descriptor is loaded two packets ahead), and the window code takes the
+    // prefetched words instead of loading them.  Every packet then waits on one dependent HBM
+    // round trip less.  The prefetch only reads the packet's data bytes [0, len) (room bytes are
+    // zeroed at packet start); a packet too short, a per-packet headroom array or another entry
+    // program takes the normal window code.  Any jump or call to slot 0 disables it; a tail call
+    // clears the flag, so only the packet's own first pass through slot 0 uses the words.
+    void analyze_xpf() {
+        if (!xpf_knob || ctx != CTX_XDP || !prefetch || !window || stage || !fast_paths) return;
+        for (auto &p : P) {
+            if (p.n == 0) continue;
+            bool to0 = false;
+            std::vector<uint32_t> preds(p.n + 1, 0);
+            std::vector<bool> special(p.n + 1, false);
+            for (uint32_t i = 0; i < p.n; i++) {
+                const DInsn &x = p.ins[i];
+                const uint32_t h = AUX_H(x.aux);
+                if ((h == H_JA || h == H_JCC || h == H_CALL_LOCAL) && (x.aux & AUX_JT_OK)) {
+                    const int64_t t = jump_target(x, i);
+                    if (t == 0) to0 = true;
+                    if (t >= 0 && t <= (int64_t)p.n) {
+                        preds[t]++;
+                        if (h == H_CALL_LOCAL) special[t] = true;
+                    }
+                }
+                if (h == H_CALL_LOCAL) special[i + 1] = true;
+                if ((!ends_block(x) || h == H_JCC || (h == H_CALL && (uint32_t)x.k == 12)) && (x.aux & AUX_FALL_OK)) preds[i + 1]++;
+            }
+            if (to0) continue;
+            // the first issue point of the program's early loads
+            uint32_t hp = UINT32_MAX;
+            for (auto &s : spec_at)
+                if (s.first.first == p.id) hp = std::min(hp, s.first.second);
+            if (hp == UINT32_MAX) continue;
+            // symbolic scan of slots [0, hp): 0 unknown, 1 the xdp_md, 2 data + rel[r]
+            int kind[11] = {};
+            int64_t rel[11] = {};
+            kind[1] = 1;
+            bool ok = true;
+            for (uint32_t i = 1; i <= hp; i++) {   // slots 1..hp are reached only by falling through
+                const DInsn &prev = p.ins[i - 1];
+                if (special[i] || preds[i] != 1 || !(AUX_H(prev.aux) == H_JCC || !ends_block(prev)) || !(prev.aux & AUX_FALL_OK)) ok = false;
+            }
+            for (uint32_t i = 0; i < hp && ok; i++) {
+                const DInsn &x = p.ins[i];
+                const uint32_t h = AUX_H(x.aux), op = insn_op(x), d = insn_dst(x), sr = insn_src(x);
+                switch (h) {
+                case H_NOP: case H_JCC: break;
+                case H_ALU64:
+                    if (d > 10) { ok = false; break; }
+                    if (op == 0xbf && sr <= 10) { kind[d] = kind[sr]; rel[d] = rel[sr]; }
+                    else if (op == 0x07 && kind[d] == 2) rel[d] += (int64_t)(int32_t)(uint32_t)x.k;
+                    else kind[d] = 0;
+                    break;
+                case H_ALU32: case H_LDIMM:
+                    if (d > 10) { ok = false; break; }
+                    kind[d] = 0;
+                    break;
+                case H_LDX:
+                    if (d > 10 || sr > 10) { ok = false; break; }
+                    if (op == 0x61 && kind[sr] == 1 && insn_off(x) == 0) { kind[d] = 2; rel[d] = 0; }
+                    else kind[d] = 0;
+                    break;
+                default: ok = false;   // stores, calls, jumps, exits: not traced
+                }
+            }
+            if (!ok) continue;
+            // the window group the emitter makes at hp (emit_spec's grouping)
+            std::map<uint32_t, std::vector<uint32_t>> by_base;
+            for (uint32_t j : spec_at[{p.id, hp}])
+                if (AUX_H(p.ins[j].aux) != H_LDABS) by_base[insn_src(p.ins[j])].push_back(j);
+            for (auto &bb : by_base) {
+                int64_t lo = INT64_MAX, hi = INT64_MIN;
+                for (uint32_t j : bb.second) {
+                    lo = std::min<int64_t>(lo, insn_off(p.ins[j]));
+                    hi = std::max<int64_t>(hi, (int64_t)insn_off(p.ins[j]) + AUX_SZ(p.ins[j].aux));
+                }
+                if (bb.second.size() < 2 || hi - lo > 32 || kind[bb.first] != 2) continue;
+                const int64_t off = rel[bb.first] + lo;
+                if (off < 0 || off > 4096) continue;
+                xpf.on = true;
+                xpf.prog = p.id;
+                xpf.hp = hp;
+                xpf.base = bb.first;
+                xpf.off = off;
+                xpf.words = (uint32_t)((hi - lo + 7) / 8);
+                return;
+            }
+        }
+    }
+    // Lane value cache.  One lane runs every packet of its vCPU, so the lane's row of a per-CPU
+    // array (vCPU c's E * S bytes, at most 32) is touched by no other lane during a launch: the
+    // row is loaded into four registers when the lane starts, loads and stores that fall inside it
+    // become register operations, and it is written back once when the lane ends (only if it was
+    // written).  Before any cold path (which may touch the row in memory: map update, generic
+    // loads and stores) the row is written back and the cache is switched off for the rest of the
+    // lane.  The cached map is the one named by the map hint of the first helper-1 site whose R1
+    // comes from an LD_IMM64 in the same block that names a per-CPU array with E * S <= 32, a
+    // multiple of 8 (vc_ok, from the VM's maps: the choice is part of the source, so kernels for
+    // other maps carry no cache registers); the row is cached when the lane's CPU ID is in [0, V)
+    // (the map is checked again at run time).
+    // cfg 2 measured: one 32-byte load and store per vCPU instead of a counter read-modify-write
+    // (and its L2 write-back) per packet.
+    void analyze_vc() {
+        if (!vc_knob || !fast_paths) return;
+        for (auto &p : P) {
+            if (p.n == 0) continue;
+            const std::vector<uint32_t> Lb = leaders(p);
+            size_t b = 0;
+            for (uint32_t i = 0; i < p.n; i++) {
+                while (b + 1 < Lb.size() && Lb[b + 1] <= i) b++;
+                const DInsn &x = p.ins[i];
+                if (AUX_H(x.aux) != H_CALL || (uint32_t)x.k != 1) continue;
+                const uint32_t save = blk_start;
+                blk_start = Lb[b];
+                const int64_t j = r1_def(p, i);
+                blk_start = save;
+                if (j >= 0 && vc_ok.count(p.base + (uint32_t)j)) {
+                    vc_on = true;
+                    vc_slot = p.base + (uint32_t)j;
+                    return;
+                }
+            }
+        }
+    }
+    // issue the prefetch of the window of the packet at (noff_, nlen_)
+    void emit_xpf_issue(const char *pre) {
+        E.line("%sif (xpf_on_ && nidx_ != NO_PKT && %uu <= nlen_) {", pre, (uint32_t)xpf.off + 8 * xpf.words);
+        E.line("%s  const uint8_t *xp_ = kp.pkt_data + noff_ + kp.headroom + %uu;", pre, (uint32_t)xpf.off);
+        for (uint32_t q = 0; q < xpf.words; q++) E.line("%s  xn%u_ = ld_n(xp_ + %uu, 8u);", pre, q, 8 * q);
+        E.line("%s  xn_ok_ = 1u; } else xn_ok_ = 0u;", pre);
+    }
     void emit_spec_one(const ProgView &p, uint32_t j, const char *pre) {
         const DInsn &x = p.ins[j];
         const uint32_t n = AUX_SZ(x.aux);
@@ -664,17 +850,27 @@ class Gen {
                 continue;
             }
             const uint32_t words = (uint32_t)((hi - lo + 7) / 8);
+            auto cut = [&](const char *wn) {   // the fields out of the window words <wn><q>_
+                const std::string w(wn);
+                for (uint32_t j : js) {
+                    const uint32_t o = (uint32_t)(insn_off(p.ins[j]) - lo), n = AUX_SZ(p.ins[j].aux), q = o / 8, r = o % 8;
+                    std::string v = r == 0 ? w + std::to_string(q) + "_" : "(" + w + std::to_string(q) + "_ >> " + std::to_string(8 * r) + ")";
+                    if (r + n > 8) v = "(" + v + " | (" + w + std::to_string(q + 1) + "_ << " + std::to_string(64 - 8 * r) + "))";
+                    if (n < 8) v = "(" + v + " & 0x" + (n == 1 ? std::string("ffull") : n == 2 ? std::string("ffffull") : std::string("ffffffffull")) + ")";
+                    E.line("        sp%u_%u_ = (%s)%s;", p.id, j, n == 8 ? "uint64_t" : "uint32_t", v.c_str());
+                }
+            };
             E.line("    { const uint32_t wo_ = %s - P;   // window of %u bytes for slots", addr(bb.first, (int32_t)lo).c_str(), 8 * words);
+            if (xpf.on && p.id == xpf.prog && i == xpf.hp && bb.first == xpf.base && words == xpf.words) {
+                E.line("      if (xc_ok_) {   // prefetched while the previous packet ran (analyze_xpf)");
+                E.line("        xc_ok_ = 0u;");
+                cut("xc");
+                E.line("      } else");
+            }
             E.line("      if ((uint64_t)wo_ + %uu <= L.M) {", 8 * words);
             for (uint32_t q = 0; q < words; q++)
                 E.line("        const uint64_t w%u_ = %s(L.pkt + wo_ + %uu, 8u);", q, nt ? "ld_n_nt" : "ld_n", 8 * q);
-            for (uint32_t j : js) {
-                const uint32_t o = (uint32_t)(insn_off(p.ins[j]) - lo), n = AUX_SZ(p.ins[j].aux), q = o / 8, r = o % 8;
-                std::string v = r == 0 ? "w" + std::to_string(q) + "_" : "(w" + std::to_string(q) + "_ >> " + std::to_string(8 * r) + ")";
-                if (r + n > 8) v = "(" + v + " | (w" + std::to_string(q + 1) + "_ << " + std::to_string(64 - 8 * r) + "))";
-                if (n < 8) v = "(" + v + " & 0x" + (n == 1 ? std::string("ffull") : n == 2 ? std::string("ffffull") : std::string("ffffffffull")) + ")";
-                E.line("        sp%u_%u_ = (%s)%s;", p.id, j, n == 8 ? "uint64_t" : "uint32_t", v.c_str());
-            }
+            cut("w");
             E.line("      } else {");
             for (uint32_t j : js) emit_spec_one(p, j, "        ");
             E.line("      } }");
@@ -800,6 +996,12 @@ class Gen {
             f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord(std::string(nt ? "ld_n_nt" : "ld_n") + "(L.pkt + " + o + ", " + N + ")", n),
                          "{ st_n(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
                              (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
+            // the lane's cached per-CPU row (analyze_vc): every access inside the row while the
+            // cache is valid is served here, so memory and registers never disagree
+            if (vc_on)
+                f.push_back({"vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + " + N + " <= vcb_",
+                             "vc_load(vc0_, vc1_, vc2_, vc3_, ga_ - vclo_, " + N + ")",
+                             "{ vc_store(vc0_, vc1_, vc2_, vc3_, ga_ - vclo_, " + N + ", " + v + "); vcd_ = 1u; }"});
             // the map value region the last lookup returned (translation cache, resolve()):
             // [t_lo, t_lo + t_n - 1] with GetEntry's inclusive end, t_n = 0 when empty
             f.push_back({"(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n",
@@ -1060,6 +1262,7 @@ class Gen {
             const int64_t j = fast_paths && tail_inline ? reg_def(p, i, 2) : -1;
             auto jump_table = [&](const char *var) {
                 E.line("        L.tailcalls++;");
+            if (xpf.on) E.line("        xc_ok_ = 0u;");
                 E.line("        switch (%s) {", var);
                 for (auto &q : P) {
                     if (q.n == 0) E.line("        case %u: TERM(MIMIC_ERR_PC_OOB, %u);", q.id, i);
@@ -1260,10 +1463,11 @@ std::map<CacheKey, hipFunction_t> g_cache;
 }  // namespace
 
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
-                             JitInfo *info) {
+                             JitInfo *info, const std::vector<uint32_t> *vc_slots) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
     Gen g(v, ctx_kind);
+    if (vc_slots) g.vc_ok.insert(vc_slots->begin(), vc_slots->end());
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;

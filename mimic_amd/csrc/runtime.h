@@ -168,6 +168,32 @@ DEV T ld_nt(const T *p) { return __builtin_nontemporal_load(gp(p)); }
 template <typename T>
 DEV void st_nt(T *p, T v) { __builtin_nontemporal_store(v, gp(p)); }
 
+// Lane value cache (JIT, jit.cpp analyze_vc): a lane's own per-CPU array row (<= 32 bytes) held
+// in four 64-bit registers w0..w3, little-endian like the arena.  An access of n (1..8) bytes at
+// byte offset o of the row, o + n <= row size, any alignment: selects, no dynamic indexing (which
+// would put the row in scratch).
+DEV uint64_t vc_sel(uint32_t q, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
+    return q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : q == 3 ? w3 : 0ull;
+}
+DEV uint64_t vc_load(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint32_t o, uint32_t n) {
+    const uint32_t q = o >> 3, sh = (o & 7) * 8;
+    const uint64_t lo = vc_sel(q, w0, w1, w2, w3);
+    uint64_t v = lo;
+    if (sh) v = (lo >> sh) | (vc_sel(q + 1, w0, w1, w2, w3) << (64 - sh));
+    return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
+}
+DEV void vc_store(uint64_t &w0, uint64_t &w1, uint64_t &w2, uint64_t &w3, uint32_t o, uint32_t n, uint64_t v) {
+    const uint32_t q = o >> 3, sh = (o & 7) * 8;
+    const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+    v &= m;
+    const uint64_t lm = m << sh, lv = v << sh;
+    const uint64_t hm = sh ? m >> (64 - sh) : 0ull, hv = sh ? v >> (64 - sh) : 0ull;
+    w0 = q == 0 ? ((w0 & ~lm) | lv) : w0;
+    w1 = q == 1 ? ((w1 & ~lm) | lv) : q == 0 ? ((w1 & ~hm) | hv) : w1;
+    w2 = q == 2 ? ((w2 & ~lm) | lv) : q == 1 ? ((w2 & ~hm) | hv) : w2;
+    w3 = q == 3 ? ((w3 & ~lm) | lv) : q == 2 ? ((w3 & ~hm) | hv) : w3;
+}
+
 // private memory: byte offset o of lane l lives at priv + ((o>>3)*priv_lanes + l)*8 + (o&7)
 DEV uint8_t *priv_b(const KParams &kp, uint32_t lane, uint32_t o) {
     return kp.priv + (((size_t)(o >> 3) * kp.priv_lanes + lane) << 3) + (o & 7);
@@ -511,6 +537,32 @@ DEV uint32_t array_value_addr(const DMap &m, int32_t sub, uint32_t k) {
 }
 DEV uint8_t *array_value_ptr(const KParams &kp, const DMap &m, int32_t sub, uint32_t k) {
     return kp.arena + m.dev_off + (sub > 0 ? (size_t)sub * m.dev_stride : 0) + (size_t)k * m.value_size;
+}
+
+// lane value cache (vc_load / vc_store above): open the lane's row of per-CPU array m when it
+// qualifies, and write it back
+DEV void vc_open(const KParams &kp, const DMap &m, int32_t cpu, uint8_t *&p, uint32_t &lo, uint32_t &nb, uint32_t &valid,
+                 uint64_t &w0, uint64_t &w1, uint64_t &w2, uint64_t &w3) {
+    const uint64_t rb = (uint64_t)m.max_entries * m.value_size;
+    if (m.family != FAM_PERCPU_ARRAY || cpu < 0 || (uint32_t)cpu >= m.ncpu || rb == 0 || rb > 32 || (rb & 7)) return;
+    uint8_t *q = array_value_ptr(kp, m, cpu, 0);
+    if ((uintptr_t)q & 7) return;
+    p = q;
+    lo = m.backing_addr + (cpu > 0 ? (uint32_t)cpu * m.addr_period : 0u);
+    nb = (uint32_t)rb;
+    const GAS uint64_t *s = (const GAS uint64_t *)q;
+    w0 = s[0];
+    if (rb > 8) w1 = s[1];
+    if (rb > 16) w2 = s[2];
+    if (rb > 24) w3 = s[3];
+    valid = 1u;
+}
+DEV void vc_writeback(uint8_t *p, uint32_t nb, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
+    GAS uint64_t *d = (GAS uint64_t *)p;
+    d[0] = w0;
+    if (nb > 8) d[1] = w1;
+    if (nb > 16) d[2] = w2;
+    if (nb > 24) d[3] = w3;
 }
 
 // memmove of n bytes from a VM region into the arena (map update, emulator_linux_map_array.go:112)

@@ -30,15 +30,43 @@ def _progs_args(raws: Sequence[bytes]):
     return bufs, arr, ns
 
 
-def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP) -> str:
+def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int]] = ()) -> str:
+    """vc: (program index, slot) of the LD_IMM64 slots that name a per-CPU array whose per-vCPU
+    row is at most 32 bytes, a multiple of 8 -- what a VM with those maps generates (see
+    ``vc_slots``)."""
     lib = _lib.load()
     keep, arr, ns = _progs_args(raws)
-    n = lib.mimic_jit_source_for_ctx(arr, ns, len(raws), ctx, None, 0)
+    flat = [v for pair in vc for v in pair]
+    vca = (C.c_uint32 * max(len(flat), 1))(*flat)
+    n = lib.mimic_jit_source_vc(arr, ns, len(raws), ctx, vca, len(vc), None, 0)
     if n < 0:
         raise ValueError(f"cannot decode programs ({n})")
     buf = C.create_string_buffer(n + 1)
-    lib.mimic_jit_source_for_ctx(arr, ns, len(raws), ctx, buf, n + 1)
+    lib.mimic_jit_source_vc(arr, ns, len(raws), ctx, vca, len(vc), buf, n + 1)
     return buf.value.decode()
+
+
+def vc_slots(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict]) -> List[Tuple[int, int]]:
+    """The (program index, slot) pairs of kernel_source's ``vc`` for programs (raw, relocations
+    [(slot, map name), ...]) loaded next to ``maps`` (name, type, value_size, max_entries): the
+    LD_IMM64 slots whose constant is the object of a per-CPU array (type 6) whose row E * S is at
+    most 32 bytes and a multiple of 8.  A PseudoMapValue slot names the object only when its
+    offset is 0 (Q16: the constant is the object address + offset)."""
+    by_name = {m["name"]: m for m in maps}
+    out = []
+    for pi, (raw, rel) in enumerate(progs):
+        for r in rel:
+            slot, name = r[0], r[1]
+            m = by_name.get(name)
+            if m is None or m["type"] != 6:
+                continue
+            rb = m["max_entries"] * m["value_size"]
+            if not (0 < rb <= 32 and rb % 8 == 0):
+                continue
+            src, off = raw[8 * slot + 1] >> 4, int.from_bytes(raw[8 * slot + 2:8 * slot + 4], "little", signed=True)
+            if src == 1 or (src == 2 and off == 0):
+                out.append((pi, slot))
+    return out
 
 
 def code_object(src: str) -> bytes:
@@ -102,7 +130,7 @@ def _cache_dir() -> str:
     return d
 
 
-def prewarm(kernels: Iterable[Tuple[Sequence[bytes], int]], workers: int = 0) -> Dict[str, float]:
+def prewarm(kernels: Iterable[Tuple], workers: int = 0) -> Dict[str, float]:
     """Compile the kernels of (raws, ctx) program sets into MIMIC_JIT_CACHE using `workers`
     parallel processes (0: min(16, cpus) - 1).  Returns {"kernels": n, "seconds": t}."""
     import time
@@ -110,8 +138,8 @@ def prewarm(kernels: Iterable[Tuple[Sequence[bytes], int]], workers: int = 0) ->
     t0 = time.time()
     _cache_dir()
     srcs: Dict[str, None] = {}
-    for raws, ctx in kernels:
-        srcs[kernel_source(list(raws), ctx)] = None
+    for k in kernels:
+        srcs[kernel_source(list(k[0]), *k[1:])] = None
     todo = sorted(srcs, key=len, reverse=True)        # longest first: better packing
     if not todo:
         return {"kernels": 0, "seconds": 0.0}

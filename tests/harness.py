@@ -58,9 +58,12 @@ def build_oracle(sc: Scenario):
 
 
 def kernel_of(sc: Scenario, ctx: int = 0):
-    """The JIT kernel a scenario's VM runs: (raw programs in load order, batch context) -- what
-    a test module's jit_kernels() lists for the session prewarm (conftest.py)."""
-    return [raw for _, raw, _ in sc.progs], ctx
+    """The JIT kernel a scenario's VM runs: (raw programs in load order, batch context, the
+    LD_IMM64 slots the lane value cache may use) -- what a test module's jit_kernels() lists for
+    the session prewarm (conftest.py)."""
+    from mimic_amd import jit as J
+
+    return [raw for _, raw, _ in sc.progs], ctx, J.vc_slots([(raw, rel) for _, raw, rel in sc.progs], sc.maps)
 
 
 def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0, exec_mode: Optional[str] = None):

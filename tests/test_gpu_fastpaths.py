@@ -5,7 +5,7 @@ sock pointer accesses, early LD_ABS / LD_IND).  Every run compares per-packet R0
 import numpy as np
 import pytest
 
-from harness import (Scenario, assert_same, kernel_of, run_engine, run_engine_skb, run_oracle, run_oracle_skb,
+from harness import (Scenario, assert_same, kernel_of, packets_to_buffer, run_engine, run_engine_skb, run_oracle, run_oracle_skb,
                      run_sequence_engine, run_sequence_oracle, assert_same_sequence)
 from mimic_amd import asm as A
 from mimic_amd import workloads as W
@@ -306,6 +306,90 @@ def test_early_ld_abs(gpu, store):
     e = run_engine_skb(sc, buf, off, lens, cpu, ifindex=1)
     assert_same(o, e)
     assert e["last_exec"] == "jit"
+
+
+# ---------------------------------------------------------------------------------------------
+# cross-packet window prefetch (analyze_xpf, MIMIC_JIT_XPF=1, off by default: measured slower):
+# packet j + 1's first header window is loaded while packet j runs.  Short packets, per-packet headroom, a base of data + c, packet stores followed
+# by a tail call back into the entry program (which must reread the stored bytes), and every
+# schedule must give the oracle's results.
+# ---------------------------------------------------------------------------------------------
+def _xpf_prog(c=0, tail=False):
+    items = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),
+        A.ldx(4, 3, 6, 4),
+        A.mov64_reg(4, 2),
+    ]
+    if c:
+        items.append(A.alu64("add", 4, c))
+    base = 4 if c else 2
+    items += [
+        A.mov64_reg(0, 2),
+        A.alu64("add", 0, 40),
+        A.jmp("jgt", 0, 3, "out", reg=True),
+        A.ldx(2, 5, base, 12),
+        A.ldx(4, 7, base, 14),
+        A.jmp("jeq", 5, 0xFFFF, "out"),
+        A.ldx(4, 8, base, 20),
+        A.alu64("xor", 7, 8, reg=True),
+        A.alu64("xor", 7, 5, reg=True),
+    ]
+    if tail:   # bump byte 12 of the window, then re-enter this program through the prog array
+        items += [
+            A.mov64_reg(9, 5),
+            A.alu64("add", 9, 1),
+            A.stx(1, base, 12, 9),
+            A.mov64_reg(1, 6),
+            A.ld_map_fd(2, "progs"),
+            A.mov64_reg(3, 7),
+            A.alu64("and", 3, 1),
+            A.call(A.FN_TAIL_CALL),
+        ]
+    items += [
+        A.mov64_reg(0, 7),
+        A.exit_(),
+        "out",
+        A.mov64_imm(0, 2),
+        A.exit_(),
+    ]
+    return _prog("xw", items)
+
+
+XPF_CASES = [(0, False), (14, False), (0, True), (6, True)]
+
+
+def _xpf_scenario(c, tail):
+    if not tail:
+        return Scenario(vcpus=8, progs=[_xpf_prog(c)])
+    return Scenario(vcpus=8, maps=[dict(name="progs", type=3, key_size=4, value_size=4, max_entries=2)],
+                    progs=[_xpf_prog(c, True)], prog_array=[("progs", 0, 0), ("progs", 1, 0)], max_tail_calls=3)
+
+
+@pytest.mark.parametrize("case", range(len(XPF_CASES)))
+@pytest.mark.parametrize("room", ["none", "uniform", "per_packet"])
+@pytest.mark.parametrize("sched", ["interleaved", "chunked", "explicit"])
+def test_cross_packet_window_prefetch(gpu, case, room, sched, monkeypatch):
+    monkeypatch.setenv("MIMIC_JIT_XPF", "1")
+    sc = _xpf_scenario(*XPF_CASES[case])
+    import mimic_amd as M
+    from mimic_amd import jit as J
+
+    assert "xpf_on_" in J.kernel_source(*kernel_of(sc))
+    n = 3000
+    rng = np.random.default_rng(case)
+    headroom = {"none": 0, "uniform": 16, "per_packet": rng.integers(0, 4, n) * 8}[room]
+    tailroom = 8 if room == "uniform" else 0
+    pkts = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in rng.choice([20, 36, 40, 41, 60, 64, 128], n)]
+    buf, off, lens = packets_to_buffer(pkts, headroom, tailroom)
+    mode = {"interleaved": M.SCHED_INTERLEAVED, "chunked": M.SCHED_CHUNKED, "explicit": M.SCHED_EXPLICIT}[sched]
+    cpu = rng.integers(0, 8, n).astype(np.int32) if sched == "explicit" else W.schedule_cpu(n, 8, sched)
+    o = run_oracle(sc, buf, off, lens, cpu, headroom=headroom, tailroom=tailroom)
+    e = run_engine(sc, buf, off, lens, cpu if sched == "explicit" else None, headroom=headroom, tailroom=tailroom,
+                   schedule=mode)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
+    assert len(set(o["r0"].tolist())) > 100
 
 
 def jit_kernels():

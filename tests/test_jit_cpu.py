@@ -89,24 +89,42 @@ def test_skb_and_xdp_kernels_differ_only_in_context():
 # register budget of the generated kernels (code-object metadata of the hipRTC build): the
 # kernels are latency-bound, so occupancy is what hides the per-packet HBM round trips
 # ---------------------------------------------------------------------------------------------
-def _resources(raws, ctx=_lib.CTX_XDP):
+def _resources(raws, ctx=_lib.CTX_XDP, vc=()):
     from mimic_amd import jit as J
 
-    return J.kernel_resources(J.code_object(J.kernel_source(raws, ctx)))
+    return J.kernel_resources(J.code_object(J.kernel_source(raws, ctx, vc)))
 
 
-@pytest.mark.parametrize("fn,vgprs,waves", [("prog_classifier", 104, 4), ("prog_parse5", 120, 4)])
+@pytest.mark.parametrize("fn,vgprs,waves", [("prog_classifier", 120, 4), ("prog_parse5", 120, 4)])
 def test_hot_kernels_register_budget(fn, vgprs, waves):
-    """cfg 2 / cfg 3 kernels: unified VGPRs within budget, no VGPR spills, no scratch.  At most a
-    few SGPRs may spill (into VGPR lanes): keeping the per-packet result pointers in SGPRs measured
-    faster than reloading them (jit.cpp, MIMIC_JIT_KQ).  parse5's early packet loads (jit.cpp,
-    analyze_spec) cost it the fifth wave and measured faster anyway: 1.155 vs 1.193 ms per launch;
-    forcing 5 waves (MIMIC_JIT_WAVES=5) measured 1.47 ms.  The classifier's deferred key store
-    (analyze_elide) costs it the fifth wave too and measured 29.1 vs 32.4 us per launch; forced to
-    5 waves (8 VGPRs spilled) 29.6 us."""
-    r = _resources([getattr(W, fn)().raw])
+    """cfg 2 / cfg 3 kernels as the bench's VM generates them (the classifier with its lane value
+    cache): unified VGPRs within budget, no VGPR spills, no scratch.  At most a few SGPRs may
+    spill (into VGPR lanes): keeping the per-packet result pointers in SGPRs measured faster than
+    reloading them (jit.cpp, MIMIC_JIT_KQ).  parse5's early packet loads (jit.cpp, analyze_spec)
+    cost it the fifth wave and measured faster anyway: 1.155 vs 1.193 ms per launch; forcing 5
+    waves (MIMIC_JIT_WAVES=5) measured 1.47 ms.  The classifier's deferred key store
+    (analyze_elide) costs it the fifth wave too and measured 29.1 vs 32.4 us per launch; its lane
+    value cache (analyze_vc, 115 VGPRs) measured 25.5 vs 28.1 us."""
+    from mimic_amd import jit as J
+
+    p = getattr(W, fn)()
+    r = _resources([p.raw], vc=J.vc_slots([(p.raw, p.relocs)], p.maps))
     assert r["vgpr_total"] <= vgprs and r["waves_per_simd"] >= waves, r
     assert r["vgpr_spill"] == 0 and r["sgpr_spill"] <= 4 and r["scratch"] == 0, r
+
+
+def test_lane_value_cache_selection():
+    """The lane value cache is generated only for per-CPU arrays whose row fits four registers."""
+    from mimic_amd import jit as J
+
+    p = W.prog_classifier()
+    assert J.vc_slots([(p.raw, p.relocs)], p.maps) == [(0, 27)]
+    assert "vc_open" in J.kernel_source([p.raw], 0, [(0, 27)])
+    assert "vc_open" not in J.kernel_source([p.raw], 0, [])
+    for E, S, ok in [(4, 8, True), (2, 16, True), (1, 8, True), (5, 4, False), (8, 8, False), (3, 4, False)]:
+        m = dict(p.maps[0], max_entries=E, value_size=S)
+        assert (J.vc_slots([(p.raw, p.relocs)], [m]) != []) == ok
+    assert J.vc_slots([(p.raw, p.relocs)], [dict(p.maps[0], type=2)]) == []   # a plain array: shared by every lane
 
 
 def test_small_kernel_resources():
@@ -128,9 +146,9 @@ def test_every_gpu_test_kernel_generates():
     from mimic_amd import jit as J
 
     count = 0
-    for name in ("test_gpu_kat", "test_gpu_skb", "test_gpu_parity", "test_gpu_hash", "test_gpu_fastpaths"):
+    for name in ("test_gpu_kat", "test_gpu_skb", "test_gpu_parity", "test_gpu_hash", "test_gpu_fastpaths", "test_gpu_vc"):
         mod = importlib.import_module(name)
-        for raws, ctx in mod.jit_kernels():
-            assert "mimic_jit_kernel" in J.kernel_source(raws, ctx)
+        for k in mod.jit_kernels():
+            assert "mimic_jit_kernel" in J.kernel_source(*k)
             count += 1
     assert count > 20
