@@ -222,14 +222,38 @@ DEV void priv_store(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n, ui
 // first write to a word stores the whole zero-extended word.
 // ---------------------------------------------------------------------------------------
 #define STK_FINE 512u
+// LDS stack window (JIT kernels that define MIMIC_LDS_STACK_Q, jit.cpp): the stack bytes
+// [256 - 8Q, 256) -- the top of frame 0, where R10 - k lands in programs without BPF-to-BPF
+// calls -- live in LDS instead of the lane's private memory in HBM, word q of thread t at
+// mimic_lstk_[q * 256 + t] (a wave's same-word accesses hit consecutive banks).  The validity
+// bits work the same for both stores; the window is touched only by its own lane.
+#ifdef MIMIC_LDS_STACK_Q
+#define STK_LDS_LO (256u - 8u * MIMIC_LDS_STACK_Q)
+__shared__ uint64_t mimic_lstk_[MIMIC_LDS_STACK_Q * 256];
+DEV bool stk_in_lds(uint32_t o) { return o - STK_LDS_LO < 8u * MIMIC_LDS_STACK_Q; }
+DEV uint64_t &stk_lw(uint32_t o) { return mimic_lstk_[((o - STK_LDS_LO) >> 3) * 256u + threadIdx.x]; }
+#else
+DEV bool stk_in_lds(uint32_t) { return false; }
+DEV uint64_t &stk_lw(uint32_t) { __builtin_trap(); }
+#endif
 DEV bool stk_valid(const KParams &kp, const Lane &L, uint32_t o) {
     return o < STK_FINE ? ((L.sm0 >> (o >> 3)) & 1) : ((L.sm1 >> ((o - STK_FINE) >> kp.chunk_shift)) & 1);
+}
+// the whole 8-byte word holding stack byte o (o & ~7) := w
+DEV void stk_word_set(const KParams &kp, const Lane &L, uint32_t o, uint64_t w) {
+    if (stk_in_lds(o)) stk_lw(o) = w;
+    else *gp((uint64_t *)priv_b(kp, L.lane, o & ~7u)) = w;
+}
+// one stack byte (valid or not: the caller checks)
+DEV uint32_t stk_byte(const KParams &kp, const Lane &L, uint32_t o) {
+    if (stk_in_lds(o)) return (uint32_t)(stk_lw(o) >> (8 * (o & 7))) & 0xffu;
+    return *gp(priv_b(kp, L.lane, o));
 }
 DEV void stk_touch(const KParams &kp, Lane &L, uint32_t o) {
     if (o < STK_FINE) {
         const uint32_t q = o >> 3;
         if (!((L.sm0 >> q) & 1)) {
-            *gp((uint64_t *)priv_b(kp, L.lane, q << 3)) = 0;
+            stk_word_set(kp, L, q << 3, 0);
             L.sm0 |= 1ull << q;
         }
     } else {
@@ -244,32 +268,48 @@ DEV void stk_touch(const KParams &kp, Lane &L, uint32_t o) {
 DEV uint64_t stack_load(const KParams &kp, const Lane &L, uint32_t o, uint32_t n) {
     if ((o & 7) + n <= 8) {
         if (!stk_valid(kp, L, o)) return 0;
+        if (stk_in_lds(o)) {
+            const uint64_t v = stk_lw(o) >> (8 * (o & 7));
+            return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
+        }
         return ld_n(priv_b(kp, L.lane, o), n);
     }
     uint64_t v = 0;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t oo = o + i;
-        if (stk_valid(kp, L, oo)) v |= (uint64_t)*gp(priv_b(kp, L.lane, oo)) << (8 * i);
+        if (stk_valid(kp, L, oo)) v |= (uint64_t)stk_byte(kp, L, oo) << (8 * i);
     }
     return v;
 }
 DEV void stack_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t v) {
     if ((o & 7) + n <= 8) {
+        const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+        const uint32_t sh = 8 * (o & 7);
         if (o < STK_FINE && !((L.sm0 >> (o >> 3)) & 1)) {
             // first write to this word: store the whole word, zero-extended around the value
-            const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
-            *gp((uint64_t *)priv_b(kp, L.lane, o & ~7u)) = (v & m) << (8 * (o & 7));
+            stk_word_set(kp, L, o, (v & m) << sh);
             L.sm0 |= 1ull << (o >> 3);
             return;
         }
         stk_touch(kp, L, o);
+        if (stk_in_lds(o)) {
+            uint64_t &w = stk_lw(o);
+            w = (w & ~(m << sh)) | ((v & m) << sh);
+            return;
+        }
         st_n(priv_b(kp, L.lane, o), n, v);
         return;
     }
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t oo = o + i;
         stk_touch(kp, L, oo);
-        *gp(priv_b(kp, L.lane, oo)) = (uint8_t)(v >> (8 * i));
+        if (stk_in_lds(oo)) {
+            uint64_t &w = stk_lw(oo);
+            const uint32_t sh = 8 * (oo & 7);
+            w = (w & ~(0xffull << sh)) | ((uint64_t)(uint8_t)(v >> (8 * i)) << sh);
+        } else {
+            *gp(priv_b(kp, L.lane, oo)) = (uint8_t)(v >> (8 * i));
+        }
     }
 }
 

@@ -392,8 +392,64 @@ def test_cross_packet_window_prefetch(gpu, case, room, sched, monkeypatch):
     assert len(set(o["r0"].tolist())) > 100
 
 
+# ---------------------------------------------------------------------------------------------
+# LDS stack window (runtime.h, MIMIC_LDS_STACK_Q): frame 0's top 128 bytes live in LDS, the rest
+# of the stack in HBM.  Stores and loads of every size at offsets around the window's lower edge
+# (R10 - 128), unaligned and straddling it, never-written bytes (read as zero), a stack address
+# read back through another register (the generic path), and a BPF-to-BPF call (frame 1 above).
+# ---------------------------------------------------------------------------------------------
+def _stack_window_prog(variant):
+    items = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),
+        A.ldx(4, 3, 6, 4),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 16),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(8, 7, 2, 0),
+        A.ldx(8, 8, 2, 8),
+        A.mov64_imm(0, 0),
+    ]
+    offs = [-140, -136, -133, -131, -130, -129, -128, -127, -125, -121, -120, -117, -8, -3, -256]
+    for k, o in enumerate(offs):
+        n = (1, 2, 4, 8)[(k + variant) % 4]
+        items += [A.stx(n, 10, o, 7 if k % 2 else 8), A.alu64("rsh", 7, 3), A.alu64("add", 8, 0x1357)]
+    for k, o in enumerate(offs + [-144, -200, -64]):   # read back with other sizes / alignments
+        n = (8, 4, 2, 1)[(k + variant) % 4]
+        o2 = o - (k % 3)
+        if o2 < -256:
+            o2 = -256
+        items += [A.ldx(n, 5, 10, o2), A.alu64("xor", 0, 5, reg=True), A.alu64("lsh", 0, 1)]
+    items += [A.mov64_reg(9, 10), A.alu64("add", 9, -130), A.ldx(4, 5, 9, 0), A.alu64("add", 0, 5, reg=True),
+              A.stx(2, 9, 1, 0), A.ldx(8, 5, 10, -136), A.alu64("xor", 0, 5, reg=True)]
+    if variant == 1:   # a BPF-to-BPF call: the callee's frame lies above the window
+        items += [A.mov64_reg(1, 0), A.call("sub"), A.alu64("xor", 0, 1, reg=True)]
+    items += [A.exit_(), "out", A.mov64_imm(0, 2), A.exit_()]
+    if variant == 1:
+        items += ["sub", A.stx(8, 10, -128, 1), A.stx(1, 10, -129, 1), A.ldx(8, 0, 10, -129), A.ldx(8, 2, 10, -8),
+                  A.alu64("add", 0, 2, reg=True), A.exit_()]
+    return _prog("stkw", items)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_lds_stack_window(gpu, variant):
+    from mimic_amd import jit as J
+
+    sc = Scenario(vcpus=4, progs=[_stack_window_prog(variant)])
+    assert "MIMIC_LDS_STACK_Q" in J.kernel_source(*kernel_of(sc))
+    n = 2048
+    buf, off, lens = W.make_packets(n, sizes=(14, 64, 128), weights=(1, 2, 2))
+    cpu = W.schedule_cpu(n, 4, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
+    assert len(set(o["r0"].tolist())) > 1000
+
+
 def jit_kernels():
-    ks = [kernel_of(sc) for sc in _escape_scenarios()]
+    ks = [kernel_of(Scenario(vcpus=4, progs=[_stack_window_prog(v)])) for v in range(4)]
+    ks += [kernel_of(sc) for sc in _escape_scenarios()]
     ks += [kernel_of(_hash_scenario(*c)) for c in HASH_CASES]
     ks += [kernel_of(_tail_scenario(b)) for b in (0, 3)]
     ks += [kernel_of(_ptr_scenario(g), ctx=1) for g in _ptr_groups()]

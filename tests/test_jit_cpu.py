@@ -133,9 +133,23 @@ def test_small_kernel_resources():
 
 
 def test_cfg4_cfg5_kernels_have_no_vgpr_scratch_spill():
-    """cfg 4 (hash insert) and cfg 5 (sk_buff tail-call chain) kernels: no VGPR spills to scratch."""
+    """cfg 4 (hash insert) kernel: no VGPR spills to scratch.  Its LDS stack window costs it the
+    third wave (169 VGPRs) and measured faster anyway: 0.179 vs 0.197 ms per launch; forced back to
+    3 waves (MIMIC_JIT_WAVES=3) 0.180 ms."""
     r = _resources([W.prog_flowtrack().raw])
-    assert r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 3, r
+    assert r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 2 and r["lds"] == 16 * 256 * 8, r
+
+
+def test_lds_stack_window_selection():
+    """The LDS stack window is generated when a stack store is made for real: not for the
+    classifier (its one key store is deferred into the lookup's cold path) and not for sk_buff
+    kernels (their LDS holds the SkbRec slots)."""
+    from mimic_amd import jit as J
+
+    assert "MIMIC_LDS_STACK_Q 16" in J.kernel_source([W.prog_flowtrack().raw])
+    assert "MIMIC_LDS_STACK_Q" not in J.kernel_source([W.prog_classifier().raw])
+    progs, _, _ = W.skb_programs()
+    assert "MIMIC_LDS_STACK_Q" not in J.kernel_source([p.raw for p in progs], _lib.CTX_SKB)
 
 
 def test_every_gpu_test_kernel_generates():
