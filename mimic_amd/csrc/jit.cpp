@@ -100,6 +100,8 @@ class Gen {
         xpf_knob = xv && xv[0] == '1';
         const char *lq = getenv("MIMIC_JIT_LDSSTK");   // 8-byte words of the LDS stack window (0: none)
         if (lq) lds_stack_q = (uint32_t)std::min(32, std::max(0, atoi(lq)));
+        const char *dv = getenv("MIMIC_JIT_DISPATCH");   // 0: a jump table at every tail-call site
+        dispatch_knob = !(dv && dv[0] == '0');
         const char *vcv = getenv("MIMIC_JIT_VC");   // 0: no lane value cache
         vc_knob = !(vcv && vcv[0] == '0');
         const char *fw = getenv("MIMIC_JIT_FWD");   // 0: no stack-store -> lookup key forwarding
@@ -199,6 +201,19 @@ class Gen {
     static constexpr uint32_t kColdInlineSites = 48;
     bool stage = false;        // MIMIC_JIT_STAGE=1: LDS packet window
     bool has_tail() const { return any_tail; }
+    // Tail calls jump between programs.  With a jump table at every tail-call site as well as at
+    // the entry, the programs form a cycle with several entries (irreducible control flow), which
+    // the AMDGPU backend must restructure -- at a large register cost (cfg 5: 282 VGPRs without
+    // the slow paths).  One dispatch block (D_) that the entry and every tail call go through
+    // keeps the cycle single-entry.  MIMIC_JIT_DISPATCH=0: the per-site jump tables.
+    bool dispatch_knob = true;
+    bool dispatch_on() const { return dispatch_knob && any_tail; }
+    std::string nonempty_cases() const {
+        std::string c;
+        for (auto &q : P)
+            if (q.n) c += "    case " + std::to_string(q.id) + "u:";
+        return c;
+    }
     uint32_t ctx = CTX_XDP;    // the batch context this kernel is generated for
 
     std::string source() {
@@ -413,13 +428,32 @@ class Gen {
         E.line("    int st_ = 0;");
         E.line("    int32_t epc_ = -1;");
         if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
-        E.line("    switch (kp.entry_prog) {");
-        for (auto &p : P) {
-            if (p.n == 0) E.line("    case %u: steps = 1; TERM(MIMIC_ERR_PC_OOB, 0);", p.id);  // vm.go:297-299
-            else E.line("    case %u: goto P%u_0;", p.id, p.id);
+        if (dispatch_on()) {
+            // one dispatch block for the entry and every tail call (see dispatch_on)
+            E.line("    uint32_t cur_;   // no initializer: the TERM gotos above jump past it");
+            E.line("    cur_ = kp.entry_prog;");
+            E.line("    switch (cur_) {");
+            for (auto &p : P)
+                if (p.n == 0) E.line("    case %u: steps = 1; TERM(MIMIC_ERR_PC_OOB, 0);", p.id);  // vm.go:297-299
+            E.line("%s", nonempty_cases().c_str());
+            E.line("      break;");
+            E.line("    default: TERM(MIMIC_ERR_PC_OOB, 0);");
+            E.line("    }");
+            E.line("  D_:");
+            E.line("    switch (cur_) {");
+            for (auto &p : P)
+                if (p.n) E.line("    case %u: goto P%u_0;", p.id, p.id);
+            E.line("    default: TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
+            E.line("    }");
+        } else {
+            E.line("    switch (kp.entry_prog) {");
+            for (auto &p : P) {
+                if (p.n == 0) E.line("    case %u: steps = 1; TERM(MIMIC_ERR_PC_OOB, 0);", p.id);  // vm.go:297-299
+                else E.line("    case %u: goto P%u_0;", p.id, p.id);
+            }
+            E.line("    default: TERM(MIMIC_ERR_PC_OOB, 0);");
+            E.line("    }");
         }
-        E.line("    default: TERM(MIMIC_ERR_PC_OOB, 0);");
-        E.line("    }");
         for (auto &p : P) program(p);
         E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
         E.line("  L_term:");
@@ -1282,11 +1316,14 @@ class Gen {
                 E.line("        L.tailcalls++;");
             if (xpf.on) E.line("        xc_ok_ = 0u;");
                 E.line("        switch (%s) {", var);
-                for (auto &q : P) {
-                    if (q.n == 0) E.line("        case %u: TERM(MIMIC_ERR_PC_OOB, %u);", q.id, i);
-                    else E.line("        case %u: goto P%u_0;", q.id, q.id);
+                if (dispatch_on()) {
+                    E.line("%s", nonempty_cases().c_str());
+                    E.line("          cur_ = (uint32_t)(%s); goto D_;", var);
+                } else {
+                    for (auto &q : P)
+                        if (q.n) E.line("        case %u: goto P%u_0;", q.id, q.id);
                 }
-                E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);
+                E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);   // empty or unknown program
                 E.line("        }");
             };
             if (j >= 0) {
