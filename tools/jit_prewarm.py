@@ -14,8 +14,10 @@ os.makedirs(os.environ["MIMIC_JIT_CACHE"], exist_ok=True)
 from mimic_amd import _lib, jit as J, workloads as W  # noqa: E402
 
 if __name__ == "__main__":
-    kernels = [([getattr(W, fn)().raw], _lib.CTX_XDP)
-               for fn in ("prog_pass8", "prog_classifier", "prog_parse5", "prog_flowtrack", "prog_flowcount")]
+    kernels = []
+    for fn in ("prog_pass8", "prog_classifier", "prog_parse5", "prog_flowtrack", "prog_flowcount"):
+        p = getattr(W, fn)()
+        kernels.append(([p.raw], _lib.CTX_XDP, J.vc_slots([(p.raw, p.relocs)], p.maps)))
     t0 = time.time()
     out = J.prewarm(kernels)
     print(f"{len(kernels)} kernels in {time.time() - t0:.1f} s", out)
