@@ -106,6 +106,7 @@ struct mimic_vm {
     hipEvent_t kp_ev[KP_SLOTS] = {};
     bool kp_used[KP_SLOTS] = {};
     int kp_next = 0, kp_last = -1;
+    bool kp_pending = false;   // kernels launched with slot kp_last since its event was last recorded
     hipStream_t kp_last_stream = nullptr;
     // host-resident pipeline (mimic_run_xdp_host): NB rotating device staging slots
     // (packet window, its descriptors, its results); launch parameters are copied on the H2D
@@ -162,6 +163,21 @@ static int kp_slot(mimic_vm *vm, const KParams &kp, hipStream_t st, const KParam
     }
     int slot = vm->kp_last;
     if (slot < 0 || st != vm->kp_last_stream || memcmp(&vm->h_kp[slot], &kp, sizeof kp) != 0) {
+        // The slot we leave: its event goes behind everything enqueued so far on its stream
+        // (which includes its last kernel).  Recorded here, once per slot switch, instead of after
+        // every launch (an event between back-to-back kernels of one stream widens the gap between
+        // them).  When the caller moved to another stream, the old one may be gone already: wait
+        // for the device instead, after which no slot is in use.
+        if (vm->kp_last >= 0 && vm->kp_pending) {
+            if (st == vm->kp_last_stream) {
+                HIP_OK(vm, hipEventRecord(vm->kp_ev[vm->kp_last], st));
+                vm->kp_used[vm->kp_last] = true;
+            } else {
+                HIP_OK(vm, hipDeviceSynchronize());
+                for (auto &u : vm->kp_used) u = false;
+            }
+            vm->kp_pending = false;
+        }
         slot = vm->kp_next;
         vm->kp_next = (slot + 1) % mimic_vm::KP_SLOTS;
         if (vm->kp_used[slot]) HIP_OK(vm, hipEventSynchronize(vm->kp_ev[slot]));  // its last kernel is done
@@ -1308,8 +1324,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (slot < 0) return slot;
         if (jit ? mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
-        HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));
-        vm->kp_used[slot] = true;
+        vm->kp_pending = true;   // the slot's event is recorded when kp_slot leaves it
     }
     vm->last_lanes = lanes;
     vm->last_stream = st;

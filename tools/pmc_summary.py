@@ -6,7 +6,9 @@ Input (tools/profile.sh): under DIR, one rocprofv3 output directory per pass:
   fetch_<cfg>  --pmc FETCH_SIZE                  (HBM read bytes, KiB per dispatch)
   write_<cfg>  --pmc WRITE_SIZE                  (HBM write bytes, KiB per dispatch)
   sq_<cfg>     --pmc SQ_* + GRBM_GUI_ACTIVE      (instruction mix, VALU busy)
-Per-dispatch values are averaged over the dispatches of the engine's kernel.  FETCH_SIZE is
+Per-dispatch values are averaged over the engine kernel's dispatches of the bench's timed region:
+the first --skip dispatches (the bench's warmup; for cfg 4 the first one inserts every flow) are
+left out.  FETCH_SIZE is
 also reported doubled (MI355X_MICROARCH.md: on gfx950 it counts 1/2 of wide streaming reads);
 `bytes_per_launch` = doubled FETCH + WRITE, an upper estimate for this kernel's mixed-width
 loads.  The summary is keyed to the kernel source hash, packets and vCPUs of the run, which is
@@ -38,8 +40,9 @@ def col(r, *names):
     raise KeyError(names)
 
 
-def counters(d, kernel):
-    """counter name -> mean over the kernel's dispatches of the per-dispatch value"""
+def counters(d, kernel, skip=0):
+    """counter name -> mean over the kernel's dispatches (after the first `skip`) of the
+    per-dispatch value"""
     per = {}
     for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
         if kernel not in col(r, "Kernel_Name", "Kernel-Name", "KernelName"):
@@ -48,15 +51,36 @@ def counters(d, kernel):
         name = col(r, "Counter_Name", "Counter-Name")
         per.setdefault(name, {}).setdefault(disp, 0.0)
         per[name][disp] += float(col(r, "Counter_Value", "Counter-Value"))
-    return {k: sum(v.values()) / len(v) for k, v in per.items() if v}
+    out = {}
+    for k, v in per.items():
+        vals = [v[d] for d in sorted(v, key=lambda x: int(x))][skip:]
+        if vals:
+            out[k] = sum(vals) / len(vals)
+    return out
 
 
-def kernel_stats(d, kernel):
+def kernel_stats(d, kernel, skip=0):
+    """rocprofv3's --stats line for the kernel (every dispatch), plus the mean / median of the
+    per-dispatch durations of the kernel trace after the first `skip` dispatches (timed_*)"""
+    out = None
     for r in rows(os.path.join(d, "**", "*kernel_stats.csv")):
         if r.get("Name") == kernel:
-            return {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
-                    "max_ns": float(r["MaxNs"])}
-    return None
+            out = {"calls": int(r["Calls"]), "all_avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                   "max_ns": float(r["MaxNs"])}
+            break
+    durs = []
+    for r in rows(os.path.join(d, "**", "*kernel_trace.csv")):
+        if col(r, "Kernel_Name", "Kernel-Name", "KernelName").startswith(kernel):
+            durs.append((int(col(r, "Dispatch_Id", "Correlation_Id")), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    durs = [x for _, x in sorted(durs)][skip:]
+    if out is not None and durs:
+        srt = sorted(durs)
+        out["timed_launches"] = len(durs)
+        out["avg_ns"] = sum(durs) / len(durs)
+        out["median_ns"] = float(srt[len(srt) // 2])
+    elif out is not None:
+        out["avg_ns"] = out["all_avg_ns"]
+    return out
 
 
 def main():
@@ -69,6 +93,7 @@ def main():
     ap.add_argument("--vcpus", type=int, default=0)
     ap.add_argument("--out", default="")
     ap.add_argument("--command", default="")
+    ap.add_argument("--skip", type=int, default=2, help="leading dispatches to leave out (the bench's warmup)")
     a = ap.parse_args()
     import bench
 
@@ -76,10 +101,10 @@ def main():
     n = a.packets or cfg["packets"]
     vcpus = a.vcpus or cfg.get("vcpus") or max(64, n // 4)
     c = a.config
-    ks = kernel_stats(os.path.join(a.dir, f"kt_{c}"), a.kernel)
-    fetch = counters(os.path.join(a.dir, f"fetch_{c}"), a.kernel).get("FETCH_SIZE")
-    write = counters(os.path.join(a.dir, f"write_{c}"), a.kernel).get("WRITE_SIZE")
-    sq = counters(os.path.join(a.dir, f"sq_{c}"), a.kernel)
+    ks = kernel_stats(os.path.join(a.dir, f"kt_{c}"), a.kernel, a.skip)
+    fetch = counters(os.path.join(a.dir, f"fetch_{c}"), a.kernel, a.skip).get("FETCH_SIZE")
+    write = counters(os.path.join(a.dir, f"write_{c}"), a.kernel, a.skip).get("WRITE_SIZE")
+    sq = counters(os.path.join(a.dir, f"sq_{c}"), a.kernel, a.skip)
     out = {"config": c, "round": a.tag, "kernel": a.kernel, "kernel_src_hash": bench.kernel_src_hash_of(c),
            "packets": n, "vcpus": vcpus, "kernel_stats": ks}
     if fetch is not None and write is not None:
