@@ -51,6 +51,8 @@ struct HostMap {
     // hash families (hashmap.h)
     uint64_t keys_dev_off, ht_dev_off;
     uint32_t keys_addr, ht_cap, rec_q, nlocks, fl_cap;
+    // a delete may have left tombstones (hashmap.h): only then can the table need a rebuild
+    mutable bool may_tomb = false;
 };
 
 // can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
@@ -83,6 +85,7 @@ struct mimic_vm {
     Seg *d_segs = nullptr;
     DMap *d_maps = nullptr;
     bool tables_dirty = true;
+    bool prog_deletes = false;   // some loaded program calls map_delete_elem (helper 3)
     uint8_t *priv = nullptr;
     uint64_t priv_bytes = 0;
     uint32_t priv_lanes = 0;
@@ -397,6 +400,9 @@ static void build_host_tables(const std::vector<HostProg> &progs, std::vector<DI
 static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     build_host_tables(vm->progs, vm->h_all, vm->h_dp);
+    vm->prog_deletes = false;
+    for (auto &x : vm->h_all)
+        if (AUX_H(x.aux) == H_CALL && (uint32_t)x.k == 3) vm->prog_deletes = true;
     // map hints of LD_IMM64 constants that are map objects (AUX_MAPHINT): the JIT's inline
     // helpers check the map at run time, so a hint only selects a fast path
     for (auto &x : vm->h_all) {
@@ -803,6 +809,7 @@ static int hash_op(mimic_vm *vm, const HostMap &m, uint32_t op, const void *key,
     hipError_t e = hipMemcpy(d, key, m.key_size, hipMemcpyHostToDevice);
     if (e == hipSuccess && value) e = hipMemcpy(d + kb, value, m.value_size, hipMemcpyHostToDevice);
     const DMap dm = to_dmap(m);
+    if (op == 2) m.may_tomb = true;
     if (e == hipSuccess && mimic_launch_hash_op(vm->arena, &dm, op, d, d + kb, cpu, dout, vm->stream))
         e = hipErrorLaunchFailure;
     if (e == hipSuccess) e = hipMemcpyAsync(slot, dout, 4, hipMemcpyDeviceToHost, vm->stream);
@@ -1291,8 +1298,13 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.skb_base = vm->d_skb_state + 1;
     }
     // compact hash tables whose buckets are mostly tombstones (device-side check, no host sync)
+    // (skipped while no delete can have run on the map: without tombstones live entries stay
+    // below half of the table, so the check would always decline -- and a kernel between the
+    // batches costs a launch gap)
     for (auto &m : vm->maps) {
         if (!is_hash(m)) continue;
+        if (vm->prog_deletes) m.may_tomb = true;
+        if (!m.may_tomb) continue;
         const DMap dm = to_dmap(m);
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
