@@ -136,6 +136,7 @@ struct mimic_vm {
     size_t skb_cap = 0, skb_scan_cap = 0;
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
     hipStream_t skb_stream = nullptr;
+    bool skb_release_pending = false;   // mimic_skb_release ran and skb_stream may still be busy
 };
 
 
@@ -156,6 +157,8 @@ static int fail(mimic_vm *vm, int code, const char *fmt, ...) {
         hipError_t e_ = (call);                                                                 \
         if (e_ != hipSuccess) return fail((vm), MIMIC_EDEVICE, "%s: %s", #call, hipGetErrorString(e_)); \
     } while (0)
+
+static int skb_settle(mimic_vm *vm);
 
 // the device copy of kp for a JIT launch on stream st (see mimic_vm::d_kp)
 static int kp_slot(mimic_vm *vm, const KParams &kp, hipStream_t st, const KParams **out) {
@@ -601,6 +604,7 @@ int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id)
     if (vm->skb_leaked)   // first fit would now place it in the freed stack / sk_buff hole or after the leaks
         return fail(vm, MIMIC_ENOTSUP, "adding maps after sk_buff batches is not supported (mimic_skb_release first)");
     hipSetDevice(vm->s.device);
+    if (int rc = skb_settle(vm)) return rc;
     std::string name = spec->name ? spec->name : "";
     for (auto &m : vm->maps)
         if (m.name == name) return fail(vm, MIMIC_EINVAL, "map with name '%s' already exists in emulator", name.c_str());
@@ -792,6 +796,7 @@ static int array_cpu(mimic_vm *vm, const HostMap &m, int32_t cpu, uint64_t *base
 
 // wait for the last batch before touching map state from the host
 static int settle(mimic_vm *vm) {
+    if (int rc = skb_settle(vm)) return rc;
     if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
     return 0;
 }
@@ -981,6 +986,7 @@ int mimic_program_load(mimic_vm *vm, const char *name, const void *insns, uint32
     if (!vm || (!insns && n_slots) || !prog_id) return MIMIC_EINVAL;
     if (vm->skb_leaked)
         return fail(vm, MIMIC_ENOTSUP, "adding programs after sk_buff batches is not supported (mimic_skb_release first)");
+    if (int rc = skb_settle(vm)) return rc;
     uint64_t total = n_slots;
     for (auto &q : vm->progs) total += q.ins.size();
     if (n_slots >= (1u << MIMIC_PC_BITS) || total >= 0x7fffffffull) return fail(vm, MIMIC_EINVAL, "program too long");
@@ -1088,8 +1094,18 @@ int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, con
 int mimic_skb_release(mimic_vm *vm) {
     if (!vm) return MIMIC_EINVAL;
     hipSetDevice(vm->s.device);
-    if (vm->skb_stream) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
+    // No host wait here: the next sk_buff batch on the same stream is ordered behind the last one
+    // anyway (a wait would leave the GPU idle for a host round trip per batch); anything else that
+    // needs the sk_buff work finished calls skb_settle() first.
+    vm->skb_release_pending = vm->skb_stream != nullptr;
     vm->skb_leaked = false;
+    return 0;
+}
+
+// wait for the sk_buff batches mimic_skb_release let go of (map / program loads, xdp_md batches)
+static int skb_settle(mimic_vm *vm) {
+    if (vm->skb_release_pending && vm->skb_stream) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
+    vm->skb_release_pending = false;
     return 0;
 }
 
@@ -1151,6 +1167,10 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     if (!vm || !b || !res) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
+    if (!skb) {
+        const int rc = skb_settle(vm);
+        if (rc) return rc;
+    }
     if (!skb && vm->skb_leaked)   // the xdp entries would land in the freed hole or after the leaks
         return fail(vm, MIMIC_ENOTSUP, "xdp_md batches after sk_buff batches are not supported (mimic_skb_release first)");
     const uint32_t ctx = skb ? CTX_SKB : CTX_XDP;
