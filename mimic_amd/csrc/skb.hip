@@ -32,28 +32,46 @@ struct SkbLdsBytes {
     }
 };
 
-// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them
+// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  The records leave
+// through LDS: each thread puts its record there and the block writes its 256 records (40 KiB,
+// contiguous in rec) with consecutive threads on consecutive 8-byte words.  Stored one record per
+// thread, every store instruction of a wave would touch 64 records 160 bytes apart.
+#define PREP_RQ (sizeof(SkbRec) / 8)
+static_assert(sizeof(SkbRec) % 8 == 0, "SkbRec is copied as 8-byte words");
+static_assert(PREP_RQ * 2 >= PREP_W / 4, "the record area holds the window");
 extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, SkbRec *__restrict__ rec,
                                                                           uint64_t *__restrict__ foot) {
-    __shared__ uint32_t win[(PREP_W / 4) * PREP_T];
-    const uint32_t t = threadIdx.x, i = blockIdx.x * blockDim.x + t;
-    if (i >= n) return;   // no block-wide barrier below: each thread reads only its own window
-    const uint32_t L = pkt_len[i];
-    const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
-    // 8-byte chunks that start inside the packet (a chunk may run into the 64-byte tailroom)
-    for (uint32_t c = 0; c < PREP_W / 8; c++) {
-        if (8 * c >= L) break;
-        const uint64_t v = *(const u64u *)(pkt + 8 * c);
-        win[(2 * c) * PREP_T + t] = (uint32_t)v;
-        win[(2 * c + 1) * PREP_T + t] = (uint32_t)(v >> 32);
-    }
+    __shared__ uint64_t area[PREP_RQ * PREP_T];   // the windows first, then the records
+    uint32_t *win = (uint32_t *)area;
+    const uint32_t t = threadIdx.x, i0 = blockIdx.x * PREP_T, i = i0 + t;
+    if (i0 >= n) return;   // whole block past the batch (uniform: the barriers below are safe)
+    const bool live = i < n;
     SkbRec r;
-    skb_init(SkbLdsBytes{win, pkt, t}, L, r);
-    rec[i] = r;
-    foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
+    if (live) {
+        const uint32_t L = pkt_len[i];
+        const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
+        // 8-byte chunks that start inside the packet (a chunk may run into the 64-byte tailroom)
+        for (uint32_t c = 0; c < PREP_W / 8; c++) {
+            if (8 * c >= L) break;
+            const uint64_t v = *(const u64u *)(pkt + 8 * c);
+            win[(2 * c) * PREP_T + t] = (uint32_t)v;
+            win[(2 * c + 1) * PREP_T + t] = (uint32_t)(v >> 32);
+        }
+        skb_init(SkbLdsBytes{win, pkt, t}, L, r);
+        foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
+    }
+    __syncthreads();   // every window read
+    if (live) {
+        const uint64_t *rw = (const uint64_t *)&r;
+        for (uint32_t q = 0; q < PREP_RQ; q++) area[t * PREP_RQ + q] = rw[q];
+    }
+    __syncthreads();
+    const uint32_t words = (n - i0 < PREP_T ? n - i0 : PREP_T) * PREP_RQ;
+    uint64_t *dst = (uint64_t *)(rec + i0);
+    for (uint32_t w = t; w < words; w += PREP_T) dst[w] = area[w];
 }
 
 // state[0] = the VM's next leak address, state[1] = this batch's leak base
