@@ -2,7 +2,8 @@
 import numpy as np
 import pytest
 
-from harness import Scenario, assert_same, kernel_of, packets_to_buffer, run_engine, run_oracle, single
+from harness import (Scenario, assert_same, build_engine, build_oracle, kernel_of, packets_to_buffer, run_engine,
+                     run_oracle, single)
 import mimic_amd as M
 from mimic_amd import asm as A
 from mimic_amd import workloads as W
@@ -269,4 +270,44 @@ def test_sum_u64_readout(gpu, V, E):
         want += np.frombuffer(m.Values(c), np.uint64)
     assert m.SumU64() == [int(x) for x in want]
     assert m.SumU64(1, V) == [int(x) for x in want - np.frombuffer(m.Values(0), np.uint64)]
+    vm.close()
+
+
+def test_batches_across_streams_and_parameter_slots(gpu):
+    """Back-to-back asynchronous batches on three streams (the VM's own and two torch streams),
+    each batch a different packet window (new launch parameters: the engine's 8 parameter slots
+    are reused several times over).  A parameter slot's event is recorded when the slot is left,
+    and a stream change waits for the device (engine.cpp kp_slot), so every batch must give the
+    oracle's per-packet results and the per-CPU counters must add up over all batches in order."""
+    import torch
+
+    import mimic_amd as M
+
+    p = W.prog_classifier()
+    V = 64
+    sc = _prog_scenario(p, V)
+    n, chunk = 8192, 512
+    buf, off, lens = W.make_packets(n, seed=11)
+    vm, maps, pids = build_engine(sc)
+    streams = [None, torch.cuda.Stream(), torch.cuda.Stream()]
+    keep = []
+    for k in range(24):
+        a = (k * 331) % (n - chunk)
+        sel = slice(a, a + chunk)
+        batch = M.XDPBatch.from_numpy(buf, off[sel], lens[sel], device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+        res = vm.RunXDPBatch(pids[0], batch, stream=streams[(k // 2) % 3], sync=False)
+        keep.append((sel, batch, res))
+    torch.cuda.synchronize()
+    total = 0
+    ovm, _, opids = build_oracle(sc)
+    for sel, batch, res in keep:
+        cpu = W.schedule_cpu(chunk, V, "interleaved")
+        o = ovm.run_xdp_batch(opids[0], buf.copy(), off[sel], lens[sel], cpu)
+        got = res.numpy(chunk)
+        assert np.array_equal(np.asarray(o["r0"], np.uint64), np.asarray(got["r0"], np.uint64))
+        assert np.array_equal(np.asarray(o["status"]), np.asarray(got["status"]))
+        total += chunk
+    ovm.close()
+    cnt = sum(int(np.frombuffer(maps["verdicts"].Values(c), np.uint64).sum()) for c in range(V))
+    assert cnt == total
     vm.close()
