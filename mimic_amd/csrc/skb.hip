@@ -53,12 +53,15 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     if (live) {
         const uint32_t L = pkt_len[i];
         const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
-        // 8-byte chunks that start inside the packet (a chunk may run into the 64-byte tailroom)
-        for (uint32_t c = 0; c < PREP_W / 8; c++) {
-            if (8 * c >= L) break;
-            const uint64_t v = *(const u64u *)(pkt + 8 * c);
-            win[(2 * c) * PREP_T + t] = (uint32_t)v;
-            win[(2 * c + 1) * PREP_T + t] = (uint32_t)(v >> 32);
+        // 16-byte chunks that start inside the packet (a chunk may run into the 64-byte tailroom)
+        typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+        for (uint32_t c = 0; c < PREP_W / 16; c++) {
+            if (16 * c >= L) break;
+            const u32x4u v = *(const u32x4u *)(pkt + 16 * c);
+            win[(4 * c) * PREP_T + t] = v.x;
+            win[(4 * c + 1) * PREP_T + t] = v.y;
+            win[(4 * c + 2) * PREP_T + t] = v.z;
+            win[(4 * c + 3) * PREP_T + t] = v.w;
         }
         skb_init(SkbLdsBytes{win, pkt, t}, L, r);
         foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
