@@ -220,10 +220,7 @@ int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *batch,
                   const mimic_xdp_results *results, void *hip_stream);
 /* Drop the sock / flow-keys / packet entries earlier sk_buff processes leaked: the state of a
  * fresh VM with the same maps and programs (no reference counterpart; the reference never
- * frees them).  Needed before adding maps / programs or running xdp_md batches again.  It does
- * not wait for the device: the next sk_buff batch on the same stream is ordered behind the last
- * one, and map / program loads, xdp_md batches and host map operations wait for the released
- * batches first. */
+ * frees them).  Needed before adding maps / programs or running xdp_md batches again. */
 int mimic_skb_release(mimic_vm *vm);
 
 /* ---- single processes: the NewProcess / SetCPUID / Step / Run / Cleanup surface ---------------
