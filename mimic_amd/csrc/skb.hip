@@ -33,18 +33,20 @@ struct SkbLdsBytes {
 };
 
 // packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  The records leave
-// through LDS: each thread puts its record there and the block writes its 256 records (40 KiB,
-// contiguous in rec) with consecutive threads on consecutive 8-byte words.  Stored one record per
-// thread, every store instruction of a wave would touch 64 records 160 bytes apart.
+// through LDS: each thread puts its record there and the block writes its records (contiguous in
+// rec) with consecutive threads on consecutive 8-byte words -- stored one record per thread,
+// every store instruction of a wave would touch 64 records 160 bytes apart.  Half a block's
+// records at a time, in the windows' 32 KiB (5 blocks per CU instead of 4 with 40 KiB).
 #define PREP_RQ (sizeof(SkbRec) / 8)
+#define PREP_HALF (PREP_T / 2)
 static_assert(sizeof(SkbRec) % 8 == 0, "SkbRec is copied as 8-byte words");
-static_assert(PREP_RQ * 2 >= PREP_W / 4, "the record area holds the window");
+static_assert(PREP_RQ * PREP_HALF <= (PREP_W / 8) * PREP_T, "half the records fit the window area");
 extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, SkbRec *__restrict__ rec,
                                                                           uint64_t *__restrict__ foot) {
-    __shared__ uint64_t area[PREP_RQ * PREP_T];   // the windows first, then the records
+    __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
     uint32_t *win = (uint32_t *)area;
     const uint32_t t = threadIdx.x, i0 = blockIdx.x * PREP_T, i = i0 + t;
     if (i0 >= n) return;   // whole block past the batch (uniform: the barriers below are safe)
@@ -67,14 +69,19 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
         foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
     __syncthreads();   // every window read
-    if (live) {
-        const uint64_t *rw = (const uint64_t *)&r;
-        for (uint32_t q = 0; q < PREP_RQ; q++) area[t * PREP_RQ + q] = rw[q];
+    const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
+    for (uint32_t h = 0; h < 2; h++) {
+        if (live && t / PREP_HALF == h) {
+            const uint64_t *rw = (const uint64_t *)&r;
+            for (uint32_t q = 0; q < PREP_RQ; q++) area[(t % PREP_HALF) * PREP_RQ + q] = rw[q];
+        }
+        __syncthreads();
+        const uint32_t first = h * PREP_HALF;
+        const uint32_t words = cnt > first ? (cnt - first < PREP_HALF ? cnt - first : PREP_HALF) * PREP_RQ : 0u;
+        uint64_t *dst = (uint64_t *)(rec + i0 + first);
+        for (uint32_t w = t; w < words; w += PREP_T) dst[w] = area[w];
+        __syncthreads();
     }
-    __syncthreads();
-    const uint32_t words = (n - i0 < PREP_T ? n - i0 : PREP_T) * PREP_RQ;
-    uint64_t *dst = (uint64_t *)(rec + i0);
-    for (uint32_t w = t; w < words; w += PREP_T) dst[w] = area[w];
 }
 
 // state[0] = the VM's next leak address, state[1] = this batch's leak base
