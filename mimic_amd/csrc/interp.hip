@@ -52,8 +52,13 @@ static __device__ void step_save(const KParams &kp, const Lane &L, const uint64_
 #define NREGS 11
 #define KEY_DONE 0xffffffffu
 
-extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams *__restrict__ kpp) {
+// The batch kernel and the Process.Step kernel are one body: STEP compiles the step-state paths
+// (restore a suspended process, save it at the end) in or out, so the batch kernel carries none
+// of their registers (146 -> the batch kernel's own budget, 3 -> 4 waves per SIMD).
+template <bool STEP>
+static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp) {
     const KParams &kp = *kpp;  // device copy (engine.cpp kp_slot): fields load where used
+    StepState *const STP = STEP ? kp.step : nullptr;
     // eBPF registers r0..r10 of every lane live in LDS, [wave][reg][lane] (8-byte words): a
     // wave-uniform register number addresses 64 consecutive words (conflict-free ds_read_b64),
     // and multi-register updates (exit, helpers) need no register-array copies.
@@ -65,7 +70,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
     const bool lane_valid = g < kp.lanes;
     Lane L;
     L.lane = g;
-    L.cpu = kp.step ? kp.step->cpu : lane_cpu(kp, g);
+    L.cpu = STP ? STP->cpu : lane_cpu(kp, g);
 
     uint32_t ex_begin = 0, ex_count = 0;
     if (lane_valid && kp.sched == SCHED_EXPLICIT) {
@@ -120,12 +125,12 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
             if (kp.err_pc) kp.err_pc[i] = (int32_t)(epc_);             \
             lane_steps += steps;                                       \
             key = KEY_DONE;                                            \
-            if (kp.step) step_save(kp, L, RB, (st_), (epc_), steps, cur_prog); \
+            if (STP) step_save(kp, L, RB, (st_), (epc_), steps, cur_prog); \
         } while (0)
         // Process.Step: a stepped process resumes where its last launch suspended it
         bool resumed = false;
-        if (i != 0xffffffffu && kp.step && kp.step->started) {
-            const StepState *S = kp.step;
+        if (i != 0xffffffffu && STP && STP->started) {
+            const StepState *S = STP;
 #pragma unroll
             for (int q = 0; q < NREGS; q++) REG(q) = S->r[q];
             __builtin_memcpy(&L, S->lane, sizeof(Lane));
@@ -366,7 +371,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
                     }
 
                     if (st == EXIT_SIG) {
-                        TERM(MIMIC_OK, kp.step ? (int32_t)pc : -1);   // a stepped process keeps PC at the exit
+                        TERM(MIMIC_OK, STP ? (int32_t)pc : -1);   // a stepped process keeps PC at the exit
                     } else if (st) {
                         TERM(st, pc);
                     } else if (jmp == 0) {                 // PC+1 (vm.go:328-337)
@@ -391,6 +396,9 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel(const KParams
     if (lane_valid && kp.lane_steps) kp.lane_steps[g] = lane_steps;
 #undef REG
 }
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(const KParams *__restrict__ kpp) { xdp_body<false>(kpp); }
+extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KParams *__restrict__ kpp) { xdp_body<true>(kpp); }
 
 // Sum of a per-CPU u64 array over cpus: out[k] = sum_c base[c*stride + 8k] (the "sum over CPUs"
 // readout of a per-CPU counter map).  The per-CPU backings are contiguous ([cpu][key], stride =
@@ -512,7 +520,8 @@ extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t
 extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st) {
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
-    hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
+    if (kp->step) hipLaunchKernelGGL(mimic_xdp_step_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
+    else hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
