@@ -286,8 +286,13 @@ class Gen {
         // KParams is read through a pointer to a device copy: fields are loaded (scalar) where
         // they are used instead of all being preloaded into SGPRs from the kernarg segment
         // (which spills SGPRs and costs VGPRs / occupancy)
-        if (waves > 0)
-            E.line((std::string("extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(") + std::to_string(waves) +
+        // Register budget: kernels small enough to inline their slow paths are built for 4 waves
+        // per SIMD -- 262 144 lanes then run in one round on the 1 024 SIMDs.  cfg 4 (169 VGPRs,
+        // 2 waves): 0.172 -> 0.137 ms per launch; cfg 2 and 3 fit 4 waves anyway.  Large kernels
+        // (cfg 5) keep the compiler's choice: forcing 2 waves there spills 264 VGPRs (1.2 vs 0.7 ms).
+        const int wv = waves > 0 ? waves : (cold_inline ? 4 : 0);
+        if (wv > 0)
+            E.line((std::string("extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(") + std::to_string(wv) +
                    "))) void mimic_jit_kernel(const KParams *__restrict__ kpp) {").c_str());
         else
             E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");

@@ -132,12 +132,14 @@ def test_small_kernel_resources():
     assert r["waves_per_simd"] == 8 and r["lds"] == 0 and r["scratch"] == 0, r
 
 
-def test_cfg4_cfg5_kernels_have_no_vgpr_scratch_spill():
-    """cfg 4 (hash insert) kernel: no VGPR spills to scratch.  Its LDS stack window costs it the
-    third wave (169 VGPRs) and measured faster anyway: 0.179 vs 0.197 ms per launch; forced back to
-    3 waves (MIMIC_JIT_WAVES=3) 0.180 ms."""
+def test_cfg4_kernel_register_budget():
+    """cfg 4 (hash insert) kernel: built for 4 waves per SIMD like every kernel that inlines its
+    slow paths (jit.cpp), so the 262 144 lanes run in one round.  That spills about 40 VGPRs of
+    its slow paths to scratch and measured faster anyway: 0.137 vs 0.172 ms per launch at its
+    natural 169 VGPRs / 2 waves.  Its LDS stack window is there too."""
     r = _resources([W.prog_flowtrack().raw])
-    assert r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 2 and r["lds"] == 16 * 256 * 8, r
+    assert r["vgpr_total"] <= 128 and r["waves_per_simd"] >= 4 and r["lds"] == 16 * 256 * 8, r
+    assert r["vgpr_spill"] <= 64, r
 
 
 def test_lds_stack_window_selection():
