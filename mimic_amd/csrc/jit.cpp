@@ -201,6 +201,7 @@ class Gen {
     static constexpr uint32_t kColdInlineSites = 48;
     bool stage = false;        // MIMIC_JIT_STAGE=1: LDS packet window
     bool has_tail() const { return any_tail; }
+    bool has_early_loads() const { return !spec_use.empty(); }
     // Tail calls jump between programs.  With a jump table at every tail-call site as well as at
     // the entry, the programs form a cycle with several entries (irreducible control flow), which
     // the AMDGPU backend must restructure -- at a large register cost (cfg 5: 282 VGPRs without
@@ -1523,16 +1524,19 @@ std::map<CacheKey, hipFunction_t> g_cache;
 }  // namespace
 
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
-                             JitInfo *info, const std::vector<uint32_t> *vc_slots) {
+                             JitInfo *info, const std::vector<uint32_t> *vc_slots, bool no_early_loads) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
     Gen g(v, ctx_kind);
     if (vc_slots) g.vc_ok.insert(vc_slots->begin(), vc_slots->end());
+    if (no_early_loads) g.speculate = 0;
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;
         info->max_n = g.max_n;
         info->tail_calls = g.has_tail();
+        info->early_loads = g.has_early_loads();
+        info->cold_inline = g.cold_inline;
     }
     return src;
 }

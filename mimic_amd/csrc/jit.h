@@ -12,12 +12,14 @@ struct JitInfo {
     bool checks_budget;  // the kernel has the per-block budget checks (loops / BPF-to-BPF calls)
     uint32_t max_n;      // longest program
     bool tail_calls;     // some program calls bpf_tail_call
+    bool early_loads;    // the kernel issues packet loads early (analyze_spec)
+    bool cold_inline;    // the slow paths are inlined (small kernel, 4-wave register budget)
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // vc_slots: kernel-wide indices of LD_IMM64 slots whose constant is the object of a per-CPU array
 // with E * S <= 32 bytes, a multiple of 8 (the lane value cache may cache that map's row)
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
-                             JitInfo *info, const std::vector<uint32_t> *vc_slots = nullptr);
+                             JitInfo *info, const std::vector<uint32_t> *vc_slots = nullptr, bool no_early_loads = false);
 // 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
 // batch with a smaller budget must run on the interpreter
 uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);

@@ -130,19 +130,51 @@ def _cache_dir() -> str:
     return d
 
 
+def _no_early_load_source(k) -> str:
+    """The form of kernel k the engine falls back to when its 4-wave build spills (engine.cpp:
+    the kernel without early packet loads, MIMIC_JIT_SPEC=0)."""
+    old = os.environ.get("MIMIC_JIT_SPEC")
+    os.environ["MIMIC_JIT_SPEC"] = "0"
+    try:
+        return kernel_source(list(k[0]), *k[1:])
+    finally:
+        if old is None:
+            del os.environ["MIMIC_JIT_SPEC"]
+        else:
+            os.environ["MIMIC_JIT_SPEC"] = old
+
+
 def prewarm(kernels: Iterable[Tuple], workers: int = 0) -> Dict[str, float]:
-    """Compile the kernels of (raws, ctx) program sets into MIMIC_JIT_CACHE using `workers`
-    parallel processes (0: min(16, cpus) - 1).  Returns {"kernels": n, "seconds": t}."""
+    """Compile the kernels of (raws, ctx[, vc]) program sets into MIMIC_JIT_CACHE using `workers`
+    parallel processes (0: min(16, cpus) - 1), then, for those whose 4-wave build spills, the
+    form without early loads the engine will also try.  Returns {"kernels": n, "seconds": t}."""
     import time
 
     t0 = time.time()
     _cache_dir()
-    srcs: Dict[str, None] = {}
+    kernels = list(kernels)
+    srcs: Dict[str, Tuple] = {}
     for k in kernels:
-        srcs[kernel_source(list(k[0]), *k[1:])] = None
+        srcs.setdefault(kernel_source(list(k[0]), *k[1:]), k)
+    info = _compile_parallel(list(srcs), workers)
+    alt: Dict[str, None] = {}
+    for src, k in srcs.items():
+        if "issued early" in src and "amdgpu_waves_per_eu(4)" in src:
+            try:
+                if kernel_resources(code_object(src))["scratch"] > 0:
+                    alt[_no_early_load_source(k)] = None
+            except RuntimeError:
+                pass
+    info2 = _compile_parallel(list(alt), workers)
+    return {"kernels": len(srcs) + len(alt), "seconds": time.time() - t0,
+            "worker_failures": info["worker_failures"] + info2["worker_failures"],
+            "failed_after_retry": info["failed_after_retry"] + info2["failed_after_retry"]}
+
+
+def _compile_parallel(srcs, workers: int) -> Dict[str, int]:
     todo = sorted(srcs, key=len, reverse=True)        # longest first: better packing
     if not todo:
-        return {"kernels": 0, "seconds": 0.0}
+        return {"worker_failures": 0, "failed_after_retry": 0}
     if workers <= 0:
         workers = max(1, min(16, os.cpu_count() or 1) - 1)
     workers = min(workers, len(todo))
@@ -170,8 +202,7 @@ def prewarm(kernels: Iterable[Tuple], workers: int = 0) -> Dict[str, float]:
         # missing after that are compiled by the engine when first used
         retry = [w for w, rc in enumerate(rcs) if rc]
         rcs2 = [p.wait() for p in [launch(w) for w in retry]]
-    return {"kernels": len(todo), "seconds": time.time() - t0, "worker_failures": len(retry),
-            "failed_after_retry": sum(1 for rc in rcs2 if rc)}
+    return {"worker_failures": len(retry), "failed_after_retry": sum(1 for rc in rcs2 if rc)}
 
 
 def _worker(list_file: str) -> int:
