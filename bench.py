@@ -210,7 +210,17 @@ def host_threads() -> int:
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
 
 
-def read_profile(cfg_name: str, kernel: str, src_hash: str, n: int, vcpus: int):
+def default_batches(cfg_name: str, n: int) -> int:
+    """Batches the timed region rotates over by default: enough that their packets, descriptors
+    and results exceed ROTATE_BYTES (mean packet size of the config's mix)."""
+    cfg = CONFIGS[cfg_name]
+    w = np.asarray(cfg["weights"], np.float64)
+    mean = float((np.asarray(cfg["sizes"], np.float64) * w).sum() / w.sum())
+    return max(1, -(-ROTATE_BYTES // int(n * (mean + 21))))
+
+
+def read_profile(cfg_name: str, kernel: str, src_hash: str, n: int, vcpus: int, batches: int = 1,
+                 sched: str = "interleaved"):
     """The committed rocprofv3 summary of exactly this kernel (source hash) on this workload."""
     import glob
 
@@ -221,7 +231,8 @@ def read_profile(cfg_name: str, kernel: str, src_hash: str, n: int, vcpus: int):
         except Exception:
             continue
         if (d.get("config") == cfg_name and d.get("kernel") == kernel and d.get("kernel_src_hash") == src_hash
-                and d.get("packets") == n and d.get("vcpus") == vcpus):
+                and d.get("packets") == n and d.get("vcpus") == vcpus and d.get("batches", 1) == batches
+                and d.get("schedule", "interleaved") == sched):
             best = dict(d, file=os.path.relpath(f, ROOT))
     return best
 
@@ -254,7 +265,7 @@ def host_resident_rate(vm, pid, wl, sched, chunks: int = 0, reps: int = 5):
             "ok_frac": float((st == 0).mean())}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -263,17 +274,114 @@ def main():
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--vcpus", type=int, default=0, help="vCPUs per GPU (default: the config's, else packets/4)")
     ap.add_argument("--sched", default="interleaved", choices=["chunked", "interleaved"])
+    ap.add_argument("--batches", type=int, default=0,
+                    help="distinct input batches the timed launches rotate over (default: enough that the "
+                         f"working set exceeds {ROTATE_BYTES >> 20} MiB, so no batch is served from the "
+                         "256 MiB Infinity Cache)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-resident", action="store_true", help="skip the PCIe-inclusive rate")
-    args = ap.parse_args()
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="CPU rehearsal of the --gpus N launcher: gloo ranks run the setup / readout "
+                         "collectives with no engine and rank 0 prints the launch facts")
+    return ap.parse_args(argv)
+
+
+# Working set the timed region must exceed: MI355X_MICROARCH.md's 256 MiB Infinity Cache (MALL)
+# serves re-read lines and FETCH_SIZE counts those hits, so a batch re-launched from cache would
+# report a cache rate as an HBM rate.
+ROTATE_BYTES = 384 << 20
+
+
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) outside torch.distributed: start N ranks with torch.distributed.run,
+    one process per GPU, and exit with its status.  Nothing here touches the GPU (counting
+    devices does not initialise HIP on this image); the ranks are children, not an exec."""
+    import socket
+    import subprocess
+
+    if not args.launch_selftest:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            sys.stderr.write(f"bench.py --gpus {args.gpus}: only {have} GPU(s) visible on this node; "
+                             f"one rank per GPU needs {args.gpus}\n")
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+def selftest_rank(args, ws, rank, local) -> None:
+    """--launch-selftest: what a rank does around the engine, on gloo/CPU -- program broadcast,
+    max-over-ranks time, counter all-reduce, hash-replica merge -- then rank 0 reports."""
+    import torch.distributed as dist
+
+    from mimic_amd import dist as D
+    from mimic_amd import workloads as W
+
+    dist.init_process_group("gloo")
+    p = getattr(W, CONFIGS[args.config].get("prog", "prog_classifier"))()
+    raw = D.broadcast_bytes(p.raw if rank == 0 else None, "cpu")
+    ranks = D.allgather_records(bytes([rank, local]), 2, "cpu")
+    elapsed = D.allreduce_max_f64(0.001 * (rank + 1), "cpu")
+    counters = D.allreduce_sum_u64([rank + 1, 1], "cpu")
+    merged = D.merge_hash_replicas({bytes([rank]) * 4: bytes(8)}, 4, 8, "cpu")
+    if rank == 0:
+        print(json.dumps({"n_gpus": ws, "gpus_flag": args.gpus, "program_ok": raw == p.raw,
+                          "ranks": [b[0] for b in ranks], "local_ranks": [b[1] for b in ranks],
+                          "elapsed_max": elapsed, "counters": counters, "hash_keys": len(merged)}), flush=True)
+    dist.destroy_process_group()
+
+
+def make_batches(wl, args, n, rank, dev, sched):
+    """The timed launches rotate over `nb` distinct seeded batches of the config's workload (each
+    its own packets, descriptors and results)."""
+    import mimic_amd as M
+    from mimic_amd import workloads as W
+
+    nb = args.batches or default_batches(args.config, n)
+    out = []
+    for b in range(nb):
+        w = wl if b == 0 else Workload(args.config, n, W.SEED + rank + 1000 * b)
+        if wl.skb:
+            batch = M.SKBBatch.from_numpy(w.buf, w.off, w.lens, device=dev, ifindex=1, schedule=sched)
+        else:
+            batch = M.XDPBatch.from_numpy(w.buf, w.off, w.lens, device=dev, ingress=1, schedule=sched)
+        out.append((w, batch, M.XDPResults.empty(n, dev, full=False)))
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    ws, rank, local = dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if ws != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}; launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop --gpus\n")
+        return 2
+    if args.launch_selftest:
+        selftest_rank(args, ws, rank, local)
+        return 0
     # compiled JIT kernels persist here across runs
     os.environ.setdefault("MIMIC_JIT_CACHE", os.path.join(ROOT, ".jitcache"))
     os.makedirs(os.environ["MIMIC_JIT_CACHE"], exist_ok=True)
 
     import torch
 
-    ws, rank, local = dist_env()
+    if torch.cuda.device_count() <= local:
+        sys.stderr.write(f"bench.py rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} "
+                         f"GPU(s) visible\n")
+        return 2
     if ws > 1:
         import torch.distributed as dist
 
@@ -298,23 +406,20 @@ def main():
     pid = pids[0]
 
     sched = M.SCHED_INTERLEAVED if args.sched == "interleaved" else M.SCHED_CHUNKED
-    if wl.skb:
-        batch = M.SKBBatch.from_numpy(wl.buf, wl.off, wl.lens, device=dev, ifindex=1, schedule=sched)
-    else:
-        batch = M.XDPBatch.from_numpy(wl.buf, wl.off, wl.lens, device=dev, ingress=1, schedule=sched)
-    res = M.XDPResults.empty(n, dev, full=False)  # R0 + status per packet; steps via per-lane counters
+    batches = make_batches(wl, args, n, rank, dev, sched)
+    nb = len(batches)
     stream = torch.cuda.Stream(device=dev)
 
-    if wl.skb:
-        def step():
+    def launch(k):
+        w, batch, res = batches[k % nb]
+        if wl.skb:
             vm.RunSKBBatch(pid, batch, res, stream=stream, sync=False)
             vm.SKBRelease()   # the batch's leaked sk_buff entries: a long run would exhaust 32-bit addresses
-    else:
-        def step():
+        else:
             vm.RunXDPBatch(pid, batch, res, stream=stream, sync=False)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        launch(k)
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
@@ -325,7 +430,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for k in range(args.steps):
-        step()
+        launch(args.warmup + k)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if ws > 1:
@@ -333,13 +438,10 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     region_ms = ev0.elapsed_time(ev1)
-    steps_per_batch = vm.LastSteps()
-    st = res.status[:n].cpu().numpy()
+    st = np.concatenate([res.status[:n].cpu().numpy() for _, _, res in batches])
+    timed = [(args.warmup + k) % nb for k in range(args.steps)]
     if ws > 1:
         elapsed = D.allreduce_max_f64(elapsed, dev)
-        steps_total_batch = float(D.allreduce_sum_u64([steps_per_batch], dev)[0])
-    else:
-        steps_total_batch = float(steps_per_batch)
 
     # sum-over-CPUs readout of the per-CPU counters (RCCL all-reduce across ranks); shared hash
     # maps: one replica per GPU, (key, value) records merged
@@ -357,15 +459,27 @@ def main():
         local_sum = maps[pcm[0]["name"]].SumU64(b0, b0 + cnt)
         counters = D.allreduce_sum_u64(local_sum, dev) if ws > 1 else local_sum
 
+    # eBPF instructions per batch (exact per-lane step counts): one more untimed launch of each
+    # batch after the readout above
+    steps_of = []
+    for b in range(nb):
+        launch(b)
+        torch.cuda.synchronize(dev)
+        steps_of.append(vm.LastSteps())
+    steps_timed = float(sum(steps_of[b] for b in timed))
+    if ws > 1:
+        steps_timed = float(D.allreduce_sum_u64([int(steps_timed)], dev)[0])
+
     if rank == 0:
         total_pkts = n * ws * args.steps
         value = total_pkts / elapsed / 1e6
         avg_launch_s = region_ms / args.steps / 1e3   # per launch, gaps between launches included
-        alg = algorithmic_bytes(wl.lens, vpg, wl.maps, wl.cfg.get("reads_packet", True))
+        alg = sum(algorithmic_bytes(batches[b][0].lens, vpg, wl.maps, wl.cfg.get("reads_packet", True))
+                  for b in timed) / len(timed)
         achieved = alg / avg_launch_s
         kernel = "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel"
         src_hash = wl.kernel_src_hash()
-        prof = read_profile(args.config, kernel, src_hash, n, vpg)
+        prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched)
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",
             "value": round(value, 3),
@@ -380,11 +494,12 @@ def main():
             "dtype": "u64",
             "data": "synthetic (seeded PCG64 packet mix, SURVEY.md 8(d))",
             "config": {"workload": cfg["workload"], "packets_per_gpu": n, "vcpus_per_gpu": vpg,
-                       "schedule": args.sched, "parallelism": f"dp{ws}",
+                       "schedule": args.sched, "parallelism": f"dp{ws}", "batches_rotated": nb,
+                       "working_set_bytes": sum(int(w.buf.nbytes) + 21 * n for w, _, _ in batches),
                        "program_slots": sum(len(p.raw) // 8 for p in wl.progs), "engine": vm.LastExec(),
                        "kernel_src_hash": src_hash},
-            "insns_per_s": round(steps_total_batch * args.steps / elapsed, 1),
-            "mean_insns_per_packet": round(steps_total_batch / (n * ws), 3),
+            "insns_per_s": round(steps_timed / elapsed, 1),
+            "mean_insns_per_packet": round(steps_timed / (n * ws * args.steps), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
                          "traffic": prof["bytes_per_launch"] if prof else None,
@@ -410,4 +525,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -167,6 +167,11 @@ int mimic_map_entries(mimic_vm *vm, uint32_t map_id, void *keys_out, int32_t *sl
                       uint32_t *n_out);
 /* Raw value backing of (map, cpu): E*S bytes, slot order (D2H copy). */
 int mimic_map_read_values(mimic_vm *vm, uint32_t map_id, int32_t cpu, void *out, size_t cap);
+/* Value backings of vCPUs [cpu_begin, cpu_end) of a per-CPU map ([0, 1) otherwise), cpu-major:
+ * (cpu_end - cpu_begin) * E*S bytes in one D2H copy -- LinuxMap.Values(cpuid) for every cpu of a range
+ * (emulator_linux_map_array.go:223-233, emulator_linux_map_hash.go:628-640). */
+int mimic_map_read_values_range(mimic_vm *vm, uint32_t map_id, int32_t cpu_begin, int32_t cpu_end, void *out,
+                                size_t cap);
 /* Sum over vCPUs [cpu_begin, cpu_end) of a per-CPU map's u64 values -> out[E] (device reduction). */
 int mimic_map_sum_u64(mimic_vm *vm, uint32_t map_id, int32_t cpu_begin, int32_t cpu_end, uint64_t *out, size_t cap);
 /* MemoryController.GetEntryByObject(map).Addr */

@@ -946,6 +946,30 @@ int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, siz
     return (int)n;
 }
 
+int mimic_map_read_values_range(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_end, void *out, size_t cap) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    uint32_t c0 = 0, c1 = 1;
+    if (m.family == FAM_PERCPU_ARRAY || m.family == FAM_PERCPU_HASH) {
+        if (cpu_begin < 0 || cpu_end > (int32_t)m.ncpu || cpu_begin >= cpu_end) return fail(vm, MIMIC_EINVAL, "bad cpu range");
+        c0 = (uint32_t)cpu_begin;
+        c1 = (uint32_t)cpu_end;
+    } else if (cpu_begin != 0 || cpu_end != 1) {
+        return fail(vm, MIMIC_EINVAL, "bad cpu range");
+    }
+    const uint64_t row = (uint64_t)m.max_entries * m.value_size, n = row * (c1 - c0);
+    if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
+    if (n == 0) return 0;
+    if ((rc = settle(vm))) return rc;
+    if (m.dev_stride == row || c1 - c0 == 1)
+        HIP_OK(vm, hipMemcpy(out, vm->arena + m.dev_off + (uint64_t)c0 * m.dev_stride, n, hipMemcpyDeviceToHost));
+    else
+        HIP_OK(vm, hipMemcpy2D(out, row, vm->arena + m.dev_off + (uint64_t)c0 * m.dev_stride, m.dev_stride, row,
+                               c1 - c0, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int mimic_map_sum_u64(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_end, uint64_t *out, size_t cap) {
     int rc = map_check(vm, id);
     if (rc) return rc;
@@ -1398,6 +1422,8 @@ struct mimic_process {
     uint64_t priv_bytes = 0;
     StepState h;                      // host copy after the last launch
     int32_t cpu = -1;
+    uint32_t static_next = 0;         // the VM's static layout the saved state's addresses assume
+    uint8_t *arena = nullptr;
 };
 
 static void process_release(mimic_process *p) {
@@ -1429,8 +1455,15 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     hipSetDevice(vm->s.device);
     // the VM may have grown (maps / programs) since the process was made: its private plan too
     const PrivPlan pp = priv_plan(vm);
+    // a started process's saved registers, stack / packet pointers and translation cache hold
+    // addresses of the layout it started in: a map or program loaded since moved its entries
+    // (the reference's entries would have stayed put) and may have moved the arena
+    if (p->h.started && (vm->next_addr != p->static_next || vm->arena != p->arena))
+        return fail(vm, MIMIC_ENOTSUP, "a map or program was loaded after the process started; its layout changed");
     if ((uint64_t)pp.q_per_lane * 8 > p->priv_bytes && p->h.started)
         return fail(vm, MIMIC_ENOTSUP, "the VM's process layout changed under a started process");
+    p->static_next = vm->next_addr;
+    p->arena = vm->arena;
     if ((uint64_t)pp.q_per_lane * 8 > p->priv_bytes) {
         hipFree(p->d_priv);
         p->d_priv = nullptr;
@@ -1743,6 +1776,11 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
         chunks = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(2, bytes >> 24));
     }
     chunks = std::max<uint32_t>(1, std::min(chunks, n));
+    // pkt_out: each sub-batch copies its whole byte window back, so the packets of the whole batch
+    // (not only of one sub-batch) must be ascending and non-overlapping -- checked before any copy
+    // or launch, so a refused batch changes nothing (maps, results, pkt_out)
+    if (hb->pkt_out && !host_window(hb, 0, n, room).ascending)
+        return fail(vm, MIMIC_EINVAL, "pkt_out needs ascending, non-overlapping packets");
     // CHUNKED over the whole batch = EXPLICIT with cpu(i) = vcpu_begin + i / ceil(n / lanes)
     std::vector<int32_t> cpu_chunked;
     uint32_t sched = hb->schedule;
@@ -1783,10 +1821,6 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
         const HostWindow w = host_window(hb, a, m, room);
         auto t1 = clk::now();
         t_scan += std::chrono::duration<double, std::micro>(t1 - t0).count();
-        if (hb->pkt_out && !w.ascending) {
-            hipStreamSynchronize(vm->s_d2h);
-            return fail(vm, MIMIC_EINVAL, "pkt_out needs ascending, non-overlapping packets (sub-batch %u)", c);
-        }
         int rc = slot_reserve(vm, sl, std::max<uint64_t>(w.hi - w.lo, 1), m);
         if (rc) return rc;
         if (sl.used) HIP_OK(vm, hipStreamWaitEvent(h2d, sl.e_out, 0));  // the slot's last D2H is done

@@ -168,6 +168,20 @@ class LinuxMap:
         _check(vm.h, vm.lib.mimic_map_read_values(vm.h, self.id, cpuid, buf, max(n, 1)), "read values")
         return buf.raw[:n]
 
+    def ValuesRange(self, cpu_begin: int = 0, cpu_end: Optional[int] = None):
+        """Values(c) for every cpu c of [cpu_begin, cpu_end) in one device copy: a numpy uint8 array
+        of shape (cpu_end - cpu_begin, MaxEntries * ValueSize)."""
+        import numpy as np
+
+        vm = self._vm
+        if cpu_end is None:
+            cpu_end = self.Indices()
+        row = self.Spec.MaxEntries * self.Spec.ValueSize
+        out = np.zeros((max(cpu_end - cpu_begin, 0), row), np.uint8)
+        _check(vm.h, vm.lib.mimic_map_read_values_range(vm.h, self.id, cpu_begin, cpu_end, out.ctypes.data,
+                                                        out.nbytes), "read values range")
+        return out
+
     def SumU64(self, cpu_begin: int = 0, cpu_end: Optional[int] = None) -> List[int]:
         """Per-key sum over vCPUs of a u64-valued map (device reduction)."""
         vm = self._vm
@@ -232,13 +246,14 @@ class LinuxHashMap(LinuxMap):  # emulator_linux_map_hash.go:21-255
         sl = (C.c_int32 * max(E, 1))()
         n = C.c_uint32()
         _check(vm.h, vm.lib.mimic_map_entries(vm.h, self.id, kb, sl, max(E, 1), C.byref(n)), "entries")
-        return [(kb.raw[i * K:(i + 1) * K], int(sl[i])) for i in range(n.value)]
+        raw = kb.raw          # one copy of the key buffer (.raw copies on every access)
+        return [(raw[i * K:(i + 1) * K], int(s)) for i, s in enumerate(sl[:n.value])]
 
     def Contents(self) -> Dict[bytes, List[bytes]]:
         """key -> [value bytes of cpu 0 .. Indices()-1] (one bulk read per cpu)."""
         S = self.Spec.ValueSize
         ents = self.Entries()
-        vals = [self.Values(c) for c in range(self.Indices())]
+        vals = [bytes(r) for r in self.ValuesRange(0, self.Indices())]
         return {k: [v[s * S:(s + 1) * S] for v in vals] for k, s in ents}
 
     def ValueOf(self, key: bytes, cpuid: int = 0) -> Optional[bytes]:

@@ -321,7 +321,7 @@ def _flow_pool(rng, n_flows: int = 65536):
 
 
 def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: int = 64, headroom: int = 0,
-                 tailroom: int = 0):
+                 tailroom: int = 0, _rows: bool = True):
     """Synthetic frames -> (buf uint8[total], off uint64[n], lens uint32[n]).  Vectorised over
     packet kinds; every packet memory (headroom + L + tailroom bytes, the frame at +headroom)
     starts at a multiple of `align` bytes."""
@@ -334,64 +334,114 @@ def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: i
     if n > 1:
         off[1:] = np.cumsum(slot)[:-1]
     total = int(slot.sum())
-    buf = np.zeros(total, dtype=np.uint8)
-    # random payload bytes everywhere first (headers overwritten below)
-    buf[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = _random_fill(total, rng)   # random payload bytes everywhere first (headers overwritten below)
     kind = rng.choice(3, n, p=[0.90, 0.05, 0.05])           # ipv4 / ipv6 / arp
     flow = rng.integers(0, 65536, n)
     proto = pool["proto"][flow]
-    idx = off.astype(np.int64) + headroom
+    # the header bytes (frame offsets 0..57) of every packet are gathered as one row per packet
+    # (windows of the buffer at each packet's 64-byte-aligned slot when the slots allow it, else
+    # byte gathers), written column by column per packet kind, and scattered back
+    W = -(-(headroom + 58) // 64) * 64
+    use_rows = _rows and align % 64 == 0 and n > 0 and int(slot.min()) >= W
+    win = np.lib.stride_tricks.as_strided(buf, shape=(total // 64 - W // 64 + 1, W), strides=(64, 1)) \
+        if use_rows else None
 
-    def put(col, vals):
-        vals = np.asarray(vals, dtype=np.uint8)
-        buf[idx[:, None] + col] = vals
+    def part(lo, hi):
+        sl = slice(lo, hi)
+        if use_rows:
+            rix = off[sl] // 64
+            rows = np.ascontiguousarray(win[rix])
+            _write_headers(rows, headroom, kind[sl], flow[sl], proto[sl], lens[sl], pool)
+            win[rix] = rows
+        else:
+            bidx = (off[sl] + headroom)[:, None] + np.arange(58)
+            rows = buf[bidx]
+            _write_headers(rows, 0, kind[sl], flow[sl], proto[sl], lens[sl], pool)
+            buf[bidx] = rows
 
-    # Ethernet: dst, src MACs random (already), ethertype
-    et = np.where(kind == 0, ETH_P_IP, np.where(kind == 1, ETH_P_IPV6, ETH_P_ARP)).astype(np.uint16)
-    buf[idx + 12] = (et >> 8).astype(np.uint8)
-    buf[idx + 13] = (et & 0xFF).astype(np.uint8)
-    v4 = idx[kind == 0]
-    f4 = flow[kind == 0]
-    p4 = proto[kind == 0]
-    l4 = lens[kind == 0]
-    buf[v4 + 14] = 0x45
-    buf[v4 + 15] = 0
-    tl = (l4 - 14).astype(np.uint16)
-    buf[v4 + 16] = (tl >> 8).astype(np.uint8)
-    buf[v4 + 17] = (tl & 0xFF).astype(np.uint8)
-    buf[v4 + 20] = 0x40
-    buf[v4 + 21] = 0
-    buf[v4 + 22] = 64
-    buf[v4 + 23] = p4.astype(np.uint8)
-    for k in range(4):
-        buf[v4 + 26 + k] = ((pool["src4"][f4] >> (24 - 8 * k)) & 0xFF).astype(np.uint8)
-        buf[v4 + 30 + k] = ((pool["dst4"][f4] >> (24 - 8 * k)) & 0xFF).astype(np.uint8)
-    buf[v4 + 34] = (pool["sport"][f4] >> 8).astype(np.uint8)
-    buf[v4 + 35] = (pool["sport"][f4] & 0xFF).astype(np.uint8)
-    buf[v4 + 36] = (pool["dport"][f4] >> 8).astype(np.uint8)
-    buf[v4 + 37] = (pool["dport"][f4] & 0xFF).astype(np.uint8)
-    v6 = idx[kind == 1]
-    f6 = flow[kind == 1]
-    buf[v6 + 14] = 0x60
-    buf[v6 + 20] = proto[kind == 1].astype(np.uint8)
-    buf[v6 + 21] = 64
-    for k in range(16):
-        buf[v6 + 22 + k] = pool["src6"][f6, k]
-        buf[v6 + 38 + k] = pool["dst6"][f6, k]
-    plen6 = np.maximum(lens[kind == 1] - 54, 0).astype(np.uint16)   # IPv6 payload length
-    buf[v6 + 18] = (plen6 >> 8).astype(np.uint8)
-    buf[v6 + 19] = (plen6 & 0xFF).astype(np.uint8)
-    ok6 = lens[kind == 1] >= 58
-    buf[v6[ok6] + 54] = (pool["sport"][f6[ok6]] >> 8).astype(np.uint8)
-    buf[v6[ok6] + 55] = (pool["sport"][f6[ok6]] & 0xFF).astype(np.uint8)
-    buf[v6[ok6] + 56] = (pool["dport"][f6[ok6]] >> 8).astype(np.uint8)
-    buf[v6[ok6] + 57] = (pool["dport"][f6[ok6]] & 0xFF).astype(np.uint8)
-    va = idx[kind == 2]
-    buf[va + 14] = 0
-    buf[va + 15] = 1
-    buf[va + 16] = 8
-    buf[va + 17] = 0
+    # packet ranges are disjoint byte ranges of the buffer: written in parallel threads
+    step = 1 << 20
+    cuts = [(lo, min(n, lo + step)) for lo in range(0, n, step)]
+    if len(cuts) <= 1:
+        for lo, hi in cuts:
+            part(lo, hi)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(min(8, len(cuts))) as ex:
+            list(ex.map(lambda c: part(*c), cuts))
     return buf, off.astype(np.uint64), lens.astype(np.uint32)
+
+
+def _be(v: np.ndarray, nbytes: int) -> np.ndarray:
+    """big-endian bytes of unsigned integers: shape (len(v), nbytes) uint8"""
+    v = np.asarray(v, dtype=np.uint64)
+    return np.stack([((v >> (8 * (nbytes - 1 - k))) & 0xFF).astype(np.uint8) for k in range(nbytes)], axis=1)
+
+
+def _write_headers(rows: np.ndarray, b: int, kind, flow, proto, lens, pool) -> None:
+    """Ethernet / IPv4 / IPv6 / ARP header fields into rows[i, b + frame offset] (frame bytes
+    0..57; MACs and the fields not written stay random)."""
+    et = np.where(kind == 0, ETH_P_IP, np.where(kind == 1, ETH_P_IPV6, ETH_P_ARP))
+    rows[:, b + 12:b + 14] = _be(et, 2)
+    s4 = np.nonzero(kind == 0)[0]
+    if len(s4):
+        h = rows[s4]
+        f4 = flow[s4]
+        h[:, b + 14] = 0x45
+        h[:, b + 15] = 0
+        h[:, b + 16:b + 18] = _be((lens[s4] - 14) & 0xFFFF, 2)
+        h[:, b + 20] = 0x40
+        h[:, b + 21] = 0
+        h[:, b + 22] = 64
+        h[:, b + 23] = proto[s4]
+        h[:, b + 26:b + 30] = _be(pool["src4"][f4], 4)
+        h[:, b + 30:b + 34] = _be(pool["dst4"][f4], 4)
+        h[:, b + 34:b + 36] = _be(pool["sport"][f4], 2)
+        h[:, b + 36:b + 38] = _be(pool["dport"][f4], 2)
+        rows[s4] = h
+    s6 = np.nonzero(kind == 1)[0]
+    if len(s6):
+        h = rows[s6]
+        f6 = flow[s6]
+        h[:, b + 14] = 0x60
+        h[:, b + 20] = proto[s6]
+        h[:, b + 21] = 64
+        h[:, b + 22:b + 38] = pool["src6"][f6]
+        h[:, b + 38:b + 54] = pool["dst6"][f6]
+        h[:, b + 18:b + 20] = _be(np.maximum(lens[s6] - 54, 0), 2)   # IPv6 payload length
+        ok6 = lens[s6] >= 58
+        h[ok6, b + 54:b + 56] = _be(pool["sport"][f6[ok6]], 2)
+        h[ok6, b + 56:b + 58] = _be(pool["dport"][f6[ok6]], 2)
+        rows[s6] = h
+    sa = np.nonzero(kind == 2)[0]
+    if len(sa):
+        rows[sa, b + 14:b + 18] = np.array([0, 1, 8, 0], np.uint8)
+
+
+def _random_fill(total: int, rng) -> np.ndarray:
+    """`total` random bytes: 64-bit PCG64 draws in parallel chunks, each chunk its own stream
+    spawned from one seed taken from `rng` (deterministic for a given rng state)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    buf = np.empty(-(-total // 8) * 8, dtype=np.uint8)
+    words = buf.view(np.uint64)
+    nw = len(words)
+    chunk = 1 << 23
+    parts = -(-nw // chunk)
+    seqs = np.random.SeedSequence(int(rng.integers(0, 2 ** 63))).spawn(max(parts, 1))
+
+    def fill(k):
+        a, b = k * chunk, min(nw, (k + 1) * chunk)
+        words[a:b] = np.random.PCG64(seqs[k]).random_raw(b - a)
+
+    if parts <= 1:
+        for k in range(parts):
+            fill(k)
+    else:
+        with ThreadPoolExecutor(min(8, parts)) as ex:
+            list(ex.map(fill, range(parts)))
+    return buf[:total]
 
 
 IMIX = dict(sizes=(64, 576, 1500), weights=(7, 4, 1))

@@ -92,11 +92,22 @@ typedef struct {
     void *obj;
 } entry;
 
+#define MC_BLK 256
+typedef struct mc_blk { entry *e; size_t n; } mc_blk;
+
 struct orc_vm {
     int vcpus, frame_size, frame_count, max_tail_calls;
-    entry *e;
-    size_t n, cap;
-    size_t tight; /* entries [0,tight) form a gap-free chain from MEM_START (first-fit can never use them) */
+    struct mc_blk *blk; /* the entry list, sorted by address, in blocks (mc_insert_at) */
+    size_t nblk, cap_blk, n;
+    /* acceleration indexes of the entry list (same results as the literal loops they stand in for):
+     * gaps between entries keyed by their start address in a binary trie with a per-node maximum
+     * of the free bytes, so first fit is "lowest start whose gap holds size"; and entry address
+     * by object pointer (open addressing), so DelEntryByObj needs no scan */
+    struct gap_node { uint32_t c[2]; uint32_t mx; } *gn;
+    uint32_t gn_n, gn_cap;
+    void **ok; uint32_t *ov; uint8_t *os; /* object index: key, entry address, state 0 empty 1 used 2 tomb */
+    uint32_t o_cap, o_used, o_fill;
+    int o_dup;          /* an object was entered twice: fall back to the literal scans */
     orc_map **maps;
     int nmaps;
     program **progs;
@@ -141,66 +152,247 @@ const char *orc_last_error(orc_vm *vm) { return vm->err; }
 /* MemoryController, memory_controller.go                                     */
 /* ------------------------------------------------------------------------- */
 
+/* ---- acceleration indexes (test infrastructure speed only; the literal loops stay the spec) ---- */
+static uint32_t gn_new(orc_vm *vm) {
+    if (vm->gn_n == vm->gn_cap) {
+        vm->gn_cap = vm->gn_cap ? vm->gn_cap * 2 : 1024;
+        vm->gn = (struct gap_node *)realloc(vm->gn, vm->gn_cap * sizeof *vm->gn);
+    }
+    memset(&vm->gn[vm->gn_n], 0, sizeof *vm->gn);
+    return vm->gn_n++;
+}
+
+/* the gap starting at `start` has `avail` bytes before the next entry (0 = no gap there) */
+static void gap_set(orc_vm *vm, uint32_t start, uint32_t avail) {
+    if (vm->gn_n == 0) { gn_new(vm); gn_new(vm); } /* 0 = null, 1 = root */
+    if (avail == 0 && vm->gn[1].mx == 0) return;
+    uint32_t path[33];
+    uint32_t at = 1;
+    for (int b = 31; b >= 0; b--) {
+        path[31 - b] = at;
+        uint32_t bit = (start >> b) & 1u;
+        if (!vm->gn[at].c[bit]) {
+            if (avail == 0) return; /* nothing stored there */
+            uint32_t nn = gn_new(vm);
+            vm->gn[at].c[bit] = nn;
+        }
+        at = vm->gn[at].c[bit];
+    }
+    vm->gn[at].mx = avail;
+    for (int d = 31; d >= 0; d--) {
+        uint32_t n = path[d], l = vm->gn[n].c[0], r = vm->gn[n].c[1];
+        uint32_t ml = l ? vm->gn[l].mx : 0, mr = r ? vm->gn[r].mx : 0;
+        vm->gn[n].mx = ml > mr ? ml : mr;
+    }
+}
+
+/* lowest gap start whose gap holds `size` bytes (fits iff size < avail, as AddEntry tests) */
+static int gap_first_fit(orc_vm *vm, uint32_t size, uint32_t *start) {
+    if (vm->gn_n == 0 || vm->gn[1].mx <= size) return 0;
+    uint32_t at = 1, key = 0;
+    for (int b = 31; b >= 0; b--) {
+        uint32_t l = vm->gn[at].c[0];
+        if (l && vm->gn[l].mx > size) {
+            at = l;
+        } else {
+            at = vm->gn[at].c[1];
+            key |= 1u << b;
+        }
+    }
+    *start = key;
+    return 1;
+}
+
+static uint32_t obj_hash(const void *p, uint32_t cap) {
+    uint64_t x = (uint64_t)(uintptr_t)p;
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+    return (uint32_t)x & (cap - 1);
+}
+
+static void obj_put(orc_vm *vm, void *obj, uint32_t addr);
+
+static void obj_grow(orc_vm *vm) {
+    uint32_t oc = vm->o_cap;
+    void **ok = vm->ok; uint32_t *ov = vm->ov; uint8_t *os = vm->os;
+    vm->o_cap = oc ? oc * 2 : 1024;
+    if (vm->o_used * 4 < oc) vm->o_cap = oc; /* mostly tombstones: rehash at the same size */
+    vm->ok = (void **)calloc(vm->o_cap, sizeof(void *));
+    vm->ov = (uint32_t *)calloc(vm->o_cap, sizeof(uint32_t));
+    vm->os = (uint8_t *)calloc(vm->o_cap, 1);
+    vm->o_used = vm->o_fill = 0;
+    for (uint32_t i = 0; i < oc; i++)
+        if (os[i] == 1) obj_put(vm, ok[i], ov[i]);
+    free(ok); free(ov); free(os);
+}
+
+static void obj_put(orc_vm *vm, void *obj, uint32_t addr) {
+    if ((vm->o_fill + 1) * 2 > vm->o_cap) obj_grow(vm);
+    uint32_t i = obj_hash(obj, vm->o_cap), tomb = UINT32_MAX;
+    for (;; i = (i + 1) & (vm->o_cap - 1)) {
+        if (vm->os[i] == 1 && vm->ok[i] == obj) { vm->o_dup = 1; return; }
+        if (vm->os[i] == 2 && tomb == UINT32_MAX) tomb = i;
+        if (vm->os[i] == 0) break;
+    }
+    if (tomb != UINT32_MAX) i = tomb; else vm->o_fill++;
+    vm->ok[i] = obj; vm->ov[i] = addr; vm->os[i] = 1;
+    vm->o_used++;
+}
+
+static int obj_find(orc_vm *vm, void *obj, uint32_t *slot) {
+    if (!vm->o_cap) return 0;
+    for (uint32_t i = obj_hash(obj, vm->o_cap);; i = (i + 1) & (vm->o_cap - 1)) {
+        if (vm->os[i] == 0) return 0;
+        if (vm->os[i] == 1 && vm->ok[i] == obj) { *slot = i; return 1; }
+    }
+}
+
+/* The sorted entry list (memory_controller.go's []Entry) is kept in blocks of at most MC_BLK
+ * entries so an insertion or deletion moves one block's tail, not the whole list; a position is
+ * (block, index in block), the end position is (nblk - 1, its n) or (0, 0) when empty. */
+typedef struct { size_t b, k; } mc_pos;
+
+static entry *mc_at(orc_vm *vm, mc_pos p) { return &vm->blk[p.b].e[p.k]; }
+static int mc_is_end(orc_vm *vm, mc_pos p) { return vm->nblk == 0 || p.k >= vm->blk[p.b].n; }
+static mc_pos mc_first(orc_vm *vm) { (void)vm; mc_pos p = {0, 0}; return p; }
+static mc_pos mc_end(orc_vm *vm) {
+    mc_pos p = {vm->nblk ? vm->nblk - 1 : 0, vm->nblk ? vm->blk[vm->nblk - 1].n : 0};
+    return p;
+}
+static mc_pos mc_next(orc_vm *vm, mc_pos p) {
+    if (++p.k >= vm->blk[p.b].n && p.b + 1 < vm->nblk) { p.b++; p.k = 0; }
+    return p;
+}
+static int mc_prev(orc_vm *vm, mc_pos p, mc_pos *out) { /* 0 at the first entry */
+    if (p.k > 0) { p.k--; *out = p; return 1; }
+    if (p.b == 0) return 0;
+    out->b = p.b - 1;
+    out->k = vm->blk[p.b - 1].n - 1;
+    return 1;
+}
+
+/* sort.Search over the list: the first entry with Addr >= addr */
+static mc_pos mc_lower_bound(orc_vm *vm, uint32_t addr) {
+    if (vm->n == 0) return mc_end(vm);
+    size_t lo = 0, hi = vm->nblk;
+    while (lo < hi) { /* first block whose last entry has Addr >= addr */
+        size_t mid = (lo + hi) / 2;
+        if (vm->blk[mid].e[vm->blk[mid].n - 1].addr >= addr) hi = mid; else lo = mid + 1;
+    }
+    if (lo == vm->nblk) return mc_end(vm);
+    mc_blk *B = &vm->blk[lo];
+    size_t l = 0, h = B->n;
+    while (l < h) {
+        size_t mid = (l + h) / 2;
+        if (B->e[mid].addr >= addr) h = mid; else l = mid + 1;
+    }
+    mc_pos p = {lo, l};
+    return p;
+}
+
+static uint32_t mc_end1(const entry *e) { /* first address after an entry and its one-byte gap */
+    return e->addr + e->size + 1;
+}
+
+static void mc_insert_at(orc_vm *vm, mc_pos p, const entry *ne) {
+    if (vm->nblk == 0) {
+        vm->blk = (mc_blk *)calloc(1, sizeof(mc_blk));
+        vm->blk[0].e = (entry *)malloc(MC_BLK * sizeof(entry));
+        vm->nblk = vm->cap_blk = 1;
+        p.b = p.k = 0;
+    }
+    if (vm->blk[p.b].n == MC_BLK) { /* split the full block in halves */
+        if (vm->nblk == vm->cap_blk) {
+            vm->cap_blk *= 2;
+            vm->blk = (mc_blk *)realloc(vm->blk, vm->cap_blk * sizeof(mc_blk));
+        }
+        memmove(&vm->blk[p.b + 2], &vm->blk[p.b + 1], (vm->nblk - p.b - 1) * sizeof(mc_blk));
+        vm->nblk++;
+        mc_blk *A = &vm->blk[p.b], *N = &vm->blk[p.b + 1];
+        N->e = (entry *)malloc(MC_BLK * sizeof(entry));
+        N->n = MC_BLK / 2;
+        memcpy(N->e, A->e + MC_BLK / 2, N->n * sizeof(entry));
+        A->n = MC_BLK / 2;
+        if (p.k > A->n) { p.b++; p.k -= MC_BLK / 2; }
+    }
+    mc_blk *B = &vm->blk[p.b];
+    memmove(&B->e[p.k + 1], &B->e[p.k], (B->n - p.k) * sizeof(entry));
+    B->e[p.k] = *ne;
+    B->n++;
+    vm->n++;
+}
+
+static void mc_remove_at(orc_vm *vm, mc_pos p) {
+    mc_blk *B = &vm->blk[p.b];
+    memmove(&B->e[p.k], &B->e[p.k + 1], (B->n - p.k - 1) * sizeof(entry));
+    B->n--;
+    vm->n--;
+    if (B->n == 0 && vm->nblk > 1) {
+        free(B->e);
+        memmove(&vm->blk[p.b], &vm->blk[p.b + 1], (vm->nblk - p.b - 1) * sizeof(mc_blk));
+        vm->nblk--;
+    }
+}
+
 /* AddEntry, memory_controller.go:58-112 (first fit from memStart+1, one-byte gaps). */
 static int mc_add(orc_vm *vm, void *obj, objkind kind, uint32_t size, uint32_t *addr_out) {
-    size_t i = 0;
+    mc_pos at = mc_end(vm);
     uint32_t addr = MEM_START + 1;
-    if (vm->n > 0) {
-        /* entries before vm->tight are a contiguous chain; the reference loop would
-         * only step through them, so start the literal loop at the last one of them. */
-        size_t s = vm->tight < vm->n ? vm->tight : vm->n - 1;
-        addr = s == 0 ? MEM_START + 1 : vm->e[s - 1].addr + vm->e[s - 1].size + 1;
-        for (size_t j = s; j < vm->n; j++) {
-            entry *cur = &vm->e[j];
+    uint64_t tail = vm->n ? (uint64_t)mc_end1(mc_at(vm, (mc_pos){vm->nblk - 1, vm->blk[vm->nblk - 1].n - 1}))
+                          : MEM_START + 1;
+    int fast = !vm->o_dup && tail + size <= 0xFFFFFFFFull; /* no gap start + size can wrap 32 bits */
+    if (fast && vm->n > 0) {
+        uint32_t g;
+        if (gap_first_fit(vm, size, &g)) {   /* the first entry whose preceding gap holds size */
+            addr = g;
+            at = mc_lower_bound(vm, g);
+        } else {                             /* past the last entry */
+            addr = (uint32_t)tail;
+            if (0xFFFFFFFFu - addr < size) {
+                set_err(vm, "out of memory");
+                return -1;
+            }
+        }
+    } else if (vm->n > 0) {
+        /* the literal loop of memory_controller.go:70-90 */
+        for (mc_pos j = mc_first(vm); !mc_is_end(vm, j); j = mc_next(vm, j)) {
+            entry *cur = mc_at(vm, j);
             if ((uint32_t)(addr + size) < cur->addr) {
-                i = j;
+                at = j;
                 break;
             }
             addr = cur->addr + cur->size + 1;
-            if (j == vm->n - 1) {
+            if (mc_is_end(vm, mc_next(vm, j))) {
                 uint32_t avail = 0xFFFFFFFFu - addr;
                 if (avail < size) {
                     set_err(vm, "out of memory");
                     return -1;
                 }
-                i = j + 1;
             }
         }
     }
-    if (vm->n == vm->cap) {
-        vm->cap = vm->cap ? vm->cap * 2 : 64;
-        vm->e = (entry *)realloc(vm->e, vm->cap * sizeof(entry));
+    entry ne = {addr, size, kind, obj};
+    int in_gap = !mc_is_end(vm, at);
+    mc_insert_at(vm, at, &ne);
+    if (in_gap) { /* the gap this entry went into now starts after it */
+        mc_pos nx = mc_lower_bound(vm, addr + 1);
+        gap_set(vm, addr, 0);
+        gap_set(vm, addr + size + 1, mc_at(vm, nx)->addr - (addr + size + 1));
     }
-    memmove(&vm->e[i + 1], &vm->e[i], (vm->n - i) * sizeof(entry));
-    vm->e[i].addr = addr;
-    vm->e[i].size = size;
-    vm->e[i].kind = kind;
-    vm->e[i].obj = obj;
-    vm->n++;
-    /* maintain the gap-free prefix: [0,i) is unchanged, re-extend from i */
-    if (vm->tight > i) vm->tight = i;
-    while (vm->tight < vm->n) {
-        uint32_t expect = vm->tight == 0 ? MEM_START + 1 : vm->e[vm->tight - 1].addr + vm->e[vm->tight - 1].size + 1;
-        if (vm->e[vm->tight].addr != expect) break;
-        vm->tight++;
-    }
+    obj_put(vm, obj, addr);
     if (addr_out) *addr_out = addr;
     return 0;
 }
 
 /* GetEntry, memory_controller.go:117-145 (inclusive upper bound at :137). */
 static entry *mc_get(orc_vm *vm, uint32_t addr, uint32_t *off) {
-    size_t lo = 0, hi = vm->n;
-    while (lo < hi) { /* sort.Search: first entry with Addr >= addr */
-        size_t mid = (lo + hi) / 2;
-        if (vm->e[mid].addr >= addr) hi = mid; else lo = mid + 1;
-    }
-    if (lo < vm->n && vm->e[lo].addr == addr) {
+    if (vm->n == 0) return NULL;
+    mc_pos lo = mc_lower_bound(vm, addr), pv;
+    if (!mc_is_end(vm, lo) && mc_at(vm, lo)->addr == addr) {
         *off = 0;
-        return &vm->e[lo];
+        return mc_at(vm, lo);
     }
-    if (lo != 0) {
-        entry *prev = &vm->e[lo - 1];
+    if (mc_prev(vm, lo, &pv)) {
+        entry *prev = mc_at(vm, pv);
         if (addr >= prev->addr && (uint64_t)addr <= (uint64_t)prev->addr + prev->size) {
             *off = addr - prev->addr;
             return prev;
@@ -210,26 +402,54 @@ static entry *mc_get(orc_vm *vm, uint32_t addr, uint32_t *off) {
 }
 
 /* DelEntryByObj, memory_controller.go:202-232. */
-static void mc_del_obj(orc_vm *vm, void *obj) {
-    for (size_t j = vm->n; j-- > 0;) {
-        if (vm->e[j].obj == obj) {
-            memmove(&vm->e[j], &vm->e[j + 1], (vm->n - j - 1) * sizeof(entry));
-            vm->n--;
-            if (vm->tight > j) vm->tight = j;
-            return;
-        }
+static void mc_del_at(orc_vm *vm, mc_pos j) {
+    mc_pos pv;
+    uint32_t before = mc_prev(vm, j, &pv) ? mc_end1(mc_at(vm, pv)) : MEM_START + 1;
+    entry *e = mc_at(vm, j);
+    uint32_t addr = e->addr;
+    gap_set(vm, before, 0);
+    gap_set(vm, mc_end1(e), 0);
+    uint32_t slot;
+    if (obj_find(vm, e->obj, &slot) && vm->ov[slot] == addr) {
+        vm->os[slot] = 2;
+        vm->o_used--;
     }
+    mc_remove_at(vm, j);
+    mc_pos nx = mc_lower_bound(vm, addr);
+    if (!mc_is_end(vm, nx)) gap_set(vm, before, mc_at(vm, nx)->addr - before); /* the two gaps merge */
+}
+
+static int mc_find_obj(orc_vm *vm, void *obj, mc_pos *out) {
+    uint32_t slot;
+    if (!vm->o_dup) {
+        if (!obj_find(vm, obj, &slot)) return 0;
+        mc_pos j = mc_lower_bound(vm, vm->ov[slot]);
+        if (mc_is_end(vm, j) || mc_at(vm, j)->obj != obj) return 0;
+        *out = j;
+        return 1;
+    }
+    if (vm->n == 0) return 0;
+    mc_pos j = mc_end(vm), pv; /* the literal scan, last entry first */
+    while (mc_prev(vm, j, &pv)) {
+        if (mc_at(vm, pv)->obj == obj) { *out = pv; return 1; }
+        j = pv;
+    }
+    return 0;
+}
+
+static void mc_del_obj(orc_vm *vm, void *obj) {
+    mc_pos j;
+    if (mc_find_obj(vm, obj, &j)) mc_del_at(vm, j);
 }
 
 static entry *mc_by_obj(orc_vm *vm, void *obj) {
-    for (size_t j = vm->n; j-- > 0;)
-        if (vm->e[j].obj == obj) return &vm->e[j];
-    return NULL;
+    mc_pos j;
+    return mc_find_obj(vm, obj, &j) ? mc_at(vm, j) : NULL;
 }
 
 uint32_t orc_mem_next_free(orc_vm *vm) {
     if (vm->n == 0) return MEM_START + 1;
-    return vm->e[vm->n - 1].addr + vm->e[vm->n - 1].size + 1;
+    return mc_end1(mc_at(vm, (mc_pos){vm->nblk - 1, vm->blk[vm->nblk - 1].n - 1}));
 }
 
 /* ------------------------------------------------------------------------- */
@@ -349,6 +569,10 @@ orc_vm *orc_vm_new(int vcpus, int frame_size, int frame_count, int max_tail_call
     vm->frame_size = frame_size > 0 ? frame_size : 256;  /* vm.go:60 */
     vm->frame_count = frame_count > 0 ? frame_count : 8; /* vm.go:62 */
     vm->max_tail_calls = max_tail_calls;   /* emulator_linux_.go:78 default 33 */
+    /* MIMIC_ORACLE_LITERAL_MC=1: first fit and DelEntryByObj by the literal scans only (the tests
+     * check the indexes against them) */
+    const char *lit = getenv("MIMIC_ORACLE_LITERAL_MC");
+    if (lit && lit[0] == '1') vm->o_dup = 1;
     return vm;
 }
 
@@ -388,7 +612,12 @@ void orc_vm_free(orc_vm *vm) {
     free(vm->leaks);
     free(vm->maps);
     free(vm->progs);
-    free(vm->e);
+    for (size_t b = 0; b < vm->nblk; b++) free(vm->blk[b].e);
+    free(vm->blk);
+    free(vm->gn);
+    free(vm->ok);
+    free(vm->ov);
+    free(vm->os);
     free(vm);
 }
 

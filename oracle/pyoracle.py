@@ -186,7 +186,9 @@ class OracleVM:
         n = self.lib.orc_map_slots(self.h, mid, sl, kb, max(E, 1))
         if n < 0:
             raise OracleError("map_entries")
-        return [(kb.raw[i * K:(i + 1) * K], int(sl[i])) for i in range(n)]
+        raw = kb.raw
+        slots = np.frombuffer(sl, np.int32)
+        return [(raw[i * K:(i + 1) * K], int(slots[i])) for i in range(n)]
 
     def map_addr(self, mid: int) -> int:
         return self.lib.orc_map_addr(self.h, mid)

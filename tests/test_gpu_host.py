@@ -83,3 +83,39 @@ def test_pcap_to_host_pipeline(gpu):
     for c in range(V):
         assert maps["flows"].Values(c) == o["maps"]["flows"][c]
     vm.close()
+
+
+@pytest.mark.parametrize("order", ["swap_across_subbatches", "descending", "overlap"])
+def test_host_pipeline_pkt_out_order_refused_before_any_launch(gpu, order):
+    """pkt_out copies each sub-batch's byte window back whole, so the packets of the WHOLE batch
+    must be ascending and non-overlapping.  A batch that is not is refused before any copy or
+    launch: maps, r0 / status and pkt_out stay untouched (engine.cpp mimic_run_xdp_host)."""
+    import mimic_amd as M
+
+    p = W.prog_classifier()
+    sc = Scenario(vcpus=8, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    n = 4000
+    buf, off, lens = W.make_packets(n, seed=5)
+    off = off.copy()
+    if order == "swap_across_subbatches":   # sub-batch 0's last packet and sub-batch 1's first trade places
+        a, b = n // 4 - 1, n // 4 + 3
+        off[a], off[b] = off[b], off[a]
+    elif order == "descending":
+        off = off[::-1].copy()
+    else:
+        off[n - 1] = off[n - 2] + 10
+    vm, maps, pids = build_engine(sc)
+    out = np.full_like(buf, 0xA5)
+    r0 = np.full(n, 77, np.uint64)
+    st = np.full(n, 99, np.uint8)
+    with pytest.raises(M.MimicError, match="ascending"):
+        vm.RunXDPHost(pids[0], buf, off, lens, schedule=M.SCHED_INTERLEAVED, chunks=4, pkt_out=out, r0=r0,
+                      status=st)
+    assert (out == 0xA5).all() and (r0 == 77).all() and (st == 99).all()
+    assert all(not any(maps["verdicts"].Values(c)) for c in range(8))
+    # without pkt_out the same order is fine (results go by index)
+    r0b, stb = vm.RunXDPHost(pids[0], buf, off, lens, schedule=M.SCHED_INTERLEAVED, chunks=4)
+    cpu = W.schedule_cpu(n, 8, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    assert np.array_equal(r0b, o["r0"].astype(np.uint64)) and np.array_equal(stb, o["status"].astype(np.uint8))
+    vm.close()

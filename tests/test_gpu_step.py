@@ -123,3 +123,29 @@ def test_step_then_run_and_exit_again(gpu):
     assert a.Step() is True and a.Registers.PC == pc
     assert a.Packet() == pkt
     evm.close()
+
+
+def test_step_after_layout_change_is_refused(gpu):
+    """A map loaded between two Steps moves the VM's next free address (and may move its map
+    arena): the started process's saved R10 / packet pointers would point into the old layout, so
+    the next Step is refused (ENOTSUP) instead of running on stale addresses.  A process that has
+    not started yet picks up the new layout."""
+    p = W.prog_classifier()
+    sc = Scenario(vcpus=4, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    vm, maps, pids = build_engine(sc)
+    pkt = bytes(W.make_packets(1)[0][:64])
+    e = vm.NewProcess(pids[0], M.LinuxContextXDP(Packet=pkt))
+    e.SetCPUID(1)
+    e.Step()
+    e.Step()
+    fresh = vm.NewProcess(pids[0], M.LinuxContextXDP(Packet=pkt))
+    fresh.SetCPUID(1)
+    extra = M.LinuxArrayMap(M.MapSpec("late", M.MapType.Array, 4, 8, 1 << 16))
+    vm.emulator.AddMap("late", extra)
+    with pytest.raises(M.MimicError, match="layout changed"):
+        e.Step()
+    fresh.Run()
+    assert fresh.Registers.R0 in (1, 2)
+    e.Cleanup()
+    fresh.Cleanup()
+    vm.close()

@@ -51,3 +51,37 @@ def test_skb_workload_variety_hits_every_walk_branch():
         f = W.skb_variant(rng, int(rng.choice([14, 40, 64, 128, 576])))
         kinds.add(f[12:14] if len(f) >= 14 else b"short")
     assert {b"\x08\x00", b"\x86\xdd", b"\x81\x00", b"\x88\xa8", b"short"} <= kinds
+
+
+def test_oracle_memory_indexes_match_literal_scans(monkeypatch):
+    """The oracle's first-fit gap index and object index (oracle/mimic_oracle.c mc_add /
+    mc_del_obj) give exactly the addresses of the literal MemoryController loops
+    (memory_controller.go:58-112, 202-232): sk_buff batches (leaked entries, freed stack and
+    context holes of many sizes) returning skb->data, and the cfg-5 chain, both ways."""
+    from harness import Scenario
+    from mimic_amd import asm as A
+    from mimic_amd import workloads as W
+
+    S = A.SKB
+    raw, rel = A.assemble([A.ldx(4, 0, 1, S["data"]), A.ldx(4, 2, 1, S["data_end"]), A.alu64("lsh", 2, 32),
+                           A.alu64("or", 0, 2, reg=True), A.exit_()])
+    rng = np.random.default_rng(9)
+    pk = [bytes(rng.integers(0, 256, int(rng.choice([0, 1, 14, 60, 64, 200, 576, 1500])), dtype=np.uint8))
+          for _ in range(1500)]
+    from harness import skb_packets_to_buffer
+    buf, off, lens = skb_packets_to_buffer(pk)
+    cpu = rng.integers(0, 4, len(pk)).astype(np.int32)
+    progs, maps, pa = W.skb_programs()
+    cases = [(Scenario(vcpus=4, progs=[("addr", raw, rel)]), None),
+             (Scenario(vcpus=4, maps=maps, progs=[(p.name, p.raw, p.relocs) for p in progs], prog_array=pa),
+              [500, 501, 1200])]
+    for sc, splits in cases:
+        monkeypatch.setenv("MIMIC_ORACLE_LITERAL_MC", "1")
+        lit = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=1, splits=splits)
+        monkeypatch.setenv("MIMIC_ORACLE_LITERAL_MC", "0")
+        fast = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=1, splits=splits)
+        for k in ("r0", "status", "steps", "err_pc", "pkt"):
+            assert np.array_equal(lit[k], fast[k]), k
+        assert lit["maps"] == fast["maps"]
+        if splits is None:
+            assert len(set(lit["r0"].tolist())) > 1000   # addresses drift over the batch (leaks)

@@ -40,7 +40,7 @@ def col(r, *names):
     raise KeyError(names)
 
 
-def counters(d, kernel, skip=0):
+def counters(d, kernel, skip=0, keep=None):
     """counter name -> mean over the kernel's dispatches (after the first `skip`) of the
     per-dispatch value"""
     per = {}
@@ -54,12 +54,13 @@ def counters(d, kernel, skip=0):
     out = {}
     for k, v in per.items():
         vals = [v[d] for d in sorted(v, key=lambda x: int(x))][skip:]
+        vals = vals[:keep] if keep else vals
         if vals:
             out[k] = sum(vals) / len(vals)
     return out
 
 
-def kernel_stats(d, kernel, skip=0):
+def kernel_stats(d, kernel, skip=0, keep=None):
     """rocprofv3's --stats line for the kernel (every dispatch), plus the mean / median of the
     per-dispatch durations of the kernel trace after the first `skip` dispatches (timed_*)"""
     out = None
@@ -73,6 +74,7 @@ def kernel_stats(d, kernel, skip=0):
         if col(r, "Kernel_Name", "Kernel-Name", "KernelName").startswith(kernel):
             durs.append((int(col(r, "Dispatch_Id", "Correlation_Id")), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     durs = [x for _, x in sorted(durs)][skip:]
+    durs = durs[:keep] if keep else durs
     if out is not None and durs:
         srt = sorted(durs)
         out["timed_launches"] = len(durs)
@@ -94,6 +96,10 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--command", default="")
     ap.add_argument("--skip", type=int, default=2, help="leading dispatches to leave out (the bench's warmup)")
+    ap.add_argument("--keep", type=int, default=10, help="dispatches kept after --skip (the bench's timed steps; "
+                                                         "its trailing per-batch step-count launches are left out)")
+    ap.add_argument("--batches", type=int, default=0, help="batches the bench rotated over (0: its default)")
+    ap.add_argument("--sched", default="interleaved")
     a = ap.parse_args()
     import bench
 
@@ -101,12 +107,13 @@ def main():
     n = a.packets or cfg["packets"]
     vcpus = a.vcpus or cfg.get("vcpus") or max(64, n // 4)
     c = a.config
-    ks = kernel_stats(os.path.join(a.dir, f"kt_{c}"), a.kernel, a.skip)
-    fetch = counters(os.path.join(a.dir, f"fetch_{c}"), a.kernel, a.skip).get("FETCH_SIZE")
-    write = counters(os.path.join(a.dir, f"write_{c}"), a.kernel, a.skip).get("WRITE_SIZE")
-    sq = counters(os.path.join(a.dir, f"sq_{c}"), a.kernel, a.skip)
+    ks = kernel_stats(os.path.join(a.dir, f"kt_{c}"), a.kernel, a.skip, a.keep)
+    fetch = counters(os.path.join(a.dir, f"fetch_{c}"), a.kernel, a.skip, a.keep).get("FETCH_SIZE")
+    write = counters(os.path.join(a.dir, f"write_{c}"), a.kernel, a.skip, a.keep).get("WRITE_SIZE")
+    sq = counters(os.path.join(a.dir, f"sq_{c}"), a.kernel, a.skip, a.keep)
     out = {"config": c, "round": a.tag, "kernel": a.kernel, "kernel_src_hash": bench.kernel_src_hash_of(c),
-           "packets": n, "vcpus": vcpus, "kernel_stats": ks}
+           "packets": n, "vcpus": vcpus, "batches": a.batches or bench.default_batches(c, n),
+           "schedule": a.sched, "kernel_stats": ks}
     if fetch is not None and write is not None:
         out["fetch_size_kib_per_launch"] = fetch
         out["write_size_kib_per_launch"] = write
