@@ -45,6 +45,11 @@ CONFIGS = {
     "flowtrack": dict(prog="prog_flowtrack", packets=1 << 21, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 18,
                       workload="cfg4 per-GPU shard: 2M IMIX xdp_md (16M over 8 GPUs), 5-tuple parse + "
                                "insert-if-absent into a shared hash map K=16 S=8 E=131072"),
+    "flowtrack_insert": dict(prog="prog_flowtrack", packets=1 << 21, sizes=(64, 576, 1500), weights=(7, 4, 1),
+                             vcpus=1 << 18, reset_maps=True,
+                             workload="cfg4 per-GPU shard, inserting: 2M IMIX xdp_md into a FRESH shared hash map "
+                                      "K=16 S=8 E=131072 every step (map reset in the timed region), ~118K inserts "
+                                      "per batch"),
     "skb": dict(kind="skb", packets=1 << 20, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 16,
                 workload="cfg5: 1M IMIX sk_buff contexts, 5-program tail-call chain (~230 slots): __sk_buff "
                          "fields, LD_ABS/IND parse, hash flow lookups, per-CPU counters"),
@@ -410,8 +415,12 @@ def main(argv=None):
     nb = len(batches)
     stream = torch.cuda.Stream(device=dev)
 
+    reset = [maps[m["name"]] for m in wl.maps] if cfg.get("reset_maps") else []
+
     def launch(k):
         w, batch, res = batches[k % nb]
+        for m in reset:   # a fresh map per step: every flow of the batch is inserted again
+            m.Reset(stream)
         if wl.skb:
             vm.RunSKBBatch(pid, batch, res, stream=stream, sync=False)
             vm.SKBRelease()   # the batch's leaked sk_buff entries: a long run would exhaust 32-bit addresses

@@ -167,6 +167,12 @@ int mimic_map_entries(mimic_vm *vm, uint32_t map_id, void *keys_out, int32_t *sl
                       uint32_t *n_out);
 /* Raw value backing of (map, cpu): E*S bytes, slot order (D2H copy). */
 int mimic_map_read_values(mimic_vm *vm, uint32_t map_id, int32_t cpu, void *out, size_t cap);
+/* Not in the reference API: the map's state back to a fresh NewLinuxHashMap / NewLinuxArrayMap at
+ * the same addresses (values and keys zeroed; hash: every bucket empty, freelist 0..E-1 in order,
+ * emulator_linux_map_hash.go:56-64), queued on hip_stream (NULL: the VM's stream).  What a caller
+ * re-creating the map per batch would get, without a new layout; the bench's inserting-batch line
+ * uses it. */
+int mimic_map_reset(mimic_vm *vm, uint32_t map_id, void *hip_stream);
 /* Value backings of vCPUs [cpu_begin, cpu_end) of a per-CPU map ([0, 1) otherwise), cpu-major:
  * (cpu_end - cpu_begin) * E*S bytes in one D2H copy -- LinuxMap.Values(cpuid) for every cpu of a range
  * (emulator_linux_map_array.go:223-233, emulator_linux_map_hash.go:628-640). */

@@ -104,6 +104,7 @@ EXPORTS = {
     "mimic_map_entries": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_size_t,
                                     C.POINTER(C.c_uint32)]),
     "mimic_map_read_values": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_void_p, C.c_size_t]),
+    "mimic_map_reset": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "mimic_map_read_values_range": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_void_p, C.c_size_t]),
     "mimic_map_sum_u64": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_void_p, C.c_size_t]),
     "mimic_map_addr": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),

@@ -29,6 +29,7 @@ extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStrea
 extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
                                     int32_t cpu, int32_t *out, hipStream_t st);
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
+extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
 extern "C" size_t mimic_skb_scan_bytes(uint32_t n);
@@ -128,6 +129,11 @@ struct mimic_vm {
     hipStream_t s_h2d = nullptr, s_h2d2 = nullptr, s_d2h = nullptr;   // sub-batches alternate H2D streams
     hipStream_t kp_copy_stream = nullptr;
     hipEvent_t kp_copy_ev = nullptr;
+    // device-resident batches copy their launch parameters on a side stream: the copy runs while
+    // the previous kernel does, so back-to-back batches with different parameters keep no copy
+    // (and its completion latency) between their kernels on the compute stream
+    hipStream_t s_kp = nullptr;
+    hipEvent_t kp_side_ev = nullptr;
     // sk_buff batches (skb.h): per-packet records, footprints, their prefix, scan scratch, and
     // the device word pair {next leak address, this batch's leak base}
     SkbRec *d_skb_rec = nullptr;
@@ -193,7 +199,14 @@ static int kp_slot(mimic_vm *vm, const KParams &kp, hipStream_t st, const KParam
             HIP_OK(vm, hipEventRecord(vm->kp_copy_ev, vm->kp_copy_stream));
             HIP_OK(vm, hipStreamWaitEvent(st, vm->kp_copy_ev, 0));
         } else {
-            HIP_OK(vm, hipMemcpyAsync(vm->d_kp + slot, vm->h_kp + slot, sizeof kp, hipMemcpyHostToDevice, st));
+            if (!vm->s_kp) {
+                HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_kp, hipStreamNonBlocking));
+                HIP_OK(vm, hipEventCreateWithFlags(&vm->kp_side_ev, hipEventDisableTiming));
+            }
+            // the slot's earlier kernels are done (its event was waited for above)
+            HIP_OK(vm, hipMemcpyAsync(vm->d_kp + slot, vm->h_kp + slot, sizeof kp, hipMemcpyHostToDevice, vm->s_kp));
+            HIP_OK(vm, hipEventRecord(vm->kp_side_ev, vm->s_kp));
+            HIP_OK(vm, hipStreamWaitEvent(st, vm->kp_side_ev, 0));
         }
         vm->kp_last = slot;
         vm->kp_last_stream = st;
@@ -584,6 +597,8 @@ void mimic_vm_destroy(mimic_vm *vm) {
             if (e) hipEventDestroy(e);
     }
     if (vm->kp_copy_ev) hipEventDestroy(vm->kp_copy_ev);
+    if (vm->kp_side_ev) hipEventDestroy(vm->kp_side_ev);
+    if (vm->s_kp) hipStreamDestroy(vm->s_kp);
     hipFree(vm->d_skb_rec);
     hipFree(vm->d_skb_foot);
     hipFree(vm->d_skb_prefix);
@@ -944,6 +959,26 @@ int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, siz
     if ((rc = settle(vm))) return rc;
     HIP_OK(vm, hipMemcpy(out, vm->arena + base, n, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    if (m.type == 3) return fail(vm, MIMIC_ENOTSUP, "program arrays are not reset");   // ebpf.ProgramArray
+    hipSetDevice(vm->s.device);
+    if ((rc = skb_settle(vm))) return rc;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
+    if (vm->last_stream && vm->last_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
+    HIP_OK(vm, hipMemsetAsync(vm->arena + m.dev_off, 0, (size_t)m.dev_stride * m.ncpu, st));
+    if (is_hash(m)) {
+        HIP_OK(vm, hipMemsetAsync(vm->arena + m.keys_dev_off, 0, (size_t)m.max_entries * m.key_size, st));
+        const DMap dm = to_dmap(m);
+        if (mimic_launch_hash_reset(vm->arena, &dm, st))
+            return fail(vm, MIMIC_EDEVICE, "reset: %s", hipGetErrorString(hipGetLastError()));
+    }
+    vm->last_stream = st;
+    return 0;
 }
 
 int mimic_map_read_values_range(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_end, void *out, size_t cap) {
@@ -1390,7 +1425,10 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (bound && kp.budget < bound) jit = false;
     }
     vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
-    {  // launch parameters are read from a device copy
+    if (jit && ji.karg) {  // launch parameters by value: the runtime copies them into the kernarg segment
+        if (mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, nullptr, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    } else {  // launch parameters are read from a device copy
         const KParams *dkp = nullptr;
         const int slot = kp_slot(vm, kp, st, &dkp);
         if (slot < 0) return slot;

@@ -130,49 +130,46 @@ HDEV void h_acquire(uint32_t *lk) {
         __builtin_amdgcn_s_sleep(2);
     }
 }
+HDEV bool h_try_acquire(uint32_t *lk) {
+    uint32_t e = 0;
+    return __hip_atomic_compare_exchange_strong(lk, &e, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 HDEV void h_release(uint32_t *lk) {
     h_drain();
     __hip_atomic_store(lk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// find-or-insert under the key's stripe lock (ONE lane at a time per wave).
-// Returns the slot, or -1 when the freelist is empty (E2BIG).  *inserted = a new slot.
+// Probe under the key's stripe lock: the key's slot (found) or -1, and the first reusable
+// bucket on its probe path (freep: a tombstone or the terminating EMPTY).
 template <class KS>
-HDEV int32_t h_insert_locked(const HT &t, const KS &ks, uint64_t h, bool *inserted) {
-    *inserted = false;
-    uint32_t *lk = h_lock(t, h);
-    h_acquire(lk);
-    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32), K = t.K;
-    uint32_t p = (uint32_t)h & mask, freep = HT_EMPTY;
-    int32_t found = -1;
+HDEV int32_t h_probe_held(const HT &t, const KS &ks, uint64_t h, uint32_t *freep) {
+    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32);
+    uint32_t p = (uint32_t)h & mask;
+    *freep = HT_EMPTY;
     for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
         const uint64_t *r = h_rec(t, p);
         const uint64_t w = h_ld(r);
         const uint32_t s = (uint32_t)w;
         if (s == HT_EMPTY) {
-            if (freep == HT_EMPTY) freep = p;
-            break;
+            if (*freep == HT_EMPTY) *freep = p;
+            return -1;
         }
         if (s == HT_TOMB) {
-            if (freep == HT_EMPTY) freep = p;
+            if (*freep == HT_EMPTY) *freep = p;
             continue;
         }
-        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, K)) {
-            found = (int32_t)s;
-            break;
-        }
+        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K)) return (int32_t)s;
     }
-    if (found >= 0) {
-        h_release(lk);
-        return found;
-    }
-    const int32_t idx = h_fl_pop(t);
-    if (idx < 0) {
-        h_release(lk);
-        return -1;
-    }
-    // claim a free bucket (another stripe may take the same one first: then probe on)
-    p = freep == HT_EMPTY ? ((uint32_t)h & mask) : freep;
+    return -1;
+}
+
+// A new key into slot `idx` (popped), lock held: claim a free bucket from freep on (another
+// stripe may take it first: then probe on), write the key words, publish tag | slot.  Returns
+// whether the bucket was EMPTY (the table's `used` count grows).
+template <class KS>
+HDEV bool h_place_held(const HT &t, const KS &ks, uint64_t h, uint32_t freep, int32_t idx) {
+    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32);
+    uint32_t p = freep == HT_EMPTY ? ((uint32_t)h & mask) : freep;
     uint64_t *r = nullptr;
     bool was_empty = false;
     for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
@@ -186,21 +183,37 @@ HDEV int32_t h_insert_locked(const HT &t, const KS &ks, uint64_t h, bool *insert
         }
     }
     // live + busy <= E < ht_cap, so a free bucket always exists
-    const uint32_t nq = (K + 7) >> 3;
+    const uint32_t nq = (t.K + 7) >> 3;
     for (uint32_t q = 0; q < nq; q++) h_st(r + 1 + q, ks.word(q));
     h_drain();
     h_st(r, ((uint64_t)tag << 32) | (uint32_t)idx);
-    if (was_empty) __hip_atomic_fetch_add(&h_ctl(t)->used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return was_empty;
+}
+
+// find-or-insert with the key's stripe lock `lk` held, ONE lane (host-side map operations);
+// releases the lock.  Returns the slot, or -1 when the freelist is empty (E2BIG).
+template <class KS>
+HDEV int32_t h_insert_held(const HT &t, const KS &ks, uint64_t h, uint32_t *lk, bool *inserted) {
+    *inserted = false;
+    uint32_t freep;
+    const int32_t found = h_probe_held(t, ks, h, &freep);
+    if (found >= 0) {
+        h_release(lk);
+        return found;
+    }
+    const int32_t idx = h_fl_pop(t);
+    if (idx >= 0) {
+        if (h_place_held(t, ks, h, freep, idx))
+            __hip_atomic_fetch_add(&h_ctl(t)->used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *inserted = true;
+    }
     h_release(lk);
-    *inserted = true;
     return idx;
 }
 
-// delete under the stripe lock: the deleted slot or -1 (absent)
+// delete with the key's stripe lock `lk` held, ONE lane; releases it.  The deleted slot or -1
 template <class KS>
-HDEV int32_t h_delete_locked(const HT &t, const KS &ks, uint64_t h) {
-    uint32_t *lk = h_lock(t, h);
-    h_acquire(lk);
+HDEV int32_t h_delete_held(const HT &t, const KS &ks, uint64_t h, uint32_t *lk) {
     uint32_t p = 0;
     const int32_t idx = h_find(t, ks, h, &p);
     if (idx >= 0) {
@@ -210,6 +223,150 @@ HDEV int32_t h_delete_locked(const HT &t, const KS &ks, uint64_t h) {
     }
     h_release(lk);
     return idx;
+}
+
+// Wave-cooperative locking.  A lane may never spin on a lock while a lane of its own wave holds
+// one (the holder could not run on: the wave waits for the spinner at the reconvergence point,
+// and two such waves deadlock).  So the lanes of a wave that need a stripe lock go in rounds: in
+// a round, one lane per distinct lock (the lowest) tries its lock once; winners run their critical
+// section and release, the others retry next round.  Two lanes of a wave with one key (one lock)
+// thus never overlap, lanes with different locks insert concurrently, and a single lane
+// (sequential runs) takes its lock in the first round.
+HDEV bool h_round_leader(uint64_t pend, uint32_t lkid) {
+    const uint32_t me = __lane_id();
+    bool lead = false;
+    for (uint64_t rem = pend; rem;) {  // one leader per distinct lock among the pending lanes
+        const uint32_t l = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)lkid, (int)l);
+        rem &= ~__ballot(lkid == v);
+        lead |= me == l;
+    }
+    return lead;
+}
+
+HDEV uint64_t h_bcast64(uint64_t v, uint32_t l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// find-or-insert for the calling lanes of a wave (the helper path).  The lanes holding their
+// locks in a round take their freelist slots with ONE pair of atomics for the round (the
+// freelist counters are single words every inserting lane of the GPU would otherwise hit: the
+// same-address atomics serialise in L2 and set the insert rate); ranks within the round follow
+// lane order.  A lone lane pops exactly like h_fl_pop, so sequential runs get the reference's
+// FIFO slots.  Returns the slot or -1 (E2BIG); *inserted = a new slot.
+template <class KS>
+HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted) {
+    uint32_t *lk = h_lock(t, h);
+    const uint32_t me = __lane_id();
+    const uint32_t lkid = (uint32_t)((uintptr_t)lk >> 2);
+    HashCtl *c = h_ctl(t);
+    bool done = false;
+    int32_t idx = -1;
+    *inserted = false;
+    for (;;) {
+        const uint64_t pend = __ballot(!done);
+        if (!pend) break;
+        const bool lead = h_round_leader(pend, lkid);
+        const bool mine = !done && lead && h_try_acquire(lk);
+        uint32_t freep = HT_EMPTY;
+        const int32_t found = mine ? h_probe_held(t, ks, h, &freep) : -1;
+        const bool need = mine && found < 0;
+        const uint64_t needm = __ballot(need);
+        int32_t slot = -1;
+        if (needm) {
+            const uint32_t k = (uint32_t)__builtin_popcountll(needm), first = (uint32_t)__builtin_ctzll(needm);
+            uint32_t got = 0;
+            uint64_t base = 0;
+            if (me == first) {
+                const int32_t a = __hip_atomic_fetch_add(&c->avail, -(int32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                got = a <= 0 ? 0u : ((uint32_t)a < k ? (uint32_t)a : k);
+                if (got < k)
+                    __hip_atomic_fetch_add(&c->avail, (int32_t)(k - got), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (got) base = __hip_atomic_fetch_add(&c->head, (unsigned long long)got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            got = (uint32_t)__builtin_amdgcn_readlane((int)got, (int)first);
+            base = h_bcast64(base, first);
+            const uint32_t rank = (uint32_t)__builtin_popcountll(needm & ((1ull << me) - 1));
+            if (need && rank < got) {
+                int32_t *f = h_ring(t) + ((base + rank) & (t.fl_cap - 1));
+                // the push that fills this position has already reserved it (avail counted it)
+                while ((slot = __hip_atomic_exchange(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        bool empty_used = false;
+        if (mine) {
+            if (found >= 0) {
+                idx = found;
+            } else if (slot >= 0) {
+                empty_used = h_place_held(t, ks, h, freep, slot);
+                idx = slot;
+                *inserted = true;
+            } else {
+                idx = -1;   // the freelist is empty: E2BIG
+            }
+            h_release(lk);
+            done = true;
+        }
+        const uint64_t um = __ballot(empty_used);
+        if (um && me == (uint32_t)__builtin_ctzll(um))
+            __hip_atomic_fetch_add(&c->used, (uint32_t)__builtin_popcountll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!done) __builtin_amdgcn_s_sleep(1);
+    }
+    return idx;
+}
+
+// delete for the calling lanes of a wave: lock rounds as above; the freed slots of a round go to
+// the freelist tail with one reservation and one `avail` release for the round (after every
+// ring position of the round is written).
+template <class KS>
+HDEV void h_delete_wave(const HT &t, const KS &ks, uint64_t h) {
+    uint32_t *lk = h_lock(t, h);
+    const uint32_t me = __lane_id();
+    const uint32_t lkid = (uint32_t)((uintptr_t)lk >> 2);
+    HashCtl *c = h_ctl(t);
+    bool done = false;
+    for (;;) {
+        const uint64_t pend = __ballot(!done);
+        if (!pend) break;
+        const bool lead = h_round_leader(pend, lkid);
+        const bool mine = !done && lead && h_try_acquire(lk);
+        int32_t idx = -1;
+        if (mine) {
+            uint32_t p = 0;
+            idx = h_find(t, ks, h, &p);
+            if (idx >= 0) {
+                uint64_t *r = h_rec(t, p);
+                h_st(r, (h_ld(r) & ~0xffffffffull) | HT_TOMB);
+            }
+        }
+        const uint64_t pm = __ballot(idx >= 0);
+        if (pm) {
+            const uint32_t k = (uint32_t)__builtin_popcountll(pm), first = (uint32_t)__builtin_ctzll(pm);
+            uint64_t base = 0;
+            if (me == first) base = __hip_atomic_fetch_add(&c->tail, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            base = h_bcast64(base, first);
+            if (idx >= 0) {
+                int32_t *f = h_ring(t) + ((base + (uint32_t)__builtin_popcountll(pm & ((1ull << me) - 1))) & (t.fl_cap - 1));
+                for (;;) {
+                    int32_t e = -1;
+                    if (__hip_atomic_compare_exchange_strong(f, &e, idx, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT))
+                        break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                h_drain();
+            }
+            if (me == first) __hip_atomic_fetch_add(&c->avail, (int32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (mine) {
+            h_release(lk);
+            done = true;
+        }
+        if (!done) __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 // key words taken from device bytes (host-side map operations)

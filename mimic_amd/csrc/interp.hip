@@ -452,7 +452,11 @@ extern "C" __global__ void mimic_hash_op_kernel(uint8_t *arena, DMap m, uint32_t
     } else if (op == 1) {
         idx = h_find(t, ks, h, nullptr);
         bool ins = false;
-        if (idx < 0) idx = h_insert_locked(t, ks, h, &ins);
+        if (idx < 0) {   // one thread: it may wait for its stripe lock
+            uint32_t *lk = h_lock(t, h);
+            h_acquire(lk);
+            idx = h_insert_held(t, ks, h, lk, &ins);
+        }
         if (idx >= 0) {  // keys.Write + values[cpu].Write (emulator_linux_map_hash.go:188-200)
             uint8_t *kd = arena + m.keys_dev_off + (size_t)idx * m.key_size;
             for (uint32_t i = 0; i < m.key_size; i++) kd[i] = key[i];
@@ -461,7 +465,9 @@ extern "C" __global__ void mimic_hash_op_kernel(uint8_t *arena, DMap m, uint32_t
             for (uint32_t i = 0; i < m.value_size; i++) vd[i] = val[i];
         }
     } else {
-        idx = h_delete_locked(t, ks, h);
+        uint32_t *lk = h_lock(t, h);
+        h_acquire(lk);
+        idx = h_delete_held(t, ks, h, lk);
     }
     *out = idx;
 }
@@ -504,6 +510,35 @@ extern "C" __global__ __launch_bounds__(1024) void mimic_hash_rebuild_kernel(uin
     }
     __syncthreads();
     if (threadIdx.x == 0) c->used = live;
+}
+
+// A hash map's index back to its NewLinuxHashMap state (emulator_linux_map_hash.go:56-64): every
+// bucket EMPTY, every stripe lock free, the freelist ring 0..E-1, head 0 / tail E / avail E.
+extern "C" __global__ void mimic_hash_reset_kernel(uint8_t *arena, DMap m) {
+    const HT t = h_table(arena, m);
+    const size_t nrec = (size_t)t.cap * t.rec_q;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    uint64_t *rec = (uint64_t *)t.base;
+    for (size_t i = g; i < nrec; i += stride) rec[i] = ~0ull;
+    uint32_t *lk = h_locks(t);
+    for (size_t i = g; i < t.nlocks; i += stride) lk[i] = 0;
+    int32_t *ring = h_ring(t);
+    for (size_t i = g; i < t.fl_cap; i += stride) ring[i] = i < m.max_entries ? (int32_t)i : -1;
+    if (g == 0) {
+        HashCtl *c = h_ctl(t);
+        c->head = 0;
+        c->tail = m.max_entries;
+        c->avail = (int32_t)m.max_entries;
+        c->used = 0;
+    }
+}
+
+extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_t st) {
+    const size_t work = std::max<size_t>((size_t)m->ht_cap * m->rec_q, m->fl_cap);
+    const uint32_t blocks = (uint32_t)std::min<size_t>((work + 255) / 256, 2048);
+    hipLaunchKernelGGL(mimic_hash_reset_kernel, dim3(blocks), dim3(256), 0, st, arena, *m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,

@@ -106,6 +106,8 @@ class Gen {
         vc_knob = !(vcv && vcv[0] == '0');
         const char *fw = getenv("MIMIC_JIT_FWD");   // 0: no stack-store -> lookup key forwarding
         forward = !(fw && fw[0] == '0');
+        const char *ka = getenv("MIMIC_JIT_KARG");   // 0: launch parameters through a device copy (slots)
+        if (ka) karg = atoi(ka);
         const char *nr = getenv("MIMIC_JIT_NTRES");   // 0: per-packet results stored as plain stores
         ntres = !(nr && nr[0] == '0');
         const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
@@ -172,6 +174,9 @@ class Gen {
     bool skb_lds_knob = true;  // MIMIC_JIT_SKBLDS=0: no LDS copy of the sk_buff record
     bool skb_lds = false;
     static constexpr uint32_t kSrecQ = 21;   // 8-byte words per LDS record slot (SkbRec is 20)
+    int karg = 2;              // MIMIC_JIT_KARG: 2 launch parameters by value in the kernarg segment, read
+                               // through an opaque constant-space pointer; 1 the same, plain; 0 a
+                               // pointer to a device copy (a copy + event per new batch between kernels)
     bool hash_fast = true;     // MIMIC_JIT_HASH=0: no inline hash-map lookups
     bool tail_inline = true;   // MIMIC_JIT_TAIL=0: no inline tail calls
     bool census = false;       // MIMIC_JIT_CENSUS=1: diagnostics (tools/cold_census.py)
@@ -292,11 +297,23 @@ class Gen {
         // 2 waves): 0.172 -> 0.137 ms per launch; cfg 2 and 3 fit 4 waves anyway.  Large kernels
         // (cfg 5) keep the compiler's choice: forcing 2 waves there spills 264 VGPRs (1.2 vs 0.7 ms).
         const int wv = waves > 0 ? waves : (cold_inline ? 4 : 0);
+        const std::string param = karg ? "const KParams kp_arg_" : "const KParams *__restrict__ kpp";
         if (wv > 0)
-            E.line((std::string("extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(") + std::to_string(wv) +
-                   "))) void mimic_jit_kernel(const KParams *__restrict__ kpp) {").c_str());
+            E.line("%s", (std::string("extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(") +
+                          std::to_string(wv) + "))) void mimic_jit_kernel(" + param + ") {").c_str());
         else
-            E.line("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(const KParams *__restrict__ kpp) {");
+            E.line("%s", ("extern \"C\" __global__ __launch_bounds__(256) void mimic_jit_kernel(" + param + ") {").c_str());
+        if (karg == 2) {
+            // the parameters stay in the kernarg segment (constant address space): an opaque
+            // constant-space pointer keeps every field a scalar load where it is used (not all
+            // preloaded into SGPRs at entry)
+            E.line("  (void)kp_arg_;   // the first (only) kernel argument: at offset 0 of the kernarg segment");
+            E.line("  const KParams __attribute__((address_space(4))) *kp4_ = (const KParams __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();");
+            E.line("  asm volatile(\"\" : \"+s\"(kp4_));");
+            E.line("  const KParams *kpp = (const KParams *)kp4_;");
+        } else if (karg == 1) {
+            E.line("  const KParams *kpp = &kp_arg_;");
+        }
         E.line("  const KParams &kp = *kpp;");
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
         E.line("  if (g >= kp.lanes) return;");
@@ -1537,6 +1554,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->tail_calls = g.has_tail();
         info->early_loads = g.has_early_loads();
         info->cold_inline = g.cold_inline;
+        info->karg = g.karg != 0;
     }
     return src;
 }
@@ -1585,9 +1603,8 @@ int mimic_jit_prebuild_source(const std::string &src, std::string *log) {
 int mimic_jit_launch(hipFunction_t fn, const JitInfo &info, const KParams *kp, const KParams *d_kp, hipStream_t st) {
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
-    (void)info;
     const KParams *p = d_kp;
-    void *args[] = {(void *)&p};
+    void *args[] = {info.karg ? (void *)kp : (void *)&p};   // by value (kernarg segment) or a device copy
     return hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
 }
 

@@ -741,13 +741,8 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
     int32_t idx = h_find(t, ks, h, nullptr);
     bool inserted = false;
     if (idx < 0) {
-        // a new key: the lanes of this wave that insert take the stripe locks one at a time
-        uint64_t need = __ballot(1);
-        const uint32_t me = __lane_id();
-        while (need) {
-            if (me == (uint32_t)__builtin_ctzll(need)) idx = h_insert_locked(t, ks, h, &inserted);
-            need &= need - 1;
-        }
+        // a new key: find-or-insert under its stripe lock, the wave's lanes in lock rounds
+        idx = h_insert_wave(t, ks, h, &inserted);
     }
     if (idx < 0) {
         o.r0 = 7; // syscall.E2BIG: the freelist is empty
@@ -780,12 +775,7 @@ DEV HelperOut helper_delete(const KParams &kp, const Lane &L, uint64_t r1, uint6
     const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
     const uint64_t h = h_hash(ks, m.key_size);
     const HT t = h_table(kp.arena, m);
-    uint64_t need = __ballot(1);
-    const uint32_t me = __lane_id();
-    while (need) {
-        if (me == (uint32_t)__builtin_ctzll(need)) h_delete_locked(t, ks, h);
-        need &= need - 1;
-    }
+    h_delete_wave(t, ks, h);
     o.r0 = 0;
     o.set_r0 = true;
     return o;

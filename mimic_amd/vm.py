@@ -168,6 +168,13 @@ class LinuxMap:
         _check(vm.h, vm.lib.mimic_map_read_values(vm.h, self.id, cpuid, buf, max(n, 1)), "read values")
         return buf.raw[:n]
 
+    def Reset(self, stream=None) -> None:
+        """Not in the reference API: back to a freshly created map at the same addresses (zeroed
+        values, hash maps empty with the freelist 0..E-1), queued on `stream` (mimic_map_reset)."""
+        vm = self._vm
+        st = stream.cuda_stream if stream is not None else None
+        _check(vm.h, vm.lib.mimic_map_reset(vm.h, self.id, st), "reset")
+
     def ValuesRange(self, cpu_begin: int = 0, cpu_end: Optional[int] = None):
         """Values(c) for every cpu c of [cpu_begin, cpu_end) in one device copy: a numpy uint8 array
         of shape (cpu_end - cpu_begin, MaxEntries * ValueSize)."""

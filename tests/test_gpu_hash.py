@@ -148,3 +148,40 @@ def test_hash_helpers_random_programs(gpu, seed):
         cpu = np.zeros(len(pk), dtype=np.int32)
         assert_same(run_oracle(sc, b, off, lens, cpu, step_budget=4000),
                     run_engine(sc, b, off, lens, cpu, step_budget=4000))
+
+
+@pytest.mark.parametrize("mtype", [1, 5, 6])
+def test_map_reset_is_a_fresh_map(gpu, mtype):
+    """mimic_map_reset: after any history (inserts, deletes, a full freelist), the map behaves
+    exactly like a newly created one at the same addresses -- sequential updates get the slots
+    0, 1, 2, ... of the fresh freelist (emulator_linux_map_hash.go:56-64) and values read zero."""
+    spec = dict(name="h", type=mtype, key_size=4 if mtype == 6 else 6, value_size=8, max_entries=5)
+    sc = Scenario(vcpus=3, maps=[spec])
+    evm, emaps, _ = build_engine(sc)
+    em = emaps["h"]
+    rng = np.random.default_rng(8)
+    keys = [bytes(rng.integers(0, 256, spec["key_size"], dtype=np.uint8)) for _ in range(9)]
+    if mtype == 6:
+        keys = [int(i).to_bytes(4, "little") for i in range(5)]
+    for step in range(60):
+        key = keys[int(rng.integers(0, len(keys)))]
+        em.Update(key, bytes(rng.integers(0, 256, 8, dtype=np.uint8)), 0, int(rng.integers(0, 3)))
+        if mtype != 6 and rng.random() < 0.3:
+            em.Delete(key)
+    em.Reset()
+    ovm, omids, _ = build_oracle(sc)   # a fresh map
+    om = omids["h"]
+    ncpu = 3 if mtype in (5, 6) else 1
+    for c in range(ncpu):
+        assert em.Values(c) == ovm.map_values(om, c) == bytes(40)
+    if mtype != 6:
+        assert em.Entries() == []
+    for step, key in enumerate(keys):
+        val = bytes([step]) * 8
+        assert em.Update(key, val, 0, step % ncpu) == ovm.map_update(om, key, val, 0, step % ncpu), step
+    for c in range(ncpu):
+        assert em.Values(c) == ovm.map_values(om, c)
+    if mtype != 6:
+        assert sorted(em.Entries()) == sorted(ovm.map_entries(om))
+    evm.close()
+    ovm.close()
