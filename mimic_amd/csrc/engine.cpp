@@ -30,6 +30,7 @@ extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, 
                                     int32_t cpu, int32_t *out, hipStream_t st);
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
 extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_t st);
+extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
 extern "C" size_t mimic_skb_scan_bytes(uint32_t n);
@@ -54,6 +55,7 @@ struct HostMap {
     uint32_t keys_addr, ht_cap, rec_q, nlocks, fl_cap;
     // a delete may have left tombstones (hashmap.h): only then can the table need a rebuild
     mutable bool may_tomb = false;
+    mutable bool pop_dirty = false;   // a pop-only launch left head / avail to normalise (hashmap.h)
 };
 
 // can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
@@ -720,7 +722,7 @@ int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id)
         // index region (hashmap.h h_table): records | rebuild copy | locks | freelist ring | HashCtl
         const uint64_t rec_bytes = (uint64_t)m.ht_cap * m.rec_q * 8;
         const uint64_t lock_off = 2 * rec_bytes, fl_off = lock_off + (uint64_t)m.nlocks * 4,
-                       ctl_off = fl_off + (uint64_t)m.fl_cap * 4;
+                       ctl_off = (fl_off + (uint64_t)m.fl_cap * 4 + 127) & ~127ull;   // hashmap.h h_ctl
         if (!rc) rc = arena_reserve(vm, ctl_off + sizeof(HashCtl), &m.ht_dev_off);
         if (rc) return rc;
         HIP_OK(vm, hipMemset(vm->arena + m.ht_dev_off, 0xff, rec_bytes));
@@ -830,6 +832,10 @@ static int hash_op(mimic_vm *vm, const HostMap &m, uint32_t op, const void *key,
     if (e == hipSuccess && value) e = hipMemcpy(d + kb, value, m.value_size, hipMemcpyHostToDevice);
     const DMap dm = to_dmap(m);
     if (op == 2) m.may_tomb = true;
+    if (e == hipSuccess && m.pop_dirty) {   // the host op may push (delete) or pop with the semaphore
+        if (mimic_launch_hash_normalize(vm->arena, &dm, vm->stream)) e = hipErrorLaunchFailure;
+        m.pop_dirty = false;
+    }
     if (e == hipSuccess && mimic_launch_hash_op(vm->arena, &dm, op, d, d + kb, cpu, dout, vm->stream))
         e = hipErrorLaunchFailure;
     if (e == hipSuccess) e = hipMemcpyAsync(slot, dout, 4, hipMemcpyDeviceToHost, vm->stream);
@@ -972,6 +978,7 @@ int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
     if (vm->last_stream && vm->last_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
     HIP_OK(vm, hipMemsetAsync(vm->arena + m.dev_off, 0, (size_t)m.dev_stride * m.ncpu, st));
     if (is_hash(m)) {
+        m.pop_dirty = false;
         HIP_OK(vm, hipMemsetAsync(vm->arena + m.keys_dev_off, 0, (size_t)m.max_entries * m.key_size, st));
         const DMap dm = to_dmap(m);
         if (mimic_launch_hash_reset(vm->arena, &dm, st))
@@ -1380,11 +1387,20 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     // (skipped while no delete can have run on the map: without tombstones live entries stay
     // below half of the table, so the check would always decline -- and a kernel between the
     // batches costs a launch gap)
+    // A launch whose programs never delete pops the freelists without the `avail` semaphore
+    // (hashmap.h h_insert_wave pop_only); one that may delete first normalises maps left so.
+    kp.hash_pop_only = vm->prog_deletes ? 0u : 1u;
     for (auto &m : vm->maps) {
         if (!is_hash(m)) continue;
+        const DMap dm = to_dmap(m);
+        if (vm->prog_deletes && m.pop_dirty) {
+            if (mimic_launch_hash_normalize(vm->arena, &dm, st))
+                return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+            m.pop_dirty = false;
+        }
+        if (!vm->prog_deletes) m.pop_dirty = true;
         if (vm->prog_deletes) m.may_tomb = true;
         if (!m.may_tomb) continue;
-        const DMap dm = to_dmap(m);
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }

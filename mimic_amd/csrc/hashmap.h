@@ -47,7 +47,18 @@ HDEV uint64_t *h_rec(const HT &t, uint32_t p) { return (uint64_t *)t.base + (siz
 HDEV uint64_t *h_tmp(const HT &t) { return (uint64_t *)(t.base + h_rec_bytes(t)); }
 HDEV uint32_t *h_locks(const HT &t) { return (uint32_t *)(t.base + 2 * h_rec_bytes(t)); }
 HDEV int32_t *h_ring(const HT &t) { return (int32_t *)(h_locks(t) + t.nlocks); }
-HDEV HashCtl *h_ctl(const HT &t) { return (HashCtl *)(h_ring(t) + t.fl_cap); }
+HDEV HashCtl *h_ctl(const HT &t) {   // 128-byte aligned after the ring (engine.cpp: ctl_off)
+    return (HashCtl *)(((uintptr_t)(h_ring(t) + t.fl_cap) + 127) & ~(uintptr_t)127);
+}
+HDEV uint32_t *h_used_shard(HashCtl *c) {   // the calling wave's shard of the `used` count
+    const uint32_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (HT_USED_SHARDS - 1);
+    return &c->used_sh[32 * w];
+}
+HDEV uint32_t h_used_total(const HashCtl *c) {
+    uint32_t u = c->used0;
+    for (uint32_t s = 0; s < HT_USED_SHARDS; s++) u += c->used_sh[32 * s];
+    return u;
+}
 
 // key hash over the zero-padded little-endian key words (any good 64-bit mix; the reference's
 // sha256 only names Go-map buckets, which no program can observe)
@@ -204,7 +215,7 @@ HDEV int32_t h_insert_held(const HT &t, const KS &ks, uint64_t h, uint32_t *lk, 
     const int32_t idx = h_fl_pop(t);
     if (idx >= 0) {
         if (h_place_held(t, ks, h, freep, idx))
-            __hip_atomic_fetch_add(&h_ctl(t)->used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&h_ctl(t)->used0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *inserted = true;
     }
     h_release(lk);
@@ -256,8 +267,13 @@ HDEV uint64_t h_bcast64(uint64_t v, uint32_t l) {
 // same-address atomics serialise in L2 and set the insert rate); ranks within the round follow
 // lane order.  A lone lane pops exactly like h_fl_pop, so sequential runs get the reference's
 // FIFO slots.  Returns the slot or -1 (E2BIG); *inserted = a new slot.
+//
+// pop_only (no program of the launch deletes, so no push runs concurrently): the round takes its
+// positions with one add to head and no `avail` semaphore; positions at or past tail are E2BIG.
+// head may then pass tail, and avail is stale: mimic_hash_normalize_kernel sets head = min(head,
+// tail), avail = tail - head before any operation that pushes (engine.cpp hash_normalize).
 template <class KS>
-HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted) {
+HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted, bool pop_only = false) {
     uint32_t *lk = h_lock(t, h);
     const uint32_t me = __lane_id();
     const uint32_t lkid = (uint32_t)((uintptr_t)lk >> 2);
@@ -279,7 +295,13 @@ HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted
             const uint32_t k = (uint32_t)__builtin_popcountll(needm), first = (uint32_t)__builtin_ctzll(needm);
             uint32_t got = 0;
             uint64_t base = 0;
-            if (me == first) {
+            if (pop_only) {
+                if (me == first) {
+                    base = __hip_atomic_fetch_add(&c->head, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long tl = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    got = base >= tl ? 0u : (tl - base < k ? (uint32_t)(tl - base) : k);
+                }
+            } else if (me == first) {
                 const int32_t a = __hip_atomic_fetch_add(&c->avail, -(int32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 got = a <= 0 ? 0u : ((uint32_t)a < k ? (uint32_t)a : k);
                 if (got < k)
@@ -291,9 +313,14 @@ HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted
             const uint32_t rank = (uint32_t)__builtin_popcountll(needm & ((1ull << me) - 1));
             if (need && rank < got) {
                 int32_t *f = h_ring(t) + ((base + rank) & (t.fl_cap - 1));
-                // the push that fills this position has already reserved it (avail counted it)
-                while ((slot = __hip_atomic_exchange(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0)
-                    __builtin_amdgcn_s_sleep(1);
+                if (pop_only) {   // positions below tail were written before this launch
+                    slot = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    // the push that fills this position has already reserved it (avail counted it)
+                    while ((slot = __hip_atomic_exchange(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0)
+                        __builtin_amdgcn_s_sleep(1);
+                }
             }
         }
         bool empty_used = false;
@@ -312,7 +339,7 @@ HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted
         }
         const uint64_t um = __ballot(empty_used);
         if (um && me == (uint32_t)__builtin_ctzll(um))
-            __hip_atomic_fetch_add(&c->used, (uint32_t)__builtin_popcountll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(h_used_shard(c), (uint32_t)__builtin_popcountll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!done) __builtin_amdgcn_s_sleep(1);
     }
     return idx;

@@ -479,7 +479,7 @@ extern "C" __global__ __launch_bounds__(1024) void mimic_hash_rebuild_kernel(uin
     const HT t = h_table(arena, m);
     HashCtl *c = h_ctl(t);
     if (threadIdx.x == 0) {
-        go = force || (uint64_t)c->used * 4 > (uint64_t)m.ht_cap * 3;
+        go = force || (uint64_t)h_used_total(c) * 4 > (uint64_t)m.ht_cap * 3;
         live = 0;
     }
     __syncthreads();
@@ -509,7 +509,25 @@ extern "C" __global__ __launch_bounds__(1024) void mimic_hash_rebuild_kernel(uin
         atomicAdd(&live, 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) c->used = live;
+    if (threadIdx.x == 0) {
+        c->used0 = live;
+        for (uint32_t sh = 0; sh < HT_USED_SHARDS; sh++) c->used_sh[32 * sh] = 0;
+    }
+}
+
+// After a pop-only launch (hashmap.h h_insert_wave): head back to at most tail, avail = what is
+// left between them -- the state the pops would have left with the semaphore.
+extern "C" __global__ void mimic_hash_normalize_kernel(uint8_t *arena, DMap m) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    HashCtl *c = h_ctl(h_table(arena, m));
+    const unsigned long long tl = c->tail, hd = c->head < tl ? c->head : tl;
+    c->head = hd;
+    c->avail = (int32_t)(tl - hd);
+}
+
+extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st) {
+    hipLaunchKernelGGL(mimic_hash_normalize_kernel, dim3(1), dim3(64), 0, st, arena, *m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // A hash map's index back to its NewLinuxHashMap state (emulator_linux_map_hash.go:56-64): every
@@ -530,7 +548,8 @@ extern "C" __global__ void mimic_hash_reset_kernel(uint8_t *arena, DMap m) {
         c->head = 0;
         c->tail = m.max_entries;
         c->avail = (int32_t)m.max_entries;
-        c->used = 0;
+        c->used0 = 0;
+        for (uint32_t sh = 0; sh < HT_USED_SHARDS; sh++) c->used_sh[32 * sh] = 0;
     }
 }
 

@@ -66,13 +66,18 @@ struct DMap {
     uint32_t pad_h;
 };
 
-// freelist ring + table counters of one hash map (device, agent-scope atomics)
+// freelist ring + table counters of one hash map (device, agent-scope atomics).  head is on a
+// 128-byte line of its own (every inserting wave of the GPU adds to it), and inserts count the
+// buckets they fill in HT_USED_SHARDS counters on lines of their own (used = used0 + the shards).
+#define HT_USED_SHARDS 16
 struct HashCtl {
     unsigned long long head;   // next ring position to pop
+    uint32_t pad0[30];
     unsigned long long tail;   // next ring position to push
-    int32_t avail;             // free slots not yet claimed
-    uint32_t used;             // buckets that are not EMPTY (live + tombstones + busy)
-    uint32_t pad[2];
+    int32_t avail;             // free slots not yet claimed (stale after a pop-only launch: normalised)
+    uint32_t used0;            // buckets that are not EMPTY (live + tombstones + busy), minus the shards
+    uint32_t pad1[28];
+    uint32_t used_sh[HT_USED_SHARDS * 32];   // shard s at [32 s]
 };
 #define HT_EMPTY 0xffffffffu
 #define HT_TOMB 0xfffffffeu
@@ -191,6 +196,10 @@ struct KParams {
     // only.  The process state is restored from / saved to *step around the launch, and the
     // step budget suspends the process instead of ending it.
     struct StepState *step;
+    // no program of this launch deletes from a hash map: freelist pops need no `avail`
+    // semaphore (no push can run concurrently) -- one head reservation per wave round
+    uint32_t hash_pop_only;
+    uint32_t pad_k;
 };
 
 // The state of one stepped process between launches (engine.cpp mimic_process_*): the

@@ -742,7 +742,7 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
     bool inserted = false;
     if (idx < 0) {
         // a new key: find-or-insert under its stripe lock, the wave's lanes in lock rounds
-        idx = h_insert_wave(t, ks, h, &inserted);
+        idx = h_insert_wave(t, ks, h, &inserted, kp.hash_pop_only != 0);
     }
     if (idx < 0) {
         o.r0 = 7; // syscall.E2BIG: the freelist is empty

@@ -185,3 +185,37 @@ def test_map_reset_is_a_fresh_map(gpu, mtype):
         assert sorted(em.Entries()) == sorted(ovm.map_entries(om))
     evm.close()
     ovm.close()
+
+
+def test_pop_only_launch_fills_to_capacity_then_host_ops(gpu):
+    """A launch whose programs never delete pops the freelist without the `avail` semaphore
+    (hashmap.h h_insert_wave pop_only): many lanes inserting more distinct keys than MaxEntries
+    must still fill exactly E slots (each slot once) and answer E2BIG to the rest.  The host ops
+    after it (normalised freelist): a new key is E2BIG, a delete frees one slot, the next insert
+    takes exactly that slot (FIFO, emulator_linux_map_hash.go:179-186, 244-250)."""
+    E = 700
+    p = W.prog_flowtrack(max_entries=E)
+    sc = _sc(p, 512)
+    n = 20000
+    buf, off, lens = W.make_packets(n, **W.IMIX, seed=3)
+    cpu = W.schedule_cpu(n, 512, "interleaved")
+    vm, maps, pids = build_engine(sc)
+    import mimic_amd as M
+
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+    e = vm.RunXDPBatch(pids[0], batch).numpy(n)
+    fm = maps["flows"]
+    ents = fm.Entries()
+    assert len(ents) == E and sorted(s for _, s in ents) == list(range(E))
+    assert (e["r0"] == 1).sum() > 0 and (e["status"] == 0).all()   # some flows dropped (E2BIG)
+    newkey = b"\xfe" * 16
+    assert fm.Update(newkey, bytes(8)) == 7          # E2BIG
+    victim, vslot = ents[5]
+    assert fm.Delete(victim) == 0
+    assert fm.Update(newkey, b"\x01" * 8) == 0
+    assert dict(fm.Entries())[newkey] == vslot
+    # a second pop-only launch after the host ops: the table stays full, nothing changes
+    e2 = vm.RunXDPBatch(pids[0], batch).numpy(n)
+    assert sorted(s for _, s in fm.Entries()) == list(range(E))
+    assert (e2["status"] == 0).all()
+    vm.close()
