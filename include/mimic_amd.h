@@ -254,6 +254,12 @@ int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32
                       uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
                       mimic_process **out);
 /* Process.SetCPUID: id < 0 or id > V is an error (vm.go:268-283); never called = -1 (vm.go:214). */
+/* VM.NewProcess(prog, &LinuxContextSKBuff{Packet, Dev{IFIndex}}) (vm.go:198-235, context_sk_buff.go:42-107):
+ * the context's Load runs here (its sk_buff / sock / flow-keys / packet entries take the VM's next
+ * leak addresses, as the reference's would); Step / Run / Packet as for xdp_md processes, the
+ * packet memory being 32 + len + 64 bytes (headroom, frame, tailroom; emulator_linux_sk_buff.go:113-116). */
+int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
+                          mimic_process **out);
 int mimic_process_set_cpu(mimic_process *p, int32_t id);
 /* n x Process.Step (vm.go:291-340), stopping early when the process exits or fails; the
  * registers after the last step in *out.  Stepping a process that hit a fatal error returns

@@ -125,6 +125,7 @@ EXPORTS = {
     "mimic_jit_cache_source": (C.c_int, [C.c_char_p]),
     "mimic_process_new": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "mimic_process_new_skb": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     "mimic_process_set_cpu": (C.c_int, [C.c_void_p, C.c_int32]),
     "mimic_process_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "mimic_process_run": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p]),

@@ -89,6 +89,7 @@ struct mimic_vm {
     DMap *d_maps = nullptr;
     bool tables_dirty = true;
     bool prog_deletes = false;   // some loaded program calls map_delete_elem (helper 3)
+    bool prog_updates = false;   // some loaded program calls map_update_elem (helper 2)
     uint8_t *priv = nullptr;
     uint64_t priv_bytes = 0;
     uint32_t priv_lanes = 0;
@@ -419,8 +420,11 @@ static int upload_tables(mimic_vm *vm) {
     if (!vm->tables_dirty) return 0;
     build_host_tables(vm->progs, vm->h_all, vm->h_dp);
     vm->prog_deletes = false;
-    for (auto &x : vm->h_all)
+    vm->prog_updates = false;
+    for (auto &x : vm->h_all) {
         if (AUX_H(x.aux) == H_CALL && (uint32_t)x.k == 3) vm->prog_deletes = true;
+        if (AUX_H(x.aux) == H_CALL && (uint32_t)x.k == 2) vm->prog_updates = true;
+    }
     // map hints of LD_IMM64 constants that are map objects (AUX_MAPHINT): the JIT's inline
     // helpers check the map at run time, so a hint only selects a fast path
     for (auto &x : vm->h_all) {
@@ -1131,6 +1135,9 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
     uint8_t *priv;
     uint64_t priv_bytes;
     uint64_t budget;
+    // an sk_buff process: its own record, leak prefix and leak base (made once, at NewProcess)
+    SkbRec *skb_rec = nullptr;
+    const uint64_t *skb_prefix = nullptr, *skb_base = nullptr;
 };
 
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
@@ -1175,8 +1182,13 @@ static int skb_settle(mimic_vm *vm) {
     return 0;
 }
 
-// the sk_buff records, footprints and leak addresses of a batch (skb.hip), on stream st
-static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st) {
+// the sk_buff records, footprints and leak addresses of a batch (skb.hip), on stream st; `into`
+// (a stepped process's own arrays, one packet) instead of the VM's batch arrays
+struct SkbInto {
+    SkbRec *rec;
+    uint64_t *foot, *prefix;
+};
+static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, const SkbInto *into = nullptr) {
     const uint32_t n = b->n;
     if (vm->skb_stream && vm->skb_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
     if (n > vm->skb_cap || !vm->d_skb_state) {
@@ -1203,7 +1215,8 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st) {
     }
     // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
     const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
-    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, vm->d_skb_rec, vm->d_skb_foot, vm->d_skb_prefix,
+    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, into ? into->rec : vm->d_skb_rec,
+                              into ? into->foot : vm->d_skb_foot, into ? into->prefix : vm->d_skb_prefix,
                               vm->d_skb_scan, vm->skb_scan_cap, vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;
@@ -1374,7 +1387,13 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     default:
         return fail(vm, MIMIC_EINVAL, "unknown schedule %u", b->schedule);
     }
-    if (skb) {
+    if (skb && step && step->skb_rec) {   // a stepped sk_buff process: Load ran at NewProcess
+        kp.ctx_kind = CTX_SKB;
+        kp.skb_ifindex = skb->ifindex;
+        kp.skb_rec = step->skb_rec;
+        kp.skb_prefix = step->skb_prefix;
+        kp.skb_base = step->skb_base;
+    } else if (skb) {
         rc = skb_prepare(vm, b, st);
         if (rc) return rc;
         kp.ctx_kind = CTX_SKB;
@@ -1390,6 +1409,8 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     // A launch whose programs never delete pops the freelists without the `avail` semaphore
     // (hashmap.h h_insert_wave pop_only); one that may delete first normalises maps left so.
     kp.hash_pop_only = vm->prog_deletes ? 0u : 1u;
+    // no program can write a hash map: during the launch every table is read-only
+    kp.hash_ro = (vm->prog_deletes || vm->prog_updates) ? 0u : 1u;
     for (auto &m : vm->maps) {
         if (!is_hash(m)) continue;
         const DMap dm = to_dmap(m);
@@ -1478,6 +1499,11 @@ struct mimic_process {
     int32_t cpu = -1;
     uint32_t static_next = 0;         // the VM's static layout the saved state's addresses assume
     uint8_t *arena = nullptr;
+    // LinuxContextSKBuff processes (context_sk_buff.go): the record, leak prefix (0) and leak base
+    // of the process's Load, made at NewProcess like the reference's
+    bool skb = false;
+    uint32_t ifindex = 0;
+    uint8_t *d_skbmem = nullptr;      // SkbRec | foot | prefix | base
 };
 
 static void process_release(mimic_process *p) {
@@ -1490,6 +1516,7 @@ static void process_release(mimic_process *p) {
     hipFree(p->d_epc);
     hipFree(p->d_state);
     hipFree(p->d_priv);
+    hipFree(p->d_skbmem);
 }
 
 static void process_regs(const mimic_process *p, mimic_process_regs *out) {
@@ -1543,8 +1570,14 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     r.status = p->d_st;
     r.steps = p->d_steps;
     r.err_pc = p->d_epc;
-    const StepRun sr{p->d_state, p->d_priv, p->priv_bytes, budget};
-    int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, nullptr, &sr);
+    StepRun sr{p->d_state, p->d_priv, p->priv_bytes, budget};
+    SkbRun skr{p->ifindex};
+    if (p->skb) {
+        sr.skb_rec = (SkbRec *)p->d_skbmem;
+        sr.skb_prefix = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 8);
+        sr.skb_base = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 16);
+    }
+    int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, p->skb ? &skr : nullptr, &sr);
     if (rc) return rc;
     HIP_OK(vm, hipMemcpyAsync(&p->h, p->d_state, sizeof p->h, hipMemcpyDeviceToHost, vm->stream));
     HIP_OK(vm, hipStreamSynchronize(vm->stream));
@@ -1553,12 +1586,23 @@ static int process_advance(mimic_process *p, uint64_t budget) {
 
 extern "C" {
 
+static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
+                        uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
+                        mimic_process **out);
+
 int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
                       uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
                       mimic_process **out) {
     if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (vm->skb_leaked) return fail(vm, MIMIC_ENOTSUP, "xdp_md processes after sk_buff batches are not supported");
+    return process_make(vm, prog_id, packet, len, headroom, tailroom, ingress_ifindex, rx_queue_index, egress_ifindex,
+                        out);
+}
+
+static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
+                        uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
+                        mimic_process **out) {
     hipSetDevice(vm->s.device);
     mimic_process *p = new mimic_process();
     p->vm = vm;
@@ -1590,6 +1634,52 @@ int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32
         return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
     }
     *out = p;
+    return 0;
+}
+
+int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
+                          mimic_process **out) {
+    if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
+    if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
+    // the packet memory is SKB_HEADROOM + len + SKB_TAILROOM with the frame at +SKB_HEADROOM
+    // (context_sk_buff.go:42-107), run by the interpreter's stepping kernel as a one-packet batch
+    int rc = process_make(vm, prog_id, nullptr, 0, SKB_HEADROOM, SKB_TAILROOM + len, 0, 0, 0, out);
+    if (rc) return rc;
+    mimic_process *p = *out;
+    p->skb = true;
+    p->ifindex = ifindex;
+    p->len = len;
+    p->T = SKB_TAILROOM;
+    hipError_t e = hipSuccess;
+    if (len) e = hipMemcpy(p->d_pkt + SKB_HEADROOM, packet, len, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_len, &len, 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_skbmem, sizeof(SkbRec) + 24);
+    if (e != hipSuccess) {
+        mimic_process_free(p);
+        *out = nullptr;
+        return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
+    }
+    // LinuxContextSKBuff.Load now, as NewProcess does in the reference: the record and the leak
+    // addresses (the VM's leak cursor moves past this process's sock / flow keys / packet)
+    if ((rc = upload_tables(vm))) return rc;
+    mimic_xdp_batch b{};
+    b.n = 1;
+    b.pkt_data = p->d_pkt;
+    b.pkt_off = p->d_off;
+    b.pkt_len = p->d_len;
+    const SkbInto into{(SkbRec *)p->d_skbmem, (uint64_t *)(p->d_skbmem + sizeof(SkbRec)),
+                       (uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 8)};
+    if ((rc = skb_prepare(vm, &b, vm->stream, &into))) return rc;
+    HIP_OK(vm, hipMemcpyAsync(p->d_skbmem + sizeof(SkbRec) + 16, vm->d_skb_state + 1, 8, hipMemcpyDeviceToDevice,
+                              vm->stream));
+    uint32_t lw = 0;
+    HIP_OK(vm, hipMemcpyAsync(&lw, p->d_skbmem, 4, hipMemcpyDeviceToHost, vm->stream));   // SkbRec.len
+    HIP_OK(vm, hipStreamSynchronize(vm->stream));
+    if (lw & SKB_LOAD_FAILED) {   // NewProcess returns the context's Load error (vm.go:226-229); nothing leaked
+        mimic_process_free(p);
+        *out = nullptr;
+        return fail(vm, MIMIC_EINVAL, "load context: the sk_buff context did not decode (ERR_CTX_LOAD)");
+    }
     return 0;
 }
 

@@ -102,6 +102,33 @@ HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos) {
     return -1;
 }
 
+// lookup while no writer can run (KParams.hash_ro: no program of the launch updates or deletes,
+// and host operations are ordered before the launch): the record -- state word and key words --
+// is read with plain loads, all at once, and compared without the re-read that guards against a
+// concurrent delete + reuse.  Same result as h_find on an unchanging table.
+template <class KS>
+HDEV int32_t h_find_ro(const HT &t, const KS &ks, uint64_t h) {
+    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32), nq = (t.K + 7) >> 3;
+    uint32_t p = (uint32_t)h & mask;
+    for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+        const uint64_t *r = h_rec(t, p);
+        uint64_t w[5];
+#pragma unroll
+        for (uint32_t q = 0; q < 5; q++)
+            if (q <= nq) w[q] = r[q];
+        const uint32_t s = (uint32_t)w[0];
+        if (s == HT_EMPTY) return -1;
+        if (s < HT_BUSY && (uint32_t)(w[0] >> 32) == tag) {
+            bool eq = true;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++)
+                if (q < nq) eq &= w[1 + q] == ks.word(q);
+            if (eq) return (int32_t)s;
+        }
+    }
+    return -1;
+}
+
 // freelist (emulator_linux_map_hash.go:179-186 pop, :244-250 push)
 HDEV int32_t h_fl_pop(const HT &t) {
     HashCtl *c = h_ctl(t);

@@ -271,6 +271,14 @@ class Gen {
         }
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
+        {   // no program of the set updates or deletes: hash tables are read-only in every launch
+            // of this kernel (engine.cpp sets KParams.hash_ro from the same program set)
+            bool writes = false;
+            for (auto &p : P)
+                for (uint32_t i = 0; i < p.n; i++)
+                    if (AUX_H(p.ins[i].aux) == H_CALL && ((uint32_t)p.ins[i].k == 2 || (uint32_t)p.ins[i].k == 3)) writes = true;
+            E.line("#define MIMIC_HASH_RO %d", writes ? 0 : 1);
+        }
         E.line("#include \"runtime.h\"");
         E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
         // Around a cold call the lane state and the argument / result registers go through the
@@ -406,12 +414,10 @@ class Gen {
         if (ctx == CTX_SKB) {
             // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107, skb.h)
             E.line("    uint64_t r1 = 0;");
-            E.line("    const int ls_ = skb_load(kp, L, i, r1);");
-            if (skb_lds) {   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
-                E.line("    if (!ls_) { const GAS uint64_t *s_ = (const GAS uint64_t *)L.rec; uint64_t *d_ = srec_ + %uu * threadIdx.x;", kSrecQ);
-                E.line("      for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) d_[q] = s_[q];");
-                E.line("      L.rec = (SkbRec *)d_; }");
-            }
+            if (skb_lds)   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
+                E.line("    const int ls_ = skb_load_lds(kp, L, i, r1, srec_ + %uu * threadIdx.x);", kSrecQ);
+            else
+                E.line("    const int ls_ = skb_load(kp, L, i, r1);");
             // the window starts at the packet (skb.data = packet memory + 32)
             if (stage && fast_paths)
                 E.line("    const uint32_t W_ = ls_ ? 0u : win_stage(pwin_, tl_, L.pkt + SKB_HEADROOM, L.M - SKB_HEADROOM);");

@@ -199,7 +199,9 @@ struct KParams {
     // no program of this launch deletes from a hash map: freelist pops need no `avail`
     // semaphore (no push can run concurrently) -- one head reservation per wave round
     uint32_t hash_pop_only;
-    uint32_t pad_k;
+    // no program of this launch writes a hash map (no update / delete helper): the tables are
+    // read-only while it runs, so lookups read a bucket record with plain (cached) loads at once
+    uint32_t hash_ro;
 };
 
 // The state of one stepped process between launches (engine.cpp mimic_process_*): the

@@ -19,6 +19,12 @@ typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef uint64_t __attribute__((aligned(1))) u64u;
 
 #define DEV static __device__ __forceinline__
+// hash tables read-only during the launch (KParams.hash_ro); a JIT kernel knows it at compile time
+#ifdef MIMIC_HASH_RO
+#define HASH_RO(kp) (MIMIC_HASH_RO != 0)
+#else
+#define HASH_RO(kp) ((kp).hash_ro != 0)
+#endif
 
 // Read-only tables are read through the constant address space so that wave-uniform
 // indices become scalar (s_load) fetches through the scalar cache.
@@ -698,7 +704,9 @@ DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint6
     // LinuxHashMap.Lookup :134-155 / LinuxPerCPUHashMap.Lookup :537-561
     if (m.family == FAM_PERCPU_HASH && (L.cpu < 0 || (uint32_t)L.cpu >= m.ncpu)) { o.st = MIMIC_ERR_HELPER_MAP_OP; return o; }
     const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
-    const int32_t idx = h_find(h_table(kp.arena, m), ks, h_hash(ks, m.key_size), nullptr);
+    const HT t = h_table(kp.arena, m);
+    const uint64_t h = h_hash(ks, m.key_size);
+    const int32_t idx = HASH_RO(kp) ? h_find_ro(t, ks, h) : h_find(t, ks, h, nullptr);
     o.r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
     o.set_r0 = true;
     if (idx >= 0) {
@@ -872,6 +880,37 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1) {
     return 0;
 }
 
+// skb_load for a JIT kernel that keeps the process's SkbRec in an LDS slot `d`: the record's words,
+// the packet offset and the leak prefix are loaded together (one memory round trip, not the
+// record length first and the rest after it), then the record goes to LDS.
+DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d) {
+    const GAS uint64_t *s = (const GAS uint64_t *)(kp.skb_rec + i);
+    constexpr uint32_t NQ = sizeof(SkbRec) / 8;
+    uint64_t w[NQ];
+#pragma unroll
+    for (uint32_t q = 0; q < NQ; q++) w[q] = s[q];
+    const uint64_t po = kp.pkt_off[i], pre = kp.skb_prefix[i], base = *kp.skb_base;
+#pragma unroll
+    for (uint32_t q = 0; q < NQ; q++) d[q] = w[q];
+    const uint32_t lw = (uint32_t)w[0];
+    L.pkt = kp.pkt_data + po;
+    L.rec = nullptr;
+    L.ka = 0;
+    L.pa = 0;
+    L.M = 0;
+    if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
+    const uint64_t ka = base + pre;
+    if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
+    L.rec = (SkbRec *)d;
+    L.ka = (uint32_t)ka;
+    L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
+    L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
+    for (uint32_t b = 0; b < SKB_HEADROOM; b += 8) *(u64u *)(L.pkt + b) = 0;
+    for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
+    r1 = kp.static_next + kp.stack_size + 1;
+    return 0;
+}
+
 // ---------------------------------------------------------------------------------------
 // Cold paths of the JIT kernels: real (non-inlined) functions, so that a kernel holds one
 // copy of the generic memory controller / helpers instead of one per instruction (hipRTC
@@ -1012,7 +1051,9 @@ DEV bool hash_lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1,
     ks.w1 = K > 8 ? stack_load(kp, L, ko + 8, K - 8 < 8 ? K - 8 : 8) : 0;
     ks.w2 = K > 16 ? stack_load(kp, L, ko + 16, K - 16 < 8 ? K - 16 : 8) : 0;
     ks.w3 = K > 24 ? stack_load(kp, L, ko + 24, K - 24) : 0;
-    const int32_t idx = h_find(h_table(kp.arena, m), ks, h_hash(ks, K), nullptr);
+    const HT t = h_table(kp.arena, m);
+    const uint64_t h = h_hash(ks, K);
+    const int32_t idx = HASH_RO(kp) ? h_find_ro(t, ks, h) : h_find(t, ks, h, nullptr);
     r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
     if (idx >= 0) {
         L.t_lo = hash_value_addr(m, L.cpu, 0);

@@ -19,9 +19,16 @@ reader the hot path needs, with the engine's raw-slot boundary as the output:
   offset in the second slot's immediate (the reference ignores it, using inst.Offset: Q16);
 * the "maps" section holds struct bpf_map_def {type, key_size, value_size, max_entries, flags}
   per map symbol; data sections become datasec array maps (key 4, value = section size, one
-  entry) with the section bytes as their contents.
-
-BTF-defined maps (".maps") need BTF parsing and are rejected with a clear error.
+  entry) with the section bytes as their contents;
+* BTF-defined maps (the ".maps" section every current clang / libbpf object uses): the .BTF
+  section's DATASEC ".maps" lists one VAR per map, whose STRUCT type encodes the attributes the
+  way libbpf's __uint / __type macros do -- `type`, `max_entries`, `map_flags`, `key_size`,
+  `value_size`, `pinning` as a pointer to an array whose element count is the value, `key` /
+  `value` as a pointer to the key / value type (its BTF size is the key / value size).  This is
+  cilium/ebpf v0.9.0's loadBTFMaps + mapSpecFromBTF (elf_reader.go) with its errors for unknown
+  members and for both `key` and `key_size` (or `value` and `value_size`); `values` (map-in-map
+  and program-array initial contents) is rejected.  LD_IMM64 relocations against a ".maps"
+  symbol are map references like the legacy section's.
 """
 from __future__ import annotations
 
@@ -114,12 +121,185 @@ def _parse(elf: bytes):
     return secs, syms, rels
 
 
+# BTF kinds (linux/btf.h, as cilium/ebpf v0.9.0 btf/types.go reads them)
+BTF_INT, BTF_PTR, BTF_ARRAY, BTF_STRUCT, BTF_UNION, BTF_ENUM, BTF_FWD, BTF_TYPEDEF, BTF_VOLATILE, BTF_CONST, \
+    BTF_RESTRICT, BTF_FUNC, BTF_FUNC_PROTO, BTF_VAR, BTF_DATASEC, BTF_FLOAT, BTF_DECL_TAG, BTF_TYPE_TAG, \
+    BTF_ENUM64 = range(1, 20)
+BTF_MAGIC = 0xEB9F
+
+
+@dataclass
+class _BtfType:
+    kind: int
+    name: str
+    size_or_type: int
+    vlen: int
+    kind_flag: int
+    extra: object = None    # ARRAY: (elem, index, nelems); STRUCT/UNION: [(name, type, bit offset)];
+                            # DATASEC: [(type, offset, size)]; VAR: linkage
+
+
+def parse_btf(data: bytes) -> List[Optional[_BtfType]]:
+    """The .BTF section's type table (index = type id; id 0 = void -> None).  btf/btf.go +
+    btf/types.go of cilium/ebpf v0.9.0 read the same header, type records and string table."""
+    if len(data) < 24:
+        raise MimicError("BTF section too short")
+    magic, version, flags, hdr_len, type_off, type_len, str_off, str_len = struct.unpack_from("<HBBIIIII", data, 0)
+    if magic != BTF_MAGIC:
+        raise MimicError(f"BTF magic {magic:#x} (big-endian or not BTF)")
+    base = hdr_len
+    types_b = data[base + type_off:base + type_off + type_len]
+    strs = data[base + str_off:base + str_off + str_len]
+
+    def name(o: int) -> str:
+        if o >= len(strs):
+            raise MimicError(f"BTF string offset {o} out of range")
+        e = strs.index(b"\0", o)
+        return strs[o:e].decode()
+
+    out: List[Optional[_BtfType]] = [None]
+    o = 0
+    while o < len(types_b):
+        name_off, info, st = struct.unpack_from("<III", types_b, o)
+        o += 12
+        kind, vlen, kflag = (info >> 24) & 0x1F, info & 0xFFFF, info >> 31
+        t = _BtfType(kind, name(name_off), st, vlen, kflag)
+        if kind == BTF_INT or kind == BTF_VAR or kind == BTF_DECL_TAG:
+            t.extra = struct.unpack_from("<I", types_b, o)[0]
+            o += 4
+        elif kind == BTF_ARRAY:
+            t.extra = struct.unpack_from("<III", types_b, o)
+            o += 12
+        elif kind in (BTF_STRUCT, BTF_UNION):
+            mem = []
+            for _ in range(vlen):
+                mn, mt, moff = struct.unpack_from("<III", types_b, o)
+                o += 12
+                mem.append((name(mn), mt, (moff & 0xFFFFFF) if kflag else moff))
+            t.extra = mem
+        elif kind == BTF_ENUM:
+            o += 8 * vlen
+        elif kind == BTF_ENUM64:
+            o += 12 * vlen
+        elif kind == BTF_FUNC_PROTO:
+            o += 8 * vlen
+        elif kind == BTF_DATASEC:
+            t.extra = [struct.unpack_from("<III", types_b, o + 12 * k) for k in range(vlen)]
+            o += 12 * vlen
+        elif kind in (BTF_PTR, BTF_FWD, BTF_TYPEDEF, BTF_VOLATILE, BTF_CONST, BTF_RESTRICT, BTF_FUNC, BTF_FLOAT,
+                      BTF_TYPE_TAG):
+            pass
+        else:
+            raise MimicError(f"BTF type {len(out)}: unknown kind {kind}")
+        out.append(t)
+    return out
+
+
+def _btf_resolve(types, tid: int) -> int:
+    """skip typedefs and qualifiers (btf.UnderlyingType / skipQualifiers)"""
+    for _ in range(64):
+        t = types[tid] if 0 < tid < len(types) else None
+        if t is None or t.kind not in (BTF_TYPEDEF, BTF_VOLATILE, BTF_CONST, BTF_RESTRICT, BTF_TYPE_TAG):
+            return tid
+        tid = t.size_or_type
+    raise MimicError("BTF: qualifier chain too long")
+
+
+def btf_sizeof(types, tid: int) -> int:
+    """btf.Sizeof: the byte size of a type"""
+    tid = _btf_resolve(types, tid)
+    t = types[tid] if 0 < tid < len(types) else None
+    if t is None:
+        raise MimicError("BTF: size of void")
+    if t.kind in (BTF_INT, BTF_ENUM, BTF_ENUM64, BTF_STRUCT, BTF_UNION, BTF_DATASEC, BTF_FLOAT):
+        return t.size_or_type
+    if t.kind == BTF_PTR:
+        return 8
+    if t.kind == BTF_ARRAY:
+        elem, _, n = t.extra
+        return n * btf_sizeof(types, elem)
+    if t.kind == BTF_VAR:
+        return btf_sizeof(types, t.size_or_type)
+    raise MimicError(f"BTF: type {tid} (kind {t.kind}) has no size")
+
+
+def _btf_uint(types, tid: int, what: str) -> int:
+    """uintFromBTF: __uint(name, N) is `int (*name)[N]` -- a pointer to an array of N elements"""
+    p = types[_btf_resolve(types, tid)]
+    if p is None or p.kind != BTF_PTR:
+        raise MimicError(f"BTF map {what}: not a pointer")
+    a = types[_btf_resolve(types, p.size_or_type)]
+    if a is None or a.kind != BTF_ARRAY:
+        raise MimicError(f"BTF map {what}: not a pointer to an array")
+    return a.extra[2]
+
+
+def _btf_maps(secs, syms) -> Dict[str, CollectionMap]:
+    """cilium/ebpf v0.9.0 loadBTFMaps / mapSpecFromBTF over the ".maps" DATASEC."""
+    btf_sec = next((s for s in secs if s.name == ".BTF"), None)
+    if btf_sec is None:
+        raise MimicError("BTF-defined maps (.maps) without a .BTF section")
+    types = parse_btf(btf_sec.data)
+    ds = next((t for t in types if t is not None and t.kind == BTF_DATASEC and t.name == ".maps"), None)
+    if ds is None:
+        raise MimicError(".BTF has no DATASEC \".maps\"")
+    maps: Dict[str, CollectionMap] = {}
+    for vt, _off, _size in ds.extra:
+        var = types[vt]
+        if var is None or var.kind != BTF_VAR:
+            raise MimicError(f"DATASEC .maps entry {vt} is not a VAR")
+        st = types[_btf_resolve(types, var.size_or_type)]
+        if st is None or st.kind != BTF_STRUCT:
+            raise MimicError(f"map {var.name}: expected a struct, got kind {st.kind if st else 0}")
+        mtype = key_size = value_size = max_entries = None
+        key_typed = value_typed = False
+        for mname, mt, _bits in st.extra:
+            if mname == "type":
+                mtype = _btf_uint(types, mt, f"{var.name}.type")
+            elif mname == "map_flags" or mname == "pinning" or mname == "map_extra" or mname == "numa_node":
+                _btf_uint(types, mt, f"{var.name}.{mname}")
+            elif mname == "max_entries":
+                max_entries = _btf_uint(types, mt, f"{var.name}.max_entries")
+            elif mname == "key":
+                if key_size is not None:
+                    raise MimicError(f"map {var.name}: both key and key_size")
+                p = types[_btf_resolve(types, mt)]
+                if p is None or p.kind != BTF_PTR:
+                    raise MimicError(f"map {var.name}: key is not a pointer")
+                key_size = btf_sizeof(types, p.size_or_type)
+                key_typed = True
+            elif mname == "key_size":
+                if key_typed:
+                    raise MimicError(f"map {var.name}: both key and key_size")
+                key_size = _btf_uint(types, mt, f"{var.name}.key_size")
+            elif mname == "value":
+                if value_size is not None:
+                    raise MimicError(f"map {var.name}: both value and value_size")
+                p = types[_btf_resolve(types, mt)]
+                if p is None or p.kind != BTF_PTR:
+                    raise MimicError(f"map {var.name}: value is not a pointer")
+                value_size = btf_sizeof(types, p.size_or_type)
+                value_typed = True
+            elif mname == "value_size":
+                if value_typed:
+                    raise MimicError(f"map {var.name}: both value and value_size")
+                value_size = _btf_uint(types, mt, f"{var.name}.value_size")
+            elif mname == "values":
+                raise MimicError(f"map {var.name}: initial values (map-in-map / program array) are not supported")
+            else:
+                raise MimicError(f"map {var.name}: unrecognized field {mname!r}")
+        if mtype is None:
+            raise MimicError(f"map {var.name}: no type")
+        maps[var.name] = CollectionMap(var.name, mtype, key_size or 0, value_size or 0, max_entries or 0)
+    return maps
+
+
 def _map_defs(secs, syms) -> Dict[str, CollectionMap]:
     maps: Dict[str, CollectionMap] = {}
     for s in secs:
         if s.name == ".maps":
-            raise MimicError("BTF-defined maps (.maps) are not supported: use the legacy \"maps\" section")
-        if s.name == "maps" or s.name.startswith("maps/"):
+            maps.update(_btf_maps(secs, syms))
+        elif s.name == "maps" or s.name.startswith("maps/"):
             for y in syms:
                 if y.shndx != s.idx or y.type == STT_SECTION or not y.name:
                     continue
@@ -206,7 +386,7 @@ def load_collection_spec(elf: bytes) -> CollectionSpec:
                         body[8 * k + 4:8 * k + 8] = b"\0\0\0\0"
                         body[8 * k + 12:8 * k + 16] = struct.pack("<I", voff & 0xFFFFFFFF)
                         refs.append((base + k, tsec.name))
-                    elif tsec.name == "maps" or tsec.name.startswith("maps/"):
+                    elif tsec.name in ("maps", ".maps") or tsec.name.startswith("maps/"):
                         body[8 * k + 1] = (regs & 0x0F) | (PSEUDO_MAP_FD << 4)
                         refs.append((base + k, t.name))
                     else:

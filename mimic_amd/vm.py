@@ -583,9 +583,12 @@ class Registers:
 
 
 class Process:
-    """A process of the VM (vm.go:238-374).  Run() alone is a one-packet batch on the JIT kernel;
-    Step() advances the process one instruction at a time on the device (a single-lane
-    interpreter launch per call, mimic_process_step) and a Run() after Step() continues it."""
+    """A process of the VM (vm.go:238-374), held on the device (mimic_process_*): Step()
+    advances it one instruction at a time (a single-lane interpreter launch per call), Run()
+    runs it to the end (continuing a stepped process), and every register is readable after
+    either.  An sk_buff process's context Load runs at NewProcess, as in the reference
+    (context_sk_buff.go:42-107: its leaked entries take the VM's next addresses then).  Batches
+    of processes run through VM.RunXDPBatch / RunSKBBatch instead."""
 
     def __init__(self, vm: VM, prog_id: int, ctx=None):
         self.VM = vm
@@ -600,6 +603,8 @@ class Process:
         self._native = None
         self._exited = False
         self.Registers.R10 = vm.StackAddress() + vm.settings.stack_frame_size   # vm.go:224
+        if isinstance(ctx, LinuxContextSKBuff):
+            self._ensure_native()
 
     def CPUID(self) -> int:
         return self.cpuID
@@ -618,13 +623,16 @@ class Process:
         if self._native is not None:
             return
         ctx = self.Context or LinuxContextXDP()
-        if isinstance(ctx, LinuxContextSKBuff):
-            raise MimicError("Step on sk_buff contexts is not supported (Run is)")
         h = C.c_void_p()
         pkt = bytes(ctx.Packet)
-        _check(self.VM.h, self.VM.lib.mimic_process_new(self.VM.h, self.prog_id, pkt, len(pkt), ctx.Headroom,
-                                                         ctx.Tailroom, ctx.IngessIfIndex, ctx.RxQueueIndex,
-                                                         ctx.EgressIfIndex, C.byref(h)), "NewProcess")
+        if isinstance(ctx, LinuxContextSKBuff):   # its Load (leak addresses) happens here, as in NewProcess
+            _check(self.VM.h, self.VM.lib.mimic_process_new_skb(self.VM.h, self.prog_id, pkt, len(pkt),
+                                                                 ctx.Dev.IFIndex if ctx.Dev else 0, C.byref(h)),
+                   "NewProcess")
+        else:
+            _check(self.VM.h, self.VM.lib.mimic_process_new(self.VM.h, self.prog_id, pkt, len(pkt), ctx.Headroom,
+                                                             ctx.Tailroom, ctx.IngessIfIndex, ctx.RxQueueIndex,
+                                                             ctx.EgressIfIndex, C.byref(h)), "NewProcess")
         self._native = h
         if self.cpuID >= 0:
             _check(self.VM.h, self.VM.lib.mimic_process_set_cpu(h, self.cpuID), "SetCPUID")
@@ -654,34 +662,20 @@ class Process:
         return self._exited
 
     def Run(self, step_budget: int = 0) -> None:  # vm.go:343-360
-        # cpuID stays -1 when SetCPUID was never called (vm.go:214) and may equal V (vm.go:273):
-        # the reference runs such processes; only per-CPU map operations fail in them
-        # (emulator_linux_map_array.go:236-238) and bpf_get_smp_processor_id returns the ID as set
-        if self._native is not None:
-            regs = L.ProcessRegs()
-            _check(self.VM.h, self.VM.lib.mimic_process_run(self._native, step_budget, C.byref(regs)), "Run")
-            self._take(regs)
-            self.ErrPC = self.Registers.PC if self.Status else -1
-            if self.Status:
-                raise MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[self.Status]} at PC({self.ErrPC})")
-            return
-        ctx = self.Context or LinuxContextXDP()
-        dev = f"cuda:{self.VM.settings.device}"
-        if isinstance(ctx, LinuxContextSKBuff):
-            batch = SKBBatch.from_packets([ctx.Packet], device=dev, ifindex=ctx.Dev.IFIndex if ctx.Dev else 0,
-                                          schedule=L.SCHED_EXPLICIT, cpu=[self.cpuID], step_budget=step_budget)
-            res = self.VM.RunSKBBatch(self.prog_id, batch)
-        else:
-            batch = XDPBatch.from_packets([ctx.Packet], device=dev, headroom=ctx.Headroom, tailroom=ctx.Tailroom,
-                                          ingress=ctx.IngessIfIndex, rxq=ctx.RxQueueIndex, egress=ctx.EgressIfIndex,
-                                          schedule=L.SCHED_EXPLICIT, cpu=[self.cpuID], step_budget=step_budget)
-            res = self.VM.RunXDPBatch(self.prog_id, batch)
-        self.Registers.R0 = int(res.r0[0].item()) & 0xFFFFFFFFFFFFFFFF
-        self.Steps = int(res.steps[0].item())
-        self.Status = int(res.status[0].item())
-        self.ErrPC = int(res.err_pc[0].item())
-        self.PacketAfter = batch.packet_bytes(0)
-        if self.Status != 0:
+        """Process.Run: run to exit (or a fatal error, or the step budget standing in for the
+        context deadline).  Every register is readable afterwards (Registers.R0..R10, PC), as
+        after the reference's Run (Readme.md:74-78): the process runs on the device as a
+        single-lane launch that saves its whole state (mimic_process_run), continuing a process
+        that Step() has started.  cpuID stays -1 when SetCPUID was never called (vm.go:214) and may
+        equal V (vm.go:273): the reference runs such processes; only per-CPU map operations fail
+        in them (emulator_linux_map_array.go:236-238)."""
+        self._ensure_native()
+        regs = L.ProcessRegs()
+        _check(self.VM.h, self.VM.lib.mimic_process_run(self._native, step_budget, C.byref(regs)), "Run")
+        self._take(regs)
+        self.ErrPC = self.Registers.PC if self.Status else -1
+        self.PacketAfter = self.Packet()
+        if self.Status:
             raise MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[self.Status]} at PC({self.ErrPC})")
 
     def Packet(self) -> bytes:
@@ -689,7 +683,10 @@ class Process:
         if self._native is None:
             return self.PacketAfter or b""
         ctx = self.Context or LinuxContextXDP()
-        n = ctx.Headroom + len(ctx.Packet) + ctx.Tailroom
+        if isinstance(ctx, LinuxContextSKBuff):
+            n = 32 + len(ctx.Packet) + 64   # emulator_linux_sk_buff.go:113-116
+        else:
+            n = ctx.Headroom + len(ctx.Packet) + ctx.Tailroom
         buf = C.create_string_buffer(max(n, 1))
         _check(self.VM.h, self.VM.lib.mimic_process_packet(self._native, buf, max(n, 1)), "packet")
         return buf.raw[:n]

@@ -1609,6 +1609,13 @@ static void proc_cleanup(orc_proc *p) {
 
 void orc_proc_free(orc_proc *p) {
     if (!p) return;
+    /* LinuxContextSKBuff.Cleanup (context_sk_buff.go:110-119): the sk_buff entry only; the sock,
+     * flow keys and packet entries leak */
+    if (p->skb) {
+        mc_del_obj(p->vm, p->skb);
+        free(p->skb);
+        p->skb = NULL;
+    }
     proc_cleanup(p);
     free(p);
 }
@@ -2142,6 +2149,20 @@ static int skb_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t ifinde
     }
     p->R.r[1] = sa;
     return 0;
+}
+
+/* NewProcess(prog, &LinuxContextSKBuff{Packet, Dev}) for single-process stepping (vm.go:198-235,
+ * context_sk_buff.go:42-107): NULL (with *status) when the context does not load */
+orc_proc *orc_proc_new_skb(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t ifindex, int *status) {
+    if (prog_id < 0 || prog_id >= vm->nprogs) return NULL;
+    orc_proc *p = proc_new(vm, prog_id);
+    const int st = skb_load(p, pkt, L, ifindex);
+    if (status) *status = st;
+    if (st) {
+        orc_proc_free(p);
+        return NULL;
+    }
+    return p;
 }
 
 int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_results *out) {

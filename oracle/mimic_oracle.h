@@ -124,6 +124,8 @@ void orc_proc_set_reg(orc_proc *p, int r, uint64_t v);
  * exited, > 0 fatal status), Registers.PC and the current program. */
 orc_proc *orc_proc_new_xdp(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t H, uint32_t T,
                            int32_t ingress, int32_t rxq, int32_t egress);
+/* NewProcess with a LinuxContextSKBuff (its Load runs here); NULL + *status when it fails */
+orc_proc *orc_proc_new_skb(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t ifindex, int *status);
 int orc_proc_step(orc_proc *p, int32_t *err_pc);
 int64_t orc_proc_get_pc(orc_proc *p);
 int orc_proc_get_prog(orc_proc *p);

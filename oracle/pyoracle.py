@@ -75,6 +75,8 @@ def load(build: bool = True) -> C.CDLL:
         "orc_proc_call_helper": (C.c_int, [C.c_void_p, C.c_int32]),
         "orc_proc_new_xdp": (C.c_void_p, [C.c_void_p, C.c_int, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                           C.c_int32, C.c_int32, C.c_int32]),
+        "orc_proc_new_skb": (C.c_void_p, [C.c_void_p, C.c_int, C.c_char_p, C.c_uint32, C.c_uint32,
+                                          C.POINTER(C.c_int)]),
         "orc_proc_step": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
         "orc_proc_get_pc": (C.c_int64, [C.c_void_p]),
         "orc_proc_get_prog": (C.c_int, [C.c_void_p]),
@@ -90,9 +92,17 @@ def load(build: bool = True) -> C.CDLL:
 
 
 class OracleProcess:
-    def __init__(self, vm: "OracleVM", prog_id: int, xdp=None):
-        """xdp = (packet bytes, headroom, tailroom, ingress, rxq, egress): an xdp_md context."""
+    def __init__(self, vm: "OracleVM", prog_id: int, xdp=None, skb=None):
+        """xdp = (packet bytes, headroom, tailroom, ingress, rxq, egress): an xdp_md context;
+        skb = (packet bytes, ifindex): an sk_buff context (Load at construction)."""
         self.vm = vm
+        if skb is not None:
+            pkt, ifindex = skb
+            st = C.c_int(0)
+            self.p = vm.lib.orc_proc_new_skb(vm.h, prog_id, bytes(pkt), len(pkt), ifindex, C.byref(st))
+            if not self.p:
+                raise OracleError(f"sk_buff context load failed (status {st.value})")
+            return
         if xdp is None:
             self.p = vm.lib.orc_proc_new(vm.h, prog_id)
         else:

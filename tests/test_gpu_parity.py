@@ -224,7 +224,7 @@ def test_process_run_cpu_unset_and_V(gpu):
     vm.close()
 
 
-def _elf_sc():
+def _elf_sc(btf: bool = False):
     import os
     import sys
 
@@ -232,17 +232,19 @@ def _elf_sc():
 
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
-    from test_elf import OBJ, scenario_of
+    from test_elf import OBJ, OBJ_BTF, scenario_of
 
-    spec = elf.LoadCollectionSpec(OBJ)
+    spec = elf.LoadCollectionSpec(OBJ_BTF if btf else OBJ)
     return scenario_of(spec, ["xdp_count", "xdp_pass"])
 
 
+@pytest.mark.parametrize("btf", [False, True], ids=["legacy_maps", "btf_maps"])
 @pytest.mark.parametrize("exec_mode", ["jit", "interp"])
-def test_elf_object_on_the_engine(gpu, exec_mode):
-    """The committed ELF object (tests/golden/xdp_count.o) loaded through mimic_amd.elf runs on
-    the engine exactly like the oracle: BPF-to-BPF calls (with Q12), per-CPU map, .data datasec."""
-    sc = _elf_sc()
+def test_elf_object_on_the_engine(gpu, exec_mode, btf):
+    """The committed ELF objects (tests/golden/xdp_count.o with a legacy "maps" section,
+    xdp_count_btf.o with BTF-defined ".maps") loaded through mimic_amd.elf run on the engine
+    exactly like the oracle: BPF-to-BPF calls (with Q12), per-CPU map, .data datasec."""
+    sc = _elf_sc(btf)
     pk = [bytes([i % 256]) * (1 + i % 70) for i in range(300)] + [b""]
     buf, off, lens = packets_to_buffer(pk)
     cpu = (np.arange(len(pk)) % 4).astype(np.int32)

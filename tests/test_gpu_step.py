@@ -149,3 +149,123 @@ def test_step_after_layout_change_is_refused(gpu):
     e.Cleanup()
     fresh.Cleanup()
     vm.close()
+
+
+def _skb_scenario(V=4):
+    progs, maps, pa = W.skb_programs()
+    buf, off, lens = W.make_skb_packets(64, **W.IMIX, variety=0.3, seed=21)
+    init = [("flows", k, v, 0) for k, v in W.skb_flow_keys(buf, off, lens, every=1)]
+    sc = Scenario(vcpus=V, maps=maps, progs=[(p.name, p.raw, p.relocs) for p in progs], prog_array=pa, map_init=init)
+    pkts = [bytes(buf[int(off[i]) + 32:int(off[i]) + 32 + int(lens[i])]) for i in range(len(lens))]
+    return sc, pkts
+
+
+def test_skb_chain_step_trace_matches_oracle(gpu):
+    """Process.Step on sk_buff processes (LinuxContextSKBuff, context_sk_buff.go:42-107) through
+    the cfg-5 tail-call chain: after every step R0..R10, PC and the current program equal the
+    oracle's Step, for packets taking every chain (IPv4 / IPv6 / other, header variants).  The
+    processes are made and cleaned up in the same order on both sides, so their leaked sock /
+    flow-keys / packet entries (and every address a program sees) agree too."""
+    from oracle.pyoracle import OracleProcess
+
+    sc, pkts = _skb_scenario()
+    ovm, omids, opids = build_oracle(sc)
+    evm, emaps, epids = build_engine(sc)
+    seen_progs = set()
+    for k, pkt in enumerate(pkts[:24]):
+        try:
+            o = OracleProcess(ovm, opids[0], skb=(pkt, 3))
+        except Exception:
+            with pytest.raises(M.MimicError):
+                evm.NewProcess(epids[0], M.LinuxContextSKBuff(Packet=pkt, Dev=M.NetDev(3)))
+            continue
+        assert o.set_cpu(k % 4) == 0
+        e = evm.NewProcess(epids[0], M.LinuxContextSKBuff(Packet=pkt, Dev=M.NetDev(3)))
+        e.SetCPUID(k % 4)
+        n = 0
+        while True:
+            n += 1
+            rc, epc = o.step()
+            try:
+                exited, err = e.Step(), None
+            except M.MimicError as ex:
+                exited, err = True, ex
+            regs_o = [o.reg(r) for r in range(11)]
+            assert [e.Registers.Get(r) for r in range(11)] == regs_o, (k, n)
+            if rc > 0:
+                assert err is not None and M.STATUS_NAMES[e.Status] == M.STATUS_NAMES[rc], (k, n)
+                break
+            assert err is None, (k, n, err)
+            assert e.Registers.PC == o.pc() and e.ProgramID == o.prog(), (k, n)
+            seen_progs.add(o.prog())
+            if rc == -1:
+                assert exited
+                break
+            assert not exited and n < 2000
+        o.cleanup()
+        e.Cleanup()
+    assert seen_progs >= {0, 1, 2, 4}, seen_progs
+    for m in sc.maps:
+        for c in range(4 if m["type"] == 6 else 1):
+            assert emaps[m["name"]].Values(c) == ovm.map_values(omids[m["name"]], c), m["name"]
+    ovm.close()
+    evm.close()
+
+
+def test_skb_process_run_exposes_every_register(gpu):
+    """Process.Run on an sk_buff process: R0..R10 afterwards equal the oracle's registers at the
+    exit (Readme.md:74-78 reads them after Run), and the leak addresses of consecutive processes
+    follow the reference's."""
+    from oracle.pyoracle import OracleProcess
+
+    sc, pkts = _skb_scenario()
+    ovm, _, opids = build_oracle(sc)
+    evm, _, epids = build_engine(sc)
+    for k, pkt in enumerate(pkts[:16]):
+        try:
+            o = OracleProcess(ovm, opids[0], skb=(pkt, 2))
+        except Exception:
+            continue
+        o.set_cpu(1)
+        while True:
+            rc, _ = o.step()
+            if rc != 0:
+                break
+        e = evm.NewProcess(epids[0], M.LinuxContextSKBuff(Packet=pkt, Dev=M.NetDev(2)))
+        e.SetCPUID(1)
+        if rc > 0:
+            with pytest.raises(M.MimicError):
+                e.Run()
+        else:
+            e.Run()
+        assert [e.Registers.Get(r) for r in range(11)] == [o.reg(r) for r in range(11)], k
+        o.cleanup()
+        e.Cleanup()
+    ovm.close()
+    evm.close()
+
+
+def test_xdp_process_run_exposes_every_register(gpu):
+    """Run without any Step: R1..R10 are readable afterwards (not only R0)."""
+    from oracle.pyoracle import OracleProcess
+
+    p = W.prog_classifier()
+    sc = Scenario(vcpus=2, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    buf, off, lens = W.make_packets(4, seed=3)
+    ovm, _, opids = build_oracle(sc)
+    evm, _, epids = build_engine(sc)
+    for i in range(4):
+        pkt = bytes(buf[int(off[i]):int(off[i]) + int(lens[i])])
+        o = OracleProcess(ovm, opids[0], xdp=(pkt, 0, 0, 1, 0, 0))
+        o.set_cpu(i % 2)
+        while o.step()[0] == 0:
+            pass
+        e = evm.NewProcess(epids[0], M.LinuxContextXDP(Packet=pkt, IngessIfIndex=1))
+        e.SetCPUID(i % 2)
+        e.Run()
+        assert [e.Registers.Get(r) for r in range(11)] == [o.reg(r) for r in range(11)]
+        assert e.Registers.R2 != 0 and e.Registers.R10 != 0
+        o.cleanup()
+        e.Cleanup()
+    ovm.close()
+    evm.close()

@@ -73,7 +73,7 @@ def test_skb_chain_kernel_compiles():
     LD_ABS / LD_IND over the LDS window starting at skb->data."""
     progs, _, _ = W.skb_programs()
     src = _source([p.raw for p in progs], _lib.CTX_SKB)
-    assert "#define MIMIC_CTX_FIXED 1" in src and "skb_load(kp, L, i, r1)" in src
+    assert "#define MIMIC_CTX_FIXED 1" in src and "skb_load_lds(kp, L, i, r1," in src
     assert "cold_ldabs(kp, sp_" in src and "bswap_n(" in src
     assert _compiles(src) > 0
 
