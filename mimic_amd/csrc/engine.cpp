@@ -26,6 +26,7 @@
 #include "skb.h"
 
 extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st);
+extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st);
 extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
                                     int32_t cpu, int32_t *out, hipStream_t st);
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
@@ -97,6 +98,11 @@ struct mimic_vm {
     uint64_t sched_cap_start = 0, sched_cap_pkts = 0;
     uint64_t *d_lane_steps = nullptr;
     uint32_t lane_steps_cap = 0;
+    // JIT kernels with deferred slow paths: one DeferRec per lane and the launch's marker word
+    // (layout.h); the epoch numbers launches so that no flag is ever cleared
+    DeferRec *d_defer = nullptr;
+    uint32_t *d_defer_any = nullptr;
+    uint32_t defer_cap = 0, defer_epoch = 0;
     uint32_t last_lanes = 0;
     hipStream_t last_stream = nullptr;
     // execution
@@ -591,6 +597,8 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_sched_start);
     hipFree(vm->d_sched_pkts);
     hipFree(vm->d_lane_steps);
+    hipFree(vm->d_defer);
+    hipFree(vm->d_defer_any);
     hipFree(vm->d_kp);
     if (vm->h_kp) hipHostFree(vm->h_kp);
     for (auto &sl : vm->slot) {
@@ -1462,14 +1470,37 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (bound && kp.budget < bound) jit = false;
     }
     vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
+    if (jit && ji.defer) {   // the lanes' suspended processes (DeferRec) and the launch's marker
+        if (lanes > vm->defer_cap || !vm->d_defer_any) {
+            hipStreamSynchronize(st);
+            hipFree(vm->d_defer);
+            vm->d_defer = nullptr;
+            HIP_OK(vm, hipMalloc(&vm->d_defer, (uint64_t)plan * sizeof(DeferRec)));
+            HIP_OK(vm, hipMemset(vm->d_defer, 0, (uint64_t)plan * sizeof(DeferRec)));
+            vm->defer_cap = plan;
+            if (!vm->d_defer_any) {
+                HIP_OK(vm, hipMalloc(&vm->d_defer_any, 64));
+                HIP_OK(vm, hipMemset(vm->d_defer_any, 0, 64));
+            }
+        }
+        if (++vm->defer_epoch == 0) vm->defer_epoch = 1;   // 0 is what the buffers start as
+        kp.defer = vm->d_defer;
+        kp.defer_any = vm->d_defer_any;
+        kp.defer_epoch = vm->defer_epoch;
+    }
     if (jit && ji.karg) {  // launch parameters by value: the runtime copies them into the kernarg segment
         if (mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, nullptr, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+        // the interpreter finishes what the kernel deferred (a wave without a deferred lane returns at once)
+        if (ji.defer && mimic_launch_xdp_resume(&kp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     } else {  // launch parameters are read from a device copy
         const KParams *dkp = nullptr;
         const int slot = kp_slot(vm, kp, st, &dkp);
         if (slot < 0) return slot;
         if (jit ? mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+        if (jit && ji.defer && mimic_launch_xdp_resume(&kp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         vm->kp_pending = true;   // the slot's event is recorded when kp_slot leaves it
     }

@@ -52,13 +52,16 @@ static __device__ void step_save(const KParams &kp, const Lane &L, const uint64_
 #define NREGS 11
 #define KEY_DONE 0xffffffffu
 
-// The batch kernel and the Process.Step kernel are one body: STEP compiles the step-state paths
-// (restore a suspended process, save it at the end) in or out, so the batch kernel carries none
-// of their registers (146 -> the batch kernel's own budget, 3 -> 4 waves per SIMD).
-template <bool STEP>
+// The batch kernel, the Process.Step kernel and the resume kernel are one body: MODE compiles
+// the step-state paths (restore a suspended process, save it at the end) and the resume paths
+// (a process a JIT lane deferred, then the lane's remaining packets) in or out, so the batch
+// kernel carries none of their registers (146 -> the batch kernel's own budget, 3 -> 4 waves per
+// SIMD).
+enum { MODE_BATCH = 0, MODE_STEP = 1, MODE_RESUME = 2 };
+template <int MODE>
 static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp) {
-    const KParams &kp = *kpp;  // device copy (engine.cpp kp_slot): fields load where used
-    StepState *const STP = STEP ? kp.step : nullptr;
+    const KParams &kp = *kpp;  // device copy (engine.cpp kp_slot) or the kernarg segment: fields load where used
+    StepState *const STP = MODE == MODE_STEP ? kp.step : nullptr;
     // eBPF registers r0..r10 of every lane live in LDS, [wave][reg][lane] (8-byte words): a
     // wave-uniform register number addresses 64 consecutive words (conflict-free ds_read_b64),
     // and multi-register updates (exit, helpers) need no register-array copies.
@@ -67,7 +70,19 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
 #define REG(r) RB[(r) * 64]
 
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool lane_valid = g < kp.lanes;
+    // resume: only the lanes the JIT kernel deferred in this launch (defer_finish, runtime.h) run,
+    // from iteration j0 on; a wave without one returns at once
+    const DeferRec *DR = nullptr;
+    uint32_t j0 = 0;
+    if (MODE == MODE_RESUME) {
+        if (*kp.defer_any != kp.defer_epoch) return;
+        if (g < kp.lanes && kp.defer[g].flag == kp.defer_epoch) {
+            DR = kp.defer + g;
+            j0 = DR->j;
+        }
+        if (__ballot(DR != nullptr) == 0) return;
+    }
+    const bool lane_valid = g < kp.lanes && (MODE != MODE_RESUME || DR);
     Lane L;
     L.lane = g;
     L.cpu = STP ? STP->cpu : lane_cpu(kp, g);
@@ -77,14 +92,14 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         ex_begin = kp.sched_start[g];
         ex_count = kp.sched_start[g + 1] - ex_begin;
     }
-    uint64_t lane_steps = 0;
+    uint64_t lane_steps = MODE == MODE_RESUME && DR ? DR->lane_steps : 0;
     const DProg entry = cget(kp.progs, kp.entry_prog);
     const uint32_t P = kp.static_next + kp.stack_size + 1;
 
     for (uint32_t j = 0; j < kp.per_lane; j++) {
         // ---- which packet does this lane run in iteration j -----------------------------
         uint32_t i = 0xffffffffu;
-        if (lane_valid) {
+        if (lane_valid && (MODE != MODE_RESUME || j >= j0)) {
             if (kp.sched == SCHED_CHUNKED) {
                 uint64_t ii = (uint64_t)g * kp.per_lane + j;
                 if (ii < kp.n) i = (uint32_t)ii;
@@ -148,10 +163,14 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
                 key = pbase + (uint32_t)S->pc;
             }
         }
+        // resume: the process the JIT lane deferred (packet i, iteration j0) is attached to its
+        // packet again without Load's side effects (the room bytes keep what it wrote), then its
+        // registers and dynamic lane state come back and its slot runs next
+        const bool resume_here = MODE == MODE_RESUME && i != 0xffffffffu && j == j0;
         if (resumed) {
         } else if (i != 0xffffffffu && kp.ctx_kind == CTX_SKB) {   // LinuxContextSKBuff.Load (skb.h)
             uint64_t r1 = 0;
-            const int ls = skb_load(kp, L, i, r1);
+            const int ls = skb_load(kp, L, i, r1, !resume_here);
             REG(10) = kp.static_next + kp.frame_size;
             if (ls) {
                 TERM(ls, -1);
@@ -169,8 +188,10 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
             const uint32_t len = kp.pkt_len[i];
             L.pkt = kp.pkt_data + kp.pkt_off[i];
             L.M = H + len + T;
-            for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;
-            for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;
+            if (!resume_here) {
+                for (uint32_t b = 0; b < H; b++) L.pkt[b] = 0;
+                for (uint32_t b = 0; b < T; b++) L.pkt[H + len + b] = 0;
+            }
             L.data = P + H;
             L.data_end = P + H + len;
             L.ingress = (uint32_t)(kp.ingress_arr ? kp.ingress_arr[i] : kp.ingress);
@@ -183,6 +204,23 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
                 steps = 1;
                 TERM(MIMIC_ERR_PC_OOB, 0);
             }
+        }
+
+        if (resume_here) {
+#pragma unroll
+            for (int q = 0; q < NREGS; q++) REG(q) = DR->r[q];
+            L.sm0 = DR->sm0;
+            L.sm1 = DR->sm1;
+            L.xdp_dirty = DR->xdp_dirty;
+            L.nframes = DR->nframes;
+            L.tailcalls = DR->tailcalls;
+            steps = DR->steps;
+            cur_prog = DR->prog;
+            const DProg cp = kp.progs[cur_prog];
+            pn = cp.n;
+            pbase = cp.base;
+            key = pbase + (uint32_t)DR->pc;
+            resumed = true;
         }
 
         // ---- Process.Run ------------------------------------------------------------------
@@ -397,8 +435,16 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
 #undef REG
 }
 
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(const KParams *__restrict__ kpp) { xdp_body<false>(kpp); }
-extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KParams *__restrict__ kpp) { xdp_body<true>(kpp); }
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(const KParams *__restrict__ kpp) { xdp_body<MODE_BATCH>(kpp); }
+extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KParams *__restrict__ kpp) { xdp_body<MODE_STEP>(kpp); }
+// after a JIT kernel with deferred slow paths, with the same launch parameters (by value: read
+// in place from the kernarg segment, as the JIT kernels do)
+extern "C" __global__ __launch_bounds__(256) void mimic_xdp_resume_kernel(const KParams kp_arg) {
+    (void)kp_arg;
+    const KParams __attribute__((address_space(4))) *k4 =
+        (const KParams __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();
+    xdp_body<MODE_RESUME>((const KParams *)k4);
+}
 
 // Sum of a per-CPU u64 array over cpus: out[k] = sum_c base[c*stride + 8k] (the "sum over CPUs"
 // readout of a per-CPU counter map).  The per-CPU backings are contiguous ([cpu][key], stride =
@@ -568,6 +614,13 @@ extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, 
 
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st) {
     hipLaunchKernelGGL(mimic_hash_rebuild_kernel, dim3(1), dim3(1024), 0, st, arena, *m, force);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st) {
+    const uint32_t blocks = (kp->lanes + 255) / 256;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(mimic_xdp_resume_kernel, dim3(blocks), dim3(256), 0, st, *kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -131,7 +131,7 @@ class Gen {
         const char *ol = getenv("MIMIC_JIT_OPAQUE_LANE");
         opaque_lane = ol && ol[0] == '1';
         const char *cm = getenv("MIMIC_JIT_COLD");   // call | inline (default: by kernel size)
-        cold_mode = !cm ? 0 : !strcmp(cm, "call") ? 1 : !strcmp(cm, "inline") ? 2 : 0;
+        cold_mode = !cm ? 0 : !strcmp(cm, "call") ? 1 : !strcmp(cm, "inline") ? 2 : !strcmp(cm, "defer") ? 3 : 0;
         // MIMIC_JIT_STAGE=1: stage each packet's first 64 bytes in LDS.  Measured slower on MI355X
         // for every config (cfg 2: 74 us vs 37 us, cfg 3: 2.6 ms vs 1.2 ms per launch): the staging
         // waits for all eight qwords before the first use, while direct loads hit L1 / L2 anyway.
@@ -166,7 +166,7 @@ class Gen {
     bool careful_copies = true;
     uint32_t max_n = 0;
     bool fast_paths = true;    // MIMIC_JIT_FAST=0: every access through resolve()
-    int cold_mode = 0;         // MIMIC_JIT_COLD: 0 auto, 1 call, 2 inline
+    int cold_mode = 0;         // MIMIC_JIT_COLD: 0 auto, 1 call, 2 inline, 3 defer
     int kq_mode = 0;           // per-packet KParams fields through an opaque pointer (see MIMIC_JIT_KQ)
     bool opaque_lane = false;  // per-iteration opaque lane index (MIMIC_JIT_OPAQUE_LANE=1)
     bool nt = false;           // MIMIC_JIT_NT=1: streaming accesses non-temporal
@@ -201,7 +201,16 @@ class Gen {
         uint32_t prog = 0, hp = 0, base = 0, words = 0;
         int64_t off = 0;
     } xpf;
-    bool cold_inline = true;   // the cold paths are inlined at every site (else called)
+    bool cold_inline = true;   // the cold paths are inlined at every site (else called or deferred)
+    // Deferred slow paths (large kernels): a slow-path site stores the registers its slot and
+    // the slots after it can read (analyze_live), the PC, program and steps into the lane's
+    // DeferRec and leaves the packet loop (defer_finish, runtime.h); the interpreter's resume
+    // kernel (interp.hip), launched after the kernel, re-executes that slot on the generic path
+    // and finishes the lane's packets.  No call remains in the kernel: a call's ABI (caller-saved
+    // VGPRs around it, the callees' own registers, the Spill record in scratch) is what made the
+    // cfg-5 chain need 380 VGPRs + AGPRs and 240 bytes of scratch at one wave per SIMD.
+    bool defer_mode = false;
+    std::vector<std::vector<uint16_t>> live;   // [prog][slot]: registers live into the slot
     uint32_t cold_sites = 0;
     static constexpr uint32_t kColdInlineSites = 48;
     bool stage = false;        // MIMIC_JIT_STAGE=1: LDS packet window
@@ -249,6 +258,8 @@ class Gen {
         if (careful_copies) sites *= 2;
         cold_sites = sites;
         cold_inline = cold_mode == 2 || (cold_mode == 0 && sites <= kColdInlineSites);
+        defer_mode = !cold_inline && (cold_mode == 3 || cold_mode == 0) && !census && !stage && fast_paths;
+        if (defer_mode) analyze_live();
         analyze_vc();
         if (forward)
             for (auto &p : P) analyze_fwd(p);
@@ -292,6 +303,8 @@ class Gen {
             E.line("#define COLD_CALL(call_, pc_) TERM(MIMIC_ERR_ENGINE_HELPER, pc_)");
         else
             E.line("#define COLD_CALL(call_, pc_) do { VC_FLUSH(); SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
+        // defer mode: the site stored the live registers; the rest is the lane's (defer_finish)
+        E.line("#define DFR(pc_, prog_) do { VC_FLUSH(); dr_->pc = (int32_t)(pc_); dr_->prog = (prog_); dr_->steps = steps - 1u; goto L_defer; } while (0)");
         // a cold path may read or write the cached row in memory: write it back and stop caching
         if (vc_on)
             E.line("#define VC_FLUSH() do { if (vcd_) { vc_writeback(vcp_, vcb_, vc0_, vc1_, vc2_, vc3_); vcd_ = 0u; } vcv_ = 0u; } while (0)");
@@ -485,6 +498,11 @@ class Gen {
         }
         for (auto &p : P) program(p);
         E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
+        if (defer_mode) {
+            E.line("  L_defer:");
+            E.line("    defer_finish(kp, L, g, i, j, lane_steps);");
+            E.line("    break;");
+        }
         E.line("  L_term:");
         if (kq_mode == 2)   // the result pointers are loaded here, once per packet, not held in SGPRs
             E.line("    { const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
@@ -987,6 +1005,88 @@ class Gen {
         }
     }
 
+    // the slow path of slot i of the program being emitted: a call (COLD_CALL) or a deferral
+    std::string cold(const std::string &call, uint32_t i) const {
+        if (defer_mode) return defer_text(i);
+        return "COLD_CALL(" + call + ", " + std::to_string(i) + ");";
+    }
+    std::string defer_text(uint32_t i) const {
+        const uint16_t m = live.at(cur_prog).at(i) | 1u | (1u << 10);
+        std::string t = "{ DeferRec *dr_ = kp.defer + g;";
+        for (uint32_t r = 0; r < 11; r++)
+            if ((m >> r) & 1) t += " dr_->r[" + std::to_string(r) + "] = r" + std::to_string(r) + ";";
+        return t + " DFR(" + std::to_string(i) + "u, " + std::to_string(cur_prog) + "u); }";
+    }
+    // Registers live into each slot (backward dataflow over every program; a tail call continues
+    // in any program's entry): what the interpreter may read when it resumes a process deferred
+    // at that slot.  R0 is always live (every error stores it as the result), R10 too (the frame
+    // pointer).  With BPF-to-BPF calls every register is taken as live.
+    void analyze_live() {
+        const uint16_t ALL = 0x7ff;
+        live.assign(P.size(), {});
+        for (auto &p : P) live[p.id].assign(p.n, any_local ? ALL : 0);
+        if (any_local) return;
+        auto bit = [](uint32_t r) -> uint16_t { return r <= 10 ? (uint16_t)(1u << r) : (uint16_t)0; };
+        auto use_def = [&](const DInsn &x, uint16_t &use, uint16_t &def) {
+            const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x);
+            const uint16_t xs = (x.aux & AUX_X) ? bit(sr) : 0;
+            use = def = 0;
+            switch (h) {
+            case H_ALU64: case H_ALU32:
+                use = ((insn_op(x) & 0xf0) == 0xb0 ? 0 : bit(d)) | xs;
+                def = bit(d);
+                break;
+            case H_LDIMM: def = bit(d); break;
+            case H_JCC: use = bit(d) | xs; break;
+            case H_LDX: use = bit(sr); def = bit(d); break;
+            case H_ST: use = bit(d); break;
+            case H_STX: use = bit(d) | bit(sr); break;
+            case H_EXIT: use = 1; break;
+            case H_CALL:   // what the interpreter's helper reads (interp.hip H_CALL); helpers keep R1-R5 (Q8)
+                switch ((uint32_t)x.k) {
+                case 1: case 3: use = bit(1) | bit(2); break;
+                case 2: use = bit(1) | bit(2) | bit(3); break;
+                case 12: use = bit(2) | bit(3); break;
+                case 65: use = bit(1); break;
+                default: break;
+                }
+                break;
+            case H_LDABS: use = bit(6) | xs; def = 0x3f; break;  // R0 loaded, R1-R5 zeroed
+            case H_SLOW: case H_CALL_LOCAL: use = ALL; break;
+            default: break;                                  // NOP, JA, ERR
+            }
+        };
+        for (bool changed = true; changed;) {
+            changed = false;
+            uint16_t entry = 0;
+            for (auto &p : P)
+                if (p.n) entry |= live[p.id][0];
+            for (auto &p : P) {
+                for (int64_t i = (int64_t)p.n - 1; i >= 0; i--) {
+                    const DInsn &x = p.ins[i];
+                    const uint32_t h = AUX_H(x.aux);
+                    uint16_t out = 0;
+                    auto succ = [&](int64_t t) { if (t >= 0 && t < (int64_t)p.n) out |= live[p.id][t]; };
+                    const bool fall = (x.aux & AUX_FALL_OK) != 0;
+                    if (h == H_JA || h == H_JCC) {
+                        if (h == H_JCC && fall) succ(i + 1);
+                        if (x.aux & AUX_JT_OK) succ(jump_target(x, i));
+                    } else if (h != H_EXIT && h != H_ERR) {
+                        if (fall) succ(i + 1);
+                        if (h == H_CALL && (uint32_t)x.k == 12) out |= entry;
+                    }
+                    uint16_t use, def;
+                    use_def(x, use, def);
+                    const uint16_t in = (uint16_t)(use | (out & ~def) | 1u);
+                    if (in != live[p.id][i]) {
+                        live[p.id][i] = in;
+                        changed = true;
+                    }
+                }
+            }
+        }
+    }
+
     // PC+1 after slot i (vm.go:328-337)
     void fall(const ProgView &p, uint32_t i) {
         if (p.ins[i].aux & AUX_FALL_OK) E.line("    goto P%u_%u;", p.id, i + 1);
@@ -1151,14 +1251,17 @@ class Gen {
                        pre.c_str(), (uint32_t)off, (uint32_t)off, n, i, dst.c_str());
                 pre = "    else ";
             }
-            E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
-                   "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, 0, true);"
-                   " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
+            if (defer_mode)   // the generic convertAccess is a call: the resume kernel runs it
+                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) %s", pre.c_str(), defer_text(i).c_str());
+            else
+                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
+                       "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, 0, true);"
+                       " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
             pre = "    else ";
         }
         skb_ptr_fast(i, base, off, n, true, dst, pre);
         // generic GetEntry + Load (cold, out of line)
-        E.line("%s{ COLD_CALL(cold_load(kp, sp_, ga_, %uu), %u); %s = sp_.v; }", pre.c_str(), n, i, dst.c_str());
+        E.line("%s{ %s %s = sp_.v; }", pre.c_str(), cold("cold_load(kp, sp_, ga_, " + std::to_string(n) + "u)", i).c_str(), dst.c_str());
     }
 
     void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val, bool deferred = false) {
@@ -1166,8 +1269,8 @@ class Gen {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         if (!deferred && elided.count({cur_prog, i})) {   // the write happens in the lookup's cold path
             const auto f = fast_forms(base, n, val);
-            E.line("    if (!(%s)) { %sCOLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u); }", f.at(0).cond.c_str(),
-                   base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "", n, val.c_str(), i);
+            E.line("    if (!(%s)) { %s%s }", f.at(0).cond.c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
+                   cold("cold_store(kp, sp_, ga_, " + std::to_string(n) + "u, " + val + ")", i).c_str());
             return;
         }
         std::string pre = "    ";
@@ -1183,15 +1286,18 @@ class Gen {
                        pre.c_str(), (uint32_t)off, val.c_str(), (uint32_t)off, n, i);
                 pre = "    else ";
             }
-            E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
-                   "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, %s, false);"
-                   " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
+            if (defer_mode)
+                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) %s", pre.c_str(), defer_text(i).c_str());
+            else
+                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
+                       "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, %s, false);"
+                       " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
             pre = "    else ";
         }
         skb_ptr_fast(i, base, off, n, false, val, pre);
         // generic GetEntry + Store (cold); the stack / xdp_md state it may change comes back
-        E.line("%s{ %sCOLD_CALL(cold_store(kp, sp_, ga_, %uu, %s), %u);", pre.c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
-               n, val.c_str(), i);
+        E.line("%s{ %s%s", pre.c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
+               cold("cold_store(kp, sp_, ga_, " + std::to_string(n) + "u, " + val + ")", i).c_str());
         if (stage)  // a store that reached the packet updates the window too
             E.line("      if (sp_.po) win_store_rel(pwin_, tl_, W_, sp_.po - 1u, %uu, %uu, %s); }", wb(), n, ord(val, n).c_str());
         else E.line("    }");
@@ -1323,17 +1429,17 @@ class Gen {
                 } else {
                     E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) {");
                 }
-                E.line("      if (!(%s)) COLD_CALL(cold_lookup(kp, sp_), %u); } }", hfast.c_str(), i);
+                E.line("      if (!(%s)) %s } }", hfast.c_str(), cold("cold_lookup(kp, sp_)", i).c_str());
             } else {
-                E.line("    COLD_CALL(cold_lookup(kp, sp_), %u);", i);
+                E.line("    %s", cold("cold_lookup(kp, sp_)", i).c_str());
             }
             break;
         }
         case 2:
-            E.line("    COLD_CALL(cold_update(kp, sp_), %u);", i);
+            E.line("    %s", cold("cold_update(kp, sp_)", i).c_str());
             break;
         case 3:
-            E.line("    COLD_CALL(cold_delete(kp, sp_), %u);", i);
+            E.line("    %s", cold("cold_delete(kp, sp_)", i).c_str());
             break;
         case 8:
             E.line("    r0 = (uint64_t)(int64_t)L.cpu;");
@@ -1361,12 +1467,12 @@ class Gen {
                 E.line("      if (np_ >= 0) {");
                 jump_table("np_");
                 E.line("      } else if (np_ == -2) {");
-                E.line("      COLD_CALL(cold_tailcall(kp, sp_), %u);", i);
+                E.line("      %s", cold("cold_tailcall(kp, sp_)", i).c_str());
                 E.line("      if (sp_.tail) {");
                 jump_table("sp_.new_prog");
                 E.line("      } } }");
             } else {
-                E.line("    COLD_CALL(cold_tailcall(kp, sp_), %u);", i);
+                E.line("    %s", cold("cold_tailcall(kp, sp_)", i).c_str());
                 E.line("    {");
                 E.line("      if (sp_.tail) {");
                 jump_table("sp_.new_prog");
@@ -1376,7 +1482,7 @@ class Gen {
             break;
         }
         default:  // 65: bpf_xdp_adjust_tail (emulator_linux_helpers.go:842-864)
-            E.line("    COLD_CALL(cold_adjust_tail(kp, sp_), %u);", i);
+            E.line("    %s", cold("cold_adjust_tail(kp, sp_)", i).c_str());
             break;
         }
     }
@@ -1389,7 +1495,8 @@ class Gen {
         const uint32_t n = AUX_SZ(x.aux), s = insn_src(x);
         const bool ind = (x.aux & AUX_X) != 0;
         if (ind && s > 10) {  // Registers.Get panics (after the R6 check)
-            E.line("    { SPILL(); cold_ldabs(kp, sp_, 0u, %uu, true); FILL(); TERM(sp_.st ? sp_.st : MIMIC_PANIC_BADREG, %u); }", n, i);
+            if (defer_mode) E.line("    %s", defer_text(i).c_str());
+            else E.line("    { SPILL(); cold_ldabs(kp, sp_, 0u, %uu, true); FILL(); TERM(sp_.st ? sp_.st : MIMIC_PANIC_BADREG, %u); }", n, i);
             return;
         }
         const std::string N = std::to_string(n) + "u";
@@ -1409,7 +1516,7 @@ class Gen {
             E.line("    }");
             pre = "    else ";
         }
-        E.line("%sCOLD_CALL(cold_ldabs(kp, sp_, ga_, %s, false), %u);", pre.c_str(), N.c_str(), i);
+        E.line("%s%s", pre.c_str(), cold("cold_ldabs(kp, sp_, ga_, " + N + ", false)", i).c_str());
         E.line("    r1 = 0; r2 = 0; r3 = 0; r4 = 0; r5 = 0;");
     }
 
@@ -1422,7 +1529,7 @@ class Gen {
         const int32_t off = insn_off(x);
         if (cls == 1) {  // LDX with dst >= 10: the memory error comes first, inst.go:298-318
             static const uint32_t szs[4] = {4, 2, 1, 8};
-            E.line("    COLD_CALL(cold_load(kp, sp_, %s, %uu), %u);", addr(s, off).c_str(), szs[(op >> 3) & 3], i);
+            E.line("    %s", cold("cold_load(kp, sp_, " + addr(s, off) + ", " + std::to_string(szs[(op >> 3) & 3]) + "u)", i).c_str());
             E.line("    TERM(%s, %u);", d > 10 ? "MIMIC_PANIC_BADREG" : "MIMIC_ERR_R10_WRITE", i);
             return;
         }
@@ -1560,6 +1667,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->tail_calls = g.has_tail();
         info->early_loads = g.has_early_loads();
         info->cold_inline = g.cold_inline;
+        info->defer = g.defer_mode;
         info->karg = g.karg != 0;
     }
     return src;

@@ -15,6 +15,7 @@ struct JitInfo {
     bool early_loads;    // the kernel issues packet loads early (analyze_spec)
     bool cold_inline;    // the slow paths are inlined (small kernel, 4-wave register budget)
     bool karg;           // the kernel takes KParams by value (kernarg segment), not a device copy
+    bool defer;          // slow paths are deferred to the interpreter's resume kernel (launch it after)
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // vc_slots: kernel-wide indices of LD_IMM64 slots whose constant is the object of a per-CPU array

@@ -202,6 +202,32 @@ struct KParams {
     // no program of this launch writes a hash map (no update / delete helper): the tables are
     // read-only while it runs, so lookups read a bucket record with plain (cached) loads at once
     uint32_t hash_ro;
+    // JIT kernels built with deferred slow paths (jit.cpp, defer mode): a lane whose process
+    // reaches a slow path saves it in defer[lane] (flag = defer_epoch), sets *defer_any =
+    // defer_epoch and stops; the interpreter's resume kernel then finishes that process and the
+    // lane's remaining packets.  The epoch changes every launch, so nothing is ever cleared.
+    struct DeferRec *defer;
+    uint32_t *defer_any;
+    uint32_t defer_epoch;
+    uint32_t pad2;
+};
+
+// A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its
+// successors can read, the slot (PC) and program, the steps before the slot, the process's
+// dynamic lane state (stack validity, xdp_md overlay flag, frames, tail calls), and where the
+// lane is in its schedule.  Everything else of the lane (packet entry, sk_buff record, ...)
+// follows from the packet and is derived again; the resume kernel re-executes the slot on the
+// generic path.
+struct DeferRec {
+    uint64_t r[11];
+    int32_t pc;
+    uint32_t prog;
+    uint32_t steps;       // Step() calls before the slot
+    uint32_t j;           // iteration of the lane's packet loop
+    uint64_t lane_steps;  // steps of the lane's earlier packets in this launch
+    uint64_t sm0, sm1;
+    uint32_t xdp_dirty, nframes, tailcalls;
+    uint32_t flag;        // == KParams::defer_epoch: suspended in that launch
 };
 
 // The state of one stepped process between launches (engine.cpp mimic_process_*): the

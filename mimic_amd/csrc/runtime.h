@@ -859,7 +859,7 @@ DEV int ld_abs(const KParams &kp, const Lane &L, uint64_t r6, uint32_t x, uint32
 // of the skb.h layout, zeroed headroom / tailroom, R1 = the sk_buff address.  Returns 0 or
 // MIMIC_ERR_CTX_LOAD (SKBuffFromBytes failed, or AddEntry ran out of 32-bit address space;
 // then the packet memory is left untouched, as the reference never writes it).
-DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1) {
+DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool zero_rooms = true) {
     SkbRec *rec = kp.skb_rec + i;
     const uint32_t lw = rec->len;
     L.pkt = kp.pkt_data + kp.pkt_off[i];
@@ -874,8 +874,10 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1) {
     L.ka = (uint32_t)ka;
     L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
     L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
-    for (uint32_t b = 0; b < SKB_HEADROOM; b += 8) *(u64u *)(L.pkt + b) = 0;
-    for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
+    if (zero_rooms) {
+        for (uint32_t b = 0; b < SKB_HEADROOM; b += 8) *(u64u *)(L.pkt + b) = 0;
+        for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
+    }
     r1 = kp.static_next + kp.stack_size + 1;
     return 0;
 }
@@ -928,6 +930,35 @@ struct Spill {
     uint32_t tail;       // tail call taken
     uint32_t new_prog;
 };
+// The lane-state half of a deferred slow path (jit.cpp, defer mode; the site has stored the
+// registers, PC, program and steps, and written back the lane value cache): the LDS copies of
+// the process (sk_buff record, stack window) go back to HBM where the interpreter keeps them,
+// the dynamic lane state goes into the record, and the record is marked for the resume kernel
+// (interp.hip).  The lane then stops: its later packets follow this one on the resume side.
+DEV void defer_finish(const KParams &kp, const Lane &L, uint32_t g, uint32_t i, uint32_t j, uint64_t lane_steps) {
+    DeferRec *d = kp.defer + g;
+    if (L.rec && L.rec != kp.skb_rec + i) {   // the sk_buff record's LDS slot
+        const uint64_t *s = (const uint64_t *)L.rec;
+        GAS uint64_t *o = (GAS uint64_t *)(kp.skb_rec + i);
+        for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) o[q] = s[q];
+    }
+#ifdef MIMIC_LDS_STACK_Q
+    for (uint32_t q = 0; q < MIMIC_LDS_STACK_Q; q++) {
+        const uint32_t o = STK_LDS_LO + 8u * q;
+        if (stk_valid(kp, L, o)) *gp((uint64_t *)priv_b(kp, L.lane, o)) = stk_lw(o);
+    }
+#endif
+    d->sm0 = L.sm0;
+    d->sm1 = L.sm1;
+    d->xdp_dirty = L.xdp_dirty;
+    d->nframes = L.nframes;
+    d->tailcalls = L.tailcalls;
+    d->j = j;
+    d->lane_steps = lane_steps;
+    d->flag = kp.defer_epoch;
+    *gp(kp.defer_any) = kp.defer_epoch;
+}
+
 #if defined(MIMIC_COLD_INLINE) && MIMIC_COLD_INLINE
 #define COLD DEV
 #define COLD_OPAQUE() do { } while (0)

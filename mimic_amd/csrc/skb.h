@@ -74,7 +74,9 @@ struct SkbRec {  // 160 bytes
 // the field accessors are big switches reached from every generic memory access of a JIT
 // kernel: out of line (value arguments and results only, so no scratch) to keep the kernels
 // small and their hipRTC compile fast
+#ifndef SKB_COLD
 #define SKB_COLD static __device__ __noinline__
+#endif
 
 struct SkbRes {
     uint64_t v;

@@ -74,8 +74,31 @@ def test_skb_chain_kernel_compiles():
     progs, _, _ = W.skb_programs()
     src = _source([p.raw for p in progs], _lib.CTX_SKB)
     assert "#define MIMIC_CTX_FIXED 1" in src and "skb_load_lds(kp, L, i, r1," in src
-    assert "cold_ldabs(kp, sp_" in src and "bswap_n(" in src
+    assert "bswap_n(" in src
+    # a kernel this size defers its slow paths to the interpreter's resume kernel (no calls)
+    assert "DFR(" in src and "L_defer:" in src and "COLD_CALL(cold" not in src
     assert _compiles(src) > 0
+
+
+def test_skb_chain_register_budget():
+    """cfg 5's five-program chain with deferred slow paths: no call left in the kernel, so no
+    scratch (the Spill record and the call ABI's saves were 240 bytes per lane) and at least two
+    waves per SIMD (it was 380 VGPRs + AGPRs at one wave with called slow paths)."""
+    progs, _, _ = W.skb_programs()
+    r = _resources([p.raw for p in progs], _lib.CTX_SKB)
+    assert r["vgpr_total"] <= 256 and r["waves_per_simd"] >= 2, r
+    assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["agpr"] == 0, r
+
+
+def test_defer_sites_store_live_registers_only():
+    """A deferred slot stores the registers the interpreter can read from it on (plus R0, every
+    result's value, and R10): after `mov r6, r1` at slot 0 of the chain's entry, slot 1 (a load
+    through r6) needs r0, r6 and r10 only."""
+    progs, _, _ = W.skb_programs()
+    src = _source([p.raw for p in progs], _lib.CTX_SKB)
+    site = [l for l in src.splitlines() if "DFR(1u, 0u)" in l][0]
+    stored = sorted(int(x) for x in __import__("re").findall(r"dr_->r\[(\d+)\]", site))
+    assert stored == [0, 6, 10], site
 
 
 def test_skb_and_xdp_kernels_differ_only_in_context():
