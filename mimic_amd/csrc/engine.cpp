@@ -1196,7 +1196,8 @@ struct SkbInto {
     SkbRec *rec;
     uint64_t *foot, *prefix;
 };
-static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, const SkbInto *into = nullptr) {
+static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, const SkbInto *into = nullptr,
+                       bool records = true) {
     const uint32_t n = b->n;
     if (vm->skb_stream && vm->skb_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
     if (n > vm->skb_cap || !vm->d_skb_state) {
@@ -1223,7 +1224,7 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     }
     // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
     const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
-    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, into ? into->rec : vm->d_skb_rec,
+    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, into ? into->rec : records ? vm->d_skb_rec : nullptr,
                               into ? into->foot : vm->d_skb_foot, into ? into->prefix : vm->d_skb_prefix,
                               vm->d_skb_scan, vm->skb_scan_cap, vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
@@ -1395,44 +1396,6 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     default:
         return fail(vm, MIMIC_EINVAL, "unknown schedule %u", b->schedule);
     }
-    if (skb && step && step->skb_rec) {   // a stepped sk_buff process: Load ran at NewProcess
-        kp.ctx_kind = CTX_SKB;
-        kp.skb_ifindex = skb->ifindex;
-        kp.skb_rec = step->skb_rec;
-        kp.skb_prefix = step->skb_prefix;
-        kp.skb_base = step->skb_base;
-    } else if (skb) {
-        rc = skb_prepare(vm, b, st);
-        if (rc) return rc;
-        kp.ctx_kind = CTX_SKB;
-        kp.skb_ifindex = skb->ifindex;
-        kp.skb_rec = vm->d_skb_rec;
-        kp.skb_prefix = vm->d_skb_prefix;
-        kp.skb_base = vm->d_skb_state + 1;
-    }
-    // compact hash tables whose buckets are mostly tombstones (device-side check, no host sync)
-    // (skipped while no delete can have run on the map: without tombstones live entries stay
-    // below half of the table, so the check would always decline -- and a kernel between the
-    // batches costs a launch gap)
-    // A launch whose programs never delete pops the freelists without the `avail` semaphore
-    // (hashmap.h h_insert_wave pop_only); one that may delete first normalises maps left so.
-    kp.hash_pop_only = vm->prog_deletes ? 0u : 1u;
-    // no program can write a hash map: during the launch every table is read-only
-    kp.hash_ro = (vm->prog_deletes || vm->prog_updates) ? 0u : 1u;
-    for (auto &m : vm->maps) {
-        if (!is_hash(m)) continue;
-        const DMap dm = to_dmap(m);
-        if (vm->prog_deletes && m.pop_dirty) {
-            if (mimic_launch_hash_normalize(vm->arena, &dm, st))
-                return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
-            m.pop_dirty = false;
-        }
-        if (!vm->prog_deletes) m.pop_dirty = true;
-        if (vm->prog_deletes) m.may_tomb = true;
-        if (!m.may_tomb) continue;
-        if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
-            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
-    }
     bool jit = vm->exec_mode == MIMIC_EXEC_JIT && !step;   // stepping runs on the interpreter
     if (jit && !vm->jit_fn[ctx]) {
         std::string log;
@@ -1468,6 +1431,48 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     if (jit) {  // a loop-free kernel has no budget checks: tiny budgets run on the interpreter
         const uint64_t bound = mimic_jit_step_bound(ji, kp.max_tail_calls);
         if (bound && kp.budget < bound) jit = false;
+    }
+    kp.skb_rec_built = 1;
+    if (skb && step && step->skb_rec) {   // a stepped sk_buff process: Load ran at NewProcess
+        kp.ctx_kind = CTX_SKB;
+        kp.skb_ifindex = skb->ifindex;
+        kp.skb_rec = step->skb_rec;
+        kp.skb_prefix = step->skb_prefix;
+        kp.skb_base = step->skb_base;
+    } else if (skb) {
+        // a JIT kernel that walks the headers itself needs the footprints only
+        const bool own_recs = jit && ji.skb_walk;
+        rc = skb_prepare(vm, b, st, nullptr, !own_recs);
+        if (rc) return rc;
+        kp.skb_rec_built = own_recs ? 0u : 1u;
+        kp.ctx_kind = CTX_SKB;
+        kp.skb_ifindex = skb->ifindex;
+        kp.skb_rec = vm->d_skb_rec;
+        kp.skb_prefix = vm->d_skb_prefix;
+        kp.skb_base = vm->d_skb_state + 1;
+    }
+    // compact hash tables whose buckets are mostly tombstones (device-side check, no host sync)
+    // (skipped while no delete can have run on the map: without tombstones live entries stay
+    // below half of the table, so the check would always decline -- and a kernel between the
+    // batches costs a launch gap)
+    // A launch whose programs never delete pops the freelists without the `avail` semaphore
+    // (hashmap.h h_insert_wave pop_only); one that may delete first normalises maps left so.
+    kp.hash_pop_only = vm->prog_deletes ? 0u : 1u;
+    // no program can write a hash map: during the launch every table is read-only
+    kp.hash_ro = (vm->prog_deletes || vm->prog_updates) ? 0u : 1u;
+    for (auto &m : vm->maps) {
+        if (!is_hash(m)) continue;
+        const DMap dm = to_dmap(m);
+        if (vm->prog_deletes && m.pop_dirty) {
+            if (mimic_launch_hash_normalize(vm->arena, &dm, st))
+                return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+            m.pop_dirty = false;
+        }
+        if (!vm->prog_deletes) m.pop_dirty = true;
+        if (vm->prog_deletes) m.may_tomb = true;
+        if (!m.may_tomb) continue;
+        if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
     vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
     if (jit && ji.defer) {   // the lanes' suspended processes (DeferRec) and the launch's marker

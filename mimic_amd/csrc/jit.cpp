@@ -114,6 +114,10 @@ class Gen {
         skb_fields = !(sf && sf[0] == '0');
         const char *sl = getenv("MIMIC_JIT_SKBLDS");   // 0: sk_buff records read from global memory
         skb_lds_knob = !(sl && sl[0] == '0');
+        const char *sw = getenv("MIMIC_JIT_SKBWALK");   // 1: the kernel builds its sk_buff records (measured slower)
+        skb_walk_knob = sw && sw[0] == '1';
+        const char *ic = getenv("MIMIC_JIT_INC");   // 0: counter increments as three slots
+        inc_knob = !(ic && ic[0] == '0');
         const char *hf = getenv("MIMIC_JIT_HASH");   // 0: hash-map lookups always through the generic helper
         hash_fast = !(hf && hf[0] == '0');
         const char *ti = getenv("MIMIC_JIT_TAIL");   // 0: tail calls always through the generic helper
@@ -173,6 +177,13 @@ class Gen {
     bool skb_fields = true;    // MIMIC_JIT_SKBFIELD=0: no per-field sk_buff access code
     bool skb_lds_knob = true;  // MIMIC_JIT_SKBLDS=0: no LDS copy of the sk_buff record
     bool skb_lds = false;
+    // the kernel runs SKBuffFromBytes itself into the LDS slot (skb_load_walk), over a 128-byte
+    // header window per thread in LDS: the prep kernel then writes footprints only
+    // (MIMIC_JIT_SKBWALK=1; measured slower on MI355X: cfg 5 0.447 -> 0.482 ms per step at
+    // V = 128K -- the walk on the chain's critical path costs more than the record round trip)
+    bool skb_walk_knob = false;
+    bool skb_walk = false;
+    bool inc_knob = true;      // MIMIC_JIT_INC=0: no fused counter increments (fusable_inc)
     static constexpr uint32_t kSrecQ = 21;   // 8-byte words per LDS record slot (SkbRec is 20)
     int karg = 2;              // MIMIC_JIT_KARG: 2 launch parameters by value in the kernarg segment, read
                                // through an opaque constant-space pointer; 1 the same, plain; 0 a
@@ -259,7 +270,7 @@ class Gen {
         cold_sites = sites;
         cold_inline = cold_mode == 2 || (cold_mode == 0 && sites <= kColdInlineSites);
         defer_mode = !cold_inline && (cold_mode == 3 || cold_mode == 0) && !census && !stage && fast_paths;
-        if (defer_mode) analyze_live();
+        if (fast_paths) analyze_live();
         analyze_vc();
         if (forward)
             for (auto &p : P) analyze_fwd(p);
@@ -346,6 +357,8 @@ class Gen {
         // the sk_buff records of the block's lanes, 168 bytes apart (an odd number of 8-byte
         // words: lanes reading the same field hit different banks); nothing reads them back
         if (skb_lds) E.line("  __shared__ uint64_t srec_[%uu * 256u];", kSrecQ);
+        skb_walk = skb_lds && skb_walk_knob;
+        if (skb_walk) E.line("  __shared__ uint32_t swin_[(SKB_WIN / 4u) * 256u];   // header windows (skb_load_walk)");
         E.line("  Lane L;");
         E.line("  Spill sp_;");
         if (census) {
@@ -427,7 +440,9 @@ class Gen {
         if (ctx == CTX_SKB) {
             // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107, skb.h)
             E.line("    uint64_t r1 = 0;");
-            if (skb_lds)   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
+            if (skb_walk)   // the process's SkbRec built in this lane's LDS slot: every field access reads LDS
+                E.line("    const int ls_ = skb_load_walk(kp, L, i, r1, srec_ + %uu * threadIdx.x, swin_);", kSrecQ);
+            else if (skb_lds)   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
                 E.line("    const int ls_ = skb_load_lds(kp, L, i, r1, srec_ + %uu * threadIdx.x);", kSrecQ);
             else
                 E.line("    const int ls_ = skb_load(kp, L, i, r1);");
@@ -994,6 +1009,11 @@ class Gen {
                 for (uint32_t i = s; i < e; i++) {
                     if (careful) E.line("    if (steps == kp.budget) TERM(MIMIC_ERR_STEP_LIMIT, %u);", i);
                     emit_spec(p, i);
+                    if (!careful && i + 2 < e && fusable_inc(p, i)) {
+                        emit_inc(p, i);
+                        i += 2;
+                        continue;
+                    }
                     insn(p, i);
                 }
                 // falling off the end of the block
@@ -1085,6 +1105,49 @@ class Gen {
                 }
             }
         }
+    }
+
+    // Counter increments.  `ldx rD, [rB + o]; add rD, k; stx [rB + o], rD` (4 or 8 bytes, one
+    // basic block, rD dead after the store) on a map value is a read-modify-write of one word: its
+    // load is a dependent memory round trip the lane waits for before the store can go.  When the
+    // word lies in the value region the last lookup returned (the translation cache, where the
+    // three slots' fast paths would go) it is one atomic add without return instead -- the lane
+    // does not wait.  Equivalent for the lane's own sequence: a per-CPU row is touched by its lane
+    // only; a shared map's word is raced by other vCPUs either way (processPool), and the add is
+    // one of the interleavings.  Anything else (packet, stack, cached row, other entries,
+    // unaligned) takes the three slots as they are.  MIMIC_JIT_INC=0: never.
+    bool fusable_inc(const ProgView &p, uint32_t i) const {
+        if (!inc_knob || !fast_paths || live.empty()) return false;
+        const DInsn &ld = p.ins[i], &ad = p.ins[i + 1], &sx = p.ins[i + 2];
+        if (AUX_H(ld.aux) != H_LDX || AUX_H(sx.aux) != H_STX) return false;
+        const uint32_t n = AUX_SZ(ld.aux), d = insn_dst(ld), b = insn_src(ld);
+        if ((n != 4 && n != 8) || d == 0 || d > 9 || b > 9 || b == d) return false;
+        const uint32_t ah = AUX_H(ad.aux);
+        if (!(ah == H_ALU64 || (ah == H_ALU32 && n == 4)) || (insn_op(ad) & 0xf8) != 0x00 || (ad.aux & AUX_X) ||
+            insn_dst(ad) != d)
+            return false;
+        if (AUX_SZ(sx.aux) != n || insn_dst(sx) != b || insn_src(sx) != d || insn_off(sx) != insn_off(ld)) return false;
+        if ((ld.aux & AUX_FALL_OK) == 0 || (ad.aux & AUX_FALL_OK) == 0) return false;
+        if (i + 3 < p.n && (sx.aux & AUX_FALL_OK) && ((live[p.id][i + 3] >> d) & 1)) return false;
+        if (spec_use.count({p.id, i}) || spec_at.count({p.id, i + 1}) || spec_at.count({p.id, i + 2})) return false;
+        if (fwd_store.count({p.id, i + 2}) || elided.count({p.id, i + 2})) return false;
+        return true;
+    }
+    void emit_inc(const ProgView &p, uint32_t i) {
+        const DInsn &ld = p.ins[i], &ad = p.ins[i + 1];
+        const uint32_t n = AUX_SZ(ld.aux), d = insn_dst(ld), b = insn_src(ld);
+        const std::string N = std::to_string(n) + "u";
+        const uint64_t k = AUX_H(ad.aux) == H_ALU32 ? (uint32_t)ad.k : ad.k;
+        E.line("    // %u..%u: counter increment of r%u (dead after): one atomic add in the lookup's value region", i, i + 2, d);
+        E.line("    ga_ = %s;", addr(b, insn_off(ld)).c_str());
+        std::string cond = "(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n && !((uintptr_t)(L.t_ptr + (uint32_t)(ga_ - L.t_lo)) & (" + N + " - 1u))";
+        if (vc_on) cond = "!(vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + " + N + " <= vcb_) && " + cond;
+        E.line("    if (%s) { steps += 3u; atomic_add_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), %s, %s); }", cond.c_str(), N.c_str(), imm(k).c_str());
+        E.line("    else {");
+        insn(p, i);
+        insn(p, i + 1);
+        insn(p, i + 2);
+        E.line("    }");
     }
 
     // PC+1 after slot i (vm.go:328-337)
@@ -1668,6 +1731,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->early_loads = g.has_early_loads();
         info->cold_inline = g.cold_inline;
         info->defer = g.defer_mode;
+        info->skb_walk = g.skb_walk;
         info->karg = g.karg != 0;
     }
     return src;

@@ -16,6 +16,7 @@ struct JitInfo {
     bool cold_inline;    // the slow paths are inlined (small kernel, 4-wave register budget)
     bool karg;           // the kernel takes KParams by value (kernarg segment), not a device copy
     bool defer;          // slow paths are deferred to the interpreter's resume kernel (launch it after)
+    bool skb_walk;       // sk_buff kernel that builds its SkbRecs itself (prep: footprints only)
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // vc_slots: kernel-wide indices of LD_IMM64 slots whose constant is the object of a per-CPU array

@@ -209,7 +209,9 @@ struct KParams {
     struct DeferRec *defer;
     uint32_t *defer_any;
     uint32_t defer_epoch;
-    uint32_t pad2;
+    // sk_buff batches: 1 when the prep kernel wrote every packet's SkbRec; 0 when the JIT kernel
+    // builds them itself (skb_load_walk) -- then the interpreter builds the ones it needs
+    uint32_t skb_rec_built;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

@@ -855,14 +855,37 @@ DEV int ld_abs(const KParams &kp, const Lane &L, uint64_t r6, uint32_t x, uint32
     return rc ? MIMIC_ERR_LDABS : 0;
 }
 
+// The packet memory's headroom and tailroom are zero at Load (context_sk_buff.go:110-119).  They
+// are read first and written only when some byte is not zero already (a program stored there in
+// an earlier run of the buffer, or the caller's bytes): the common case writes nothing, and the
+// reads share their lines with the packet's first bytes and travel with the header loads.
+DEV void skb_rooms_clear(uint8_t *pkt, uint32_t lw) {
+    typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
+    const GAS u64x2u *h = (const GAS u64x2u *)pkt, *t = (const GAS u64x2u *)(pkt + SKB_HEADROOM + lw);
+    const u64x2u h0 = h[0], h1 = h[1], t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+    const u64x2u o = h0 | h1 | t0 | t1 | t2 | t3;
+    if (o.x | o.y) {
+        const u64x2u z = {0, 0};
+        GAS u64x2u *hw = (GAS u64x2u *)pkt, *tw = (GAS u64x2u *)(pkt + SKB_HEADROOM + lw);
+        hw[0] = z;
+        hw[1] = z;
+        for (uint32_t q = 0; q < SKB_TAILROOM / 16; q++) tw[q] = z;
+    }
+}
+static_assert(SKB_HEADROOM == 32 && SKB_TAILROOM == 64, "skb_rooms_clear covers 2 + 4 16-byte chunks");
+
 // NewProcess + LinuxContextSKBuff.Load (context_sk_buff.go:42-107) for packet i: the entries
 // of the skb.h layout, zeroed headroom / tailroom, R1 = the sk_buff address.  Returns 0 or
 // MIMIC_ERR_CTX_LOAD (SKBuffFromBytes failed, or AddEntry ran out of 32-bit address space;
-// then the packet memory is left untouched, as the reference never writes it).
-DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool zero_rooms = true) {
+// then the packet memory is left untouched, as the reference never writes it).  When the batch's
+// records were not built by the prep kernel (KParams::skb_rec_built == 0: its JIT kernel builds
+// them in LDS) the record is built here first, unless `attach_only` (a process the resume kernel
+// re-attaches: its record, rooms and packet are what the JIT lane left).
+DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool attach_only = false) {
     SkbRec *rec = kp.skb_rec + i;
-    const uint32_t lw = rec->len;
     L.pkt = kp.pkt_data + kp.pkt_off[i];
+    if (!kp.skb_rec_built && !attach_only) skb_init(SkbBytes{L.pkt + SKB_HEADROOM}, kp.pkt_len[i], *rec);
+    const uint32_t lw = rec->len;
     L.rec = nullptr;
     L.ka = 0;
     L.pa = 0;
@@ -874,10 +897,25 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool zero
     L.ka = (uint32_t)ka;
     L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
     L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
-    if (zero_rooms) {
-        for (uint32_t b = 0; b < SKB_HEADROOM; b += 8) *(u64u *)(L.pkt + b) = 0;
-        for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
-    }
+    if (!attach_only) skb_rooms_clear(L.pkt, lw);
+    r1 = kp.static_next + kp.stack_size + 1;
+    return 0;
+}
+
+// skb_load's tail once the record is in place (LDS slot d): entries, rooms, R1
+DEV int skb_attach(const KParams &kp, Lane &L, uint64_t &r1, uint64_t *d, uint32_t lw, uint64_t pre, uint64_t base) {
+    L.rec = nullptr;
+    L.ka = 0;
+    L.pa = 0;
+    L.M = 0;
+    if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
+    const uint64_t ka = base + pre;
+    if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
+    L.rec = (SkbRec *)d;
+    L.ka = (uint32_t)ka;
+    L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
+    L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
+    skb_rooms_clear(L.pkt, lw);
     r1 = kp.static_next + kp.stack_size + 1;
     return 0;
 }
@@ -894,23 +932,22 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
     const uint64_t po = kp.pkt_off[i], pre = kp.skb_prefix[i], base = *kp.skb_base;
 #pragma unroll
     for (uint32_t q = 0; q < NQ; q++) d[q] = w[q];
-    const uint32_t lw = (uint32_t)w[0];
     L.pkt = kp.pkt_data + po;
-    L.rec = nullptr;
-    L.ka = 0;
-    L.pa = 0;
-    L.M = 0;
-    if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
-    const uint64_t ka = base + pre;
-    if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
-    L.rec = (SkbRec *)d;
-    L.ka = (uint32_t)ka;
-    L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
-    L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
-    for (uint32_t b = 0; b < SKB_HEADROOM; b += 8) *(u64u *)(L.pkt + b) = 0;
-    for (uint32_t b = 0; b < SKB_TAILROOM; b += 8) *(u64u *)(L.pkt + SKB_HEADROOM + lw + b) = 0;
-    r1 = kp.static_next + kp.stack_size + 1;
-    return 0;
+    return skb_attach(kp, L, r1, d, (uint32_t)w[0], pre, base);
+}
+
+// skb_load for a JIT kernel that builds the record itself (no prep records: a 160-byte write and
+// read per packet less): SKBuffFromBytes over the packet's first bytes staged in the block's LDS
+// windows (`win`, SkbWinBytes), straight into the LDS slot `d`
+DEV int skb_load_walk(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint32_t *win) {
+    const uint64_t po = kp.pkt_off[i], pre = kp.skb_prefix[i], base = *kp.skb_base;
+    const uint32_t len = kp.pkt_len[i];
+    L.pkt = kp.pkt_data + po;
+    const uint8_t *pkt = L.pkt + SKB_HEADROOM;
+    skb_stage<256u>(win, threadIdx.x, pkt, len);
+    SkbRec &r = *(SkbRec *)d;
+    skb_init(SkbWinBytes<256u>{win, pkt, threadIdx.x}, len, r);
+    return skb_attach(kp, L, r1, d, r.len, pre, base);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -930,6 +967,13 @@ struct Spill {
     uint32_t tail;       // tail call taken
     uint32_t new_prog;
 };
+// a fused counter increment (jit.cpp fusable_inc): one atomic add without return, at the scope of
+// the lane's own plain accesses (its XCD's L2)
+DEV void atomic_add_n(uint8_t *p, uint32_t n, uint64_t v) {
+    if (n == 8) __hip_atomic_fetch_add((GAS uint64_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_add((GAS uint32_t *)p, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // The lane-state half of a deferred slow path (jit.cpp, defer mode; the site has stored the
 // registers, PC, program and steps, and written back the lane value cache): the LDS copies of
 // the process (sk_buff record, stack window) go back to HBM where the interpreter keeps them,

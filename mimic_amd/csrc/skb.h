@@ -88,6 +88,36 @@ struct SkbBytes {
     const uint8_t *p;
     __device__ uint8_t operator[](uint32_t k) const { return p[k]; }
 };
+// the header walk's bytes from a block's LDS windows: thread t's first SKB_WIN bytes of its
+// packet as dwords, dword q at w[q * T + t] (a wave reading the same header offset hits
+// consecutive dwords); bytes past the window (deep tunnels only) come from global memory
+#define SKB_WIN 128u
+template <uint32_t T>
+struct SkbWinBytes {
+    const uint32_t *w;
+    const uint8_t *p;    // the packet in global memory
+    uint32_t t;
+    __device__ uint8_t operator[](uint32_t k) const {
+        if (k < SKB_WIN) return (uint8_t)(w[(k >> 2) * T + t] >> (8 * (k & 3)));
+        return p[k];
+    }
+};
+// stage the window: 16-byte chunks that start inside the packet (one may run into the tailroom)
+template <uint32_t T>
+SKB_DEV void skb_stage(uint32_t *w, uint32_t t, const uint8_t *pkt, uint32_t L) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+#pragma unroll
+    for (uint32_t c = 0; c < SKB_WIN / 16; c++) {
+        if (16 * c < L) {
+            const u32x4u v = *(const u32x4u *)(pkt + 16 * c);
+            w[(4 * c) * T + t] = v.x;
+            w[(4 * c + 1) * T + t] = v.y;
+            w[(4 * c + 2) * T + t] = v.z;
+            w[(4 * c + 3) * T + t] = v.w;
+        }
+    }
+}
+
 template <class B>
 SKB_DEV uint16_t skb_rd16(const B &b, uint32_t k) { return (uint16_t)((b[k] << 8) | b[k + 1]); }
 

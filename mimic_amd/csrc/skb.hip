@@ -17,22 +17,13 @@
 
 // The header walk reads single bytes at data-dependent offsets.  As global byte loads each one is
 // a memory instruction touching 64 scattered lines per wave; instead each thread first copies the
-// first PREP_W bytes of its packet into LDS with 8-byte loads, and the walk reads bytes from there
-// (bytes past the window, deep tunnels only, come from global memory).  LDS layout
-// [dword][thread]: the threads of a wave reading the same header offset hit consecutive dwords.
-#define PREP_W 128u
+// first SKB_WIN bytes of its packet into LDS with 16-byte loads (skb_stage), and the walk reads
+// bytes from there (skb.h SkbWinBytes).
+#define PREP_W SKB_WIN
 #define PREP_T 256u
-struct SkbLdsBytes {
-    const uint32_t *w;   // this block's window words; thread t's dword q at w[q * PREP_T + t]
-    const uint8_t *p;    // the packet in global memory
-    uint32_t t;
-    __device__ uint8_t operator[](uint32_t k) const {
-        if (k < PREP_W) return (uint8_t)(w[(k >> 2) * PREP_T + t] >> (8 * (k & 3)));
-        return p[k];
-    }
-};
 
-// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  The records leave
+// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  rec == nullptr: the
+// footprints only (a JIT kernel that walks the headers itself builds the records in LDS).  The records leave
 // through LDS: each thread puts its record there and the block writes its records (contiguous in
 // rec) with consecutive threads on consecutive 8-byte words -- stored one record per thread,
 // every store instruction of a wave would touch 64 records 160 bytes apart.  Half a block's
@@ -55,19 +46,11 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     if (live) {
         const uint32_t L = pkt_len[i];
         const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
-        // 16-byte chunks that start inside the packet (a chunk may run into the 64-byte tailroom)
-        typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-        for (uint32_t c = 0; c < PREP_W / 16; c++) {
-            if (16 * c >= L) break;
-            const u32x4u v = *(const u32x4u *)(pkt + 16 * c);
-            win[(4 * c) * PREP_T + t] = v.x;
-            win[(4 * c + 1) * PREP_T + t] = v.y;
-            win[(4 * c + 2) * PREP_T + t] = v.z;
-            win[(4 * c + 3) * PREP_T + t] = v.w;
-        }
-        skb_init(SkbLdsBytes{win, pkt, t}, L, r);
+        skb_stage<PREP_T>(win, t, pkt, L);
+        skb_init(SkbWinBytes<PREP_T>{win, pkt, t}, L, r);
         foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
+    if (!rec) return;   // footprints only
     __syncthreads();   // every window read
     const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
     for (uint32_t h = 0; h < 2; h++) {

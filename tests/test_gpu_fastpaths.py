@@ -447,8 +447,76 @@ def test_lds_stack_window(gpu, variant):
     assert len(set(o["r0"].tolist())) > 1000
 
 
+# ---------------------------------------------------------------------------------------------
+# fused counter increments (jit.cpp fusable_inc): ldx / add / stx on a map value as one atomic add,
+# read back at once (the lane must see its own add), 8- and 4-byte (ALU32) forms, an unaligned
+# word (falls back to the three slots), and a register still live after the store (not fused)
+# ---------------------------------------------------------------------------------------------
+def _inc_prog(variant):
+    o8 = 4 if variant == 2 else 0      # variant 2: the 8-byte counter is unaligned -> fallback
+    items = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),
+        A.ldx(4, 3, 6, 4),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 1),
+        A.mov64_imm(0, 1),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(1, 7, 2, 0),
+        A.alu64("and", 7, 3),
+        A.stx(4, 10, -4, 7),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -4),
+        A.ld_map_fd(1, "cnt"),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jeq", 0, 0, "out"),
+        A.ldx(8, 1, 0, o8),
+        A.alu64("add", 1, 1),
+        A.stx(8, 0, o8, 1),
+        A.ldx(8, 8, 0, o8),                # read back after the add
+        A.ldx(4, 5, 0, 8),
+        A.alu32("add", 5, 7),
+        A.stx(4, 0, 8, 5),
+    ]
+    if variant == 3:
+        items += [A.alu64("add", 8, 5, reg=True)]   # r5 read after its store: not fused
+    items += [
+        A.ldx(4, 9, 0, 8),
+        A.alu64("lsh", 8, 32),
+        A.alu64("or", 8, 9, reg=True),
+        A.mov64_reg(0, 8),
+        "out",
+        A.exit_(),
+    ]
+    return _prog("inc", items)
+
+
+def _inc_scenario(variant):
+    mtype = 2 if variant == 1 else 6   # variant 1: a plain (shared) array, one vCPU
+    return Scenario(vcpus=1 if variant == 1 else 4, progs=[_inc_prog(variant)],
+                    maps=[dict(name="cnt", type=mtype, key_size=4, value_size=16, max_entries=4)])
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_fused_counter_increments(gpu, variant):
+    from mimic_amd import jit as J
+
+    sc = _inc_scenario(variant)
+    src = J.kernel_source(*kernel_of(sc))
+    assert src.count("atomic_add_n(") == {0: 2, 1: 2, 2: 2, 3: 1}[variant], src
+    n = 4096
+    buf, off, lens = W.make_packets(n, sizes=(14, 64), weights=(1, 3))
+    cpu = W.schedule_cpu(n, sc.vcpus, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
+    assert len(set(o["r0"].tolist())) > 100
+
+
 def jit_kernels():
     ks = [kernel_of(Scenario(vcpus=4, progs=[_stack_window_prog(v)])) for v in range(4)]
+    ks += [kernel_of(_inc_scenario(v)) for v in range(4)]
     ks += [kernel_of(sc) for sc in _escape_scenarios()]
     ks += [kernel_of(_hash_scenario(*c)) for c in HASH_CASES]
     ks += [kernel_of(_tail_scenario(b)) for b in (0, 3)]
