@@ -119,7 +119,6 @@ struct mimic_vm {
     hipEvent_t kp_ev[KP_SLOTS] = {};
     bool kp_used[KP_SLOTS] = {};
     int kp_next = 0, kp_last = -1;
-    bool kp_pending = false;   // kernels launched with slot kp_last since its event was last recorded
     hipStream_t kp_last_stream = nullptr;
     // host-resident pipeline (mimic_run_xdp_host): NB rotating device staging slots
     // (packet window, its descriptors, its results); launch parameters are copied on the H2D
@@ -151,7 +150,8 @@ struct mimic_vm {
     size_t skb_cap = 0, skb_scan_cap = 0;
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
     hipStream_t skb_stream = nullptr;
-    bool skb_release_pending = false;   // mimic_skb_release ran and skb_stream may still be busy
+    bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
+    hipEvent_t skb_ev = nullptr;
 };
 
 
@@ -184,21 +184,11 @@ static int kp_slot(mimic_vm *vm, const KParams &kp, hipStream_t st, const KParam
     }
     int slot = vm->kp_last;
     if (slot < 0 || st != vm->kp_last_stream || memcmp(&vm->h_kp[slot], &kp, sizeof kp) != 0) {
-        // The slot we leave: its event goes behind everything enqueued so far on its stream
-        // (which includes its last kernel).  Recorded here, once per slot switch, instead of after
-        // every launch (an event between back-to-back kernels of one stream widens the gap between
-        // them).  When the caller moved to another stream, the old one may be gone already: wait
-        // for the device instead, after which no slot is in use.
-        if (vm->kp_last >= 0 && vm->kp_pending) {
-            if (st == vm->kp_last_stream) {
-                HIP_OK(vm, hipEventRecord(vm->kp_ev[vm->kp_last], st));
-                vm->kp_used[vm->kp_last] = true;
-            } else {
-                HIP_OK(vm, hipDeviceSynchronize());
-                for (auto &u : vm->kp_used) u = false;
-            }
-            vm->kp_pending = false;
-        }
+        // Every launch from a slot records the slot's event on its own stream right behind the
+        // kernel (run_xdp_impl): a slot is reused once that event has passed, whatever stream the
+        // caller uses next -- no device-wide wait when the caller changes streams, no reference to
+        // a stream the caller may have destroyed.  Only the interpreter and MIMIC_JIT_KARG=0 JIT
+        // kernels read their parameters from a slot; the hot JIT kernels take them by value.
         slot = vm->kp_next;
         vm->kp_next = (slot + 1) % mimic_vm::KP_SLOTS;
         if (vm->kp_used[slot]) HIP_OK(vm, hipEventSynchronize(vm->kp_ev[slot]));  // its last kernel is done
@@ -623,6 +613,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (vm->s_d2h) hipStreamDestroy(vm->s_d2h);
     for (auto &e : vm->kp_ev)
         if (e) hipEventDestroy(e);
+    if (vm->skb_ev) hipEventDestroy(vm->skb_ev);
     if (vm->stream) hipStreamDestroy(vm->stream);
     delete vm;
 }
@@ -1178,14 +1169,20 @@ int mimic_skb_release(mimic_vm *vm) {
     // No host wait here: the next sk_buff batch on the same stream is ordered behind the last one
     // anyway (a wait would leave the GPU idle for a host round trip per batch); anything else that
     // needs the sk_buff work finished calls skb_settle() first.
-    vm->skb_release_pending = vm->skb_stream != nullptr;
+    // an engine-owned event behind the released batches: the caller may destroy its stream after this
+    if (vm->skb_stream) {
+        if (!vm->skb_ev) HIP_OK(vm, hipEventCreateWithFlags(&vm->skb_ev, hipEventDisableTiming));
+        HIP_OK(vm, hipEventRecord(vm->skb_ev, vm->skb_stream));
+        vm->skb_stream = nullptr;
+        vm->skb_release_pending = true;
+    }
     vm->skb_leaked = false;
     return 0;
 }
 
 // wait for the sk_buff batches mimic_skb_release let go of (map / program loads, xdp_md batches)
 static int skb_settle(mimic_vm *vm) {
-    if (vm->skb_release_pending && vm->skb_stream) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
+    if (vm->skb_release_pending) HIP_OK(vm, hipEventSynchronize(vm->skb_ev));
     vm->skb_release_pending = false;
     return 0;
 }
@@ -1200,6 +1197,8 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
                        bool records = true) {
     const uint32_t n = b->n;
     if (vm->skb_stream && vm->skb_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
+    // batches released on a stream the caller may have destroyed since: ordered through their event
+    if (vm->skb_release_pending) HIP_OK(vm, hipStreamWaitEvent(st, vm->skb_ev, 0));
     if (n > vm->skb_cap || !vm->d_skb_state) {
         HIP_OK(vm, hipStreamSynchronize(st));
         hipFree(vm->d_skb_rec);
@@ -1507,7 +1506,8 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         if (jit && ji.defer && mimic_launch_xdp_resume(&kp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
-        vm->kp_pending = true;   // the slot's event is recorded when kp_slot leaves it
+        HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));   // the slot is free again once this passes
+        vm->kp_used[slot] = true;
     }
     vm->last_lanes = lanes;
     vm->last_stream = st;

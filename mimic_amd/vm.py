@@ -1027,17 +1027,31 @@ class ProcessPool:
             self._run(jobs)
 
     def _run(self, jobs) -> None:
+        """One micro-batch: vCPUs round-robin, one launch per (program, context kind).  A vCPU runs
+        its jobs in enqueue order (a worker takes them from the channel in order, vm.go:548-573):
+        when the round-robin counter wraps inside the batch and a vCPU would get a job of a second
+        group, the jobs so far run first."""
         V = self.vm.settings.vcpus
         groups: Dict[Tuple[int, bool], list] = {}
+        owner: Dict[int, Tuple[int, bool]] = {}   # vCPU -> the group its jobs of this segment are in
         for job in jobs:
             err = job.Context.Err() if job.Context is not None else None
             if err is not None:
                 self._handoff(job, MimicError(err))
                 continue
-            job.Process.SetCPUID(self._next_cpu)
-            self._next_cpu = (self._next_cpu + 1) % V
+            cpu = self._next_cpu
             skb = isinstance(job.Process.Context, LinuxContextSKBuff)
-            groups.setdefault((job.Process.prog_id, skb), []).append(job)
+            key = (job.Process.prog_id, skb)
+            if owner.get(cpu, key) != key:
+                self._run_groups(groups)
+                groups, owner = {}, {}
+            job.Process.SetCPUID(cpu)
+            self._next_cpu = (cpu + 1) % V
+            owner[cpu] = key
+            groups.setdefault(key, []).append(job)
+        self._run_groups(groups)
+
+    def _run_groups(self, groups) -> None:
         for (pid, skb), js in groups.items():
             try:
                 self._launch(pid, skb, js)

@@ -20,8 +20,20 @@ def _sc(V):
     return Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
 
 
+def _order_sc(V):
+    def prog(name, op):
+        return (name, *A.assemble([
+            A.st(4, 10, -4, 0), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, "c"),
+            A.call(A.FN_MAP_LOOKUP_ELEM), A.jmp("jeq", 0, 0, "out"),
+            A.ldx(8, 1, 0, 0), op, A.stx(8, 0, 0, 1), A.mov64_reg(0, 1), A.exit_(),
+            "out", A.mov64_imm(0, 0), A.exit_()]))
+
+    return Scenario(vcpus=V, maps=[dict(name="c", type=6, key_size=4, value_size=8, max_entries=1)],
+                    progs=[prog("inc", A.alu64("add", 1, 1)), prog("tri", A.alu64("mul", 1, 3))])
+
+
 def jit_kernels():
-    return [kernel_of(_sc(1))]
+    return [kernel_of(_sc(1)), kernel_of(_order_sc(2))]
 
 
 @pytest.mark.parametrize("backlog", [16, 4096])
@@ -88,4 +100,40 @@ def test_pool_api_rules_and_errors(gpu):
     assert ev.wait(10)
     msgs = sorted(str(e) for e in errs)
     assert "context canceled" in msgs[0] and "PANIC_DIV0" in msgs[1]
+    vm.close()
+
+
+def test_pool_keeps_enqueue_order_per_vcpu_across_programs(gpu):
+    """Jobs of two programs that update one per-CPU counter non-commutatively (A: +1, B: *3),
+    enqueued in a pattern that wraps the round-robin vCPU counter inside a micro-batch: every job's
+    R0 (the counter after it) equals a sequential run of each vCPU's jobs in enqueue order."""
+    V = 2
+    sc = _order_sc(V)
+    vm, maps, pids = build_engine(sc)
+    pool = vm.GetProcessPool()
+    pool.max_batch = 7
+    pool.Start(64)
+    got = {}
+    mu = threading.Lock()
+
+    def handoff(proc, err):
+        with mu:
+            got[proc.idx] = (proc.Registers.R0, proc.CPUID(), err)
+        proc.Cleanup()
+
+    pattern = [0, 0, 1, 0, 1, 1, 0, 1, 0, 0, 0, 1, 1, 1, 0, 1] * 4
+    for i, k in enumerate(pattern):
+        proc = vm.NewProcess(pids[k], M.LinuxContextXDP(Packet=bytes(64)))
+        proc.idx = i
+        pool.Enqueue(M.ProcessPoolJob(proc, None, handoff))
+    pool.Stop()
+    t0 = time.time()
+    while len(got) < len(pattern) and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert len(got) == len(pattern) and all(g[2] is None for g in got.values())
+    val = [0] * V
+    for i, k in enumerate(pattern):
+        c = got[i][1]
+        val[c] = val[c] + 1 if k == 0 else val[c] * 3
+        assert got[i][0] == val[c], (i, got[i], val)
     vm.close()
