@@ -116,6 +116,8 @@ class Gen {
         skb_lds_knob = !(sl && sl[0] == '0');
         const char *sw = getenv("MIMIC_JIT_SKBWALK");   // 1: the kernel builds its sk_buff records (measured slower)
         skb_walk_knob = sw && sw[0] == '1';
+        const char *sml = getenv("MIMIC_JIT_SMLDS");
+        sm_lds_knob = !(sml && sml[0] == '0');
         const char *ic = getenv("MIMIC_JIT_INC");   // 0: counter increments as three slots
         inc_knob = !(ic && ic[0] == '0');
         const char *hf = getenv("MIMIC_JIT_HASH");   // 0: hash-map lookups always through the generic helper
@@ -184,6 +186,7 @@ class Gen {
     bool skb_walk_knob = false;
     bool skb_walk = false;
     bool inc_knob = true;      // MIMIC_JIT_INC=0: no fused counter increments (fusable_inc)
+    bool sm_lds_knob = true;   // MIMIC_JIT_SMLDS=0: stack validity masks in VGPRs in defer mode too
     static constexpr uint32_t kSrecQ = 21;   // 8-byte words per LDS record slot (SkbRec is 20)
     int karg = 2;              // MIMIC_JIT_KARG: 2 launch parameters by value in the kernarg segment, read
                                // through an opaque constant-space pointer; 1 the same, plain; 0 a
@@ -291,6 +294,7 @@ class Gen {
                 }
             if (any) E.line("#define MIMIC_LDS_STACK_Q %u", lds_stack_q);
         }
+        if (defer_mode && sm_lds_knob) E.line("#define MIMIC_SM_LDS 1");
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         {   // no program of the set updates or deletes: hash tables are read-only in every launch
@@ -476,7 +480,7 @@ class Gen {
             if (stage && fast_paths) E.line("    const uint32_t W_ = win_stage(pwin_, tl_, L.pkt, L.M);");
             E.line("    uint64_t r1 = P + L.M + 1;");
         }
-        E.line("    L.sm0 = 0; L.sm1 = 0; L.xdp_dirty = 0; L.nframes = 0; L.tailcalls = 0; L.t_lo = 0; L.t_n = 0; L.t_ptr = nullptr;");
+        E.line("    SM0(L) = 0; SM1(L) = 0; L.xdp_dirty = 0; L.nframes = 0; L.tailcalls = 0; L.t_lo = 0; L.t_n = 0; L.t_ptr = nullptr;");
         E.line("    uint64_t r0 = 0, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0, r9 = 0;");
         E.line("    uint64_t r10 = kp.static_next + kp.frame_size;");
         E.line("    uint32_t steps = 0;");

@@ -228,6 +228,17 @@ DEV void priv_store(const KParams &kp, uint32_t lane, uint32_t o, uint32_t n, ui
 // first write to a word stores the whole zero-extended word.
 // ---------------------------------------------------------------------------------------
 #define STK_FINE 512u
+// JIT kernels with deferred slow paths keep the validity masks in LDS (MIMIC_SM_LDS): a deferral
+// site would otherwise hold the two 64-bit masks live in VGPRs through the whole program
+// (measured on cfg 5's chain: +50 VGPRs)
+#ifdef MIMIC_SM_LDS
+__shared__ uint64_t mimic_sm_[2 * 256];
+#define SM0(L) mimic_sm_[threadIdx.x]
+#define SM1(L) mimic_sm_[256 + threadIdx.x]
+#else
+#define SM0(L) (L).sm0
+#define SM1(L) (L).sm1
+#endif
 // LDS stack window (JIT kernels that define MIMIC_LDS_STACK_Q, jit.cpp): the stack bytes
 // [256 - 8Q, 256) -- the top of frame 0, where R10 - k lands in programs without BPF-to-BPF
 // calls -- live in LDS instead of the lane's private memory in HBM, word q of thread t at
@@ -243,7 +254,7 @@ DEV bool stk_in_lds(uint32_t) { return false; }
 DEV uint64_t &stk_lw(uint32_t) { __builtin_trap(); }
 #endif
 DEV bool stk_valid(const KParams &kp, const Lane &L, uint32_t o) {
-    return o < STK_FINE ? ((L.sm0 >> (o >> 3)) & 1) : ((L.sm1 >> ((o - STK_FINE) >> kp.chunk_shift)) & 1);
+    return o < STK_FINE ? ((SM0(L) >> (o >> 3)) & 1) : ((SM1(L) >> ((o - STK_FINE) >> kp.chunk_shift)) & 1);
 }
 // the whole 8-byte word holding stack byte o (o & ~7) := w
 DEV void stk_word_set(const KParams &kp, const Lane &L, uint32_t o, uint64_t w) {
@@ -258,16 +269,16 @@ DEV uint32_t stk_byte(const KParams &kp, const Lane &L, uint32_t o) {
 DEV void stk_touch(const KParams &kp, Lane &L, uint32_t o) {
     if (o < STK_FINE) {
         const uint32_t q = o >> 3;
-        if (!((L.sm0 >> q) & 1)) {
+        if (!((SM0(L) >> q) & 1)) {
             stk_word_set(kp, L, q << 3, 0);
-            L.sm0 |= 1ull << q;
+            SM0(L) |= 1ull << q;
         }
     } else {
         const uint32_t c = (o - STK_FINE) >> kp.chunk_shift;
-        if (!((L.sm1 >> c) & 1)) {
+        if (!((SM1(L) >> c) & 1)) {
             const uint32_t q0 = (STK_FINE + (c << kp.chunk_shift)) >> 3, nq = (1u << kp.chunk_shift) >> 3;
             for (uint32_t q = 0; q < nq; q++) *gp((uint64_t *)priv_b(kp, L.lane, (q0 + q) << 3)) = 0;
-            L.sm1 |= 1ull << c;
+            SM1(L) |= 1ull << c;
         }
     }
 }
@@ -291,10 +302,10 @@ DEV void stack_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_
     if ((o & 7) + n <= 8) {
         const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
         const uint32_t sh = 8 * (o & 7);
-        if (o < STK_FINE && !((L.sm0 >> (o >> 3)) & 1)) {
+        if (o < STK_FINE && !((SM0(L) >> (o >> 3)) & 1)) {
             // first write to this word: store the whole word, zero-extended around the value
             stk_word_set(kp, L, o, (v & m) << sh);
-            L.sm0 |= 1ull << (o >> 3);
+            SM0(L) |= 1ull << (o >> 3);
             return;
         }
         stk_touch(kp, L, o);
@@ -992,8 +1003,8 @@ DEV void defer_finish(const KParams &kp, const Lane &L, uint32_t g, uint32_t i, 
         if (stk_valid(kp, L, o)) *gp((uint64_t *)priv_b(kp, L.lane, o)) = stk_lw(o);
     }
 #endif
-    d->sm0 = L.sm0;
-    d->sm1 = L.sm1;
+    d->sm0 = SM0(L);
+    d->sm1 = SM1(L);
     d->xdp_dirty = L.xdp_dirty;
     d->nframes = L.nframes;
     d->tailcalls = L.tailcalls;

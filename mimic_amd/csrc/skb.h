@@ -335,6 +335,7 @@ SKB_DEV int skb_walk(const B &pkt, uint32_t L, SkbRec &r) {
 // r.snap[k] = packet byte b + k (0 at or past L), k < SKB_SNAP
 template <class B>
 SKB_DEV void skb_snap(const B &pkt, uint32_t b, uint32_t L, SkbRec &r) {
+#pragma unroll
     for (uint32_t k = 0; k < SKB_SNAP; k++) r.snap[k] = b + k < L ? pkt[b + k] : 0;
 }
 // from the LDS window: 10 dwords cut out of 11 with funnel shifts instead of 40 byte reads (the
@@ -342,6 +343,7 @@ SKB_DEV void skb_snap(const B &pkt, uint32_t b, uint32_t L, SkbRec &r) {
 template <uint32_t T>
 SKB_DEV void skb_snap(const SkbWinBytes<T> &pkt, uint32_t b, uint32_t L, SkbRec &r) {
     if (b + SKB_SNAP + 4 > SKB_WIN) {
+#pragma unroll
         for (uint32_t k = 0; k < SKB_SNAP; k++) r.snap[k] = b + k < L ? pkt[b + k] : 0;
         return;
     }
@@ -351,7 +353,7 @@ SKB_DEV void skb_snap(const SkbWinBytes<T> &pkt, uint32_t b, uint32_t L, SkbRec 
 #pragma unroll
     for (uint32_t k = 0; k < SKB_SNAP / 4; k++) {
         const uint32_t hi = pkt.w[(q0 + k + 1) * T + pkt.t];
-        uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+        uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh >> 3);
         const int32_t n = valid - 4 * (int32_t)k;
         v = n >= 4 ? v : n <= 0 ? 0u : (v & ((1u << (8 * n)) - 1u));
         __builtin_memcpy(&r.snap[4 * k], &v, 4);
@@ -359,19 +361,150 @@ SKB_DEV void skb_snap(const SkbWinBytes<T> &pkt, uint32_t b, uint32_t L, SkbRec 
     }
 }
 
+// the record before the walk: zero, make(net.IP, 4/16) capacities, time.Time{}
+SKB_DEV void skb_rec_reset(SkbRec &r) {
+    uint64_t *w = (uint64_t *)&r;
+    for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) w[q] = 0;
+    r.ip[0].n = 4; r.ip[1].n = 4; r.ip[2].n = 16; r.ip[3].n = 16;
+    r.tstamp = SKB_TSTAMP_ZERO;
+}
+// the one IP slice window programs can read (IPv4: src..dst+11, IPv6: src..dst+23)
+SKB_DEV uint32_t skb_snap_base(const SkbRec &r) {
+    return r.family == 10 && r.ip[2].kind == 2 ? r.ip[2].off : (r.ip[0].kind == 2 ? r.ip[0].off : 0u);
+}
+
 // SKBuffFromBytes + the parts of LinuxContextSKBuff.Load that do not depend on addresses
 template <class B>
 SKB_DEV void skb_init(const B &pkt, uint32_t L, SkbRec &r) {
-    uint64_t *w = (uint64_t *)&r;
-    for (uint32_t q = 0; q < sizeof(SkbRec) / 8; q++) w[q] = 0;
-    r.ip[0].n = 4; r.ip[1].n = 4; r.ip[2].n = 16; r.ip[3].n = 16;   // make(net.IP, 4/16)
-    r.tstamp = SKB_TSTAMP_ZERO;
+    skb_rec_reset(r);
     const int err = skb_walk(pkt, L, r);
     r.len = L | (err ? SKB_LOAD_FAILED : 0u);
-    // the one IP slice window programs can read (IPv4: src..dst+11, IPv6: src..dst+23)
-    uint32_t b = r.family == 10 && r.ip[2].kind == 2 ? r.ip[2].off : (r.ip[0].kind == 2 ? r.ip[0].off : 0u);
+    const uint32_t b = skb_snap_base(r);
     r.snap_base = b;
     skb_snap(pkt, b, L, r);
+}
+
+// ---------------------------------------------------------------------------------------
+// The common frames without a walk: Ethernet + IPv4 (no options) / IPv6 (no extension headers)
+// + TCP / UDP (no tunnel port), or a non-IP EtherType, decoded straight from the packet's first
+// 128 bytes held in registers (w[q] = bytes 4q..4q+3) at constant offsets -- the same decisions
+// skb_walk makes for these frames, in the same order.  Everything else (802.3 / LLC, VLAN tags,
+// IPv4 options, IPv6 extension headers, IP-in-IP, UDP tunnels) returns false: the general walk
+// decodes it.  No frame taken here fails Load (only a second layer of one kind does).
+// ---------------------------------------------------------------------------------------
+#define SKW8(k) ((w[(k) >> 2] >> (8 * ((k) & 3))) & 0xffu)
+#define SKW16(k) ((SKW8(k) << 8) | SKW8((k) + 1))
+template <uint32_t O>   // the transport header's offset: 34 (IPv4) or 54 (IPv6)
+SKB_DEV bool skb_fast_l4(const uint32_t *w, uint32_t t, uint32_t len, SkbRec &r) {
+    if (len == 0) return true;
+    if (t == 6) {            // TCP: ports when the header is complete
+        if (len >= 20) {
+            r.sport = SKW16(O);
+            r.dport = SKW16(O + 2);
+        }
+        return true;
+    }
+    if (t == 4 || t == 41) return false;   // IP in IP
+    if (t != 17) return true;
+    if (len < 8) return true;
+    r.sport = SKW16(O);
+    r.dport = SKW16(O + 2);
+    const uint32_t ulen = SKW16(O + 4);
+    uint32_t plen;
+    if (ulen >= 8) plen = (ulen > len ? len : ulen) - 8;
+    else if (ulen == 0) plen = len - 8;
+    else return true;
+    if (plen == 0) return true;
+    uint32_t port = r.sport;
+    switch (r.dport) {
+    case 53: case 123: case 4789: case 67: case 68: case 546: case 547: case 5060: case 6343:
+    case 6081: case 3784: case 2152: case 623: case 1812:
+        port = r.dport;
+        break;
+    default:
+        break;
+    }
+    return !(port == 4789 || port == 6081 || port == 2152);   // tunnels decode another layer
+}
+SKB_DEV bool skb_fast(const uint32_t *w, uint32_t L, SkbRec &r) {
+    if (L < 14) return true;                       // no Ethernet layer
+    const uint32_t t = SKW16(12);
+    if (t < 0x0600 || t == 0x8100 || t == 0x88a8 || t == 0x6558) return false;
+    r.protocol = (uint16_t)t;
+    if (L == 14 || (t != 0x0800 && t != 0x86DD)) return true;
+    const uint32_t len = L - 14, v = SKW8(14) >> 4;
+    if (v == 4) {
+        r.family = 2;
+        if (len < 20) {
+            r.ip[0].kind = 1;
+            r.ip[1].kind = 1;
+            return true;
+        }
+        r.ip[0].kind = 2; r.ip[0].off = 26;
+        r.ip[1].kind = 2; r.ip[1].off = 30;
+        const uint32_t ihl = SKW8(14) & 0x0f, ff = SKW16(20);
+        uint32_t tl = SKW16(16);
+        if (tl == 0) tl = len;
+        if (tl < 20 || ihl < 5 || ihl * 4 > tl) return true;
+        uint32_t dl = len;
+        if (len > tl) dl = tl;
+        else if (len < tl && ihl * 4 > len) return true;
+        if (ihl != 5) return false;                // options
+        if ((ff & 0x2000) || (ff & 0x1fff)) return true;
+        return skb_fast_l4<34>(w, SKW8(23), dl - 20, r);
+    }
+    if (v == 6) {
+        r.family = 10;
+        if (len < 40) {
+            r.ip[2].kind = 1;
+            r.ip[3].kind = 1;
+            return true;
+        }
+        r.ip[2].kind = 2; r.ip[2].off = 22;
+        r.ip[3].kind = 2; r.ip[3].off = 38;
+        const uint32_t next = SKW8(20), plen = SKW16(18);
+        if (next == 0 || plen == 0) return true;
+        uint32_t pl = len - 40;
+        if (pl > plen) pl = plen;
+        if (next == 43 || next == 60) return false;   // extension headers
+        if (next == 44) return true;                  // a fragment
+        return skb_fast_l4<54>(w, next, pl, r);
+    }
+    return true;
+}
+// r.snap from the registers for a constant base B (0, 22 or 26), bytes at or past L zero
+template <uint32_t B>
+SKB_DEV void skb_snap_regs(const uint32_t *w, uint32_t L, SkbRec &r) {
+    const int32_t valid = (int32_t)L - (int32_t)B;
+#pragma unroll
+    for (uint32_t k = 0; k < SKB_SNAP / 4; k++) {
+        const uint32_t q = (B >> 2) + k;
+        uint32_t v = __builtin_amdgcn_alignbyte(w[q + 1], w[q], B & 3);   // v_alignbyte: stays in registers
+        const int32_t n = valid - 4 * (int32_t)k;
+        v = n >= 4 ? v : n <= 0 ? 0u : (v & ((1u << (8 * n)) - 1u));
+        __builtin_memcpy(&r.snap[4 * k], &v, 4);
+    }
+}
+#undef SKW8
+#undef SKW16
+
+// skb_init over the packet's first SKB_WIN bytes in registers (w), the general walk through the
+// block's LDS window (win, column t) for the frames skb_fast does not take
+template <uint32_t T>
+SKB_DEV void skb_init_regs(const uint32_t *w, uint32_t *win, uint32_t t, const uint8_t *pkt, uint32_t L, SkbRec &r) {
+    skb_rec_reset(r);
+    if (skb_fast(w, L, r)) {
+        r.len = L;
+        const uint32_t b = skb_snap_base(r);
+        r.snap_base = b;
+        if (b == 26) skb_snap_regs<26>(w, L, r);
+        else if (b == 22) skb_snap_regs<22>(w, L, r);
+        else skb_snap_regs<0>(w, L, r);
+        return;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < SKB_WIN / 4; q++) win[q * T + t] = w[q];
+    skb_init(SkbWinBytes<T>{win, pkt, t}, L, r);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -46,8 +46,21 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     if (live) {
         const uint32_t L = pkt_len[i];
         const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
-        skb_stage<PREP_T>(win, t, pkt, L);
-        skb_init(SkbWinBytes<PREP_T>{win, pkt, t}, L, r);
+        // the first 128 bytes into registers (16-byte chunks that start inside the packet; one may
+        // run into the 64-byte tailroom); common frames decode from there (skb_fast), the rest
+        // through this thread's LDS window
+        typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+        uint32_t w[SKB_WIN / 4];
+#pragma unroll
+        for (uint32_t c = 0; c < SKB_WIN / 16; c++) {
+            u32x4u v = {0, 0, 0, 0};
+            if (16 * c < L) v = *(const u32x4u *)(pkt + 16 * c);
+            w[4 * c] = v.x;
+            w[4 * c + 1] = v.y;
+            w[4 * c + 2] = v.z;
+            w[4 * c + 3] = v.w;
+        }
+        skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
         foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
     if (!rec) return;   // footprints only
