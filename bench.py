@@ -50,7 +50,9 @@ CONFIGS = {
                              workload="cfg4 per-GPU shard, inserting: 2M IMIX xdp_md into a FRESH shared hash map "
                                       "K=16 S=8 E=131072 every step (map reset in the timed region), ~118K inserts "
                                       "per batch"),
-    "skb": dict(kind="skb", packets=1 << 20, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 16,
+    # V = 128K: the chain kernel holds 2 waves per SIMD (242 VGPRs), so 131 072 lanes fill the 1 024
+    # SIMDs once (64K: 1 wave, 0.553 ms; 256K: two rounds, 0.428 ms; 128K: 0.409 ms per step)
+    "skb": dict(kind="skb", packets=1 << 20, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 17,
                 workload="cfg5: 1M IMIX sk_buff contexts, 5-program tail-call chain (~230 slots): __sk_buff "
                          "fields, LD_ABS/IND parse, hash flow lookups, per-CPU counters"),
 }

@@ -904,6 +904,8 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
     const uint64_t ka = *kp.skb_base + kp.skb_prefix[i];
     if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
+    if (!attach_only)   // the writable state at Load (the prep kernel writes the derived words only)
+        for (uint32_t q = 0; q < 8; q++) ((uint64_t *)rec)[SKB_DERIVED_Q + q] = skb_writable_word(q);
     L.rec = rec;
     L.ka = (uint32_t)ka;
     L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
@@ -936,13 +938,14 @@ DEV int skb_attach(const KParams &kp, Lane &L, uint64_t &r1, uint64_t *d, uint32
 // record length first and the rest after it), then the record goes to LDS.
 DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d) {
     const GAS uint64_t *s = (const GAS uint64_t *)(kp.skb_rec + i);
-    constexpr uint32_t NQ = sizeof(SkbRec) / 8;
-    uint64_t w[NQ];
+    uint64_t w[SKB_DERIVED_Q];
 #pragma unroll
-    for (uint32_t q = 0; q < NQ; q++) w[q] = s[q];
+    for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) w[q] = s[q];
     const uint64_t po = kp.pkt_off[i], pre = kp.skb_prefix[i], base = *kp.skb_base;
 #pragma unroll
-    for (uint32_t q = 0; q < NQ; q++) d[q] = w[q];
+    for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) d[q] = w[q];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) d[SKB_DERIVED_Q + q] = skb_writable_word(q);
     L.pkt = kp.pkt_data + po;
     return skb_attach(kp, L, r1, d, (uint32_t)w[0], pre, base);
 }

@@ -67,6 +67,14 @@ struct SkbRec {  // 160 bytes
 };
 
 #define SKB_TSTAMP_ZERO (-62135596800ll)   // time.Time{}.Unix()
+// The record's first SKB_DERIVED_Q words are what the header walk derives; the rest is the
+// writable state, the same constants for every process at Load (zeros, tstamp = time.Time{}).
+// The prep kernel writes only the derived words; whoever loads the process sets the rest
+// (skb_load: in HBM; the JIT: in its LDS slot).
+#define SKB_DERIVED_Q 12u
+static_assert(__builtin_offsetof(SkbRec, mark) == 8 * SKB_DERIVED_Q, "writable state follows the derived words");
+static_assert(__builtin_offsetof(SkbRec, tstamp) == 8 * (SKB_DERIVED_Q + 2), "tstamp is word 14");
+static_assert(sizeof(SkbRec) == 8 * (SKB_DERIVED_Q + 8), "8 writable words");
 
 #ifndef SKB_DEV
 #define SKB_DEV static __device__ __forceinline__
@@ -77,6 +85,10 @@ struct SkbRec {  // 160 bytes
 #ifndef SKB_COLD
 #define SKB_COLD static __device__ __noinline__
 #endif
+
+SKB_DEV uint64_t skb_writable_word(uint32_t q) {   // word SKB_DERIVED_Q + q of a loaded record
+    return q == 2 ? (uint64_t)SKB_TSTAMP_ZERO : 0ull;
+}
 
 struct SkbRes {
     uint64_t v;
@@ -502,6 +514,10 @@ SKB_DEV void skb_init_regs(const uint32_t *w, uint32_t *win, uint32_t t, const u
         else skb_snap_regs<0>(w, L, r);
         return;
     }
+#ifdef MIMIC_PREP_FAST_ONLY   // measurement only (tools/prep_probe.py): no general walk
+    r.len = L;
+    return;
+#endif
 #pragma unroll
     for (uint32_t q = 0; q < SKB_WIN / 4; q++) win[q * T + t] = w[q];
     skb_init(SkbWinBytes<T>{win, pkt, t}, L, r);

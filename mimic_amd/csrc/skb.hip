@@ -23,15 +23,20 @@
 #define PREP_T 256u
 
 // packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  rec == nullptr: the
-// footprints only (a JIT kernel that walks the headers itself builds the records in LDS).  The records leave
-// through LDS: each thread puts its record there and the block writes its records (contiguous in
-// rec) with consecutive threads on consecutive 8-byte words -- stored one record per thread,
-// every store instruction of a wave would touch 64 records 160 bytes apart.  Half a block's
-// records at a time, in the windows' 32 KiB (5 blocks per CU instead of 4 with 40 KiB).
+// footprints only (a JIT kernel that walks the headers itself builds the records in LDS).  Only
+// the records' derived words are written (skb.h SKB_DERIVED_Q: the writable state is constant at
+// Load and set by whoever loads the process).  They leave through LDS: each thread puts its
+// words there and the block writes them with consecutive threads on consecutive 8-byte words --
+// stored one record per thread, every store instruction of a wave would touch 64 records 160
+// bytes apart.  The block's derived words (24 KiB) fit the windows' 32 KiB.
 #define PREP_RQ (sizeof(SkbRec) / 8)
-#define PREP_HALF (PREP_T / 2)
+#ifdef MIMIC_PREP_PLAIN   // measurement: cached record stores
+#define PREP_ST(p, v) (*(p) = (v))
+#else   // records are streamed out: non-temporal stores
+#define PREP_ST(p, v) __builtin_nontemporal_store((v), (p))
+#endif
 static_assert(sizeof(SkbRec) % 8 == 0, "SkbRec is copied as 8-byte words");
-static_assert(PREP_RQ * PREP_HALF <= (PREP_W / 8) * PREP_T, "half the records fit the window area");
+static_assert(SKB_DERIVED_Q * PREP_T <= (PREP_W / 8) * PREP_T, "a block's derived words fit the window area");
 extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
@@ -60,24 +65,51 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
             w[4 * c + 2] = v.z;
             w[4 * c + 3] = v.w;
         }
+#ifdef MIMIC_PREP_NOWALK   // measurement only (tools/prep_probe.py): loads and footprints, no decode
+        r.len = w[0] == 0x12345678u ? SKB_LOAD_FAILED : L;
+#else
         skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
+#endif
         foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
     if (!rec) return;   // footprints only
-    __syncthreads();   // every window read
-    const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
-    for (uint32_t h = 0; h < 2; h++) {
-        if (live && t / PREP_HALF == h) {
-            const uint64_t *rw = (const uint64_t *)&r;
-            for (uint32_t q = 0; q < PREP_RQ; q++) area[(t % PREP_HALF) * PREP_RQ + q] = rw[q];
-        }
-        __syncthreads();
-        const uint32_t first = h * PREP_HALF;
-        const uint32_t words = cnt > first ? (cnt - first < PREP_HALF ? cnt - first : PREP_HALF) * PREP_RQ : 0u;
-        uint64_t *dst = (uint64_t *)(rec + i0 + first);
-        for (uint32_t w = t; w < words; w += PREP_T) dst[w] = area[w];
-        __syncthreads();
+#ifdef MIMIC_PREP_DIRECT   // measurement: each thread writes its own derived words (16-byte stores)
+    if (live) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        const u64x2 *rv = (const u64x2 *)&r;
+        u64x2 *o = (u64x2 *)(rec + i);
+#pragma unroll
+        for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) PREP_ST(o + u, rv[u]);
     }
+    return;
+#else
+    __syncthreads();   // every window read
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 *area2 = (u64x2 *)area;
+    if (live) {
+        const u64x2 *rv = (const u64x2 *)&r;
+#pragma unroll
+        for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) area2[t * (SKB_DERIVED_Q / 2) + u] = rv[u];
+    }
+    __syncthreads();
+    // the block's records are contiguous in rec: 16-byte units, consecutive threads on consecutive
+    // units (the writable words between the records are not written)
+    const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
+    u64x2 *dst = (u64x2 *)(rec + i0);
+    constexpr uint32_t DU = SKB_DERIVED_Q / 2, RU = sizeof(SkbRec) / 16;
+    for (uint32_t w = t; w < cnt * DU; w += PREP_T) {
+        const uint32_t k = w / DU, u = w - k * DU;
+        PREP_ST(dst + (size_t)k * RU + u, area2[w]);
+    }
+#endif
+}
+
+// the prep kernel alone (tools/prep_probe.py)
+extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
+                                   SkbRec *rec, uint64_t *foot, hipStream_t st) {
+    hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
+                       rec, foot);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // state[0] = the VM's next leak address, state[1] = this batch's leak base

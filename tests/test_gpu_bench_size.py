@@ -187,7 +187,7 @@ def test_cfg5_skb_chain_bench_size_exact(gpu):
     from harness import run_oracle_skb
 
     wl, n, V = _workload("skb")
-    assert n == 1 << 20 and V == 1 << 16
+    assert n == 1 << 20 and V == 1 << 17
     sc = _scenario(wl, V)
     from mimic_amd import workloads as W
 
