@@ -295,6 +295,7 @@ class Gen {
             if (any) E.line("#define MIMIC_LDS_STACK_Q %u", lds_stack_q);
         }
         if (defer_mode && sm_lds_knob) E.line("#define MIMIC_SM_LDS 1");
+        if (const char *rm = getenv("MIMIC_JIT_ROOMS")) E.line("#define MIMIC_ROOMS_MODE %d", atoi(rm));   // measurement knob
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         {   // no program of the set updates or deletes: hash tables are read-only in every launch

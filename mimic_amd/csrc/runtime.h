@@ -871,11 +871,18 @@ DEV int ld_abs(const KParams &kp, const Lane &L, uint64_t r6, uint32_t x, uint32
 // an earlier run of the buffer, or the caller's bytes): the common case writes nothing, and the
 // reads share their lines with the packet's first bytes and travel with the header loads.
 DEV void skb_rooms_clear(uint8_t *pkt, uint32_t lw) {
+#if defined(MIMIC_ROOMS_MODE) && MIMIC_ROOMS_MODE == 2   // measurement only (MIMIC_JIT_ROOMS=2): rooms untouched
+    return;
+#endif
     typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
     const GAS u64x2u *h = (const GAS u64x2u *)pkt, *t = (const GAS u64x2u *)(pkt + SKB_HEADROOM + lw);
     const u64x2u h0 = h[0], h1 = h[1], t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
     const u64x2u o = h0 | h1 | t0 | t1 | t2 | t3;
+#if defined(MIMIC_ROOMS_MODE) && MIMIC_ROOMS_MODE == 0   // MIMIC_JIT_ROOMS=0: always written (round 2)
+    if (true) {
+#else
     if (o.x | o.y) {
+#endif
         const u64x2u z = {0, 0};
         GAS u64x2u *hw = (GAS u64x2u *)pkt, *tw = (GAS u64x2u *)(pkt + SKB_HEADROOM + lw);
         hw[0] = z;
