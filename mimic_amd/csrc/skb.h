@@ -103,7 +103,7 @@ struct SkbBytes {
 // the header walk's bytes from a block's LDS windows: thread t's first SKB_WIN bytes of its
 // packet as dwords, dword q at w[q * T + t] (a wave reading the same header offset hits
 // consecutive dwords); bytes past the window (deep tunnels only) come from global memory
-#define SKB_WIN 128u
+#define SKB_WIN 112u   // 7 chunks of 16 B: every header skb_fast reads, and the prep block's LDS stays under 32 KiB (5 blocks per CU)
 template <uint32_t T>
 struct SkbWinBytes {
     const uint32_t *w;

@@ -86,10 +86,10 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     __syncthreads();   // every window read
     typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
     u64x2 *area2 = (u64x2 *)area;
-    if (live) {
-        const u64x2 *rv = (const u64x2 *)&r;
+    if (live) {   // as 8-byte words: a vector view of the record would keep it in a second register layout (87 -> 161 VGPRs)
+        const uint64_t *rw = (const uint64_t *)&r;
 #pragma unroll
-        for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) area2[t * (SKB_DERIVED_Q / 2) + u] = rv[u];
+        for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) area[t * SKB_DERIVED_Q + q] = rw[q];
     }
     __syncthreads();
     // the block's records are contiguous in rec: 16-byte units, consecutive threads on consecutive
