@@ -288,6 +288,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-resident", action="store_true", help="skip the PCIe-inclusive rate")
+    ap.add_argument("--rccl", action="store_true",
+                    help="run the multi-GPU setup / readout collectives over RCCL even at world size 1 "
+                         "(a one-GPU rehearsal of the N-rank path: program broadcast, counter all-reduce, "
+                         "hash replica merge)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="CPU rehearsal of the --gpus N launcher: gloo ranks run the setup / readout "
                          "collectives with no engine and rank 0 prints the launch facts")
@@ -389,9 +393,14 @@ def main(argv=None):
         sys.stderr.write(f"bench.py rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} "
                          f"GPU(s) visible\n")
         return 2
-    if ws > 1:
+    use_dist = ws > 1 or args.rccl   # the collective paths (RCCL); at world size 1 only with --rccl
+    if use_dist:
         import torch.distributed as dist
 
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(ws))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
@@ -408,7 +417,7 @@ def main(argv=None):
     wl = Workload(args.config, n, W.SEED + rank)
 
     # program bytes: built on rank 0, broadcast over RCCL (the setup-time exchange)
-    raws = [D.broadcast_bytes(p.raw if rank == 0 else None, dev) if ws > 1 else p.raw for p in wl.progs]
+    raws = [D.broadcast_bytes(p.raw if rank == 0 else None, dev) if use_dist else p.raw for p in wl.progs]
     vm, maps, pids = wl.build_vm(M, V, local, D.shard(vpg, rank), raws)
     pid = pids[0]
 
@@ -432,7 +441,7 @@ def main(argv=None):
     for k in range(args.warmup):
         launch(k)
     torch.cuda.synchronize(dev)
-    if ws > 1:
+    if use_dist:
         dist.barrier()
     # device time of the timed region: two HIP events on the stream the kernels run on, around the
     # K back-to-back launches (an event pair per launch would itself sit between the kernels)
@@ -444,14 +453,14 @@ def main(argv=None):
         launch(args.warmup + k)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if ws > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     region_ms = ev0.elapsed_time(ev1)
     st = np.concatenate([res.status[:n].cpu().numpy() for _, _, res in batches])
     timed = [(args.warmup + k) % nb for k in range(args.steps)]
-    if ws > 1:
+    if use_dist:
         elapsed = D.allreduce_max_f64(elapsed, dev)
 
     # sum-over-CPUs readout of the per-CPU counters (RCCL all-reduce across ranks); shared hash
@@ -463,12 +472,12 @@ def main(argv=None):
     if hm and not wl.skb:
         m0 = hm[0]
         mine = {k: v[0] for k, v in maps[m0["name"]].Contents().items()}
-        merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], dev, m0["max_entries"]) if ws > 1 else mine
+        merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], dev, m0["max_entries"]) if use_dist else mine
         hash_keys = len(merged)
     if pcm:
         b0, cnt = D.shard(vpg, rank)
         local_sum = maps[pcm[0]["name"]].SumU64(b0, b0 + cnt)
-        counters = D.allreduce_sum_u64(local_sum, dev) if ws > 1 else local_sum
+        counters = D.allreduce_sum_u64(local_sum, dev) if use_dist else local_sum
 
     # eBPF instructions per batch (exact per-lane step counts): one more untimed launch of each
     # batch after the readout above
@@ -478,7 +487,7 @@ def main(argv=None):
         torch.cuda.synchronize(dev)
         steps_of.append(vm.LastSteps())
     steps_timed = float(sum(steps_of[b] for b in timed))
-    if ws > 1:
+    if use_dist:
         steps_timed = float(D.allreduce_sum_u64([int(steps_timed)], dev)[0])
 
     if rank == 0:
@@ -522,6 +531,8 @@ def main(argv=None):
             "counters_sum": counters,
             "hash_keys": hash_keys,
         }
+        if use_dist:
+            out["collectives"] = f"rccl, world size {ws}"
         if not args.no_host_resident and ws == 1 and not wl.skb:
             out["host_resident"] = host_resident_rate(vm, pid, wl, sched)
         if not args.no_cpu_baseline and ws == 1:
@@ -530,7 +541,7 @@ def main(argv=None):
             allc = cpu_baseline(wl, args.cpu_seconds, T) if T > 1 else one
             out["cpu_baseline"] = dict(one, all_cores=allc)
         print(json.dumps(out), flush=True)
-    if ws > 1:
+    if use_dist:
         dist.destroy_process_group()
     vm.close()
 
