@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <cstdlib>
 
 #include "runtime.h"
 // ---------------------------------------------------------------------------------------
@@ -436,6 +437,8 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
 }
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(const KParams *__restrict__ kpp) { xdp_body<MODE_BATCH>(kpp); }
+// the same body at the compiler's own budget (3 waves per SIMD, no spills): MIMIC_INTERP_WAVES=3
+extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel_w3(const KParams *__restrict__ kpp) { xdp_body<MODE_BATCH>(kpp); }
 extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KParams *__restrict__ kpp) { xdp_body<MODE_STEP>(kpp); }
 // after a JIT kernel with deferred slow paths, with the same launch parameters (by value: read
 // in place from the kernarg segment, as the JIT kernels do)
@@ -627,7 +630,9 @@ extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st) {
 extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st) {
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
+    static const bool w3 = [] { const char *e = getenv("MIMIC_INTERP_WAVES"); return e && e[0] == '3'; }();
     if (kp->step) hipLaunchKernelGGL(mimic_xdp_step_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
+    else if (w3) hipLaunchKernelGGL(mimic_xdp_kernel_w3, dim3(blocks), dim3(256), 0, st, d_kp);
     else hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
