@@ -524,6 +524,8 @@ def main(argv=None):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
                          "traffic": prof["bytes_per_launch"] if prof else None,
                          "traffic_over_algorithmic": round(prof["bytes_per_launch"] / alg, 3) if prof else None,
+                         # the same launch time against the bytes the counters measured (FETCH x 2 + WRITE)
+                         "frac_on_traffic": round(prof["bytes_per_launch"] / avg_launch_s / HBM_PEAK, 5) if prof else None,
                          "valu_busy": prof.get("valu_busy") if prof else None,
                          "profile": prof["file"] if prof else None,
                          "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
