@@ -34,11 +34,9 @@ extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_
 extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
-extern "C" size_t mimic_skb_scan_bytes(uint32_t n);
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
-                                     uint32_t n, SkbRec *rec, uint64_t *foot, uint64_t *prefix, void *scan_tmp,
-                                     size_t scan_bytes, uint64_t *state, uint64_t init_base, uint32_t use_init,
-                                     hipStream_t st);
+                                     uint32_t n, SkbRec *rec, uint64_t *prefix, uint64_t *state, uint64_t init_base,
+                                     uint32_t use_init, hipStream_t st);
 
 namespace {
 
@@ -142,12 +140,11 @@ struct mimic_vm {
     // (and its completion latency) between their kernels on the compute stream
     hipStream_t s_kp = nullptr;
     hipEvent_t kp_side_ev = nullptr;
-    // sk_buff batches (skb.h): per-packet records, footprints, their prefix, scan scratch, and
+    // sk_buff batches (skb.h): per-packet records, their leak prefixes (skb.hip), and
     // the device word pair {next leak address, this batch's leak base}
     SkbRec *d_skb_rec = nullptr;
-    uint64_t *d_skb_foot = nullptr, *d_skb_prefix = nullptr, *d_skb_state = nullptr;
-    void *d_skb_scan = nullptr;
-    size_t skb_cap = 0, skb_scan_cap = 0;
+    uint64_t *d_skb_prefix = nullptr, *d_skb_state = nullptr;
+    size_t skb_cap = 0;
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
     hipStream_t skb_stream = nullptr;
     bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
@@ -604,10 +601,8 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (vm->kp_side_ev) hipEventDestroy(vm->kp_side_ev);
     if (vm->s_kp) hipStreamDestroy(vm->s_kp);
     hipFree(vm->d_skb_rec);
-    hipFree(vm->d_skb_foot);
     hipFree(vm->d_skb_prefix);
     hipFree(vm->d_skb_state);
-    hipFree(vm->d_skb_scan);
     if (vm->s_h2d) hipStreamDestroy(vm->s_h2d);
     if (vm->s_h2d2) hipStreamDestroy(vm->s_h2d2);
     if (vm->s_d2h) hipStreamDestroy(vm->s_d2h);
@@ -719,7 +714,16 @@ int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id)
         m.ht_cap = 16;
         while (m.ht_cap < 2ull * spec->max_entries + 2) m.ht_cap <<= 1;
         m.rec_q = 1 + (spec->key_size + 7) / 8;
-        m.nlocks = std::min<uint32_t>(m.ht_cap, 1u << 16);
+        // stripe locks: 4 per bucket (up to 2^22).  A lane's lock is picked by its key's hash, so
+        // lanes inserting one key serialise and other keys collide only by chance.  The cfg-4
+        // inserting launch (E = 131 072, 2^19 buckets): 2^12 locks 2.0 ms, 2^16 0.53 ms, 2^19
+        // 0.44 ms, 2^21 0.41 ms (tools/run_insert_knobs.sh; MIMIC_HASH_LOCKS_LOG2 = v sets 2^v)
+        static const int lk_log2 = [] {
+            const char *e = getenv("MIMIC_HASH_LOCKS_LOG2");
+            const int v = e ? atoi(e) : 0;
+            return v >= 4 && v <= 26 ? v : 0;
+        }();
+        m.nlocks = lk_log2 ? 1u << lk_log2 : (uint32_t)std::min<uint64_t>(4ull * m.ht_cap, 1ull << 22);
         m.fl_cap = 16;
         while (m.fl_cap < 2ull * spec->max_entries + 2) m.fl_cap <<= 1;
         // index region (hashmap.h h_table): records | rebuild copy | locks | freelist ring | HashCtl
@@ -1187,11 +1191,11 @@ static int skb_settle(mimic_vm *vm) {
     return 0;
 }
 
-// the sk_buff records, footprints and leak addresses of a batch (skb.hip), on stream st; `into`
+// the sk_buff records and leak addresses of a batch (skb.hip), on stream st; `into`
 // (a stepped process's own arrays, one packet) instead of the VM's batch arrays
 struct SkbInto {
     SkbRec *rec;
-    uint64_t *foot, *prefix;
+    uint64_t *prefix;   // 2 words (skb.h skb_leak_pre)
 };
 static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, const SkbInto *into = nullptr,
                        bool records = true) {
@@ -1202,30 +1206,23 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     if (n > vm->skb_cap || !vm->d_skb_state) {
         HIP_OK(vm, hipStreamSynchronize(st));
         hipFree(vm->d_skb_rec);
-        hipFree(vm->d_skb_foot);
         hipFree(vm->d_skb_prefix);
         vm->d_skb_rec = nullptr;
-        vm->d_skb_foot = vm->d_skb_prefix = nullptr;
+        vm->d_skb_prefix = nullptr;
         const size_t cap = std::max<size_t>(n, 1024);
         HIP_OK(vm, hipMalloc(&vm->d_skb_rec, cap * sizeof(SkbRec)));
-        HIP_OK(vm, hipMalloc(&vm->d_skb_foot, cap * 8));
-        HIP_OK(vm, hipMalloc(&vm->d_skb_prefix, cap * 8));
-        if (!vm->d_skb_state) HIP_OK(vm, hipMalloc(&vm->d_skb_state, 16));
+        // within-block prefixes, then the blocks' offsets (skb.hip)
+        HIP_OK(vm, hipMalloc(&vm->d_skb_prefix, (cap + (cap >> SKB_PREP_LOG2) + 1) * 8));
+        if (!vm->d_skb_state) {   // leak cursor, batch base, the prep kernel's block counter (zero)
+            HIP_OK(vm, hipMalloc(&vm->d_skb_state, 32));
+            HIP_OK(vm, hipMemset(vm->d_skb_state, 0, 32));
+        }
         vm->skb_cap = cap;
-    }
-    const size_t sb = mimic_skb_scan_bytes(std::max<uint32_t>(n, 1));
-    if (sb > vm->skb_scan_cap) {
-        HIP_OK(vm, hipStreamSynchronize(st));
-        hipFree(vm->d_skb_scan);
-        vm->d_skb_scan = nullptr;
-        HIP_OK(vm, hipMalloc(&vm->d_skb_scan, std::max<size_t>(sb, 256)));
-        vm->skb_scan_cap = std::max<size_t>(sb, 256);
     }
     // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
     const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
     if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, into ? into->rec : records ? vm->d_skb_rec : nullptr,
-                              into ? into->foot : vm->d_skb_foot, into ? into->prefix : vm->d_skb_prefix,
-                              vm->d_skb_scan, vm->skb_scan_cap, vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
+                              into ? into->prefix : vm->d_skb_prefix, vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;
     vm->skb_stream = st;
@@ -1610,7 +1607,7 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     SkbRun skr{p->ifindex};
     if (p->skb) {
         sr.skb_rec = (SkbRec *)p->d_skbmem;
-        sr.skb_prefix = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 8);
+        sr.skb_prefix = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec));
         sr.skb_base = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 16);
     }
     int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, p->skb ? &skr : nullptr, &sr);
@@ -1703,8 +1700,8 @@ int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, ui
     b.pkt_data = p->d_pkt;
     b.pkt_off = p->d_off;
     b.pkt_len = p->d_len;
-    const SkbInto into{(SkbRec *)p->d_skbmem, (uint64_t *)(p->d_skbmem + sizeof(SkbRec)),
-                       (uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 8)};
+    // d_skbmem: the record | its 2 prefix words | the batch base
+    const SkbInto into{(SkbRec *)p->d_skbmem, (uint64_t *)(p->d_skbmem + sizeof(SkbRec))};
     if ((rc = skb_prepare(vm, &b, vm->stream, &into))) return rc;
     HIP_OK(vm, hipMemcpyAsync(p->d_skbmem + sizeof(SkbRec) + 16, vm->d_skb_state + 1, 8, hipMemcpyDeviceToDevice,
                               vm->stream));

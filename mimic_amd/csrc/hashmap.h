@@ -308,7 +308,17 @@ HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted
     bool done = false;
     int32_t idx = -1;
     *inserted = false;
-    for (;;) {
+    for (uint32_t round = 0;; round++) {
+        // a lane still waiting for its lock looks for its key without the lock first: once another
+        // lane has published it, the lock round would only find it (cfg-4 inserting launch 0.456 ->
+        // 0.441 ms).  The helper's own h_find before this call is the same lock-free check.
+        if (round && !done) {
+            const int32_t f = h_find(t, ks, h, nullptr);
+            if (f >= 0) {
+                idx = f;
+                done = true;
+            }
+        }
         const uint64_t pend = __ballot(!done);
         if (!pend) break;
         const bool lead = h_round_leader(pend, lkid);

@@ -296,6 +296,15 @@ class Gen {
         }
         if (defer_mode && sm_lds_knob) E.line("#define MIMIC_SM_LDS 1");
         if (const char *rm = getenv("MIMIC_JIT_ROOMS")) E.line("#define MIMIC_ROOMS_MODE %d", atoi(rm));   // measurement knob
+        if (const char *dv = getenv("MIMIC_JIT_DEFS")) {   // measurement knob: "A,B=2" -> #define A / #define B 2
+            std::string all(dv), d;
+            for (size_t a = 0; a <= all.size(); a++) {
+                if (a < all.size() && all[a] != ',') { d += all[a]; continue; }
+                const size_t eq = d.find('=');
+                if (!d.empty()) E.line("#define %s %s", d.substr(0, eq).c_str(), eq == std::string::npos ? "" : d.substr(eq + 1).c_str());
+                d.clear();
+            }
+        }
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         {   // no program of the set updates or deletes: hash tables are read-only in every launch

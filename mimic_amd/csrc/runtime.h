@@ -899,6 +899,10 @@ static_assert(SKB_HEADROOM == 32 && SKB_TAILROOM == 64, "skb_rooms_clear covers 
 // records were not built by the prep kernel (KParams::skb_rec_built == 0: its JIT kernel builds
 // them in LDS) the record is built here first, unless `attach_only` (a process the resume kernel
 // re-attaches: its record, rooms and packet are what the JIT lane left).
+// packet i's leak prefix: within its prep block + the block's offset (skb.hip)
+DEV uint64_t skb_leak_pre(const KParams &kp, uint32_t i) {
+    return kp.skb_prefix[i] + kp.skb_prefix[kp.n + (i >> SKB_PREP_LOG2)];
+}
 DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool attach_only = false) {
     SkbRec *rec = kp.skb_rec + i;
     L.pkt = kp.pkt_data + kp.pkt_off[i];
@@ -909,7 +913,7 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     L.pa = 0;
     L.M = 0;
     if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
-    const uint64_t ka = *kp.skb_base + kp.skb_prefix[i];
+    const uint64_t ka = *kp.skb_base + skb_leak_pre(kp, i);
     if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
     if (!attach_only)   // the writable state at Load (the prep kernel writes the derived words only)
         for (uint32_t q = 0; q < 8; q++) ((uint64_t *)rec)[SKB_DERIVED_Q + q] = skb_writable_word(q);
@@ -948,7 +952,7 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
     uint64_t w[SKB_DERIVED_Q];
 #pragma unroll
     for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) w[q] = s[q];
-    const uint64_t po = kp.pkt_off[i], pre = kp.skb_prefix[i], base = *kp.skb_base;
+    const uint64_t po = kp.pkt_off[i], pre = skb_leak_pre(kp, i), base = *kp.skb_base;
 #pragma unroll
     for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) d[q] = w[q];
 #pragma unroll
@@ -961,7 +965,7 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
 // read per packet less): SKBuffFromBytes over the packet's first bytes staged in the block's LDS
 // windows (`win`, SkbWinBytes), straight into the LDS slot `d`
 DEV int skb_load_walk(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint32_t *win) {
-    const uint64_t po = kp.pkt_off[i], pre = kp.skb_prefix[i], base = *kp.skb_base;
+    const uint64_t po = kp.pkt_off[i], pre = skb_leak_pre(kp, i), base = *kp.skb_base;
     const uint32_t len = kp.pkt_len[i];
     L.pkt = kp.pkt_data + po;
     const uint8_t *pkt = L.pkt + SKB_HEADROOM;

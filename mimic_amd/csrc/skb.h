@@ -33,6 +33,9 @@
 #define SKB_TAILROOM 64u         // :116
 #define SKB_FOOT_FIXED 219u      // (80+1) + (40+1) + (96+1): address span of one packet's leaks
 #define SKB_LOAD_FAILED 0x80000000u
+// the prep kernel's block (skb.hip): packet i's leak prefix is prefix[i] (within its block) +
+// prefix[n + (i >> SKB_PREP_LOG2)] (the block's offset in the batch)
+#define SKB_PREP_LOG2 8u
 #define SKB_SNAP 40u
 #define SKB_REC_BYTES 160u
 

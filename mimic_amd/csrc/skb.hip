@@ -1,16 +1,17 @@
 // skb.hip -- context construction for sk_buff batches (LinuxContextSKBuff.Load,
 // context_sk_buff.go:42-107, over SKBuffFromBytes, emulator_linux_sk_buff.go:108-265).
 //
-// Three stream-ordered steps before the program kernel (JIT or interpreter) runs:
+// Two stream-ordered kernels before the program kernel (JIT or interpreter) runs:
 //   1. mimic_skb_prep_kernel: one thread per packet walks the headers once and writes the
-//      packet's SkbRec (skb.h) and its leak footprint (219 + L, or 0 when Load fails);
-//   2. an exclusive scan of the footprints (hipCUB): packet i's sock / flow-keys / packet
-//      entries start at leak_base + prefix[i], exactly where a sequential reference run's
-//      first-fit AddEntry puts them (Cleanup leaks them, so they pile up);
-//   3. mimic_skb_advance_kernel: publishes this batch's leak_base and moves the VM's leak
-//      cursor past the batch (device-side: no host round trip between batches).
+//      packet's SkbRec (skb.h) and its leak prefix within its block: packet i's sock / flow-keys
+//      / packet entries start at leak_base + the sum of the footprints (219 + L, or 0 when Load
+//      fails) of the packets before it, exactly where a sequential reference run's first-fit
+//      AddEntry puts them (Cleanup leaks them, so they pile up);
+//   2. mimic_skb_blocks_kernel (one workgroup): the blocks' offsets in the batch, the batch's
+//      leak base, and the VM's leak cursor moved past the batch (device-side: no host round trip
+//      between batches).  skb.h skb_leak_pre adds the two parts.  Round 2 ran a hipCUB scan of
+//      per-packet footprints and a cursor kernel here: 24 us per 1 M packets.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
 #include "runtime.h"
@@ -23,7 +24,7 @@
 #define PREP_T 256u
 
 // packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  rec == nullptr: the
-// footprints only (a JIT kernel that walks the headers itself builds the records in LDS).  Only
+// leak prefixes only (a JIT kernel that walks the headers itself builds the records in LDS).  Only
 // the records' derived words are written (skb.h SKB_DERIVED_Q: the writable state is constant at
 // Load and set by whoever loads the process).  They leave through LDS: each thread puts its
 // words there and the block writes them with consecutive threads on consecutive 8-byte words --
@@ -37,17 +38,45 @@
 #endif
 static_assert(sizeof(SkbRec) % 8 == 0, "SkbRec is copied as 8-byte words");
 static_assert(SKB_DERIVED_Q * PREP_T <= (PREP_W / 8) * PREP_T, "a block's derived words fit the window area");
+static_assert(PREP_T == (1u << SKB_PREP_LOG2), "skb_leak_pre's block");
+
+// exclusive scan of v over the block (wave shuffles, then the waves' totals); *total = the sum
+static __device__ uint64_t prep_exscan(uint64_t v, uint64_t *wtot, uint64_t *total) {
+    const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wtot[wv] = x;
+    __syncthreads();
+    uint64_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PREP_T / 64; k++) {
+        const uint64_t s = wtot[k];
+        off += k < wv ? s : 0ull;
+        tot += s;
+    }
+    __syncthreads();   // wtot free again
+    *total = tot;
+    return off + x - v;
+}
+
+// prefix: n + ceil(n / PREP_T) words (within-block prefixes, then the blocks' sums)
 extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, SkbRec *__restrict__ rec,
-                                                                          uint64_t *__restrict__ foot) {
+                                                                          uint64_t *__restrict__ prefix) {
     __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
+    __shared__ uint64_t wtot[PREP_T / 64];
     uint32_t *win = (uint32_t *)area;
     const uint32_t t = threadIdx.x, i0 = blockIdx.x * PREP_T, i = i0 + t;
     if (i0 >= n) return;   // whole block past the batch (uniform: the barriers below are safe)
     const bool live = i < n;
     SkbRec r;
+    uint64_t f = 0;   // the leak footprint
     if (live) {
         const uint32_t L = pkt_len[i];
         const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
@@ -70,77 +99,102 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
 #else
         skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
 #endif
-        foot[i] = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
+        f = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
-    if (!rec) return;   // footprints only
+    if (rec) {
 #ifdef MIMIC_PREP_DIRECT   // measurement: each thread writes its own derived words (16-byte stores)
-    if (live) {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        const u64x2 *rv = (const u64x2 *)&r;
-        u64x2 *o = (u64x2 *)(rec + i);
+        if (live) {
+            typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+            const u64x2 *rv = (const u64x2 *)&r;
+            u64x2 *o = (u64x2 *)(rec + i);
 #pragma unroll
-        for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) PREP_ST(o + u, rv[u]);
-    }
-    return;
+            for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) PREP_ST(o + u, rv[u]);
+        }
 #else
-    __syncthreads();   // every window read
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    u64x2 *area2 = (u64x2 *)area;
-    if (live) {   // as 8-byte words: a vector view of the record would keep it in a second register layout (87 -> 161 VGPRs)
-        const uint64_t *rw = (const uint64_t *)&r;
+        __syncthreads();   // every window read
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        u64x2 *area2 = (u64x2 *)area;
+        if (live) {   // as 8-byte words: a vector view of the record would keep it in a second register layout (87 -> 161 VGPRs)
+            const uint64_t *rw = (const uint64_t *)&r;
 #pragma unroll
-        for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) area[t * SKB_DERIVED_Q + q] = rw[q];
-    }
-    __syncthreads();
-    // the block's records are contiguous in rec: 16-byte units, consecutive threads on consecutive
-    // units (the writable words between the records are not written)
-    const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
-    u64x2 *dst = (u64x2 *)(rec + i0);
-    constexpr uint32_t DU = SKB_DERIVED_Q / 2, RU = sizeof(SkbRec) / 16;
-    for (uint32_t w = t; w < cnt * DU; w += PREP_T) {
-        const uint32_t k = w / DU, u = w - k * DU;
-        PREP_ST(dst + (size_t)k * RU + u, area2[w]);
-    }
+            for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) area[t * SKB_DERIVED_Q + q] = rw[q];
+        }
+        __syncthreads();
+        // the block's records are contiguous in rec: 16-byte units, consecutive threads on consecutive
+        // units (the writable words between the records are not written)
+        const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
+        u64x2 *dst = (u64x2 *)(rec + i0);
+        constexpr uint32_t DU = SKB_DERIVED_Q / 2, RU = sizeof(SkbRec) / 16;
+        for (uint32_t w = t; w < cnt * DU; w += PREP_T) {
+            const uint32_t k = w / DU, u = w - k * DU;
+            PREP_ST(dst + (size_t)k * RU + u, area2[w]);
+        }
 #endif
+    }
+    // the leak prefix within the block, and the block's sum (mimic_skb_blocks_kernel scans those)
+    uint64_t bsum;
+    const uint64_t ex = prep_exscan(f, wtot, &bsum);
+    if (live) prefix[i] = ex;
+    if (t == 0) prefix[n + blockIdx.x] = bsum;
+}
+
+// The blocks' offsets in the batch (exclusive scan of the nb block sums at bs, in place; one
+// workgroup, thread t scans blocks [t*per, t*per+per)), then the batch's leak base and the cursor
+// past it.  state[0] = the VM's next leak address, state[1] = this batch's leak base.
+// (Finishing this in the prep kernel's last block instead needs a device-scope counter whose
+// ordering wait held every block's tail: 77 -> 94 us per 1 M packets.)
+#define BLK_T 1024u
+extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint64_t *bs, uint32_t nb, uint64_t *state,
+                                                                          uint64_t init_base, uint32_t use_init) {
+    __shared__ uint64_t wtot[BLK_T / 64];
+    const uint32_t t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
+    const uint32_t per = (nb + BLK_T - 1) / BLK_T, lo = t * per;
+    uint64_t s = 0;
+    for (uint32_t k = 0; k < per && lo + k < nb; k++) s += bs[lo + k];
+    uint64_t x = s;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wtot[wv] = x;
+    __syncthreads();
+    uint64_t o = x - s, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BLK_T / 64; k++) {
+        o += k < wv ? wtot[k] : 0ull;
+        all += wtot[k];
+    }
+    for (uint32_t k = 0; k < per && lo + k < nb; k++) {
+        const uint64_t v = bs[lo + k];
+        bs[lo + k] = o;
+        o += v;
+    }
+    if (t == 0) {
+        const uint64_t base = use_init ? init_base : state[0];
+        state[1] = base;
+        state[0] = base + all;
+    }
 }
 
 // the prep kernel alone (tools/prep_probe.py)
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
-                                   SkbRec *rec, uint64_t *foot, hipStream_t st) {
+                                   SkbRec *rec, uint64_t *prefix, uint64_t *state, hipStream_t st) {
     hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                       rec, foot);
+                       rec, prefix);
+    hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
+                       0ull, 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// state[0] = the VM's next leak address, state[1] = this batch's leak base
-extern "C" __global__ void mimic_skb_advance_kernel(uint64_t *state, const uint64_t *prefix, const uint64_t *foot,
-                                                    uint32_t n, uint64_t init_base, uint32_t use_init) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const uint64_t base = use_init ? init_base : state[0];
-    state[1] = base;
-    state[0] = base + (n ? prefix[n - 1] + foot[n - 1] : 0ull);
-}
-
-extern "C" size_t mimic_skb_scan_bytes(uint32_t n) {
-    size_t bytes = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n) !=
-        hipSuccess)
-        return 0;
-    return bytes;
-}
-
+// prefix: n + ceil(n / 256) words; state: 2 words
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
-                                     uint32_t n, SkbRec *rec, uint64_t *foot, uint64_t *prefix, void *scan_tmp,
-                                     size_t scan_bytes, uint64_t *state, uint64_t init_base, uint32_t use_init,
-                                     hipStream_t st) {
-    if (n) {
+                                     uint32_t n, SkbRec *rec, uint64_t *prefix, uint64_t *state, uint64_t init_base,
+                                     uint32_t use_init, hipStream_t st) {
+    if (n)
         hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                           rec, foot);
-        if (hipGetLastError() != hipSuccess) return -1;
-        size_t bytes = scan_bytes;
-        if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, bytes, (const uint64_t *)foot, prefix, (int)n, st) != hipSuccess)
-            return -1;
-    }
-    hipLaunchKernelGGL(mimic_skb_advance_kernel, dim3(1), dim3(64), 0, st, state, prefix, foot, n, init_base, use_init);
+                           rec, prefix);
+    hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
+                       init_base, use_init);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -15,15 +15,16 @@ d_buf = torch.from_numpy(buf).to(dev)
 d_off = torch.from_numpy(off.view("int64")).to(dev)
 d_len = torch.from_numpy(lens.view("int32")).to(dev)
 rec = torch.empty(n * 160, dtype=torch.uint8, device=dev)
-foot = torch.empty(n, dtype=torch.int64, device=dev)
+prefix = torch.empty(n + n // 256 + 1, dtype=torch.int64, device=dev)
+state = torch.zeros(4, dtype=torch.int64, device=dev)
 for so in sys.argv[1:] + ["norec:" + sys.argv[1]]:
     norec = so.startswith("norec:")
     lib = C.CDLL(so.split(":")[-1])
     f = lib.mimic_skb_prep_only
-    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     s = torch.cuda.current_stream()
-    args = (d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, None if norec else rec.data_ptr(), foot.data_ptr(),
-            C.c_void_p(s.cuda_stream))
+    args = (d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, None if norec else rec.data_ptr(), prefix.data_ptr(),
+            state.data_ptr(), C.c_void_p(s.cuda_stream))
     for _ in range(3):
         f(*args)
     torch.cuda.synchronize()
