@@ -106,7 +106,7 @@ struct SkbBytes {
 // the header walk's bytes from a block's LDS windows: thread t's first SKB_WIN bytes of its
 // packet as dwords, dword q at w[q * T + t] (a wave reading the same header offset hits
 // consecutive dwords); bytes past the window (deep tunnels only) come from global memory
-#define SKB_WIN 112u   // 7 chunks of 16 B: every header skb_fast reads, and the prep block's LDS stays under 32 KiB (5 blocks per CU)
+#define SKB_WIN 96u   // 6 chunks of 16 B: every byte skb_fast reads (up to 67), and a packet's header window stays within two 64-byte sectors of its slot
 template <uint32_t T>
 struct SkbWinBytes {
     const uint32_t *w;
@@ -402,7 +402,7 @@ SKB_DEV void skb_init(const B &pkt, uint32_t L, SkbRec &r) {
 // ---------------------------------------------------------------------------------------
 // The common frames without a walk: Ethernet + IPv4 (no options) / IPv6 (no extension headers)
 // + TCP / UDP (no tunnel port), or a non-IP EtherType, decoded straight from the packet's first
-// 128 bytes held in registers (w[q] = bytes 4q..4q+3) at constant offsets -- the same decisions
+// SKB_WIN bytes held in registers (w[q] = bytes 4q..4q+3) at constant offsets -- the same decisions
 // skb_walk makes for these frames, in the same order.  Everything else (802.3 / LLC, VLAN tags,
 // IPv4 options, IPv6 extension headers, IP-in-IP, UDP tunnels) returns false: the general walk
 // decodes it.  No frame taken here fails Load (only a second layer of one kind does).

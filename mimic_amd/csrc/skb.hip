@@ -80,7 +80,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     if (live) {
         const uint32_t L = pkt_len[i];
         const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
-        // the first 128 bytes into registers (16-byte chunks that start inside the packet; one may
+        // the first SKB_WIN bytes into registers (16-byte chunks that start inside the packet; one may
         // run into the 64-byte tailroom); common frames decode from there (skb_fast), the rest
         // through this thread's LDS window
         typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
