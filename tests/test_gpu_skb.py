@@ -112,6 +112,30 @@ def test_leaked_addresses_across_batches(gpu):
     assert len(np.unique(o["r0"][ok])) == ok.sum()   # every process got a fresh packet entry
 
 
+def test_leak_prefix_large_batches(gpu):
+    """r0 = skb->data over two batches of ~150 K packets (1 172 prep blocks in all, so the block
+    offsets kernel scans two sums per thread): the first 1 000 processes equal the oracle's, and
+    every process's packet entry follows the previous one's by its leak footprint 219 + L
+    (context_sk_buff.go:73-95: sock 80+1, flow keys 40+1, packet 32+L+64+1), across the batch
+    boundary too.  A size-independent check of the two-part leak prefix (skb.hip)."""
+    from mimic_amd import asm as A
+
+    raw, _ = A.assemble([A.ldx(4, 0, 1, A.SKB["data"]), A.exit_()])
+    sc = Scenario(vcpus=1024, progs=[("d", raw, [])])
+    n = 300_001
+    buf, off, lens = W.make_skb_packets(n, sizes=(60, 64, 200), weights=(2, 3, 1), variety=0.05)
+    cpu = W.schedule_cpu(n, 1024, "interleaved")
+    e = run_engine_skb(sc, buf, off, lens, cpu, splits=[150_001])
+    m = 1000
+    o = run_oracle_skb(sc, buf, off[:m], lens[:m], cpu[:m])
+    assert_same(o, e, check_pkt=False, n=m)
+    ok = np.asarray(e["status"]) == 0
+    assert ok.mean() > 0.9
+    d = np.asarray(e["r0"], dtype=np.int64)[ok]
+    L = np.asarray(lens, dtype=np.int64)[ok]
+    assert np.array_equal(np.diff(d), 219 + L[:-1])
+
+
 @pytest.mark.slow
 def test_cfg5_large(gpu):
     """Config 5 shape at 65 536 IMIX packets, 16 384 vCPUs: exact against the oracle.  (The
