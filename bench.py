@@ -43,10 +43,11 @@ CONFIGS = {
                    workload="cfg3: 16M IMIX 7:4:1 (64/576/1500B) xdp_md, L2/L3/L4 parse + 5-tuple hash, "
                             "per-CPU array E=256 S=8"),
     "flowtrack": dict(prog="prog_flowtrack", packets=1 << 21, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 18,
-                      workload="cfg4 per-GPU shard: 2M IMIX xdp_md (16M over 8 GPUs), 5-tuple parse + "
-                               "insert-if-absent into a shared hash map K=16 S=8 E=131072"),
+                      one_batch=True,
+                      workload="cfg4 per-GPU shard: packets [r*2M, (r+1)*2M) of ONE 2M*N IMIX xdp_md batch (16M over "
+                               "8 GPUs), 5-tuple parse + insert-if-absent into a shared hash map K=16 S=8 E=131072"),
     "flowtrack_insert": dict(prog="prog_flowtrack", packets=1 << 21, sizes=(64, 576, 1500), weights=(7, 4, 1),
-                             vcpus=1 << 18, reset_maps=True,
+                             vcpus=1 << 18, reset_maps=True, one_batch=True,
                              workload="cfg4 per-GPU shard, inserting: 2M IMIX xdp_md into a FRESH shared hash map "
                                       "K=16 S=8 E=131072 every step (map reset in the timed region), ~118K inserts "
                                       "per batch"),
@@ -85,15 +86,25 @@ def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps, reads_packet: bool = T
 # workloads
 # ---------------------------------------------------------------------------------------------
 class Workload:
-    """The programs, maps and input batch of one config (host side)."""
+    """The programs, maps and input batch of one config (host side).
 
-    def __init__(self, cfg_name: str, n: int, seed: int):
+    Configs with a shared hash map (cfg 4: "one_batch") shard ONE batch: rank r of N takes
+    packets [r*n, (r+1)*n) of an N*n batch drawn from one flow pool (workloads.flowtrack_shard),
+    so the ranks' replicas together hold the keys of that one batch (<= MaxEntries).  The
+    per-CPU configs draw each rank's packets from its own seed (their vCPUs are disjoint)."""
+
+    def __init__(self, cfg_name: str, n: int, seed: int, rank: int = 0, world: int = 1, batch: int = 0):
         from mimic_amd import workloads as W
 
         self.cfg = CONFIGS[cfg_name]
         self.name = cfg_name
         self.skb = self.cfg.get("kind") == "skb"
-        if self.skb:
+        if self.cfg.get("one_batch"):
+            p = getattr(W, self.cfg["prog"])()
+            self.progs, self.maps, self.prog_array = [p], p.maps, []
+            self.buf, self.off, self.lens = W.flowtrack_shard(n, rank, world, batch, W.SEED)
+            self.map_init = []
+        elif self.skb:
             self.progs, self.maps, self.prog_array = W.skb_programs()
             self.buf, self.off, self.lens = W.make_skb_packets(n, self.cfg["sizes"], self.cfg["weights"], seed=seed,
                                                                variety=0.05)
@@ -344,7 +355,21 @@ def selftest_rank(args, ws, rank, local) -> None:
     ranks = D.allgather_records(bytes([rank, local]), 2, "cpu")
     elapsed = D.allreduce_max_f64(0.001 * (rank + 1), "cpu")
     counters = D.allreduce_sum_u64([rank + 1, 1], "cpu")
-    merged = D.merge_hash_replicas({bytes([rank]) * 4: bytes(8)}, 4, 8, "cpu")
+    cfg = CONFIGS[args.config]
+    if cfg.get("one_batch"):
+        # cfg 4: this rank's shard of the one batch, the (key, value) records its replica would
+        # hold (what the program inserts, computed from the headers), merged over the ranks with
+        # the map's MaxEntries check -- the readout the engine ranks run, at bench size
+        n = args.packets or cfg["packets"]
+        wl = Workload(args.config, n, W.SEED, rank, ws)
+        keys = W.flow_keys_np(wl.buf, wl.off, wl.lens)
+        vals = W.flowtrack_value(keys)
+        kb = np.ascontiguousarray(keys).view(np.uint8).reshape(-1, 16)
+        mine = {bytes(k): int(v).to_bytes(8, "little") for k, v in zip(kb, vals)}
+        m0 = wl.maps[0]
+        merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], "cpu", m0["max_entries"])
+    else:
+        merged = D.merge_hash_replicas({bytes([rank]) * 4: bytes(8)}, 4, 8, "cpu")
     if rank == 0:
         print(json.dumps({"n_gpus": ws, "gpus_flag": args.gpus, "program_ok": raw == p.raw,
                           "ranks": [b[0] for b in ranks], "local_ranks": [b[1] for b in ranks],
@@ -359,9 +384,11 @@ def make_batches(wl, args, n, rank, dev, sched):
     from mimic_amd import workloads as W
 
     nb = args.batches or default_batches(args.config, n)
+    ws = dist_env()[0]
     out = []
     for b in range(nb):
-        w = wl if b == 0 else Workload(args.config, n, W.SEED + rank + 1000 * b)
+        # a one-batch config rotates over further shards of the same batch (same flow pool)
+        w = wl if b == 0 else Workload(args.config, n, W.SEED + rank + 1000 * b, rank, ws, b)
         if wl.skb:
             batch = M.SKBBatch.from_numpy(w.buf, w.off, w.lens, device=dev, ifindex=1, schedule=sched)
         else:
@@ -414,7 +441,7 @@ def main(argv=None):
     n = args.packets or cfg["packets"]
     vpg = args.vcpus or cfg.get("vcpus") or max(64, n // 4)
     V = vpg * ws
-    wl = Workload(args.config, n, W.SEED + rank)
+    wl = Workload(args.config, n, W.SEED + rank, rank, ws)
 
     # program bytes: built on rank 0, broadcast over RCCL (the setup-time exchange)
     raws = [D.broadcast_bytes(p.raw if rank == 0 else None, dev) if use_dist else p.raw for p in wl.progs]

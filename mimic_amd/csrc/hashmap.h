@@ -123,6 +123,8 @@ HDEV int32_t h_find_ro(const HT &t, const KS &ks, uint64_t h) {
 #pragma unroll
             for (uint32_t q = 0; q < 4; q++)
                 if (q < nq) eq &= w[1 + q] == ks.word(q);
+            // keys over 32 bytes (IPv6 5-tuples): the words past the preload, one by one
+            for (uint32_t q = 4; eq && q < nq; q++) eq = r[1 + q] == ks.word(q);
             if (eq) return (int32_t)s;
         }
     }

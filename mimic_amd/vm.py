@@ -1071,23 +1071,28 @@ class ProcessPool:
         ctxs = [j.Process.Context or LinuxContextXDP() for j in js]
         cpus = [j.Process.cpuID for j in js]
         if skb:
-            batch = SKBBatch.from_packets([c.Packet for c in ctxs], device=dev,
-                                          ifindex=ctxs[0].Dev.IFIndex if ctxs[0].Dev else 0,
-                                          schedule=L.SCHED_EXPLICIT, cpu=cpus)
-            res = self.vm.RunSKBBatch(pid, batch).numpy(len(js))
-            self.vm.SKBRelease()
-            hr = [SKBBatch.HEADROOM] * len(js)
-        else:
-            import numpy as np
+            # An sk_buff process ran its context Load at NewProcess (its sock / flow keys / packet
+            # took the VM's next leak addresses then, context_sk_buff.go:110-119), and the pool
+            # worker only calls Run (vm.go:570): each job runs on the device process NewProcess
+            # made (mimic_process_run), in enqueue order -- a batch launch would Load again and
+            # give the job addresses past its own.
+            for j in js:
+                try:
+                    j.Process.Run()
+                except MimicError:
+                    if not j.Process.Status:   # not a fatal status of the program: an engine error
+                        raise
+            return
+        import numpy as np
 
-            hr = [c.Headroom for c in ctxs]
-            batch = XDPBatch.from_packets([c.Packet for c in ctxs], device=dev, headroom=np.array(hr, np.uint32),
-                                          tailroom=np.array([c.Tailroom for c in ctxs], np.uint32),
-                                          ingress=np.array([c.IngessIfIndex for c in ctxs], np.int32),
-                                          rxq=np.array([c.RxQueueIndex for c in ctxs], np.int32),
-                                          egress=np.array([c.EgressIfIndex for c in ctxs], np.int32),
-                                          schedule=L.SCHED_EXPLICIT, cpu=cpus)
-            res = self.vm.RunXDPBatch(pid, batch).numpy(len(js))
+        hr = [c.Headroom for c in ctxs]
+        batch = XDPBatch.from_packets([c.Packet for c in ctxs], device=dev, headroom=np.array(hr, np.uint32),
+                                      tailroom=np.array([c.Tailroom for c in ctxs], np.uint32),
+                                      ingress=np.array([c.IngessIfIndex for c in ctxs], np.int32),
+                                      rxq=np.array([c.RxQueueIndex for c in ctxs], np.int32),
+                                      egress=np.array([c.EgressIfIndex for c in ctxs], np.int32),
+                                      schedule=L.SCHED_EXPLICIT, cpu=cpus)
+        res = self.vm.RunXDPBatch(pid, batch).numpy(len(js))
         mem = batch.pkt_data.cpu().numpy()
         offs = batch.pkt_off.cpu().numpy()
         for k, j in enumerate(js):
@@ -1097,6 +1102,6 @@ class ProcessPool:
             p.Status = int(res["status"][k])
             p.ErrPC = int(res["err_pc"][k])
             c = ctxs[k]
-            tail = SKBBatch.TAILROOM if skb else c.Tailroom
+            tail = c.Tailroom
             o = int(offs[k])
             p.PacketAfter = bytes(mem[o:o + hr[k] + len(c.Packet) + tail].tobytes())

@@ -327,6 +327,11 @@ def make_packets(n: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: i
     starts at a multiple of `align` bytes."""
     rng = np.random.Generator(np.random.PCG64(seed))
     pool = _flow_pool(rng)
+    return _build_packets(rng, pool, n, sizes, weights, align, headroom, tailroom, _rows)
+
+
+def _build_packets(rng, pool, n, sizes, weights, align, headroom, tailroom, _rows=True):
+    """make_packets' body after the flow pool: every per-packet draw comes from `rng`."""
     w = np.asarray(weights, dtype=np.float64)
     lens = np.asarray(sizes, dtype=np.int64)[rng.choice(len(sizes), n, p=w / w.sum())]
     slot = (headroom + lens + tailroom + align - 1) // align * align
@@ -445,6 +450,117 @@ def _random_fill(total: int, rng) -> np.ndarray:
 
 
 IMIX = dict(sizes=(64, 576, 1500), weights=(7, 4, 1))
+
+# ---------------------------------------------------------------------------------------------
+# one batch, sharded: packets [lo, hi) of a conceptual batch of any size
+# ---------------------------------------------------------------------------------------------
+RANGE_BLOCK = 1 << 16
+
+
+def make_packet_range(lo: int, hi: int, sizes=(64,), weights=(1.0,), seed: int = SEED, align: int = 64,
+                      block: int = RANGE_BLOCK):
+    """Packets [lo, hi) of ONE conceptual batch, as (buf, off, lens) with offsets from 0.
+
+    Every packet is drawn from one flow pool (seed `seed`), and block k of `block` packets from
+    its own stream (SeedSequence((seed, k))): packet i has the same bytes whichever range
+    contains it, so ranges [r*n, (r+1)*n) for r = 0..N-1 are the N shards of one N*n batch, and
+    their flows -- hence the keys a flow-tracking program inserts -- all come from one 65 536-flow
+    pool (the bound that keeps cfg 4's shared table within MaxEntries at any N)."""
+    assert 0 <= lo <= hi
+    pool = _flow_pool(np.random.Generator(np.random.PCG64(seed)))
+    ks = list(range(lo // block, -(-hi // block)))
+
+    def one(k):
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence((seed, k))))
+        b, o, ln = _build_packets(rng, pool, block, sizes, weights, align, 0, 0)
+        a, e = max(lo, k * block) - k * block, min(hi, (k + 1) * block) - k * block
+        if a == 0 and e == block:
+            return b, o, ln
+        start = int(o[a])
+        end = int(o[e]) if e < block else len(b)
+        return b[start:end], o[a:e] - np.uint64(start), ln[a:e]
+
+    if len(ks) <= 1:
+        parts = [one(k) for k in ks]
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(min(8, len(ks))) as ex:
+            parts = list(ex.map(one, ks))
+    if not parts:
+        return np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+    sizes_b = [len(p[0]) for p in parts]
+    base = np.concatenate([[0], np.cumsum(sizes_b)[:-1]]).astype(np.uint64)
+    buf = np.concatenate([p[0] for p in parts])
+    off = np.concatenate([p[1] + base[j] for j, p in enumerate(parts)])
+    lens = np.concatenate([p[2] for p in parts])
+    return buf, off, lens
+
+
+def flowtrack_shard(n: int, rank: int, world: int, batch: int = 0, seed: int = SEED):
+    """cfg 4's input on rank `rank` of `world`: packets [(batch*world + rank)*n, +n) of ONE IMIX
+    batch (make_packet_range).  bench.py and the shard tests build every cfg-4 shard here, so the
+    union of the ranks' replicas is the key set of one batch drawn from one flow pool: at most
+    131 072 keys (65 536 flows x {IPv4, IPv6} key forms) = the map's MaxEntries at any N."""
+    lo = (batch * world + rank) * n
+    return make_packet_range(lo, lo + n, IMIX["sizes"], IMIX["weights"], seed)
+
+
+def flowtrack_value(keys: np.ndarray) -> np.ndarray:
+    """prog_flowtrack's value for each key row (flow_keys_np): u64(key[0:8]) * 0x01000193 ^
+    u64(key[8:16]), computed in the program's 64-bit register arithmetic."""
+    k = np.ascontiguousarray(keys, np.uint32).view(np.uint64).reshape(-1, 2)
+    with np.errstate(over="ignore"):
+        return (k[:, 0] * np.uint64(0x01000193)) ^ k[:, 1]
+
+
+def flow_keys_np(buf, off, lens) -> np.ndarray:
+    """The 16-byte keys prog_flowtrack / prog_flowcount build (_flow_key_items), one row per
+    packet that reaches the map call (IPv4 frames >= 38 bytes, IPv6 frames >= 58 bytes), as a
+    structured view for np.unique.  Host-side workload arithmetic (no engine, no oracle): it
+    bounds how many keys a cfg-4 batch inserts.  The key words are little-endian loads of the
+    frame bytes, stored as they were loaded, so a key's bytes are the frame's bytes."""
+    off = np.asarray(off, np.int64)
+    L = np.asarray(lens, np.int64)
+    ok = L >= 14
+    et = np.zeros(len(L), np.int64)
+    idx = off[ok][:, None] + np.array([12, 13])
+    et[ok] = (buf[idx[:, 0]].astype(np.int64) << 8) | buf[idx[:, 1]]
+    v4 = np.nonzero((et == 0x0800) & (L >= 38))[0]
+    v6 = np.nonzero((et == 0x86DD) & (L >= 58))[0]
+
+    def u32le(rows, at):   # a 4-byte little-endian load at frame offset `at`
+        b = buf[off[rows][:, None] + at + np.arange(4)].astype(np.uint32)
+        return b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16) | (b[:, 3] << 24)
+
+    def u64le(rows, at):
+        b = buf[off[rows][:, None] + at + np.arange(8)].astype(np.uint64)
+        return sum(b[:, q] << np.uint64(8 * q) for q in range(8))
+
+    k = np.zeros((len(v4) + len(v6), 4), np.uint32)
+    k[:len(v4), 0] = u32le(v4, 26)
+    k[:len(v4), 1] = u32le(v4, 30)
+    k[:len(v4), 2] = u32le(v4, 34)
+    k[:len(v4), 3] = buf[off[v4] + 23]
+
+    def fold(rows, a, b):
+        x = u64le(rows, a) ^ u64le(rows, b)
+        return ((x ^ (x >> np.uint64(32))) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+    k[len(v4):, 0] = fold(v6, 22, 30)
+    k[len(v4):, 1] = fold(v6, 38, 46)
+    k[len(v4):, 2] = u32le(v6, 54)
+    k[len(v4):, 3] = buf[off[v6] + 20]
+    return k
+
+
+def distinct_keys(*key_arrays) -> int:
+    """Number of distinct 16-byte keys over flow_keys_np() outputs."""
+    ks = [np.ascontiguousarray(k) for k in key_arrays if len(k)]
+    if not ks:
+        return 0
+    allk = np.concatenate(ks).view(np.dtype((np.void, 16)))
+    return len(np.unique(allk))
 
 
 def schedule_cpu(n: int, vcpus: int, mode: str = "chunked") -> np.ndarray:

@@ -40,6 +40,17 @@ def test_gpus_flag_launches_that_many_ranks():
         assert d["counters"] == [n * (n + 1) // 2, n]
 
 
+def test_flowtrack_selftest_merges_bench_size_replicas():
+    """--gpus N --config flowtrack --launch-selftest: every gloo rank builds its bench-size cfg-4
+    shard (2M IMIX packets of the one batch) and the (key, value) records its replica would
+    hold; the merge with the MaxEntries check (E = 131 072) completes at N = 2 and N = 8."""
+    for n, lo in ((2, 128000), (8, 131072)):
+        p = _run(["--gpus", str(n), "--config", "flowtrack", "--launch-selftest"], _env(OMP_NUM_THREADS="2"), timeout=600)
+        assert p.returncode == 0, p.stderr[-2000:]
+        d = _json_line(p.stdout)
+        assert d["n_gpus"] == n and lo <= d["hash_keys"] <= 131072, d
+
+
 def test_world_size_must_match_gpus_flag():
     p = _run(["--gpus", "2"], _env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
     assert p.returncode == 2

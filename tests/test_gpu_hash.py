@@ -30,8 +30,53 @@ def _fuzz(seed):
 
 
 def jit_kernels():
-    ps = [W.prog_flowtrack(), W.prog_flowcount(), W.prog_flowcount(delete_every=3), W.prog_flowcount(delete_every=1)]
+    ps = [W.prog_flowtrack(), W.prog_flowcount(), W.prog_flowcount(delete_every=3), W.prog_flowcount(delete_every=1),
+          _prog_lookup40()]
     return [kernel_of(_sc(p, 1)) for p in ps] + [kernel_of(_fuzz(s)[0]) for s in range(12)]
+
+
+# Two 40-byte keys with the same first 32 bytes whose hashes (hashmap.h h_hash) share the 32-bit
+# tag and the home bucket of a 16-bucket table (found by a birthday search over the fifth word):
+# a probe for K40_B walks onto K40_A's record and only the fifth key word tells them apart.
+K40_HEAD = bytes(range(0x40, 0x60))
+K40_A = K40_HEAD + (0x5bbcc34050cdefea).to_bytes(8, "little")
+K40_B = K40_HEAD + (0x23a78ebaf790394a).to_bytes(8, "little")
+
+
+def _prog_lookup40() -> W.Program:
+    """Lookup-only program (no update / delete: the read-only probe h_find_ro) over a 40-byte
+    key copied from the packet's first 40 bytes: R0 = the value when found, 0xdead when absent,
+    1 for a short packet."""
+    from mimic_amd import asm as A
+
+    items = [A.mov64_reg(6, 1), A.ldx(4, 2, 6, 0), A.ldx(4, 3, 6, 4), A.mov64_reg(4, 2), A.alu64("add", 4, 40),
+             A.jmp("jgt", 4, 3, "short", reg=True)]
+    for q in range(5):
+        items += [A.ldx(8, 1, 2, 8 * q), A.stx(8, 10, -40 + 8 * q, 1)]
+    items += [A.mov64_reg(2, 10), A.alu64("add", 2, -40), A.ld_map_fd(1, "k40"), A.call(A.FN_MAP_LOOKUP_ELEM),
+              A.mov64_imm(7, 0xdead), A.jmp("jeq", 0, 0, "miss"), A.ldx(8, 7, 0, 0), "miss", A.mov64_reg(0, 7),
+              A.exit_(), "short", A.mov64_imm(0, 1), A.exit_()]
+    raw, rel = A.assemble(items)
+    return W.Program("lookup40", raw, rel, [dict(name="k40", type=1, key_size=40, value_size=8, max_entries=4)])
+
+
+@pytest.mark.parametrize("exec_mode", ["jit", "interp"])
+def test_lookup_40_byte_keys_compare_every_word(gpu, exec_mode):
+    """Keys longer than 32 bytes in a lookup-only launch: the fifth key word decides (ADVICE r3:
+    h_find_ro compared words 0..3 only and answered K40_B with K40_A's slot)."""
+    p = _prog_lookup40()
+    rng = np.random.default_rng(40)
+    others = [bytes(rng.integers(0, 256, 40, dtype=np.uint8)) for _ in range(3)]
+    sc = Scenario(vcpus=4, maps=p.maps, progs=[(p.name, p.raw, p.relocs)],
+                  map_init=[("k40", K40_A, (0x1111).to_bytes(8, "little"), 0),
+                            ("k40", others[0], (0x2222).to_bytes(8, "little"), 0)])
+    pk = [K40_A, K40_B, others[0], others[1], K40_B + b"tail", K40_A[:39]] * 50
+    buf, off, lens = packets_to_buffer(pk)
+    cpu = W.schedule_cpu(len(pk), 4, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu, exec_mode=exec_mode)
+    assert_same(o, e)
+    assert list(np.asarray(e["r0"][:6]).astype(np.int64)) == [0x1111, 0xdead, 0x2222, 0xdead, 0xdead, 1]
 
 
 @pytest.mark.parametrize("mtype", [1, 5])

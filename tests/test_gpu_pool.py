@@ -36,6 +36,65 @@ def jit_kernels():
     return [kernel_of(_sc(1)), kernel_of(_order_sc(2))]
 
 
+def _addr_prog():
+    """sk_buff program: R0 = flow_keys pointer << 32 | skb->data (the addresses its Load leaked)."""
+    S = A.SKB
+    raw, _ = A.assemble([A.mov64_reg(6, 1), A.ldx(4, 0, 6, S["data"]), A.ldx(4, 2, 6, S["flow_keys"]),
+                         A.alu64("lsh", 2, 32), A.alu64("or", 0, 2, reg=True), A.exit_()])
+    return raw
+
+
+def test_pool_skb_jobs_run_on_their_own_load(gpu):
+    """an sk_buff process's Load runs at NewProcess (its sock / flow keys / packet
+    take the VM's next leak addresses then); the pool worker only calls Run (vm.go:570).  Pooled
+    jobs must see the same addresses as the same processes run one at a time, and the VM's leak
+    cursor must move once per process (a process made after the pool lands where it would)."""
+    raw = _addr_prog()
+    buf, off, lens = W.make_skb_packets(12, (64, 576, 1500), (1, 1, 1), seed=5)
+    pk = [bytes(buf[int(o) + 32:int(o) + 32 + int(n)]) for o, n in zip(off, lens)]
+
+    def fresh():
+        vm = M.NewVM(M.VMOptEmulator(M.NewLinuxEmulator()), M.VMOptSetvCPUs(3))
+        return vm, vm.AddProgram(M.ProgramSpec("addr", raw))
+
+    vm1, pid1 = fresh()
+    want = []
+    for p in pk:
+        proc = vm1.NewProcess(pid1, M.LinuxContextSKBuff(Packet=p))
+        proc.Run()
+        want.append(proc.Registers.R0)
+        proc.Cleanup()
+    after1 = vm1.NewProcess(pid1, M.LinuxContextSKBuff(Packet=pk[0]))
+    after1.Run()
+
+    vm2, pid2 = fresh()
+    pool = vm2.GetProcessPool()
+    pool.Start(64)
+    got = {}
+    mu = threading.Lock()
+
+    def handoff(proc, err):
+        with mu:
+            got[proc.idx] = (proc.Registers.R0, err)
+
+    for i, p in enumerate(pk):
+        proc = vm2.NewProcess(pid2, M.LinuxContextSKBuff(Packet=p))
+        proc.idx = i
+        pool.Enqueue(M.ProcessPoolJob(proc, None, handoff))
+    pool.Stop()
+    t0 = time.time()
+    while len(got) < len(pk) and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert [got[i][1] for i in range(len(pk))] == [None] * len(pk)
+    assert [got[i][0] for i in range(len(pk))] == want
+    assert len(set(want)) == len(pk)   # every process leaked its own addresses
+    after2 = vm2.NewProcess(pid2, M.LinuxContextSKBuff(Packet=pk[0]))
+    after2.Run()
+    assert after2.Registers.R0 == after1.Registers.R0
+    vm1.close()
+    vm2.close()
+
+
 @pytest.mark.parametrize("backlog", [16, 4096])
 def test_pool_runs_jobs_like_the_oracle(gpu, backlog):
     V = 8

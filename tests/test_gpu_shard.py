@@ -5,7 +5,7 @@ steps, every vCPU's per-CPU map bytes, and (cfg 4) the merged hash replicas' key
 import numpy as np
 import pytest
 
-from harness import Scenario, build_engine, kernel_of, run_oracle
+from harness import Scenario, build_engine, build_oracle, kernel_of, run_oracle
 from mimic_amd import dist as D
 from mimic_amd import workloads as W
 
@@ -19,7 +19,8 @@ def _sc(p, vcpus):
 
 
 def jit_kernels():
-    return [kernel_of(_sc(W.prog_classifier(), 1)), kernel_of(_sc(W.prog_flowtrack(max_entries=65536), 1))]
+    return [kernel_of(_sc(W.prog_classifier(), 1)), kernel_of(_sc(W.prog_flowtrack(max_entries=65536), 1)),
+            kernel_of(_sc(W.prog_flowtrack(), 1))]
 
 
 def _run_shards(sc, buf, off, lens, cpu, nshards):
@@ -41,6 +42,42 @@ def _run_shards(sc, buf, off, lens, cpu, nshards):
         outs.append((sel, res, vals, hashes))
         vm.close()
     return outs
+
+
+def test_cfg4_bench_size_two_engines_merge_to_oracle(gpu):
+    """cfg 4 exactly as `bench.py --gpus 2 --config flowtrack` shards it, on one GPU: two engines
+    own vCPUs [0, 262144) and [262144, 524288) (VMOptShard) and each runs its 2M-packet shard of
+    the ONE batch (workloads.flowtrack_shard) into its own E = 131 072 replica.  The merged
+    replicas (MaxEntries checked) equal one oracle VM running both shards on one table, key by
+    key, and the per-packet verdicts are the single table's."""
+    import mimic_amd as M
+
+    n, vr, ws = 1 << 21, 1 << 18, 2
+    p = W.prog_flowtrack()
+    assert p.maps[0]["max_entries"] == 131072
+    sc = _sc(p, vr * ws)
+    ovm, mids, pids = build_oracle(sc)
+    blobs = []
+    for r in range(ws):
+        buf, off, lens = W.flowtrack_shard(n, r, ws)
+        b0 = r * vr
+        vm, maps, epids = build_engine(sc, shard=(b0, vr))
+        batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", ingress=1, schedule=M.SCHED_INTERLEAVED)
+        e = vm.RunXDPBatch(epids[0], batch).numpy(n)
+        mine = {k: v[0] for k, v in maps["flows"].Contents().items()}
+        vm.close()
+        del batch
+        o = ovm.run_xdp_batch(pids[0], buf, off, lens, b0 + W.schedule_cpu(n, vr, "interleaved"), ingress=1,
+                              write_back=False)
+        assert np.array_equal(np.asarray(o["r0"]).astype(np.uint64), np.asarray(e["r0"]).astype(np.uint64)), r
+        assert np.array_equal(np.asarray(o["status"]).astype(np.int64), np.asarray(e["status"]).astype(np.int64)), r
+        assert 110000 < len(mine) <= 131072
+        blobs.append(D.replica_blob(mine))
+    vals = ovm.map_values(mids["flows"], 0)
+    want = {k: vals[s * 8:(s + 1) * 8] for k, s in ovm.map_entries(mids["flows"])}
+    ovm.close()
+    merged = D.merge_records(blobs, 16, 8, max_entries=131072)
+    assert merged == want and len(want) > 120000
 
 
 def _merge_results(n, outs):
