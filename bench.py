@@ -117,8 +117,8 @@ class Workload:
             self.map_init = []
         self.ctx = 1 if self.skb else 0
 
-    def kernel_src_hash(self) -> str:
-        return kernel_src_hash_of(self.name)
+    def kernel_src_hash(self, spread_vcpus: int = 0) -> str:
+        return kernel_src_hash_of(self.name, spread_vcpus)
 
     def build_vm(self, M, V, device, shard, raws):
         emu = M.NewLinuxEmulator()
@@ -136,9 +136,10 @@ class Workload:
         return vm, maps, pids
 
 
-def kernel_src_hash_of(cfg_name: str) -> str:
-    """sha256 (16 hex) of the JIT kernel source the config's programs generate: the key that ties
-    a committed rocprofv3 summary to the exact kernel it measured."""
+def kernel_src_hash_of(cfg_name: str, spread_vcpus: int = 0) -> str:
+    """sha256 (16 hex) of the JIT kernel source the config's programs generate (spread_vcpus > 0:
+    the spread kernel a VM of that many vCPUs per engine builds): the key that ties a committed
+    rocprofv3 summary to the exact kernel it measured."""
     from mimic_amd import jit as J
     from mimic_amd import workloads as W
 
@@ -147,7 +148,13 @@ def kernel_src_hash_of(cfg_name: str) -> str:
         progs, ctx = W.skb_programs()[0], 1
     else:
         progs, ctx = [getattr(W, cfg["prog"])()], 0
-    h = hashlib.sha256(J.kernel_source([p.raw for p in progs], ctx).encode())
+    if spread_vcpus:
+        maps = progs[0].maps
+        src = J.kernel_source([p.raw for p in progs], ctx, (),
+                              J.spread_spec([(p.raw, p.relocs) for p in progs], maps, spread_vcpus))
+    else:
+        src = J.kernel_source([p.raw for p in progs], ctx)
+    h = hashlib.sha256(src.encode())
     for f in ("mimic_amd/csrc/layout.h", "mimic_amd/csrc/hashmap.h", "mimic_amd/csrc/skb.h", "mimic_amd/csrc/runtime.h",
               "include/mimic_amd.h"):   # the headers embedded into every JIT kernel
         with open(os.path.join(ROOT, f), "rb") as fh:
@@ -524,8 +531,8 @@ def main(argv=None):
         alg = sum(algorithmic_bytes(batches[b][0].lens, vpg, wl.maps, wl.cfg.get("reads_packet", True))
                   for b in timed) / len(timed)
         achieved = alg / avg_launch_s
-        kernel = "mimic_jit_kernel" if vm.LastExec() == "jit" else "mimic_xdp_kernel"
-        src_hash = wl.kernel_src_hash()
+        kernel = "mimic_jit_kernel" if vm.LastExec() in ("jit", "spread") else "mimic_xdp_kernel"
+        src_hash = wl.kernel_src_hash(vpg if vm.LastExec() == "spread" else 0)
         prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched)
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",

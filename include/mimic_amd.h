@@ -105,6 +105,7 @@ typedef struct {
 #define MIMIC_EXEC_DEFAULT 0
 #define MIMIC_EXEC_INTERP 1   /* the batch interpreter kernel (interp.hip) */
 #define MIMIC_EXEC_JIT 2      /* per-program-set kernels generated from the loaded programs, hipRTC-compiled */
+#define MIMIC_EXEC_SPREAD 3   /* mimic_last_exec only: the JIT's spread kernel (a vCPU's packets on many lanes) */
 
 typedef struct {
     const char *name;
@@ -307,6 +308,14 @@ int mimic_host_unregister(void *p);
 
 /* Execution mode the VM resolved to (MIMIC_EXEC_INTERP / MIMIC_EXEC_JIT). */
 int mimic_exec_mode(const mimic_vm *vm);
+/* Spread launches (no reference counterpart: an engine schedule for processPool's jobs,
+ * vm.go:548-573).  When every per-CPU access of the loaded xdp_md programs is a fused counter
+ * increment through one per-CPU array lookup, a vCPU's packets may run on many lanes (the final
+ * counters are sums; each packet's R0 / status / steps depend on its own bytes only).
+ * mode -1: default (env MIMIC_SPREAD, else when a batch has >= 8 packets per vCPU), 0: never,
+ * 1: whenever the programs allow it.  mimic_sync / mimic_last_steps fail if a spread launch
+ * reached per-CPU memory outside a fused increment. */
+int mimic_set_spread(mimic_vm *vm, int32_t mode);
 /* The kernel the last batch ran on (a JIT VM runs batches whose step budget is below its
  * loop-free kernels' step bound on the interpreter). */
 int mimic_last_exec(const mimic_vm *vm);
@@ -325,6 +334,13 @@ int mimic_jit_prebuild_ctx(const void *const *progs, const uint32_t *n_slots, ui
  * holds n_vc (program index, slot) pairs.  mimic_jit_source_for_ctx is this with n_vc = 0. */
 long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
                          const uint32_t *vc_slots, uint32_t n_vc, char *buf, size_t cap);
+/* The spread kernel's source (mimic_set_spread): pc = (program, slot, map id) triples of the
+ * LD_IMM64 slots naming a per-CPU array's object, shapes = (map id, E * S, S) triples, lds_rows =
+ * rows of a block's LDS counter table (min(1024, V) when rows * E * S <= 32 KiB, else 0).
+ * *spread_out = 1 when the programs allow a spread kernel. */
+long mimic_jit_source_spread(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, const uint32_t *pc,
+                             uint32_t n_pc, const uint32_t *shapes, uint32_t n_shapes, uint32_t lds_rows,
+                             int32_t *spread_out, char *buf, size_t cap);
 /* Compile a kernel source (as mimic_jit_source_for_ctx returns it) into the MIMIC_JIT_CACHE
  * directory (host only; a no-op when it is already there).  Lets a test session or a deploy
  * step build many kernels in parallel processes before any device is touched. */

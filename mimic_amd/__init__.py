@@ -5,7 +5,7 @@ interpreter (csrc/interp.hip) + C++ host engine (csrc/engine.cpp) behind the C A
 """
 from .vm import (Context, ProcessPool, ProcessPoolJob, E2BIG, LinuxArrayMap, LinuxContextSKBuff, LinuxContextXDP, NetDev, SKBBatch, LinuxEmulator, LinuxHashMap, LinuxMap, LinuxPerCPUArrayMap,
                  LinuxPerCPUHashMap, MapSpec, MapSpecToLinuxMap, MapType, MimicError, NewLinuxEmulator, NewVM, OptMaxTailCalls, Process,
-                 ProgramSpec, UnmarshalContextJSON, VM, VMOptDevice, VMOptEmulator, VMOptExecMode, VMOptSetvCPUs, VMOptShard,
+                 ProgramSpec, UnmarshalContextJSON, VM, VMOptDevice, VMOptEmulator, VMOptExecMode, VMOptSetvCPUs, VMOptShard, VMOptSpread,
                  XDPBatch, XDPResults)
 from ._lib import STATUS, STATUS_NAMES, SCHED_CHUNKED, SCHED_EXPLICIT, SCHED_INTERLEAVED
 

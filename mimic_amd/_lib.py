@@ -92,6 +92,7 @@ EXPORTS = {
     "mimic_map_lookup": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.POINTER(C.c_uint32)]),
     "mimic_map_delete": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "mimic_exec_mode": (C.c_int, [C.c_void_p]),
+    "mimic_set_spread": (C.c_int, [C.c_void_p, C.c_int32]),
     "mimic_run_xdp_host": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPHostBatch), C.c_uint32]),
     "mimic_host_register": (C.c_int, [C.c_void_p, C.c_size_t]),
     "mimic_host_unregister": (C.c_int, [C.c_void_p]),
@@ -121,6 +122,9 @@ EXPORTS = {
                                              C.c_char_p, C.c_size_t]),
     "mimic_jit_source_vc": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32,
                                        C.POINTER(C.c_uint32), C.c_uint32, C.c_char_p, C.c_size_t]),
+    "mimic_jit_source_spread": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32,
+                                           C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32,
+                                           C.c_uint32, C.POINTER(C.c_int32), C.c_char_p, C.c_size_t]),
     "mimic_jit_prebuild_ctx": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32]),
     "mimic_jit_cache_source": (C.c_int, [C.c_char_p]),
     "mimic_process_new": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,

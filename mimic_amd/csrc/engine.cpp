@@ -109,6 +109,16 @@ struct mimic_vm {
     std::vector<DProg> h_dp;
     hipFunction_t jit_fn[2] = {nullptr, nullptr};   // per CtxKind, generated on first use
     JitInfo jit_info[2]{};
+    // the spread kernel (jit.cpp analyze_spread, xdp_md only): 0 not built yet, 1 built, -1 the
+    // program set does not allow it; spread_bad is the device word a spread launch marks when a
+    // generic access reached per-CPU memory (spread_used: some launch could have marked it)
+    int spread_state = 0;
+    hipFunction_t jit_fn_spread = nullptr;
+    JitInfo jit_info_spread{};
+    uint32_t *d_spread_bad = nullptr;
+    bool spread_used = false;
+    int spread_mode = -1;   // mimic_set_spread: -1 the default policy (env MIMIC_SPREAD), 0 never, 1 whenever allowed
+    bool spread_lds = false;   // the spread kernel keeps a block's counters in LDS (else agent-scope atomics)
     int last_exec = 0;          // the kernel the last batch ran on
     // launch parameters of JIT kernels in device memory: a ring of slots written by
     // stream-ordered copies from pinned host memory (a repeated batch reuses its slot)
@@ -431,6 +441,8 @@ static int upload_tables(mimic_vm *vm) {
         }
     }
     vm->jit_fn[0] = vm->jit_fn[1] = nullptr;
+    vm->jit_fn_spread = nullptr;
+    vm->spread_state = 0;
     std::vector<DInsn> all = vm->h_all;
     std::vector<DProg> dp = vm->h_dp;
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
@@ -584,6 +596,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_sched_start);
     hipFree(vm->d_sched_pkts);
     hipFree(vm->d_lane_steps);
+    hipFree(vm->d_spread_bad);
     hipFree(vm->d_defer);
     hipFree(vm->d_defer_any);
     hipFree(vm->d_kp);
@@ -1246,6 +1259,70 @@ static PrivPlan priv_plan(const mimic_vm *vm) {
     return p;
 }
 
+// The spread kernel of the VM's xdp_md programs (jit.cpp analyze_spread), built once per program
+// set: the VM's per-CPU arrays whose values the arena keeps 8-byte aligned are the candidates; the
+// analysis names the one map the programs count into, and the kernel is then generated with an
+// LDS counter table when a block's rows fit 32 KiB.
+static int spread_build(mimic_vm *vm) {
+    if (vm->spread_state) return 0;
+    vm->spread_state = -1;
+    SpreadReq req;
+    for (size_t s = 0; s < vm->h_all.size(); s++) {
+        const DInsn &x = vm->h_all[s];
+        const uint32_t mh = AUX_MAPHINT(x.aux);
+        if (AUX_H(x.aux) != H_LDIMM || !mh || mh > vm->maps.size()) continue;
+        const HostMap &hm = vm->maps[mh - 1];
+        const DMap dm = to_dmap(hm);
+        if (hm.family != FAM_PERCPU_ARRAY || (dm.dev_off & 7) || (dm.dev_stride & 7)) continue;
+        req.slot_map[(uint32_t)s] = mh - 1;
+        req.shape[mh - 1] = {hm.max_entries * hm.value_size, hm.value_size};
+    }
+    if (req.slot_map.empty()) return 0;
+    JitInfo info{};
+    std::string src = mimic_jit_source(vm->h_dp, vm->h_all, CTX_XDP, &info, nullptr, false, &req);
+    if (!info.spread) return 0;
+    // the counted map and its row: an LDS table of min(ppb, V) rows when that fits 32 KiB
+    uint32_t row = 0;
+    for (auto &kv : req.shape) row = std::max(row, kv.second.first);
+    const uint64_t rows = std::min<uint64_t>(req.ppb, (uint64_t)vm->s.vcpu_count);
+    if (rows * row <= 32768) {
+        req.lds_rows = (uint32_t)rows;
+        src = mimic_jit_source(vm->h_dp, vm->h_all, CTX_XDP, &info, nullptr, false, &req);
+    }
+    vm->spread_lds = req.lds_rows > 0;
+    std::string log;
+    if (mimic_jit_compile(vm->s.device, src, &vm->jit_fn_spread, &log))
+        return fail(vm, MIMIC_EDEVICE, "JIT build failed (spread kernel): %s", log.c_str());
+    vm->jit_info_spread = info;
+    vm->spread_state = 1;
+    return 0;
+}
+
+// The VM's private memory for `lanes` lanes of q_per_lane qwords, qword-interleaved with stride
+// vm->priv_lanes >= lanes (a launch with fewer lanes uses the larger stride as it is)
+static int priv_ensure(mimic_vm *vm, uint32_t q_per_lane, uint32_t lanes, hipStream_t st) {
+    const uint32_t stride = std::max(lanes, vm->priv_lanes);
+    const uint64_t need = (uint64_t)q_per_lane * stride * 8;
+    if (vm->priv && need <= vm->priv_bytes) return 0;
+    hipStreamSynchronize(st);
+    hipFree(vm->priv);
+    vm->priv = nullptr;
+    HIP_OK(vm, hipMalloc(&vm->priv, std::max<uint64_t>(need, 8)));
+    vm->priv_bytes = std::max<uint64_t>(need, 8);
+    vm->priv_lanes = stride;
+    return 0;
+}
+
+// a spread launch marked per-CPU memory touched outside fused increments: its results may not be
+// the reference's, which is reported as an engine error (the stream has been synchronized)
+static int spread_check(mimic_vm *vm) {
+    if (!vm->spread_used || !vm->d_spread_bad) return 0;
+    uint32_t f = 0;
+    HIP_OK(vm, hipMemcpy(&f, vm->d_spread_bad, 4, hipMemcpyDeviceToHost));
+    if (f) return fail(vm, MIMIC_EDEVICE, "a spread launch reached per-CPU map memory outside a fused increment");
+    return 0;
+}
+
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                         hipStream_t st_in, uint64_t first_index, const SkbRun *skb, const StepRun *step) {
     if (!vm || !b || !res) return MIMIC_EINVAL;
@@ -1273,16 +1350,11 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     const PrivPlan pp = priv_plan(vm);
     const uint32_t xdp_q = pp.xdp_q, frame_q = pp.frame_q, key_q = pp.key_q, q_per_lane = pp.q_per_lane;
     const uint32_t plan = (lanes + 255) & ~255u;
-    const uint64_t need = (uint64_t)q_per_lane * plan * 8;
     if (step) {
         if (step->priv_bytes < (uint64_t)q_per_lane * 8) return fail(vm, MIMIC_EINVAL, "process private memory too small");
-    } else if (need > vm->priv_bytes || plan != vm->priv_lanes) {
-        hipStreamSynchronize(st);
-        hipFree(vm->priv);
-        vm->priv = nullptr;
-        HIP_OK(vm, hipMalloc(&vm->priv, need));
-        vm->priv_bytes = need;
-        vm->priv_lanes = plan;
+    } else {
+        rc = priv_ensure(vm, q_per_lane, plan, st);
+        if (rc) return rc;
     }
     if (lanes > vm->lane_steps_cap) {
         hipStreamSynchronize(st);
@@ -1423,10 +1495,53 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             }
         }
     }
-    const JitInfo &ji = vm->jit_info[ctx];
     if (jit) {  // a loop-free kernel has no budget checks: tiny budgets run on the interpreter
-        const uint64_t bound = mimic_jit_step_bound(ji, kp.max_tail_calls);
+        const uint64_t bound = mimic_jit_step_bound(vm->jit_info[ctx], kp.max_tail_calls);
         if (bound && kp.budget < bound) jit = false;
+    }
+    // Spread launch (jit.cpp analyze_spread): a vCPU's packets on many lanes, for batches where
+    // every vCPU has many packets (the one-lane-per-vCPU kernel would run them as one serial chain
+    // per lane, e.g. V = runtime.NumCPU(), vm.go:64).  MIMIC_SPREAD=0: never; =1: whenever the
+    // program set allows it; default: when n >= 8 V.
+    bool spread = false;
+    if (jit && !skb && b->n > 0 && (b->schedule == MIMIC_SCHED_CHUNKED || b->schedule == MIMIC_SCHED_INTERLEAVED)) {
+        const char *sv = getenv("MIMIC_SPREAD");
+        const int knob = vm->spread_mode >= 0 ? vm->spread_mode : sv && *sv ? atoi(sv) : -1;
+        if (knob == 1 || (knob != 0 && (uint64_t)b->n >= 8ull * cpu_lanes)) {
+            rc = spread_build(vm);
+            if (rc) return rc;
+            spread = vm->spread_state > 0 && mimic_jit_step_bound(vm->jit_info_spread, kp.max_tail_calls) <= kp.budget;
+            // without the LDS table every increment is a scattered agent-scope atomic: worth it only
+            // when the one-lane-per-vCPU kernel has few lanes
+            if (knob != 1 && !vm->spread_lds && cpu_lanes > 16384) spread = false;
+        }
+    }
+    const JitInfo &ji = spread ? vm->jit_info_spread : vm->jit_info[ctx];
+    hipFunction_t jfn = spread ? vm->jit_fn_spread : vm->jit_fn[ctx];
+    uint32_t run_lanes = lanes;
+    if (spread) {
+        const SpreadReq sr0;
+        const uint32_t blocks = (uint32_t)(((uint64_t)b->n + sr0.ppb - 1) / sr0.ppb);
+        run_lanes = blocks * 256u;
+        rc = priv_ensure(vm, q_per_lane, run_lanes, st);   // private memory (stack ...) per spread lane
+        if (rc) return rc;
+        if (run_lanes > vm->lane_steps_cap) {
+            hipStreamSynchronize(st);
+            hipFree(vm->d_lane_steps);
+            vm->d_lane_steps = nullptr;
+            HIP_OK(vm, hipMalloc(&vm->d_lane_steps, (uint64_t)run_lanes * sizeof(uint64_t)));
+            vm->lane_steps_cap = run_lanes;
+        }
+        if (!vm->d_spread_bad) {
+            HIP_OK(vm, hipMalloc(&vm->d_spread_bad, 64));
+            HIP_OK(vm, hipMemset(vm->d_spread_bad, 0, 64));
+        }
+        kp.lanes = run_lanes;
+        kp.priv = vm->priv;
+        kp.priv_lanes = vm->priv_lanes;
+        kp.lane_steps = vm->d_lane_steps;
+        kp.spread_bad = vm->d_spread_bad;
+        vm->spread_used = true;
     }
     kp.skb_rec_built = 1;
     if (skb && step && step->skb_rec) {   // a stepped sk_buff process: Load ran at NewProcess
@@ -1470,7 +1585,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
-    vm->last_exec = jit ? MIMIC_EXEC_JIT : MIMIC_EXEC_INTERP;
+    vm->last_exec = jit ? (spread ? MIMIC_EXEC_SPREAD : MIMIC_EXEC_JIT) : MIMIC_EXEC_INTERP;
     if (jit && ji.defer) {   // the lanes' suspended processes (DeferRec) and the launch's marker
         if (lanes > vm->defer_cap || !vm->d_defer_any) {
             hipStreamSynchronize(st);
@@ -1490,7 +1605,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.defer_epoch = vm->defer_epoch;
     }
     if (jit && ji.karg) {  // launch parameters by value: the runtime copies them into the kernarg segment
-        if (mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, nullptr, st))
+        if (mimic_jit_launch(jfn, ji, &kp, nullptr, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         // the interpreter finishes what the kernel deferred (a wave without a deferred lane returns at once)
         if (ji.defer && mimic_launch_xdp_resume(&kp, st))
@@ -1499,14 +1614,14 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         const KParams *dkp = nullptr;
         const int slot = kp_slot(vm, kp, st, &dkp);
         if (slot < 0) return slot;
-        if (jit ? mimic_jit_launch(vm->jit_fn[ctx], ji, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
+        if (jit ? mimic_jit_launch(jfn, ji, &kp, dkp, st) : mimic_launch_xdp(&kp, dkp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         if (jit && ji.defer && mimic_launch_xdp_resume(&kp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));   // the slot is free again once this passes
         vm->kp_used[slot] = true;
     }
-    vm->last_lanes = lanes;
+    vm->last_lanes = run_lanes;
     vm->last_stream = st;
     return 0;
 }
@@ -1771,7 +1886,7 @@ int mimic_sync(mimic_vm *vm, void *hip_stream) {
     hipSetDevice(vm->s.device);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
     HIP_OK(vm, hipStreamSynchronize(st));
-    return 0;
+    return spread_check(vm);
 }
 
 int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out) {
@@ -1785,10 +1900,15 @@ int mimic_last_steps(mimic_vm *vm, uint64_t *steps_out) {
     uint64_t t = 0;
     for (uint64_t v : h) t += v;
     *steps_out = t;
-    return 0;
+    return spread_check(vm);
 }
 
 int mimic_exec_mode(const mimic_vm *vm) { return vm ? vm->exec_mode : MIMIC_EINVAL; }
+int mimic_set_spread(mimic_vm *vm, int32_t mode) {
+    if (!vm || mode < -1 || mode > 1) return MIMIC_EINVAL;
+    vm->spread_mode = mode;
+    return 0;
+}
 int mimic_last_exec(const mimic_vm *vm) { return vm ? vm->last_exec : MIMIC_EINVAL; }
 
 // The JIT kernel source for a set of raw programs (slots as mimic_program_load takes them; map
@@ -1821,6 +1941,36 @@ long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint
         vc.push_back(dp[p].base + s);
     }
     const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr, &vc);
+    if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);
+    return (long)src.size();
+}
+
+// The spread kernel's source for raw programs (host only): pc = (program, slot, map id) triples of
+// the LD_IMM64 slots naming a per-CPU array's object, shapes = (map id, E * S, S) triples, lds_rows
+// as spread_build() picks it.  *spread_out = 1 when the programs allow a spread kernel (else the
+// returned source is the plain one).
+long mimic_jit_source_spread(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, const uint32_t *pc,
+                             uint32_t n_pc, const uint32_t *shapes, uint32_t n_shapes, uint32_t lds_rows,
+                             int32_t *spread_out, char *buf, size_t cap) {
+    std::vector<HostProg> hp(n_progs);
+    for (uint32_t p = 0; p < n_progs; p++) {
+        std::string err;
+        if (decode_program((const uint8_t *)progs[p], n_slots[p], hp[p].ins, &err)) return MIMIC_EINVAL;
+    }
+    std::vector<DInsn> all;
+    std::vector<DProg> dp;
+    build_host_tables(hp, all, dp);
+    SpreadReq req;
+    for (uint32_t q = 0; q < n_pc; q++) {
+        const uint32_t p = pc[3 * q], sl = pc[3 * q + 1];
+        if (p >= dp.size() || sl >= dp[p].n) return MIMIC_EINVAL;
+        req.slot_map[dp[p].base + sl] = pc[3 * q + 2];
+    }
+    for (uint32_t q = 0; q < n_shapes; q++) req.shape[shapes[3 * q]] = {shapes[3 * q + 1], shapes[3 * q + 2]};
+    req.lds_rows = lds_rows;
+    JitInfo info{};
+    const std::string src = mimic_jit_source(dp, all, MIMIC_CTX_XDP, &info, nullptr, false, &req);
+    if (spread_out) *spread_out = info.spread ? 1 : 0;
     if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);
     return (long)src.size();
 }

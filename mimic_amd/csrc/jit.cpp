@@ -205,6 +205,9 @@ class Gen {
     bool vc_knob = true;       // MIMIC_JIT_VC=0: no lane value cache (analyze_vc)
     uint32_t lds_stack_q = 16; // MIMIC_JIT_LDSSTK=Q: LDS window over the top 8Q bytes of frame 0
     bool vc_on = false;
+    const SpreadReq *spread_req = nullptr;   // the VM's per-CPU arrays: spread mode is possible (analyze_spread)
+    bool spread_on = false;
+    uint32_t spread_map = 0, spread_n = 0, spread_row = 0;   // the counted map, counter width, E * S
     std::set<uint32_t> vc_ok;  // LD_IMM64 slots (kernel-wide) naming a per-CPU array whose row can be cached
     uint32_t vc_slot = 0;      // the LD_IMM64 slot (kernel-wide index) whose map hint names the cached map
     // The cross-packet window prefetch (analyze_xpf): the entry program `prog` makes its first
@@ -279,6 +282,10 @@ class Gen {
             for (auto &p : P) analyze_fwd(p);
         if (forward && elide)
             for (auto &p : P) analyze_elide(p);
+        if (speculate && fast_paths && !stage && !all_leaders)
+            for (auto &p : P) analyze_spec(p);
+        spread_on = analyze_spread();
+        if (spread_on) vc_on = false;   // no lane owns a vCPU's row in a spread kernel
         // the LDS stack window (runtime.h) when some stack store is made for real (not deferred
         // into a cold path, analyze_elide).  Measured: cfg 4 0.197 -> 0.179 ms per launch; the
         // sk_buff kernels keep their LDS for the SkbRec slots (with the window as well: cfg 5
@@ -305,6 +312,7 @@ class Gen {
                 d.clear();
             }
         }
+        if (spread_on) E.line("#define MIMIC_SPREAD 1");
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         {   // no program of the set updates or deletes: hash tables are read-only in every launch
@@ -316,6 +324,20 @@ class Gen {
             E.line("#define MIMIC_HASH_RO %d", writes ? 0 : 1);
         }
         E.line("#include \"runtime.h\"");
+        if (spread_on) {
+            // the block's counter table: one row of SPREAD_ROWW counters per vCPU its packets run on
+            E.line("#define SPREAD_MAP %uu        // the per-CPU array the fused increments go to", spread_map);
+            E.line("#define SPREAD_N %uu          // counter width (bytes)", spread_n);
+            E.line("#define SPREAD_ROWW %uu       // counters per vCPU row (E * S / N)", spread_row / spread_n);
+            E.line("#define SPREAD_ROWS %uu       // LDS table rows (0: agent-scope atomics into the map)", spread_req->lds_rows);
+            E.line("#define SPREAD_PPB %uu        // packets per block", spread_req->ppb);
+            E.line("typedef %s spread_t;", spread_n == 8 ? "unsigned long long" : "uint32_t");
+            E.line("#if SPREAD_ROWS");
+            E.line("#define spread_add(k_) __hip_atomic_fetch_add(&sacc_[srow_ * SPREAD_ROWW + (uint32_t)(ga_ - L.t_lo) / SPREAD_N], (spread_t)(k_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)");
+            E.line("#else");
+            E.line("#define spread_add(k_) __hip_atomic_fetch_add((GAS spread_t *)(L.t_ptr + (uint32_t)(ga_ - L.t_lo)), (spread_t)(k_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)");
+            E.line("#endif");
+        }
         E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
         // Around a cold call the lane state and the argument / result registers go through the
         // Spill record (runtime.h); only what a cold path can change comes back.
@@ -362,7 +384,7 @@ class Gen {
         }
         E.line("  const KParams &kp = *kpp;");
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
-        E.line("  if (g >= kp.lanes) return;");
+        if (!spread_on) E.line("  if (g >= kp.lanes) return;");
         if (stage && fast_paths) {
             E.line("  __shared__ PWin pwin_;");
             E.line("  const uint32_t tl0_ = threadIdx.x;");
@@ -380,7 +402,23 @@ class Gen {
             E.line("#define COLD_CALL_K(k_, call_, pc_) do { coldn_ += 1u << (k_); COLD_CALL(call_, pc_); } while (0)");
         }
         E.line("  L.lane = g;");
-        E.line("  L.cpu = lane_cpu(kp, g);");
+        if (spread_on) {
+            // Spread: block b runs packets [b * SPREAD_PPB, +SPREAD_PPB) of the batch, thread t the
+            // ones at t, t + 256, ... (consecutive threads, consecutive packets); each packet's
+            // vCPU comes from the schedule.  Fused increments add into the block's LDS table, one
+            // row per vCPU lane its packets map to, (lane - lane0) mod V: at most SPREAD_PPB rows.
+            E.line("  const uint32_t blo_ = blockIdx.x * SPREAD_PPB, bhi_ = blo_ + SPREAD_PPB < kp.n ? blo_ + SPREAD_PPB : kp.n;");
+            E.line("  const uint32_t lam0_ = spread_lane(kp, blo_);");
+            E.line("  const DMap SM_ = cget(kp.maps, SPREAD_MAP);");
+            E.line("#if SPREAD_ROWS");
+            E.line("  __shared__ spread_t sacc_[SPREAD_ROWS * SPREAD_ROWW];");
+            E.line("  for (uint32_t w_ = threadIdx.x; w_ < SPREAD_ROWS * SPREAD_ROWW; w_ += 256u) sacc_[w_] = 0;");
+            E.line("  __syncthreads();");
+            E.line("#endif");
+            E.line("  uint32_t srow_ = 0, sbase_ = 0;");
+        } else {
+            E.line("  L.cpu = lane_cpu(kp, g);");
+        }
         if (vc_on) {
             // the lane's own row of the per-CPU array the hint names (analyze_vc)
             E.line("  uint64_t vc0_ = 0, vc1_ = 0, vc2_ = 0, vc3_ = 0; uint32_t vcv_ = 0u, vcd_ = 0u, vclo_ = 0u, vcb_ = 0u; uint8_t *vcp_ = nullptr;");
@@ -394,8 +432,6 @@ class Gen {
         if (ctx == CTX_SKB) E.line("  const uint32_t SK_ = P;   // the sk_buff entry (skb.h)");
         E.line("  uint32_t ga_ = 0;   // the address of the current memory access");
         for (auto &f : fwd_store) E.line("  uint32_t fwd%u_%u_ = 0;   // value of the stack store at P%u slot %u", f.first, f.second, f.first, f.second);
-        if (speculate && fast_paths && !stage && !all_leaders)
-            for (auto &p : P) analyze_spec(p);
         for (auto &u : spec_use)
             E.line("  %s sp%u_%u_ = 0;   // packet load of P%u slot %u, issued early", u.second == 8 ? "uint64_t" : "uint32_t",
                    u.first.first, u.first.second, u.first.first, u.first.second);
@@ -404,7 +440,7 @@ class Gen {
         // length are loaded while packet j runs (they travel with packet j's first loads), which
         // takes one dependent HBM round trip off every packet after the first.
         const bool pf = ctx == CTX_XDP && prefetch;
-        if (!spec_use.empty()) analyze_xpf();
+        if (!spec_use.empty() && !spread_on) analyze_xpf();
         if (pf && xpf.on) {
             // descriptors two packets ahead, the window one packet ahead (analyze_xpf)
             E.line("  const bool xpf_on_ = kp.entry_prog == %uu && !kp.headroom_arr;   // P%u slot %u window, data + %u, %u words",
@@ -418,13 +454,22 @@ class Gen {
             E.line("  if (nidx2_ != NO_PKT) { noff2_ = *gp(kp.pkt_off + nidx2_); nlen2_ = *gp(kp.pkt_len + nidx2_); }");
         } else if (pf) {
             E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
-            E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+            if (spread_on)
+                E.line("  { const uint32_t n_ = blo_ + threadIdx.x; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+            else
+                E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
-        E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
-        E.line("    uint32_t i;");
-        E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
-        E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
-        E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
+        if (spread_on) {
+            E.line("  for (uint32_t j = 0; j < SPREAD_PPB / 256u; j++) {");
+            E.line("    const uint32_t i = blo_ + j * 256u + threadIdx.x;");
+            E.line("    if (i >= bhi_) break;");
+        } else {
+            E.line("  for (uint32_t j = 0; j < kp.per_lane; j++) {");
+            E.line("    uint32_t i;");
+            E.line("    if (kp.sched == SCHED_CHUNKED) { const uint64_t ii = (uint64_t)g * kp.per_lane + j; if (ii >= kp.n) break; i = (uint32_t)ii; }");
+            E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
+            E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
+        }
         if (pf && xpf.on) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             E.line("    xc_ok_ = xn_ok_;");
@@ -436,12 +481,19 @@ class Gen {
         } else if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
+            else if (spread_on) E.line("    { const uint32_t n_ = i + 256u; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
         // fields used once per packet are read through an opaque copy of the parameter pointer:
         // loaded where used instead of hoisted out of the packet loop into SGPRs
         if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else E.line("    const KParams &kq_ = kp;");
+        if (spread_on) {   // this packet's vCPU (the schedule's lane for it) and its row of the spread map
+            E.line("    { const uint32_t lam_ = spread_lane(kp, i);");
+            E.line("      L.cpu = (int32_t)(kp.vcpu_begin + lam_);");
+            E.line("      srow_ = lam_ >= lam0_ ? lam_ - lam0_ : lam_ + kp.cpu_lanes - lam0_;");
+            E.line("      sbase_ = SM_.backing_addr + (uint32_t)L.cpu * SM_.addr_period; }");
+        }
         // The lane's private-memory and LDS addresses are loop-invariant; hoisted out of the packet
         // loop they would stay live (one VGPR pair per stack slot) through every packet.  An opaque
         // per-iteration copy of the lane index keeps each address next to its use.
@@ -551,7 +603,22 @@ class Gen {
         E.line("    lane_steps += steps;");
         E.line("  }");
         if (vc_on) E.line("  VC_FLUSH();");
-        E.line("  if (kp.lane_steps) st_nt(kp.lane_steps + g, lane_steps);");
+        if (spread_on) {
+            // the block's counters into the map: one agent-scope add per non-zero counter (a row's
+            // counters are contiguous in the arena, so consecutive threads add consecutive words)
+            E.line("#if SPREAD_ROWS");
+            E.line("  __syncthreads();");
+            E.line("  for (uint32_t w_ = threadIdx.x; w_ < SPREAD_ROWS * SPREAD_ROWW; w_ += 256u) {");
+            E.line("    const spread_t v_ = sacc_[w_];");
+            E.line("    if (!v_) continue;");
+            E.line("    const uint32_t r_ = w_ / SPREAD_ROWW, q_ = w_ - r_ * SPREAD_ROWW;");
+            E.line("    const uint32_t lr_ = lam0_ + r_ < kp.cpu_lanes ? lam0_ + r_ : lam0_ + r_ - kp.cpu_lanes;");
+            E.line("    spread_t *d_ = (spread_t *)(kp.arena + SM_.dev_off + (size_t)(kp.vcpu_begin + lr_) * SM_.dev_stride) + q_;");
+            E.line("    __hip_atomic_fetch_add((GAS spread_t *)d_, v_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);");
+            E.line("  }");
+            E.line("#endif");
+        }
+        E.line("  if (kp.lane_steps && g < kp.lanes) st_nt(kp.lane_steps + g, lane_steps);");
         E.line("}");
         if (census) {   // diagnostics: each slow-path call adds 1 to its kind's 4-bit field of coldn_
             static const char *kinds[] = {"cold_load(", "cold_store(", "cold_lookup(", "cold_update(", "cold_delete(",
@@ -934,6 +1001,127 @@ class Gen {
             }
         }
     }
+    // Spread mode.  processPool gives each vCPU one worker (vm.go:548-573), so the engine runs a
+    // vCPU's packets on one lane, in order -- with V = runtime.NumCPU() (vm.go:64) a few hundred
+    // lanes for a whole GPU.  When the only per-CPU state the programs touch is counters they
+    // increment (fused increments, fusable_inc) through a lookup of one per-CPU array, and no
+    // other memory, register or helper sees the looked-up value region, a vCPU's final counters
+    // are the sum of its packets' increments in any order, and each packet's R0 / status / steps
+    // depend on its own bytes only: then a vCPU's packets may run on many lanes at once.  Checked
+    // here over every program: a forward may-analysis of the registers that may hold a value
+    // pointer from such a lookup (taint); a value pointer may be compared, copied, moved by
+    // arithmetic, returned in R0 (the address is a function of the packet's vCPU and key), and be
+    // the base of a fused increment -- nothing else (no load or store through it, no store of it,
+    // no helper argument).  Allowed helpers: map_lookup_elem on that per-CPU array (R1 an
+    // LD_IMM64 of its object in the block) and get_smp_processor_id; no tail calls, BPF-to-BPF
+    // calls or loops (no budget checks).  What the analysis cannot see -- an address the program
+    // computes into per-CPU memory -- reaches resolve(), which marks the launch (SPREAD_GUARD).
+    bool analyze_spread() {
+        if (!spread_req || ctx != CTX_XDP || !fast_paths || !cold_inline || careful_copies || any_local || any_tail ||
+            stage || census || !inc_knob || live.empty())
+            return false;
+        int64_t map = -1;
+        uint32_t n = 0;
+        for (auto &p : P) {
+            if (!p.n) continue;
+            const std::vector<uint32_t> Lb = leaders(p);
+            std::map<uint32_t, size_t> blk;
+            for (size_t b = 0; b < Lb.size(); b++) blk[Lb[b]] = b;
+            std::vector<uint16_t> in(Lb.size(), 0);
+            std::vector<bool> seen(Lb.size(), false);
+            seen[0] = true;
+            for (bool changed = true; changed;) {
+                changed = false;
+                for (size_t b = 0; b < Lb.size(); b++) {
+                    if (!seen[b]) continue;
+                    const uint32_t s0 = Lb[b], e = b + 1 < Lb.size() ? Lb[b + 1] : p.n;
+                    uint16_t t = in[b];
+                    auto tn = [&](uint32_t r) { return r <= 10 && ((t >> r) & 1); };
+                    for (uint32_t i = s0; i < e; i++) {
+                        const DInsn &x = p.ins[i];
+                        const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x), op = insn_op(x);
+                        const bool X = (x.aux & AUX_X) != 0;
+                        switch (h) {
+                        case H_NOP: case H_JA: case H_JCC: case H_EXIT: case H_ERR:
+                            break;
+                        case H_ALU64: case H_ALU32: {
+                            if (d > 10) break;
+                            const bool mov = (op & 0xf0) == 0xb0;
+                            const bool v = (X && tn(sr)) || (!mov && tn(d));
+                            t = v ? (uint16_t)(t | (1u << d)) : (uint16_t)(t & ~(1u << d));
+                            break;
+                        }
+                        case H_LDIMM:
+                            if (d <= 10) t &= (uint16_t)~(1u << d);
+                            break;
+                        case H_LDX:
+                            if (tn(sr)) {   // through a value pointer: a fused increment, nothing else
+                                if (!(i + 2 < e && fusable_inc(p, i))) return false;
+                                const uint32_t w = AUX_SZ(x.aux);
+                                if (n && n != w) return false;
+                                n = w;
+                                t &= (uint16_t)~(1u << d);   // the counter register, dead after the store
+                                i += 2;
+                                break;
+                            }
+                            if (d <= 10) t &= (uint16_t)~(1u << d);
+                            break;
+                        case H_ST: case H_STX:
+                            if (tn(d)) return false;                  // a store through a value pointer
+                            if (h == H_STX && tn(sr)) return false;   // a value pointer stored to memory
+                            break;
+                        case H_CALL: {
+                            const uint32_t k = (uint32_t)x.k;
+                            if (k == 8) {   // get_smp_processor_id: R0 = the packet's vCPU
+                                t &= (uint16_t)~1u;
+                                break;
+                            }
+                            if (k != 1 || tn(1) || tn(2)) return false;
+                            const uint32_t save = blk_start;
+                            blk_start = s0;
+                            const int64_t j = r1_def(p, i);
+                            blk_start = save;
+                            if (j < 0) return false;
+                            auto it = spread_req->slot_map.find(p.base + (uint32_t)j);
+                            if (it == spread_req->slot_map.end() || (map >= 0 && map != (int64_t)it->second)) return false;
+                            map = it->second;
+                            t |= 1u;   // R0: the value pointer (or 0)
+                            break;
+                        }
+                        case H_SLOW:
+                            if ((op & 7) == 1) return false;   // an LDX error form (generic load)
+                            if (d <= 10) t = (tn(d) || (X && tn(sr))) ? (uint16_t)(t | (1u << d)) : (uint16_t)(t & ~(1u << d));
+                            break;
+                        default:   // LD_ABS / LD_IND, BPF-to-BPF
+                            return false;
+                        }
+                    }
+                    const DInsn &last = p.ins[e - 1];
+                    const uint32_t lh = AUX_H(last.aux);
+                    std::vector<int64_t> succ;
+                    if ((!ends_block(last) || lh == H_JCC) && (last.aux & AUX_FALL_OK)) succ.push_back(e);
+                    if ((lh == H_JA || lh == H_JCC) && (last.aux & AUX_JT_OK)) succ.push_back(jump_target(last, e - 1));
+                    for (int64_t sx : succ) {
+                        auto it = blk.find((uint32_t)sx);
+                        if (it == blk.end()) continue;
+                        const uint16_t nin = (uint16_t)(in[it->second] | t);
+                        if (!seen[it->second] || nin != in[it->second]) {
+                            in[it->second] = nin;
+                            seen[it->second] = true;
+                            changed = true;
+                        }
+                    }
+                }
+            }
+        }
+        if (map < 0 || !n) return false;
+        auto sh = spread_req->shape.find((uint32_t)map);
+        if (sh == spread_req->shape.end() || sh->second.first == 0 || sh->second.first % n) return false;
+        spread_map = (uint32_t)map;
+        spread_n = n;
+        spread_row = sh->second.first;
+        return true;
+    }
     // issue the prefetch of the window of the packet at (noff_, nlen_)
     void emit_xpf_issue(const char *pre) {
         E.line("%sif (xpf_on_ && nidx_ != NO_PKT && %uu <= nlen_) {", pre, (uint32_t)xpf.off + 8 * xpf.words);
@@ -1156,6 +1344,16 @@ class Gen {
         E.line("    ga_ = %s;", addr(b, insn_off(ld)).c_str());
         std::string cond = "(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n && !((uintptr_t)(L.t_ptr + (uint32_t)(ga_ - L.t_lo)) & (" + N + " - 1u))";
         if (vc_on) cond = "!(vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + " + N + " <= vcb_) && " + cond;
+        if (spread_on) {
+            // a counter of this packet's vCPU row in the spread map: into the block's table (or one
+            // agent-scope add), any other word takes the three slots (resolve() guards them)
+            if (n == spread_n) {
+                cond = "L.t_lo == sbase_ && (uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n && !((uint32_t)(ga_ - L.t_lo) & (" + N + " - 1u))";
+                E.line("    if (%s) { steps += 3u; spread_add(%s); }", cond.c_str(), imm(k).c_str());
+            } else {
+                E.line("    if (false) { }");
+            }
+        } else
         E.line("    if (%s) { steps += 3u; atomic_add_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), %s, %s); }", cond.c_str(), N.c_str(), imm(k).c_str());
         E.line("    else {");
         insn(p, i);
@@ -1261,8 +1459,10 @@ class Gen {
                              "vc_load(vc0_, vc1_, vc2_, vc3_, ga_ - vclo_, " + N + ")",
                              "{ vc_store(vc0_, vc1_, vc2_, vc3_, ga_ - vclo_, " + N + ", " + v + "); vcd_ = 1u; }"});
             // the map value region the last lookup returned (translation cache, resolve()):
-            // [t_lo, t_lo + t_n - 1] with GetEntry's inclusive end, t_n = 0 when empty
-            f.push_back({"(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n",
+            // [t_lo, t_lo + t_n - 1] with GetEntry's inclusive end, t_n = 0 when empty.  Not in
+            // spread kernels: there that region is per-CPU memory other lanes add to, reached by
+            // fused increments only (an access the generator did not prove goes to resolve()).
+            if (!spread_on) f.push_back({"(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n",
                          "ld_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), " + N + ")",
                          "st_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), " + N + ", " + v + ")"});
             break;
@@ -1731,12 +1931,14 @@ std::map<CacheKey, hipFunction_t> g_cache;
 }  // namespace
 
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
-                             JitInfo *info, const std::vector<uint32_t> *vc_slots, bool no_early_loads) {
+                             JitInfo *info, const std::vector<uint32_t> *vc_slots, bool no_early_loads,
+                             const SpreadReq *spread) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
     Gen g(v, ctx_kind);
     if (vc_slots) g.vc_ok.insert(vc_slots->begin(), vc_slots->end());
     if (no_early_loads) g.speculate = 0;
+    g.spread_req = spread;
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;
@@ -1747,6 +1949,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->defer = g.defer_mode;
         info->skb_walk = g.skb_walk;
         info->karg = g.karg != 0;
+        info->spread = g.spread_on;
     }
     return src;
 }

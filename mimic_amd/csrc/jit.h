@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
@@ -17,12 +18,21 @@ struct JitInfo {
     bool karg;           // the kernel takes KParams by value (kernarg segment), not a device copy
     bool defer;          // slow paths are deferred to the interpreter's resume kernel (launch it after)
     bool skb_walk;       // sk_buff kernel that builds its SkbRecs itself (prep: footprints only)
+    bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
+};
+// What a spread kernel may be built for (jit.cpp analyze_spread): the VM's per-CPU arrays.
+struct SpreadReq {
+    std::map<uint32_t, uint32_t> slot_map;   // kernel-wide LD_IMM64 slot -> per-CPU array map id (its object)
+    std::map<uint32_t, std::pair<uint32_t, uint32_t>> shape;   // map id -> (E * S, S)
+    uint32_t lds_rows = 0;   // rows of a block's LDS counter table (0: agent-scope atomics into the map)
+    uint32_t ppb = 1024;     // packets per block
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // vc_slots: kernel-wide indices of LD_IMM64 slots whose constant is the object of a per-CPU array
 // with E * S <= 32 bytes, a multiple of 8 (the lane value cache may cache that map's row)
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
-                             JitInfo *info, const std::vector<uint32_t> *vc_slots = nullptr, bool no_early_loads = false);
+                             JitInfo *info, const std::vector<uint32_t> *vc_slots = nullptr, bool no_early_loads = false,
+                             const SpreadReq *spread = nullptr);
 // 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
 // batch with a smaller budget must run on the interpreter
 uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);

@@ -212,6 +212,10 @@ struct KParams {
     // sk_buff batches: 1 when the prep kernel wrote every packet's SkbRec; 0 when the JIT kernel
     // builds them itself (skb_load_walk) -- then the interpreter builds the ones it needs
     uint32_t skb_rec_built;
+    // spread launches (jit.cpp analyze_spread): a vCPU's packets run on many lanes; a generic
+    // access that reaches per-CPU map memory would break that mode's exactness and sets *spread_bad
+    // (never cleared: the host reports it as an engine error).  nullptr in every other launch.
+    uint32_t *spread_bad;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

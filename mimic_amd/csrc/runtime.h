@@ -124,6 +124,14 @@ DEV uint32_t pkt_index(const KParams &kp, uint32_t g, uint32_t j, uint32_t ex_be
     return j < ex_count ? *(const GAS uint32_t *)(kp.sched_pkts + ex_begin + j) : NO_PKT;
 }
 
+// spread kernels: the lane (vCPU - vcpu_begin) packet i runs on under a chunked / interleaved
+// schedule -- the inverse of pkt_index (interleaved: packet ii runs on lane (ii + shift) mod lanes)
+DEV uint32_t spread_lane(const KParams &kp, uint32_t i) {
+    if (kp.sched == SCHED_CHUNKED) return i / kp.per_lane;
+    uint32_t r = i % kp.cpu_lanes + kp.sched_shift;
+    return r >= kp.cpu_lanes ? r - kp.cpu_lanes : r;
+}
+
 // the packet after packet i (the j-th of lane g) under the schedule: the chunked and
 // interleaved schedules step by 1 and by the lane count
 DEV uint32_t pkt_next(const KParams &kp, uint32_t i, uint32_t j, uint32_t ex_begin, uint32_t ex_count) {
@@ -362,6 +370,16 @@ DEV void xdp_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t 
     priv_store(kp, L.lane, kp.priv_xdp_q * 8 + o, n, v);
 }
 
+// Spread kernels (MIMIC_SPREAD, jit.cpp analyze_spread) run one vCPU's packets on many lanes:
+// exact only while per-CPU map memory is touched by fused counter increments alone.  The
+// generator proves that for every access it can see; a generic access that still resolves into
+// per-CPU memory (an address the program computed) marks the launch instead of passing silently.
+#ifdef MIMIC_SPREAD
+#define SPREAD_GUARD(kp) do { if ((kp).spread_bad) *gp((kp).spread_bad) = 1u; } while (0)
+#else
+#define SPREAD_GUARD(kp) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------
 // MemoryController.GetEntry (memory_controller.go:117-145) over the lane's address space
 // ---------------------------------------------------------------------------------------
@@ -433,6 +451,7 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
         return R;
     }
     if (a - L.t_lo < L.t_n) {
+        SPREAD_GUARD(kp);   // the translation cache holds a lookup's value region
         R.rk = RK_GLOBAL;
         R.ptr = L.t_ptr;
         R.off = a - L.t_lo;
@@ -467,6 +486,7 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
                 R.rk = RK_NOTVMMEM;
                 break;
             case SEG_PERCPU_ARRAY: {
+                SPREAD_GUARD(kp);
                 uint32_t c = off / g.period, r = off - c * g.period;
                 R.ptr = kp.arena + g.dev_off + (size_t)c * g.dev_stride;
                 R.limit = g.size;
@@ -482,6 +502,7 @@ DEV Ref resolve(const KParams &kp, const Lane &L, uint32_t a) {
                 break;
             }
             case SEG_PERCPU_VALUES: {
+                SPREAD_GUARD(kp);
                 uint32_t c = off / g.period, r = off - c * g.period;
                 R.rk = RK_GLOBAL;
                 R.ptr = kp.arena + g.dev_off + (size_t)c * g.dev_stride;

@@ -30,10 +30,12 @@ def _progs_args(raws: Sequence[bytes]):
     return bufs, arr, ns
 
 
-def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int]] = ()) -> str:
+def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int]] = (), spread=None) -> str:
     """vc: (program index, slot) of the LD_IMM64 slots that name a per-CPU array whose per-vCPU
     row is at most 32 bytes, a multiple of 8 -- what a VM with those maps generates (see
-    ``vc_slots``)."""
+    ``vc_slots``).  spread: a ``spread_spec`` -- the VM's spread kernel instead (xdp_md)."""
+    if spread is not None:
+        return spread_source(raws, *spread)[0]
     lib = _lib.load()
     keep, arr, ns = _progs_args(raws)
     flat = [v for pair in vc for v in pair]
@@ -67,6 +69,47 @@ def vc_slots(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict]) -> L
             if src == 1 or (src == 2 and off == 0):
                 out.append((pi, slot))
     return out
+
+
+def spread_spec(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict], vcpus: int, ppb: int = 1024):
+    """What the engine's spread_build() generates the spread kernel from, for programs (raw,
+    relocations) loaded next to ``maps`` (created in this order: map id = index) on a VM with
+    ``vcpus`` vCPUs: (pc, shapes, lds_rows) -- the (program, slot, map id) of every LD_IMM64 slot
+    naming a per-CPU array's object, those maps' (id, E * S, S), and the LDS table's rows
+    (min(ppb, V) when that many rows of the largest such row fit 32 KiB, else 0)."""
+    by_name = {m["name"]: (i, m) for i, m in enumerate(maps)}
+    pc, shapes = [], {}
+    for pi, (raw, rel) in enumerate(progs):
+        for r in rel:
+            slot, name = r[0], r[1]
+            if name not in by_name or by_name[name][1]["type"] != 6:
+                continue
+            mid, m = by_name[name]
+            src, off = raw[8 * slot + 1] >> 4, int.from_bytes(raw[8 * slot + 2:8 * slot + 4], "little", signed=True)
+            if src == 1 or (src == 2 and off == 0):
+                pc.append((pi, slot, mid))
+                shapes[mid] = (mid, m["max_entries"] * m["value_size"], m["value_size"])
+    row = max((s[1] for s in shapes.values()), default=0)
+    rows = min(ppb, vcpus)
+    return pc, list(shapes.values()), rows if rows * row <= 32768 else 0
+
+
+def spread_source(raws: Sequence[bytes], pc, shapes, lds_rows: int) -> Tuple[str, bool]:
+    """(source, allowed): the spread kernel's source and whether the programs allow one (else the
+    source is the plain kernel's).  jit.cpp analyze_spread decides."""
+    lib = _lib.load()
+    keep, arr, ns = _progs_args(raws)
+    pcf = [v for t in pc for v in t]
+    shf = [v for t in shapes for v in t]
+    pca = (C.c_uint32 * max(len(pcf), 1))(*pcf)
+    sha = (C.c_uint32 * max(len(shf), 1))(*shf)
+    ok = C.c_int32()
+    n = lib.mimic_jit_source_spread(arr, ns, len(raws), pca, len(pc), sha, len(shapes), lds_rows, C.byref(ok), None, 0)
+    if n < 0:
+        raise ValueError(f"cannot decode programs ({n})")
+    buf = C.create_string_buffer(n + 1)
+    lib.mimic_jit_source_spread(arr, ns, len(raws), pca, len(pc), sha, len(shapes), lds_rows, C.byref(ok), buf, n + 1)
+    return buf.value.decode(), bool(ok.value)
 
 
 def code_object(src: str) -> bytes:

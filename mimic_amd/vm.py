@@ -364,6 +364,12 @@ def VMOptExecMode(mode: str):
     return ("exec", {"default": 0, "interp": 1, "jit": 2}[mode])
 
 
+def VMOptSpread(mode: int):
+    """Spread launches (mimic_set_spread): -1 the default policy, 0 never, 1 whenever the loaded
+    programs allow it (every per-CPU access a fused counter increment)."""
+    return ("spread", mode)
+
+
 def VMOptShard(begin: int, count: int):
     """Execute only vCPUs [begin, begin+count) on this engine (multi-GPU sharding)."""
     return ("shard", (begin, count))
@@ -550,11 +556,16 @@ class VM:
 
     def LastExec(self) -> str:
         """The kernel the last batch ran on."""
-        return {0: "none", 1: "interp", 2: "jit"}[self.lib.mimic_last_exec(self.h)]
+        return {0: "none", 1: "interp", 2: "jit", 3: "spread"}[self.lib.mimic_last_exec(self.h)]
+
+    def SetSpread(self, mode: int) -> None:
+        """Spread launches (mimic_set_spread): -1 default policy, 0 never, 1 whenever allowed."""
+        _check(self.h, self.lib.mimic_set_spread(self.h, mode), "SetSpread")
 
 
 def NewVM(*opts) -> VM:  # vm.go:54-76
     emu = None
+    spread = None
     s = VMSettings(vcpus=os.cpu_count() or 1)  # VirtualCPUs defaults to runtime.NumCPU()
     for k, v in opts:
         if k == "emulator":
@@ -567,7 +578,12 @@ def NewVM(*opts) -> VM:  # vm.go:54-76
             s.vcpu_begin, s.vcpu_count = v
         elif k == "exec":
             s.exec_mode = v
-    return VM(emu, s)
+        elif k == "spread":
+            spread = v
+    vm = VM(emu, s)
+    if spread is not None:
+        vm.SetSpread(spread)
+    return vm
 
 
 class Registers:

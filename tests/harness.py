@@ -66,7 +66,16 @@ def kernel_of(sc: Scenario, ctx: int = 0):
     return [raw for _, raw, _ in sc.progs], ctx, J.vc_slots([(raw, rel) for _, raw, rel in sc.progs], sc.maps)
 
 
-def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0, exec_mode: Optional[str] = None):
+def spread_kernel_of(sc: Scenario):
+    """The spread kernel a scenario's VM builds (jit.spread_spec): for the session prewarm."""
+    from mimic_amd import jit as J
+
+    progs = [(raw, rel) for _, raw, rel in sc.progs]
+    return [raw for _, raw, _ in sc.progs], 0, (), J.spread_spec(progs, sc.maps, sc.vcpus)
+
+
+def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0, exec_mode: Optional[str] = None,
+                 spread: Optional[int] = None):
     import mimic_amd as M
 
     emu = M.NewLinuxEmulator(M.OptMaxTailCalls(sc.max_tail_calls))
@@ -75,6 +84,8 @@ def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0, exec_m
         opts.append(M.VMOptShard(*shard))
     if exec_mode is not None:
         opts.append(M.VMOptExecMode(exec_mode))
+    if spread is not None:
+        opts.append(M.VMOptSpread(spread))
     vm = M.NewVM(*opts)
     maps = {}
     for m in sc.maps:
@@ -121,10 +132,11 @@ def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, ta
 
 
 def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=0, tailroom=0, ingress=0, rxq=0,
-               egress=0, step_budget=0, schedule=None, device: int = 0, exec_mode: Optional[str] = None):
+               egress=0, step_budget=0, schedule=None, device: int = 0, exec_mode: Optional[str] = None,
+               spread: Optional[int] = None):
     import mimic_amd as M
 
-    vm, maps, pids = build_engine(sc, device, exec_mode=exec_mode)
+    vm, maps, pids = build_engine(sc, device, exec_mode=exec_mode, spread=spread)
     if schedule is None:
         schedule = M.SCHED_EXPLICIT
     batch = M.XDPBatch.from_numpy(buf, off, lens, device=f"cuda:{device}", headroom=headroom, tailroom=tailroom,

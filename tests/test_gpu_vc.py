@@ -114,7 +114,7 @@ def test_lane_value_cache(gpu, case, sched):
         cpu = W.schedule_cpu(n, 8, "interleaved")
         mode = M.SCHED_INTERLEAVED
     o = run_oracle(sc, buf, off, lens, cpu)
-    e = run_engine(sc, buf, off, lens, cpu if sched == "explicit" else None, schedule=mode)
+    e = run_engine(sc, buf, off, lens, cpu if sched == "explicit" else None, schedule=mode, spread=0)
     assert_same(o, e)
     assert e["last_exec"] == "jit"
     ok = o["status"] == 0
@@ -132,7 +132,7 @@ def test_lane_value_cache_classifier_many_packets_per_vcpu(gpu):
     buf, off, lens = W.make_packets(n, seed=5)
     cpu = W.schedule_cpu(n, V, "chunked")
     o = run_oracle(sc, buf, off, lens, cpu)
-    e = run_engine(sc, buf, off, lens, None, schedule=M.SCHED_CHUNKED)
+    e = run_engine(sc, buf, off, lens, None, schedule=M.SCHED_CHUNKED, spread=0)
     assert_same(o, e)
     assert sum(int(np.frombuffer(v, np.uint64).sum()) for v in e["maps"]["verdicts"]) == n
 
