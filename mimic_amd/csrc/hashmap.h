@@ -109,6 +109,9 @@ HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos) {
 template <class KS>
 HDEV int32_t h_find_ro(const HT &t, const KS &ks, uint64_t h) {
     const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32), nq = (t.K + 7) >> 3;
+    // keys over 32 bytes (IPv6 5-tuples): the probe that compares every key word (a second
+    // compare loop here would cost every kernel that inlines the generic lookup registers)
+    if (nq > 4) return h_find(t, ks, h, nullptr);
     uint32_t p = (uint32_t)h & mask;
     for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
         const uint64_t *r = h_rec(t, p);
@@ -123,8 +126,6 @@ HDEV int32_t h_find_ro(const HT &t, const KS &ks, uint64_t h) {
 #pragma unroll
             for (uint32_t q = 0; q < 4; q++)
                 if (q < nq) eq &= w[1 + q] == ks.word(q);
-            // keys over 32 bytes (IPv6 5-tuples): the words past the preload, one by one
-            for (uint32_t q = 4; eq && q < nq; q++) eq = r[1 + q] == ks.word(q);
             if (eq) return (int32_t)s;
         }
     }

@@ -416,6 +416,10 @@ class Gen {
             E.line("  __syncthreads();");
             E.line("#endif");
             E.line("  uint32_t srow_ = 0, sbase_ = 0;");
+            // the lane of the thread's next packet: interleaved schedules step it by 256 mod V
+            // (no division per packet), chunked ones divide
+            E.line("  const uint32_t lstep_ = 256u %% kp.cpu_lanes;");
+            E.line("  uint32_t lam_ = spread_lane(kp, blo_ + threadIdx.x);");
         } else {
             E.line("  L.cpu = lane_cpu(kp, g);");
         }
@@ -489,7 +493,8 @@ class Gen {
         if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else E.line("    const KParams &kq_ = kp;");
         if (spread_on) {   // this packet's vCPU (the schedule's lane for it) and its row of the spread map
-            E.line("    { const uint32_t lam_ = spread_lane(kp, i);");
+            E.line("    { if (kp.sched == SCHED_CHUNKED) lam_ = i / kp.per_lane;");
+            E.line("      else if (j) { lam_ += lstep_; if (lam_ >= kp.cpu_lanes) lam_ -= kp.cpu_lanes; }");
             E.line("      L.cpu = (int32_t)(kp.vcpu_begin + lam_);");
             E.line("      srow_ = lam_ >= lam0_ ? lam_ - lam0_ : lam_ + kp.cpu_lanes - lam0_;");
             E.line("      sbase_ = SM_.backing_addr + (uint32_t)L.cpu * SM_.addr_period; }");
@@ -618,7 +623,7 @@ class Gen {
             E.line("  }");
             E.line("#endif");
         }
-        E.line("  if (kp.lane_steps && g < kp.lanes) st_nt(kp.lane_steps + g, lane_steps);");
+        E.line("  if (kp.lane_steps) st_nt(kp.lane_steps + g, lane_steps);");
         E.line("}");
         if (census) {   // diagnostics: each slow-path call adds 1 to its kind's 4-bit field of coldn_
             static const char *kinds[] = {"cold_load(", "cold_store(", "cold_lookup(", "cold_update(", "cold_delete(",

@@ -121,9 +121,10 @@ def _resources(raws, ctx=_lib.CTX_XDP, vc=()):
 @pytest.mark.parametrize("fn,vgprs,waves", [("prog_classifier", 120, 4), ("prog_parse5", 120, 4)])
 def test_hot_kernels_register_budget(fn, vgprs, waves):
     """cfg 2 / cfg 3 kernels as the bench's VM generates them (the classifier with its lane value
-    cache): unified VGPRs within budget, no VGPR spills, no scratch.  At most a few SGPRs may
-    spill (into VGPR lanes): keeping the per-packet result pointers in SGPRs measured faster than
-    reloading them (jit.cpp, MIMIC_JIT_KQ).  parse5's early packet loads (jit.cpp, analyze_spec)
+    cache): unified VGPRs within budget, no VGPR spills, no scratch.  A few SGPRs may spill (into
+    VGPR lanes): keeping the per-packet result pointers in SGPRs measured faster than reloading
+    them (jit.cpp, MIMIC_JIT_KQ); the generic lookup's fallback to h_find for keys over 32 bytes
+    (hashmap.h h_find_ro, inlined into every kernel's cold lookup) costs the classifier 8 more.  parse5's early packet loads (jit.cpp, analyze_spec)
     cost it the fifth wave and measured faster anyway: 1.155 vs 1.193 ms per launch; forcing 5
     waves (MIMIC_JIT_WAVES=5) measured 1.47 ms.  The classifier's deferred key store
     (analyze_elide) costs it the fifth wave too and measured 29.1 vs 32.4 us per launch; its lane
@@ -133,7 +134,7 @@ def test_hot_kernels_register_budget(fn, vgprs, waves):
     p = getattr(W, fn)()
     r = _resources([p.raw], vc=J.vc_slots([(p.raw, p.relocs)], p.maps))
     assert r["vgpr_total"] <= vgprs and r["waves_per_simd"] >= waves, r
-    assert r["vgpr_spill"] == 0 and r["sgpr_spill"] <= 4 and r["scratch"] == 0, r
+    assert r["vgpr_spill"] == 0 and r["sgpr_spill"] <= 12 and r["scratch"] == 0, r
 
 
 def test_lane_value_cache_selection():

@@ -100,6 +100,8 @@ def main():
                                                          "its trailing per-batch step-count launches are left out)")
     ap.add_argument("--batches", type=int, default=0, help="batches the bench rotated over (0: its default)")
     ap.add_argument("--sched", default="interleaved")
+    ap.add_argument("--name", default="", help="the pass directories' suffix (default: the config)")
+    ap.add_argument("--spread", action="store_true", help="the run used the spread kernel (its source hash)")
     a = ap.parse_args()
     import bench
 
@@ -107,11 +109,13 @@ def main():
     n = a.packets or cfg["packets"]
     vcpus = a.vcpus or cfg.get("vcpus") or max(64, n // 4)
     c = a.config
-    ks = kernel_stats(os.path.join(a.dir, f"kt_{c}"), a.kernel, a.skip, a.keep)
-    fetch = counters(os.path.join(a.dir, f"fetch_{c}"), a.kernel, a.skip, a.keep).get("FETCH_SIZE")
-    write = counters(os.path.join(a.dir, f"write_{c}"), a.kernel, a.skip, a.keep).get("WRITE_SIZE")
-    sq = counters(os.path.join(a.dir, f"sq_{c}"), a.kernel, a.skip, a.keep)
-    out = {"config": c, "round": a.tag, "kernel": a.kernel, "kernel_src_hash": bench.kernel_src_hash_of(c),
+    nm = a.name or c
+    ks = kernel_stats(os.path.join(a.dir, f"kt_{nm}"), a.kernel, a.skip, a.keep)
+    fetch = counters(os.path.join(a.dir, f"fetch_{nm}"), a.kernel, a.skip, a.keep).get("FETCH_SIZE")
+    write = counters(os.path.join(a.dir, f"write_{nm}"), a.kernel, a.skip, a.keep).get("WRITE_SIZE")
+    sq = counters(os.path.join(a.dir, f"sq_{nm}"), a.kernel, a.skip, a.keep)
+    out = {"config": c, "round": a.tag, "kernel": a.kernel,
+           "kernel_src_hash": bench.kernel_src_hash_of(c, vcpus if a.spread else 0), "spread": a.spread,
            "packets": n, "vcpus": vcpus, "batches": a.batches or bench.default_batches(c, n),
            "schedule": a.sched, "kernel_stats": ks}
     if fetch is not None and write is not None:
@@ -136,7 +140,7 @@ def main():
             out["active_inst_frac_of_wave_cycles"] = round(sq.get("SQ_ACTIVE_INST_ANY", 0) / sq["SQ_WAVE_CYCLES"], 4)
     if a.command:
         out["command"] = a.command
-    path = a.out or os.path.join(ROOT, "profiles", f"{a.tag}_pmc_{c}.json")
+    path = a.out or os.path.join(ROOT, "profiles", f"{a.tag}_pmc_{nm}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out)[:600])
