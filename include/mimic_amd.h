@@ -155,6 +155,13 @@ void mimic_vm_destroy(mimic_vm *vm);
 int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id);
 /* LinuxMapUpdater.Update(key, value, flags, cpuid). emulator_linux_map.go:31-36 */
 int mimic_map_update(mimic_vm *vm, uint32_t map_id, const void *key, const void *value, uint32_t flags, int32_t cpu);
+/* n mimic_map_update calls in one: keys packed key_size bytes apart, values value_size bytes
+ * apart; rc_out[i] (optional) = the i-th call's result (0 or a positive errno).  Not in the
+ * reference API (a loop over LinuxMap.Update, emulator_linux_map_hash.go:158-203).  Host map
+ * operations run on a host image of the map's index and are staged: they reach the device before
+ * the next batch or map read, with no device round trip per call. */
+int mimic_map_update_batch(mimic_vm *vm, uint32_t map_id, const void *keys, const void *values, uint32_t n,
+                           uint32_t flags, int32_t cpu, int32_t *rc_out);
 /* LinuxMap.Lookup(key, cpuid) -> virtual address of the value (0 = not found). emulator_linux_map.go:25-27 */
 int mimic_map_lookup(mimic_vm *vm, uint32_t map_id, const void *key, int32_t cpu, uint32_t *addr_out);
 /* LinuxMapDeleter.Delete(key). emulator_linux_map.go:38-42 */

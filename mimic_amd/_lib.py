@@ -90,6 +90,8 @@ EXPORTS = {
     "mimic_map_create": (C.c_int, [C.c_void_p, C.POINTER(MapSpecC), C.POINTER(C.c_uint32)]),
     "mimic_map_update": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32]),
     "mimic_map_lookup": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.POINTER(C.c_uint32)]),
+    "mimic_map_update_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                         C.c_int32, C.c_void_p]),
     "mimic_map_delete": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "mimic_exec_mode": (C.c_int, [C.c_void_p]),
     "mimic_set_spread": (C.c_int, [C.c_void_p, C.c_int32]),

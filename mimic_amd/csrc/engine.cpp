@@ -18,17 +18,19 @@
 #include <cstring>
 #include <string>
 #include <chrono>
+#include <memory>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/mimic_amd.h"
 #include "layout.h"
+#include "hashmap.h"
 #include "jit.h"
 #include "skb.h"
 
 extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStream_t st);
 extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st);
-extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
-                                    int32_t cpu, int32_t *out, hipStream_t st);
+
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
 extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st);
@@ -39,6 +41,21 @@ extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pk
                                      uint32_t use_init, hipStream_t st);
 
 namespace {
+
+// Host image of one hash map's device index (hashmap.h): bucket records, freelist ring, counters
+// and the VM-visible keys backing.  Host map operations (LinuxMap.Update / Lookup / Delete) run
+// the sequential form of the device algorithm on this image -- the same hash, probe order and FIFO
+// freelist, so every key gets the slot the device (and the reference) would give it -- without a
+// device round trip; the image goes to the device in one upload before the device next uses the
+// map (flush_host).  valid: the image equals or is newer than the device's (a launch that may
+// write the table makes it stale: the next host operation downloads it again); dirty: newer.
+struct HashMirror {
+    bool valid = false, dirty = false;
+    std::vector<uint64_t> rec;
+    std::vector<int32_t> ring;
+    HashCtl ctl{};
+    std::vector<uint8_t> keys;
+};
 
 struct HostMap {
     std::string name;
@@ -55,6 +72,7 @@ struct HostMap {
     // a delete may have left tombstones (hashmap.h): only then can the table need a rebuild
     mutable bool may_tomb = false;
     mutable bool pop_dirty = false;   // a pop-only launch left head / avail to normalise (hashmap.h)
+    std::shared_ptr<HashMirror> mir;  // hash families: the host image of the index
 };
 
 // can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
@@ -117,6 +135,16 @@ struct mimic_vm {
     JitInfo jit_info_spread{};
     uint32_t *d_spread_bad = nullptr;
     bool spread_used = false;
+    // host map operations staged for the device (flush_host): value / array writes, deduplicated
+    // per arena offset (a later write to the same bytes replaces the earlier one)
+    struct PendWrite {
+        uint64_t off;
+        uint32_t n, at;
+    };
+    std::vector<PendWrite> pend;
+    std::vector<uint8_t> pend_data;
+    std::unordered_map<uint64_t, size_t> pend_at;
+    bool host_dirty = false;   // some pending write or dirty hash image
     int spread_mode = -1;   // mimic_set_spread: -1 the default policy (env MIMIC_SPREAD), 0 never, 1 whenever allowed
     bool spread_lds = false;   // the spread kernel keeps a block's counters in LDS (else agent-scope atomics)
     int last_exec = 0;          // the kernel the last batch ran on
@@ -626,6 +654,8 @@ void mimic_vm_destroy(mimic_vm *vm) {
     delete vm;
 }
 
+static void mirror_fresh(const HostMap &m);
+
 // MapSpecToLinuxMap (emulator_linux_map.go:57-113) + Init + AddMap
 int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id) {
     if (!vm || !spec || !map_id) return MIMIC_EINVAL;
@@ -754,6 +784,8 @@ int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id)
         c.tail = spec->max_entries;
         c.avail = (int32_t)spec->max_entries;
         HIP_OK(vm, hipMemcpy(vm->arena + m.ht_dev_off + ctl_off, &c, sizeof c, hipMemcpyHostToDevice));
+        m.mir = std::make_shared<HashMirror>();
+        mirror_fresh(m);
         auto plain = [&](uint32_t lo, uint32_t size, uint64_t dev_off) {
             Seg b{};
             b.lo = lo;
@@ -838,31 +870,199 @@ static int settle(mimic_vm *vm) {
     return 0;
 }
 
-// one hash-map operation on the device (the same code the kernel's helpers run):
-// op 0 lookup, 1 update, 2 delete; *slot = slot index or -1
-static int hash_op(mimic_vm *vm, const HostMap &m, uint32_t op, const void *key, const void *value, int32_t cpu,
-                   int32_t *slot) {
+// ---------------------------------------------------------------------------------------------
+// host map operations (HashMirror): the index region's layout (hashmap.h h_table)
+// ---------------------------------------------------------------------------------------------
+static void ht_offsets(const HostMap &m, uint64_t *rec_bytes, uint64_t *fl_off, uint64_t *ctl_off) {
+    *rec_bytes = (uint64_t)m.ht_cap * m.rec_q * 8;
+    *fl_off = 2 * *rec_bytes + (uint64_t)m.nlocks * 4;
+    *ctl_off = (*fl_off + (uint64_t)m.fl_cap * 4 + 127) & ~127ull;
+}
+
+// a freshly created table: every bucket EMPTY, the freelist 0..E-1 (emulator_linux_map_hash.go:56-64)
+static void mirror_fresh(const HostMap &m) {
+    HashMirror &x = *m.mir;
+    x.rec.assign((size_t)m.ht_cap * m.rec_q, ~0ull);
+    x.ring.assign(m.fl_cap, -1);
+    for (uint32_t i = 0; i < m.max_entries; i++) x.ring[i] = (int32_t)i;
+    x.ctl = HashCtl{};
+    x.ctl.head = 0;
+    x.ctl.tail = m.max_entries;
+    x.ctl.avail = (int32_t)m.max_entries;
+    x.keys.assign((size_t)m.max_entries * m.key_size, 0);
+    x.valid = true;
+    x.dirty = false;
+}
+
+// the device's table into the image (after the last batch), head / avail normalised as
+// mimic_hash_normalize_kernel would (a pop-only launch may leave head past tail)
+static int mirror_ensure(mimic_vm *vm, const HostMap &m) {
+    HashMirror &x = *m.mir;
+    if (x.valid) return 0;
     int rc = settle(vm);
     if (rc) return rc;
-    const size_t kb = std::max<uint32_t>(m.key_size, 1), vb = std::max<uint32_t>(m.value_size, 1);
-    uint8_t *d = nullptr;
-    HIP_OK(vm, hipMalloc(&d, kb + vb + 16));
-    int32_t *dout = (int32_t *)(d + ((kb + vb + 7) & ~size_t(7)));
-    hipError_t e = hipMemcpy(d, key, m.key_size, hipMemcpyHostToDevice);
-    if (e == hipSuccess && value) e = hipMemcpy(d + kb, value, m.value_size, hipMemcpyHostToDevice);
-    const DMap dm = to_dmap(m);
-    if (op == 2) m.may_tomb = true;
-    if (e == hipSuccess && m.pop_dirty) {   // the host op may push (delete) or pop with the semaphore
-        if (mimic_launch_hash_normalize(vm->arena, &dm, vm->stream)) e = hipErrorLaunchFailure;
-        m.pop_dirty = false;
-    }
-    if (e == hipSuccess && mimic_launch_hash_op(vm->arena, &dm, op, d, d + kb, cpu, dout, vm->stream))
-        e = hipErrorLaunchFailure;
-    if (e == hipSuccess) e = hipMemcpyAsync(slot, dout, 4, hipMemcpyDeviceToHost, vm->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(vm->stream);
-    hipFree(d);
-    if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "hash map op: %s", hipGetErrorString(e));
+    uint64_t rb, fo, co;
+    ht_offsets(m, &rb, &fo, &co);
+    x.rec.resize((size_t)m.ht_cap * m.rec_q);
+    x.ring.resize(m.fl_cap);
+    x.keys.resize((size_t)m.max_entries * m.key_size);
+    const uint8_t *base = vm->arena + m.ht_dev_off;
+    HIP_OK(vm, hipMemcpy(x.rec.data(), base, rb, hipMemcpyDeviceToHost));
+    HIP_OK(vm, hipMemcpy(x.ring.data(), base + fo, (size_t)m.fl_cap * 4, hipMemcpyDeviceToHost));
+    HIP_OK(vm, hipMemcpy(&x.ctl, base + co, sizeof(HashCtl), hipMemcpyDeviceToHost));
+    if (!x.keys.empty()) HIP_OK(vm, hipMemcpy(x.keys.data(), vm->arena + m.keys_dev_off, x.keys.size(), hipMemcpyDeviceToHost));
+    if (x.ctl.head > x.ctl.tail) x.ctl.head = x.ctl.tail;
+    x.ctl.avail = (int32_t)(x.ctl.tail - x.ctl.head);
+    x.valid = true;
+    x.dirty = false;
     return 0;
+}
+
+// a host write of n bytes at arena offset off, applied before the device next reads the arena
+static void stage_write(mimic_vm *vm, uint64_t off, const void *src, uint32_t n) {
+    if (!n) return;
+    auto it = vm->pend_at.find(off);
+    if (it != vm->pend_at.end() && vm->pend[it->second].n == n) {
+        memcpy(vm->pend_data.data() + vm->pend[it->second].at, src, n);
+    } else {
+        vm->pend_at[off] = vm->pend.size();
+        vm->pend.push_back({off, n, (uint32_t)vm->pend_data.size()});
+        vm->pend_data.insert(vm->pend_data.end(), (const uint8_t *)src, (const uint8_t *)src + n);
+    }
+    vm->host_dirty = true;
+}
+
+extern "C" int mimic_launch_scatter(uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *at,
+                                    const uint8_t *data, uint32_t n, hipStream_t st);
+
+// Everything host map operations staged goes to the device (after the last batch): dirty hash
+// images in one copy per region, pending writes as one scatter launch (a few: plain copies).
+static int flush_host(mimic_vm *vm) {
+    if (!vm->host_dirty) return 0;
+    int rc = settle(vm);
+    if (rc) return rc;
+    for (auto &m : vm->maps) {
+        if (!m.mir || !m.mir->dirty) continue;
+        HashMirror &x = *m.mir;
+        uint64_t rb, fo, co;
+        ht_offsets(m, &rb, &fo, &co);
+        uint8_t *base = vm->arena + m.ht_dev_off;
+        HIP_OK(vm, hipMemcpy(base, x.rec.data(), rb, hipMemcpyHostToDevice));
+        HIP_OK(vm, hipMemcpy(base + fo, x.ring.data(), (size_t)m.fl_cap * 4, hipMemcpyHostToDevice));
+        HIP_OK(vm, hipMemcpy(base + co, &x.ctl, sizeof(HashCtl), hipMemcpyHostToDevice));
+        if (!x.keys.empty()) HIP_OK(vm, hipMemcpy(vm->arena + m.keys_dev_off, x.keys.data(), x.keys.size(), hipMemcpyHostToDevice));
+        x.dirty = false;
+        m.pop_dirty = false;   // the uploaded counters are normalised
+    }
+    const size_t n = vm->pend.size();
+    if (n && n <= 8) {
+        for (auto &w : vm->pend) HIP_OK(vm, hipMemcpy(vm->arena + w.off, vm->pend_data.data() + w.at, w.n, hipMemcpyHostToDevice));
+    } else if (n) {
+        std::vector<uint64_t> offs(n);
+        std::vector<uint32_t> lens(n), at(n);
+        for (size_t k = 0; k < n; k++) {
+            offs[k] = vm->pend[k].off;
+            lens[k] = vm->pend[k].n;
+            at[k] = vm->pend[k].at;
+        }
+        const size_t bytes = n * 16 + vm->pend_data.size() + 16;
+        uint8_t *d = nullptr;
+        HIP_OK(vm, hipMalloc(&d, bytes));
+        uint64_t *doffs = (uint64_t *)d;
+        uint32_t *dlens = (uint32_t *)(d + n * 8), *dat = dlens + n;
+        uint8_t *ddata = d + n * 16;
+        hipError_t e = hipMemcpy(doffs, offs.data(), n * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dlens, lens.data(), n * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dat, at.data(), n * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(ddata, vm->pend_data.data(), vm->pend_data.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess && mimic_launch_scatter(vm->arena, doffs, dlens, dat, ddata, (uint32_t)n, vm->stream))
+            e = hipErrorLaunchFailure;
+        if (e == hipSuccess) e = hipStreamSynchronize(vm->stream);
+        hipFree(d);
+        if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "map writes: %s", hipGetErrorString(e));
+    }
+    vm->pend.clear();
+    vm->pend_data.clear();
+    vm->pend_at.clear();
+    vm->host_dirty = false;
+    return 0;
+}
+
+// the sequential hash algorithm on the image (hashmap.h h_find / h_probe_held / h_place_held /
+// h_fl_pop / h_fl_push with one thread): slot of the key or -1; *pos = its bucket, *freep = the
+// first reusable bucket on its probe path
+static int32_t mh_probe(const HostMap &m, const KeyBytes &ks, uint64_t h, uint32_t *pos, uint32_t *freep) {
+    const HashMirror &x = *m.mir;
+    const uint32_t mask = m.ht_cap - 1, tag = (uint32_t)(h >> 32), nq = (m.key_size + 7) >> 3;
+    uint32_t p = (uint32_t)h & mask;
+    *freep = HT_EMPTY;
+    for (uint32_t n = 0; n < m.ht_cap; n++, p = (p + 1) & mask) {
+        const uint64_t *r = &x.rec[(size_t)p * m.rec_q];
+        const uint32_t st = (uint32_t)r[0];
+        if (st == HT_EMPTY) {
+            if (*freep == HT_EMPTY) *freep = p;
+            return -1;
+        }
+        if (st == HT_TOMB) {
+            if (*freep == HT_EMPTY) *freep = p;
+            continue;
+        }
+        if (st < HT_BUSY && (uint32_t)(r[0] >> 32) == tag) {
+            bool eq = true;
+            for (uint32_t q = 0; q < nq && eq; q++) eq = r[1 + q] == ks.word(q);
+            if (eq) {
+                *pos = p;
+                return (int32_t)st;
+            }
+        }
+    }
+    return -1;
+}
+
+// LinuxHashMap.Update :158-203 / LinuxPerCPUHashMap.Update :564-612 on the image: 0 or E2BIG
+static int mh_update(mimic_vm *vm, const HostMap &m, const void *key, const void *value, int32_t cpu) {
+    HashMirror &x = *m.mir;
+    const KeyBytes ks{(const uint8_t *)key, m.key_size};
+    const uint64_t h = h_hash(ks, m.key_size);
+    uint32_t pos = 0, freep = HT_EMPTY;
+    int32_t idx = mh_probe(m, ks, h, &pos, &freep);
+    if (idx < 0) {
+        if (x.ctl.avail <= 0) return 7;   // the freelist is empty: syscall.E2BIG
+        x.ctl.avail--;
+        const uint64_t at = x.ctl.head++;
+        int32_t &f = x.ring[at & (m.fl_cap - 1)];
+        idx = f;
+        f = -1;
+        uint64_t *r = &x.rec[(size_t)freep * m.rec_q];
+        if ((uint32_t)r[0] == HT_EMPTY) x.ctl.used0++;
+        for (uint32_t q = 0; q * 8 < m.key_size; q++) r[1 + q] = ks.word(q);
+        r[0] = ((uint64_t)(uint32_t)(h >> 32) << 32) | (uint32_t)idx;
+        memcpy(x.keys.data() + (size_t)idx * m.key_size, key, m.key_size);   // keys.Write (:188-192)
+        x.dirty = true;
+        vm->host_dirty = true;
+    }
+    // values[cpu].Write(idx * S, value) (:193-200)
+    stage_write(vm, m.dev_off + (m.family == FAM_PERCPU_HASH ? (uint64_t)cpu * m.dev_stride : 0) + (uint64_t)idx * m.value_size,
+                value, m.value_size);
+    return 0;
+}
+
+// LinuxHashMap.Delete :225-255 on the image (an absent key is no error)
+static void mh_delete(mimic_vm *vm, const HostMap &m, const void *key) {
+    HashMirror &x = *m.mir;
+    const KeyBytes ks{(const uint8_t *)key, m.key_size};
+    const uint64_t h = h_hash(ks, m.key_size);
+    uint32_t pos = 0, freep;
+    const int32_t idx = mh_probe(m, ks, h, &pos, &freep);
+    if (idx < 0) return;
+    uint64_t &w = x.rec[(size_t)pos * m.rec_q];
+    w = (w & ~0xffffffffull) | HT_TOMB;
+    const uint64_t at = x.ctl.tail++;
+    x.ring[at & (m.fl_cap - 1)] = idx;   // the freelist's tail (:244-250)
+    x.ctl.avail++;
+    x.dirty = true;
+    vm->host_dirty = true;
+    m.may_tomb = true;
 }
 
 // LinuxArrayMap.Update / LinuxPerCPUArrayMap.Update (emulator_linux_map_array.go:97-113, 244-250),
@@ -876,17 +1076,31 @@ int mimic_map_update(mimic_vm *vm, uint32_t id, const void *key, const void *val
     if (is_hash(m)) {
         if (m.family == FAM_HASH) cpu = 0;  // LinuxHashMap ignores cpuid
         else if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
-        int32_t slot = -1;
-        if ((rc = hash_op(vm, m, 1, key, value, cpu, &slot))) return rc;
-        return slot < 0 ? 7 : 0;  // full freelist: syscall.E2BIG
+        if ((rc = mirror_ensure(vm, m))) return rc;
+        return mh_update(vm, m, key, value, cpu);
     }
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     if (m.key_size != 4) return fail(vm, MIMIC_EINVAL, "invalid key length, must be 4 bytes for array maps");
     uint32_t k;
     memcpy(&k, key, 4);
     if (k >= m.max_entries) return 7;  // syscall.E2BIG
-    if ((rc = settle(vm))) return rc;
-    HIP_OK(vm, hipMemcpy(vm->arena + base + (uint64_t)k * m.value_size, value, m.value_size, hipMemcpyHostToDevice));
+    stage_write(vm, base + (uint64_t)k * m.value_size, value, m.value_size);   // applied before the device reads the map
+    return 0;
+}
+
+// n LinuxMap.Update calls in one (keys packed K bytes apart, values S bytes apart): rc_out[i] =
+// what the i-th call returns (0 or a positive errno); returns 0 or the first fatal error
+int mimic_map_update_batch(mimic_vm *vm, uint32_t id, const void *keys, const void *values, uint32_t n, uint32_t flags,
+                           int32_t cpu, int32_t *rc_out) {
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    const HostMap &m = vm->maps[id];
+    for (uint32_t i = 0; i < n; i++) {
+        rc = mimic_map_update(vm, id, (const uint8_t *)keys + (size_t)i * m.key_size,
+                              (const uint8_t *)values + (size_t)i * m.value_size, flags, cpu);
+        if (rc < 0) return rc;
+        if (rc_out) rc_out[i] = rc;
+    }
     return 0;
 }
 
@@ -903,8 +1117,10 @@ int mimic_map_lookup(mimic_vm *vm, uint32_t id, const void *key, int32_t cpu, ui
             if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
             b += (uint32_t)cpu * m.addr_period;
         }
-        int32_t slot = -1;
-        if ((rc = hash_op(vm, m, 0, key, nullptr, 0, &slot))) return rc;
+        if ((rc = mirror_ensure(vm, m))) return rc;
+        const KeyBytes ks{(const uint8_t *)key, m.key_size};
+        uint32_t pos = 0, freep;
+        const int32_t slot = mh_probe(m, ks, h_hash(ks, m.key_size), &pos, &freep);
         *addr_out = slot < 0 ? 0 : b + (uint32_t)slot * m.value_size;
         return 0;
     }
@@ -923,17 +1139,17 @@ int mimic_map_delete(mimic_vm *vm, uint32_t id, const void *key) {
     if (rc) return rc;
     const HostMap &m = vm->maps[id];
     if (!is_hash(m)) return fail(vm, MIMIC_EINVAL, "can't delete from given LinuxMap");
-    int32_t slot = -1;
-    return hash_op(vm, m, 2, key, nullptr, 0, &slot);
+    if ((rc = mirror_ensure(vm, m))) return rc;
+    mh_delete(vm, m, key);
+    return 0;
 }
 
 // live (key, slot) pairs of a hash map in table order
 static int hash_entries(mimic_vm *vm, const HostMap &m, uint8_t *keys, int32_t *slots, size_t cap_entries,
                         uint32_t *n_out) {
-    int rc = settle(vm);
+    int rc = mirror_ensure(vm, m);
     if (rc) return rc;
-    std::vector<uint64_t> rec((size_t)m.ht_cap * m.rec_q);
-    HIP_OK(vm, hipMemcpy(rec.data(), vm->arena + m.ht_dev_off, rec.size() * 8, hipMemcpyDeviceToHost));
+    const std::vector<uint64_t> &rec = m.mir->rec;
     uint32_t n = 0;
     for (uint32_t p = 0; p < m.ht_cap; p++) {
         const uint64_t *r = &rec[(size_t)p * m.rec_q];
@@ -982,7 +1198,7 @@ int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, siz
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     uint64_t n = (uint64_t)m.max_entries * m.value_size;
     if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
-    if ((rc = settle(vm))) return rc;
+    if ((rc = flush_host(vm)) || (rc = settle(vm))) return rc;
     HIP_OK(vm, hipMemcpy(out, vm->arena + base, n, hipMemcpyDeviceToHost));
     return (int)n;
 }
@@ -993,7 +1209,7 @@ int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
     const HostMap &m = vm->maps[id];
     if (m.type == 3) return fail(vm, MIMIC_ENOTSUP, "program arrays are not reset");   // ebpf.ProgramArray
     hipSetDevice(vm->s.device);
-    if ((rc = skb_settle(vm))) return rc;
+    if ((rc = skb_settle(vm)) || (rc = flush_host(vm))) return rc;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
     if (vm->last_stream && vm->last_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
     HIP_OK(vm, hipMemsetAsync(vm->arena + m.dev_off, 0, (size_t)m.dev_stride * m.ncpu, st));
@@ -1003,6 +1219,7 @@ int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
         const DMap dm = to_dmap(m);
         if (mimic_launch_hash_reset(vm->arena, &dm, st))
             return fail(vm, MIMIC_EDEVICE, "reset: %s", hipGetErrorString(hipGetLastError()));
+        mirror_fresh(m);   // the image of the table the reset leaves
     }
     vm->last_stream = st;
     return 0;
@@ -1023,7 +1240,7 @@ int mimic_map_read_values_range(mimic_vm *vm, uint32_t id, int32_t cpu_begin, in
     const uint64_t row = (uint64_t)m.max_entries * m.value_size, n = row * (c1 - c0);
     if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
     if (n == 0) return 0;
-    if ((rc = settle(vm))) return rc;
+    if ((rc = flush_host(vm)) || (rc = settle(vm))) return rc;
     if (m.dev_stride == row || c1 - c0 == 1)
         HIP_OK(vm, hipMemcpy(out, vm->arena + m.dev_off + (uint64_t)c0 * m.dev_stride, n, hipMemcpyDeviceToHost));
     else
@@ -1045,6 +1262,7 @@ int mimic_map_sum_u64(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_
         c1 = (uint32_t)cpu_end;
     }
     if (m.max_entries == 0) return 0;
+    if ((rc = flush_host(vm))) return rc;
     uint64_t *d = nullptr;
     HIP_OK(vm, hipMalloc(&d, m.max_entries * sizeof(uint64_t)));
     hipStream_t st = vm->last_stream ? vm->last_stream : vm->stream;
@@ -1127,6 +1345,7 @@ int mimic_mem_read(mimic_vm *vm, uint32_t addr, void *buf, uint32_t len) {
     if (R.kind == 2) return fail(vm, MIMIC_EFAULT, "not vm memory 0x%x", addr);
     if (R.kind == 3) return fail(vm, MIMIC_EFAULT, "Can't access non-data-section array map directly");
     if ((uint64_t)R.off + len > R.limit) return fail(vm, MIMIC_EFAULT, "out of bounds");
+    if (int rc = flush_host(vm)) return rc;
     if (vm->last_stream) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
     HIP_OK(vm, hipMemcpy(buf, vm->arena + R.dev_off + R.off, len, hipMemcpyDeviceToHost));
     return 0;
@@ -1337,6 +1556,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     const uint32_t ctx = skb ? CTX_SKB : CTX_XDP;
     hipSetDevice(vm->s.device);
     int rc = upload_tables(vm);
+    if (!rc) rc = flush_host(vm);   // host map operations before this batch
     if (rc) return rc;
     hipStream_t st = st_in ? st_in : vm->stream;
     const uint32_t cpu_lanes = step ? 1u : (uint32_t)vm->s.vcpu_count;
@@ -1581,6 +1801,8 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         }
         if (!vm->prog_deletes) m.pop_dirty = true;
         if (vm->prog_deletes) m.may_tomb = true;
+        // the launch may change the table (or the rebuild below may): the host image is stale
+        if (m.mir && (vm->prog_updates || vm->prog_deletes || m.may_tomb)) m.mir->valid = false;
         if (!m.may_tomb) continue;
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));

@@ -20,11 +20,14 @@
 //     counters) is accessed with agent-scope atomics or sc1 loads/stores.  Per-XCD L2s are not
 //     coherent, so plain accesses would be wrong here.
 // The map values themselves are plain VM memory.  Concurrent vCPUs writing one shared map race
-// on them exactly as the reference's processPool workers do.
+// on them exactly as the reference's processPool workers do.  Host map operations (LinuxMap.Update
+// / Lookup / Delete from the API) run the sequential form of the same algorithm on a host image
+// of this index (engine.cpp HashMirror), which is uploaded before the device next uses the map.
 #pragma once
 #include "layout.h"
 
 #define HDEV static __device__ __forceinline__
+#define HHD static __host__ __device__ __forceinline__   // also the host mirror's (engine.cpp)
 
 HDEV uint64_t h_ld(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 HDEV void h_st(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -63,7 +66,7 @@ HDEV uint32_t h_used_total(const HashCtl *c) {
 // key hash over the zero-padded little-endian key words (any good 64-bit mix; the reference's
 // sha256 only names Go-map buckets, which no program can observe)
 template <class KS>
-HDEV uint64_t h_hash(const KS &ks, uint32_t K) {
+HHD uint64_t h_hash(const KS &ks, uint32_t K) {
     uint64_t h = 0x9e3779b97f4a7c15ull ^ K;
     const uint32_t nq = (K + 7) >> 3;
     for (uint32_t q = 0; q < nq; q++) {
@@ -132,44 +135,8 @@ HDEV int32_t h_find_ro(const HT &t, const KS &ks, uint64_t h) {
     return -1;
 }
 
-// freelist (emulator_linux_map_hash.go:179-186 pop, :244-250 push)
-HDEV int32_t h_fl_pop(const HT &t) {
-    HashCtl *c = h_ctl(t);
-    const int32_t a = __hip_atomic_fetch_add(&c->avail, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a <= 0) {
-        __hip_atomic_fetch_add(&c->avail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return -1;
-    }
-    const unsigned long long at = __hip_atomic_fetch_add(&c->head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int32_t *f = h_ring(t) + (at & (t.fl_cap - 1));
-    int32_t v;
-    // the push that fills this position has already reserved it (avail counted it)
-    while ((v = __hip_atomic_exchange(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0) __builtin_amdgcn_s_sleep(1);
-    return v;
-}
-HDEV void h_fl_push(const HT &t, int32_t idx) {
-    HashCtl *c = h_ctl(t);
-    const unsigned long long at = __hip_atomic_fetch_add(&c->tail, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int32_t *f = h_ring(t) + (at & (t.fl_cap - 1));
-    for (;;) {
-        int32_t e = -1;
-        if (__hip_atomic_compare_exchange_strong(f, &e, idx, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __hip_atomic_fetch_add(&c->avail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 HDEV uint32_t *h_lock(const HT &t, uint64_t h) {
     return h_locks(t) + ((uint32_t)h & (t.nlocks - 1));
-}
-HDEV void h_acquire(uint32_t *lk) {
-    for (;;) {
-        uint32_t e = 0;
-        if (__hip_atomic_compare_exchange_strong(lk, &e, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            return;
-        __builtin_amdgcn_s_sleep(2);
-    }
 }
 HDEV bool h_try_acquire(uint32_t *lk) {
     uint32_t e = 0;
@@ -229,41 +196,6 @@ HDEV bool h_place_held(const HT &t, const KS &ks, uint64_t h, uint32_t freep, in
     h_drain();
     h_st(r, ((uint64_t)tag << 32) | (uint32_t)idx);
     return was_empty;
-}
-
-// find-or-insert with the key's stripe lock `lk` held, ONE lane (host-side map operations);
-// releases the lock.  Returns the slot, or -1 when the freelist is empty (E2BIG).
-template <class KS>
-HDEV int32_t h_insert_held(const HT &t, const KS &ks, uint64_t h, uint32_t *lk, bool *inserted) {
-    *inserted = false;
-    uint32_t freep;
-    const int32_t found = h_probe_held(t, ks, h, &freep);
-    if (found >= 0) {
-        h_release(lk);
-        return found;
-    }
-    const int32_t idx = h_fl_pop(t);
-    if (idx >= 0) {
-        if (h_place_held(t, ks, h, freep, idx))
-            __hip_atomic_fetch_add(&h_ctl(t)->used0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *inserted = true;
-    }
-    h_release(lk);
-    return idx;
-}
-
-// delete with the key's stripe lock `lk` held, ONE lane; releases it.  The deleted slot or -1
-template <class KS>
-HDEV int32_t h_delete_held(const HT &t, const KS &ks, uint64_t h, uint32_t *lk) {
-    uint32_t p = 0;
-    const int32_t idx = h_find(t, ks, h, &p);
-    if (idx >= 0) {
-        uint64_t *r = h_rec(t, p);
-        h_st(r, (h_ld(r) & ~0xffffffffull) | HT_TOMB);
-        h_fl_push(t, idx);
-    }
-    h_release(lk);
-    return idx;
 }
 
 // Wave-cooperative locking.  A lane may never spin on a lock while a lane of its own wave holds
@@ -440,7 +372,7 @@ HDEV void h_delete_wave(const HT &t, const KS &ks, uint64_t h) {
 struct KeyBytes {
     const uint8_t *p;
     uint32_t K;
-    __device__ uint64_t word(uint32_t q) const {
+    __host__ __device__ uint64_t word(uint32_t q) const {
         uint64_t v = 0;
         const uint32_t o = q * 8, c = K - o < 8 ? K - o : 8;
         for (uint32_t i = 0; i < c; i++) v |= (uint64_t)p[o + i] << (8 * i);

@@ -489,36 +489,15 @@ extern "C" __global__ __launch_bounds__(SUM_THREADS) void mimic_sum_u64_kernel(c
 
 // One host-side hash-map operation (mimic_map_update/lookup/delete), run by the same device code
 // the helpers use so that both sides share the index and the freelist.
-extern "C" __global__ void mimic_hash_op_kernel(uint8_t *arena, DMap m, uint32_t op, const uint8_t *key,
-                                                const uint8_t *val, int32_t cpu, int32_t *out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const KeyBytes ks{key, m.key_size};
-    const uint64_t h = h_hash(ks, m.key_size);
-    const HT t = h_table(arena, m);
-    int32_t idx;
-    if (op == 0) {
-        idx = h_find(t, ks, h, nullptr);
-    } else if (op == 1) {
-        idx = h_find(t, ks, h, nullptr);
-        bool ins = false;
-        if (idx < 0) {   // one thread: it may wait for its stripe lock
-            uint32_t *lk = h_lock(t, h);
-            h_acquire(lk);
-            idx = h_insert_held(t, ks, h, lk, &ins);
-        }
-        if (idx >= 0) {  // keys.Write + values[cpu].Write (emulator_linux_map_hash.go:188-200)
-            uint8_t *kd = arena + m.keys_dev_off + (size_t)idx * m.key_size;
-            for (uint32_t i = 0; i < m.key_size; i++) kd[i] = key[i];
-            uint8_t *vd = arena + m.dev_off + (m.family == FAM_PERCPU_HASH ? (size_t)cpu * m.dev_stride : 0) +
-                          (size_t)idx * m.value_size;
-            for (uint32_t i = 0; i < m.value_size; i++) vd[i] = val[i];
-        }
-    } else {
-        uint32_t *lk = h_lock(t, h);
-        h_acquire(lk);
-        idx = h_delete_held(t, ks, h, lk);
-    }
-    *out = idx;
+// Host map writes staged by engine.cpp (stage_write / flush_host): entry k copies lens[k] bytes
+// from data + at[k] to arena + offs[k] (the host deduplicated the offsets: no two entries overlap)
+extern "C" __global__ void mimic_scatter_kernel(uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
+                                                const uint32_t *at, const uint8_t *data, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint8_t *d = arena + offs[k];
+    const uint8_t *s = data + at[k];
+    for (uint32_t b = 0; b < lens[k]; b++) d[b] = s[b];
 }
 
 // Tombstone compaction: when live + deleted buckets pass 3/4 of the table, rebuild it in
@@ -609,9 +588,10 @@ extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mimic_launch_hash_op(uint8_t *arena, const DMap *m, uint32_t op, const uint8_t *key, const uint8_t *val,
-                                    int32_t cpu, int32_t *out, hipStream_t st) {
-    hipLaunchKernelGGL(mimic_hash_op_kernel, dim3(1), dim3(64), 0, st, arena, *m, op, key, val, cpu, out);
+extern "C" int mimic_launch_scatter(uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *at,
+                                    const uint8_t *data, uint32_t n, hipStream_t st) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(mimic_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, st, arena, offs, lens, at, data, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

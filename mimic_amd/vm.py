@@ -141,9 +141,10 @@ class LinuxMap:
     def Lookup(self, key: bytes, cpuid: int = 0) -> int:
         """Virtual address of the value, 0 if absent (LinuxMap.Lookup)."""
         vm = self._vm
+        if len(key) != self.Spec.KeySize:
+            raise MimicError("size of given key doesn't match key size in map spec")
         addr = C.c_uint32()
-        kb = C.create_string_buffer(bytes(key), max(len(key), 1))
-        _check(vm.h, vm.lib.mimic_map_lookup(vm.h, self.id, kb, cpuid, C.byref(addr)), "lookup")
+        _check(vm.h, vm.lib.mimic_map_lookup(vm.h, self.id, bytes(key), cpuid, C.byref(addr)), "lookup")
         return addr.value
 
     def Update(self, key: bytes, value: bytes, flags: int = 0, cpuid: int = 0) -> int:
@@ -151,14 +152,35 @@ class LinuxMap:
         vm = self._vm
         if len(value) != self.Spec.ValueSize:
             raise MimicError(f"invalid value length, must be {self.Spec.ValueSize} bytes")
-        kb = C.create_string_buffer(bytes(key), max(len(key), 1))
-        vb = C.create_string_buffer(bytes(value), max(len(value), 1))
-        return _check(vm.h, vm.lib.mimic_map_update(vm.h, self.id, kb, vb, flags, cpuid), "update")
+        if len(key) != self.Spec.KeySize:   # emulator_linux_map_hash.go:159-161, _array.go:98-100
+            raise MimicError("size of given key doesn't match key size in map spec")
+        rc = vm.lib.mimic_map_update(vm.h, self.id, bytes(key), bytes(value), flags, cpuid)
+        return rc if rc >= 0 else _check(vm.h, rc, "update")
+
+    def UpdateBatch(self, keys, values, flags: int = 0, cpuid: int = 0):
+        """Not in the reference API: Update(keys[i], values[i]) for every i in one call (numpy
+        uint8 arrays of shape (n, KeySize) / (n, ValueSize), or concatenated bytes).  Returns the
+        per-call results (0 or a positive errno) as a numpy int32 array."""
+        import numpy as np
+
+        vm = self._vm
+        kb = np.ascontiguousarray(np.frombuffer(keys, np.uint8) if isinstance(keys, (bytes, bytearray)) else keys,
+                                  dtype=np.uint8).reshape(-1)
+        vb = np.ascontiguousarray(np.frombuffer(values, np.uint8) if isinstance(values, (bytes, bytearray)) else values,
+                                  dtype=np.uint8).reshape(-1)
+        n = len(kb) // max(self.Spec.KeySize, 1)
+        if len(kb) != n * self.Spec.KeySize or len(vb) != n * self.Spec.ValueSize:
+            raise MimicError("keys / values do not hold the same number of entries")
+        rcs = np.zeros(n, np.int32)
+        _check(vm.h, vm.lib.mimic_map_update_batch(vm.h, self.id, kb.ctypes.data, vb.ctypes.data, n, flags, cpuid,
+                                                   rcs.ctypes.data), "update batch")
+        return rcs
 
     def Delete(self, key: bytes) -> int:
         vm = self._vm
-        kb = C.create_string_buffer(bytes(key), max(len(key), 1))
-        return _check(vm.h, vm.lib.mimic_map_delete(vm.h, self.id, kb), "delete")
+        if len(key) != self.Spec.KeySize:
+            raise MimicError("size of given key doesn't match key size in map spec")
+        return _check(vm.h, vm.lib.mimic_map_delete(vm.h, self.id, bytes(key)), "delete")
 
     def Values(self, cpuid: int = 0) -> bytes:
         """Raw value backing (MaxEntries * ValueSize bytes) of one cpu."""
