@@ -317,6 +317,106 @@ HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted
     return idx;
 }
 
+// find-or-insert for the calling lanes of a wave in a pop-only launch (no program of the launch
+// deletes): no stripe lock.  A bucket then only moves EMPTY / TOMB -> BUSY -> live during the
+// launch (the one exception, a claim given back on E2BIG, happens only once the freelist is spent
+// for good), so every lane inserting key k targets the same bucket: the first reusable one on k's
+// probe path that no other key holds.  Each round a pending lane walks its path from the home
+// bucket: its key live -> found; a BUSY bucket before any reusable one -> it may be k being
+// written, wait for the next round; else it tries to claim the first reusable bucket with one CAS
+// (lanes of one key race for the same bucket, one wins).  Winners take their freelist positions
+// with one head reservation for the round (lane order), write the key words and publish tag | slot
+// in the same round (a lane never waits on a lane of its own wave), or give the bucket back when
+// the freelist is spent (E2BIG).  A lone lane pops exactly as h_insert_wave does (FIFO slots).
+template <class KS>
+HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *inserted) {
+    const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32);
+    const uint32_t me = __lane_id();
+    HashCtl *c = h_ctl(t);
+    bool done = false;
+    int32_t idx = -1;
+    *inserted = false;
+    for (;;) {
+        const uint64_t pend = __ballot(!done);
+        if (!pend) break;
+        uint32_t cand = HT_EMPTY;
+        uint64_t cw = 0;
+        bool blocked = false;
+        if (!done) {
+            uint32_t p = (uint32_t)h & mask;
+            for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+                const uint64_t *r = h_rec(t, p);
+                const uint64_t w = h_ld(r);
+                const uint32_t s = (uint32_t)w;
+                if (s == HT_EMPTY || s == HT_TOMB) {
+                    if (cand == HT_EMPTY) {
+                        cand = p;
+                        cw = w;
+                    }
+                    if (s == HT_EMPTY) break;
+                    continue;
+                }
+                if (s == HT_BUSY) {
+                    if (cand == HT_EMPTY) {   // before any reusable bucket: possibly this key
+                        blocked = true;
+                        break;
+                    }
+                    continue;
+                }
+                if ((uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K)) {
+                    idx = (int32_t)s;
+                    done = true;
+                    break;
+                }
+            }
+        }
+        const bool mine = !done && !blocked && cand != HT_EMPTY &&
+                          h_cas(h_rec(t, cand), cw, ((uint64_t)tag << 32) | HT_BUSY);
+        const uint64_t needm = __ballot(mine);
+        int32_t slot = -1;
+        if (needm) {
+            const uint32_t k = (uint32_t)__builtin_popcountll(needm), first = (uint32_t)__builtin_ctzll(needm);
+            uint32_t got = 0;
+            uint64_t base = 0;
+            if (me == first) {
+                base = __hip_atomic_fetch_add(&c->head, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long tl = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                got = base >= tl ? 0u : (tl - base < k ? (uint32_t)(tl - base) : k);
+            }
+            got = (uint32_t)__builtin_amdgcn_readlane((int)got, (int)first);
+            base = h_bcast64(base, first);
+            const uint32_t rank = (uint32_t)__builtin_popcountll(needm & ((1ull << me) - 1));
+            if (mine && rank < got) {   // positions below tail were written before this launch
+                int32_t *f = h_ring(t) + ((base + rank) & (t.fl_cap - 1));
+                slot = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        bool empty_used = false;
+        if (mine) {
+            uint64_t *r = h_rec(t, cand);
+            if (slot >= 0) {
+                const uint32_t nq = (t.K + 7) >> 3;
+                for (uint32_t q = 0; q < nq; q++) h_st(r + 1 + q, ks.word(q));
+                h_drain();
+                h_st(r, ((uint64_t)tag << 32) | (uint32_t)slot);
+                empty_used = (uint32_t)cw == HT_EMPTY;
+                idx = slot;
+                *inserted = true;
+            } else {
+                h_st(r, cw);   // the freelist is spent: E2BIG, the bucket as it was
+                idx = -1;
+            }
+            done = true;
+        }
+        const uint64_t um = __ballot(empty_used);
+        if (um && me == (uint32_t)__builtin_ctzll(um))
+            __hip_atomic_fetch_add(h_used_shard(c), (uint32_t)__builtin_popcountll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!done) __builtin_amdgcn_s_sleep(1);
+    }
+    return idx;
+}
+
 // delete for the calling lanes of a wave: lock rounds as above; the freed slots of a round go to
 // the freelist tail with one reservation and one `avail` release for the round (after every
 // ring position of the round is written).

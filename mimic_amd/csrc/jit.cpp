@@ -322,6 +322,13 @@ class Gen {
                 for (uint32_t i = 0; i < p.n; i++)
                     if (AUX_H(p.ins[i].aux) == H_CALL && ((uint32_t)p.ins[i].k == 2 || (uint32_t)p.ins[i].k == 3)) writes = true;
             E.line("#define MIMIC_HASH_RO %d", writes ? 0 : 1);
+            // no program of the set deletes: every launch of the kernel is pop-only (engine.cpp
+            // KParams.hash_pop_only from the same programs), so only the lock-free insert is built
+            bool deletes = false;
+            for (auto &p : P)
+                for (uint32_t i = 0; i < p.n; i++)
+                    if (AUX_H(p.ins[i].aux) == H_CALL && (uint32_t)p.ins[i].k == 3) deletes = true;
+            E.line("#define MIMIC_HASH_POPONLY %d", deletes ? 0 : 1);
         }
         E.line("#include \"runtime.h\"");
         if (spread_on) {

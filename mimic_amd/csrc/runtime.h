@@ -19,6 +19,17 @@ typedef uint32_t __attribute__((aligned(1))) u32u;
 typedef uint64_t __attribute__((aligned(1))) u64u;
 
 #define DEV static __device__ __forceinline__
+// pop-only launches insert without stripe locks (hashmap.h h_insert_nolock); MIMIC_JIT_DEFS=
+// MIMIC_HASH_NOLOCK=0 builds the locked rounds instead (measurement)
+#ifndef MIMIC_HASH_NOLOCK
+#define MIMIC_HASH_NOLOCK 1
+#endif
+// no program of the launch deletes (KParams.hash_pop_only); a JIT kernel knows it at compile time
+#ifdef MIMIC_HASH_POPONLY
+#define HASH_POPONLY(kp) (MIMIC_HASH_POPONLY != 0)
+#else
+#define HASH_POPONLY(kp) ((kp).hash_pop_only != 0)
+#endif
 // hash tables read-only during the launch (KParams.hash_ro); a JIT kernel knows it at compile time
 #ifdef MIMIC_HASH_RO
 #define HASH_RO(kp) (MIMIC_HASH_RO != 0)
@@ -782,7 +793,8 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
     bool inserted = false;
     if (idx < 0) {
         // a new key: find-or-insert under its stripe lock, the wave's lanes in lock rounds
-        idx = h_insert_wave(t, ks, h, &inserted, kp.hash_pop_only != 0);
+        idx = HASH_POPONLY(kp) ? (MIMIC_HASH_NOLOCK ? h_insert_nolock(t, ks, h, &inserted) : h_insert_wave(t, ks, h, &inserted, true))
+                               : h_insert_wave(t, ks, h, &inserted, false);
     }
     if (idx < 0) {
         o.r0 = 7; // syscall.E2BIG: the freelist is empty
