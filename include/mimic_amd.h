@@ -220,6 +220,29 @@ int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch,
  * batches until mimic_skb_release. */
 #define MIMIC_CTX_XDP 0
 #define MIMIC_CTX_SKB 1
+/* A user-given sock and / or flow keys of one sk_buff context (LinuxContextSKBuff.SK / .FlowKeys,
+ * JSON "sock" / "flowKeys", context_sk_buff.go:24-26; Load puts them in place of the ones
+ * SKBuffFromBytes made, :53-66).  SK fields: emulator_linux_sk_buff.go:698-718; its net.IP fields
+ * as SK.UnmarshalJSON leaves them (:721-757): the bytes net.ParseIP returns (16 for any address;
+ * To16 for the IPv6 ones), else make(net.IP, 4 / 16); length 0 = nil (an SK built without
+ * UnmarshalJSON).  FlowKeys fields (:967-982) are the initial values of the writable flow keys;
+ * its SrcIPv6orIPv4 is never readable (convertAccess slices a 16-byte copy at offsets 16..31,
+ * :1117-1140: a panic for every access), so it is not carried. */
+#define MIMIC_SKB_CUSTOM_SK 1u
+#define MIMIC_SKB_CUSTOM_FLOWKEYS 2u
+typedef struct {
+    uint32_t flags;             /* MIMIC_SKB_CUSTOM_*: which of the two the context gives (0: none) */
+    uint32_t sk_bound_dev_if, sk_family, sk_type, sk_protocol, sk_mark, sk_priority;
+    uint32_t sk_src_port, sk_dst_port, sk_state;
+    int32_t sk_rx_queue_mapping;
+    uint8_t sk_ip_len[4];       /* srcIP4, dstIP4, srcIP6, dstIP6: len() of the net.IP (0 = nil, <= 16) */
+    uint8_t sk_ip[4][16];
+    uint16_t fk_nhoff, fk_thoff, fk_addr_proto;
+    uint8_t fk_is_frag, fk_is_first_frag, fk_is_encap, fk_ip_proto;
+    uint16_t fk_n_proto, fk_sport, fk_dport;
+    uint32_t fk_flags, fk_flow_label;
+} mimic_skb_custom;
+
 typedef struct {
     uint32_t n;
     uint32_t schedule;          /* MIMIC_SCHED_* */
@@ -230,6 +253,7 @@ typedef struct {
     int32_t pad;
     const int32_t *cpu;         /* HOST array for MIMIC_SCHED_EXPLICIT */
     uint64_t step_budget;       /* 0 = MIMIC default */
+    const mimic_skb_custom *custom;   /* DEVICE array [n] of user-given sock / flow keys, or NULL (none) */
 } mimic_skb_batch;
 
 /* Batch form of: for each packet i { p := vm.NewProcess(prog, &LinuxContextSKBuff{Packet: pkt_i,
@@ -245,8 +269,8 @@ int mimic_skb_release(mimic_vm *vm);
 /* ---- single processes: the NewProcess / SetCPUID / Step / Run / Cleanup surface ---------------
  * A process holds its own packet memory, private memory (stack, frames) and register state on
  * the device, so it can be advanced instruction by instruction (the edb debugger's use of
- * Process.Step, Readme.md:8).  Steps run on the batch interpreter with one lane.  xdp_md
- * contexts only (LinuxContextXDP). */
+ * Process.Step, Readme.md:8).  Steps run on the batch interpreter with one lane; xdp_md contexts
+ * (mimic_process_new) and sk_buff contexts (mimic_process_new_skb / _ctx). */
 typedef struct mimic_process mimic_process;
 typedef struct {
     uint64_t r[11];             /* Registers.R0 .. R10 */
@@ -268,6 +292,9 @@ int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32
  * packet memory being 32 + len + 64 bytes (headroom, frame, tailroom; emulator_linux_sk_buff.go:113-116). */
 int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
                           mimic_process **out);
+/* The same with a user-given sock / flow keys (custom: HOST pointer, or NULL). */
+int mimic_process_new_skb_ctx(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
+                              const mimic_skb_custom *custom, mimic_process **out);
 int mimic_process_set_cpu(mimic_process *p, int32_t id);
 /* n x Process.Step (vm.go:291-340), stopping early when the process exits or fails; the
  * registers after the last step in *out.  Stepping a process that hit a fatal error returns

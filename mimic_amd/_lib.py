@@ -63,7 +63,24 @@ class XDPBatch(C.Structure):
 class SKBBatch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("schedule", C.c_uint32), ("pkt_data", C.c_void_p),
                 ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p), ("ifindex", C.c_uint32), ("pad", C.c_int32),
-                ("cpu", C.c_void_p), ("step_budget", C.c_uint64)]
+                ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("custom", C.c_void_p)]
+
+
+# mimic_skb_custom (include/mimic_amd.h): a user-given sock / flow keys of one sk_buff context
+SKB_CUSTOM_SK, SKB_CUSTOM_FLOWKEYS = 1, 2
+try:
+    import numpy as _np
+
+    SKB_CUSTOM_DTYPE = _np.dtype([
+        ("flags", "<u4"), ("sk_bound_dev_if", "<u4"), ("sk_family", "<u4"), ("sk_type", "<u4"), ("sk_protocol", "<u4"),
+        ("sk_mark", "<u4"), ("sk_priority", "<u4"), ("sk_src_port", "<u4"), ("sk_dst_port", "<u4"), ("sk_state", "<u4"),
+        ("sk_rx_queue_mapping", "<i4"), ("sk_ip_len", "u1", (4,)), ("sk_ip", "u1", (4, 16)),
+        ("fk_nhoff", "<u2"), ("fk_thoff", "<u2"), ("fk_addr_proto", "<u2"), ("fk_is_frag", "u1"),
+        ("fk_is_first_frag", "u1"), ("fk_is_encap", "u1"), ("fk_ip_proto", "u1"), ("fk_n_proto", "<u2"),
+        ("fk_sport", "<u2"), ("fk_dport", "<u2"), ("fk_flags", "<u4"), ("fk_flow_label", "<u4")])
+    assert SKB_CUSTOM_DTYPE.itemsize == 136
+except ImportError:   # numpy is a dependency of every batch path; the ABI loads without it
+    SKB_CUSTOM_DTYPE = None
 
 
 CTX_XDP, CTX_SKB = 0, 1
@@ -95,6 +112,8 @@ EXPORTS = {
     "mimic_map_delete": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "mimic_exec_mode": (C.c_int, [C.c_void_p]),
     "mimic_set_spread": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mimic_process_new_skb_ctx": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                                            C.POINTER(C.c_void_p)]),
     "mimic_run_xdp_host": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPHostBatch), C.c_uint32]),
     "mimic_host_register": (C.c_int, [C.c_void_p, C.c_size_t]),
     "mimic_host_unregister": (C.c_int, [C.c_void_p]),

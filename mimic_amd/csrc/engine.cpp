@@ -655,6 +655,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
 }
 
 static void mirror_fresh(const HostMap &m);
+static_assert(sizeof(mimic_skb_custom) == 136, "mimic_skb_custom: the layout _lib.SKB_CUSTOM_DTYPE and the oracle use");
 
 // MapSpecToLinuxMap (emulator_linux_map.go:57-113) + Init + AddMap
 int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id) {
@@ -1364,6 +1365,7 @@ int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out) {
 // sub-batch, the index of its first packet in the whole batch (vCPU of packet k = (shift+k) % V)
 struct SkbRun {     // the sk_buff part of a batch (mimic_run_skb)
     uint32_t ifindex;
+    const mimic_skb_custom *custom;   // device, [n] or null
 };
 struct StepRun {    // a stepped single process (mimic_process_*): its state, private memory and budget
     StepState *state;
@@ -1373,6 +1375,7 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
     // an sk_buff process: its own record, leak prefix and leak base (made once, at NewProcess)
     SkbRec *skb_rec = nullptr;
     const uint64_t *skb_prefix = nullptr, *skb_base = nullptr;
+    const mimic_skb_custom *skb_custom = nullptr;   // its user-given sock / flow keys (device, one entry) or null
 };
 
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
@@ -1395,7 +1398,7 @@ int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, con
     b.pkt_len = sb->pkt_len;
     b.cpu = sb->cpu;
     b.step_budget = sb->step_budget;
-    const SkbRun r{sb->ifindex};
+    const SkbRun r{sb->ifindex, sb->custom};
     return run_xdp_impl(vm, prog_id, &b, res, (hipStream_t)hip_stream, 0, &r);
 }
 
@@ -1770,6 +1773,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.skb_rec = step->skb_rec;
         kp.skb_prefix = step->skb_prefix;
         kp.skb_base = step->skb_base;
+        kp.skb_custom = step->skb_custom;
     } else if (skb) {
         // a JIT kernel that walks the headers itself needs the footprints only
         const bool own_recs = jit && ji.skb_walk;
@@ -1781,6 +1785,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.skb_rec = vm->d_skb_rec;
         kp.skb_prefix = vm->d_skb_prefix;
         kp.skb_base = vm->d_skb_state + 1;
+        kp.skb_custom = skb->custom;
     }
     // compact hash tables whose buckets are mostly tombstones (device-side check, no host sync)
     // (skipped while no delete can have run on the map: without tombstones live entries stay
@@ -1872,8 +1877,9 @@ struct mimic_process {
     // LinuxContextSKBuff processes (context_sk_buff.go): the record, leak prefix (0) and leak base
     // of the process's Load, made at NewProcess like the reference's
     bool skb = false;
+    bool skb_custom = false;          // a user-given sock / flow keys after the base word
     uint32_t ifindex = 0;
-    uint8_t *d_skbmem = nullptr;      // SkbRec | foot | prefix | base
+    uint8_t *d_skbmem = nullptr;      // SkbRec | prefix (2 words) | base | mimic_skb_custom
 };
 
 static void process_release(mimic_process *p) {
@@ -1946,6 +1952,7 @@ static int process_advance(mimic_process *p, uint64_t budget) {
         sr.skb_rec = (SkbRec *)p->d_skbmem;
         sr.skb_prefix = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec));
         sr.skb_base = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 16);
+        if (p->skb_custom) sr.skb_custom = (const mimic_skb_custom *)(p->d_skbmem + sizeof(SkbRec) + 24);
     }
     int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, p->skb ? &skr : nullptr, &sr);
     if (rc) return rc;
@@ -2009,6 +2016,11 @@ static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint
 
 int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
                           mimic_process **out) {
+    return mimic_process_new_skb_ctx(vm, prog_id, packet, len, ifindex, nullptr, out);
+}
+
+int mimic_process_new_skb_ctx(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
+                              const mimic_skb_custom *custom, mimic_process **out) {
     if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     // the packet memory is SKB_HEADROOM + len + SKB_TAILROOM with the frame at +SKB_HEADROOM
@@ -2023,7 +2035,10 @@ int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, ui
     hipError_t e = hipSuccess;
     if (len) e = hipMemcpy(p->d_pkt + SKB_HEADROOM, packet, len, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_len, &len, 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_skbmem, sizeof(SkbRec) + 24);
+    if (e == hipSuccess) e = hipMalloc(&p->d_skbmem, sizeof(SkbRec) + 24 + sizeof(mimic_skb_custom));
+    p->skb_custom = custom && custom->flags;
+    if (e == hipSuccess && p->skb_custom)
+        e = hipMemcpy(p->d_skbmem + sizeof(SkbRec) + 24, custom, sizeof(mimic_skb_custom), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         mimic_process_free(p);
         *out = nullptr;

@@ -1515,12 +1515,13 @@ class Gen {
         if (!k || off < 0 || off > (k == 1 ? 40 : 80) || !(n == 1 || n == 2 || n == 4 || n == 8)) return;
         const char *fn = k == 1 ? "fk_convert_" : "sk_convert_";
         const char *at = k == 1 ? "L.ka + SKB_SK_SIZE + 1u + " : "L.ka + ";
+        const char *cu = k == 1 ? "" : "(const mimic_skb_custom *)kp.skb_custom, ";   // sk_convert_ reads a user-given SK
         if (load)
-            E.line("%sif (L.rec && ga_ == %s%uu) { uint64_t v_ = 0; const int s_ = %s(*L.rec, %uu, %uu, v_, true); if (s_) TERM(s_, %u); %s = v_; }",
-                   pre.c_str(), at, (uint32_t)off, fn, (uint32_t)off, n, i, v.c_str());
+            E.line("%sif (L.rec && ga_ == %s%uu) { uint64_t v_ = 0; const int s_ = %s(*L.rec, %s%uu, %uu, v_, true); if (s_) TERM(s_, %u); %s = v_; }",
+                   pre.c_str(), at, (uint32_t)off, fn, cu, (uint32_t)off, n, i, v.c_str());
         else
-            E.line("%sif (L.rec && ga_ == %s%uu) { uint64_t v_ = %s; const int s_ = %s(*L.rec, %uu, %uu, v_, false); if (s_) TERM(s_, %u); }",
-                   pre.c_str(), at, (uint32_t)off, v.c_str(), fn, (uint32_t)off, n, i);
+            E.line("%sif (L.rec && ga_ == %s%uu) { uint64_t v_ = %s; const int s_ = %s(*L.rec, %s%uu, %uu, v_, false); if (s_) TERM(s_, %u); }",
+                   pre.c_str(), at, (uint32_t)off, v.c_str(), fn, cu, (uint32_t)off, n, i);
         pre = "    else ";
     }
 
@@ -1535,7 +1536,7 @@ class Gen {
         }
         if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {  // __sk_buff field: convertAccess directly
             if (skb_field_ok(off, n)) {   // the field the instruction names, when base is the sk_buff
-                E.line("%sif (ga_ == SK_ + %uu) { uint64_t v_ = 0; const int s_ = skb_convert_(*L.rec, kp.skb_ifindex, L.pa + SKB_HEADROOM, "
+                E.line("%sif (ga_ == SK_ + %uu) { uint64_t v_ = 0; const int s_ = skb_convert_(*L.rec, (const mimic_skb_custom *)kp.skb_custom, kp.skb_ifindex, L.pa + SKB_HEADROOM, "
                        "L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, %uu, %uu, v_, true); if (s_) TERM(s_, %u); %s = v_; }",
                        pre.c_str(), (uint32_t)off, (uint32_t)off, n, i, dst.c_str());
                 pre = "    else ";
@@ -1543,7 +1544,7 @@ class Gen {
             if (defer_mode)   // the generic convertAccess is a call: the resume kernel runs it
                 E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) %s", pre.c_str(), defer_text(i).c_str());
             else
-                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
+                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, (const mimic_skb_custom *)kp.skb_custom, kp.skb_ifindex, "
                        "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, 0, true);"
                        " if (o_.st) TERM(o_.st, %u); %s = o_.v; }", pre.c_str(), n, i, dst.c_str());
             pre = "    else ";
@@ -1570,7 +1571,7 @@ class Gen {
         }
         if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {
             if (skb_field_ok(off, n)) {
-                E.line("%sif (ga_ == SK_ + %uu) { uint64_t v_ = %s; const int s_ = skb_convert_(*L.rec, kp.skb_ifindex, L.pa + SKB_HEADROOM, "
+                E.line("%sif (ga_ == SK_ + %uu) { uint64_t v_ = %s; const int s_ = skb_convert_(*L.rec, (const mimic_skb_custom *)kp.skb_custom, kp.skb_ifindex, L.pa + SKB_HEADROOM, "
                        "L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, %uu, %uu, v_, false); if (s_) TERM(s_, %u); }",
                        pre.c_str(), (uint32_t)off, val.c_str(), (uint32_t)off, n, i);
                 pre = "    else ";
@@ -1578,7 +1579,7 @@ class Gen {
             if (defer_mode)
                 E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) %s", pre.c_str(), defer_text(i).c_str());
             else
-                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, kp.skb_ifindex, "
+                E.line("%sif ((uint32_t)(ga_ - SK_) <= SKB_STRUCT_SIZE) { const SkbRes o_ = skb_convert(L.rec, (const mimic_skb_custom *)kp.skb_custom, kp.skb_ifindex, "
                        "L.pa + SKB_HEADROOM, L.pa + L.M - SKB_HEADROOM - SKB_TAILROOM, L.ka, L.ka + SKB_SK_SIZE + 1, ga_ - SK_, %uu, %s, false);"
                        " if (o_.st) TERM(o_.st, %u); }", pre.c_str(), n, val.c_str(), i);
             pre = "    else ";

@@ -216,6 +216,8 @@ struct KParams {
     // access that reaches per-CPU map memory would break that mode's exactness and sets *spread_bad
     // (never cleared: the host reports it as an engine error).  nullptr in every other launch.
     uint32_t *spread_bad;
+    // sk_buff batches: the user-given sock / flow keys (mimic_skb_custom [n], packet-indexed), or null
+    const void *skb_custom;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

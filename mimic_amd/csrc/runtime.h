@@ -546,10 +546,11 @@ DEV uint64_t bswap_n(uint64_t v, uint32_t n) {
 // SKBuff / SK / FlowKeys .Load / .Store (convertAccess): no PlainMemory bounds check
 DEV int skb_access(const KParams &kp, const Lane &L, const Ref &R, uint32_t n, uint64_t &v, bool load) {
     SkbRes o;
+    const mimic_skb_custom *cu = (const mimic_skb_custom *)kp.skb_custom;
     if (R.rk == RK_SKB)
-        o = skb_convert(L.rec, kp.skb_ifindex, L.pa + SKB_HEADROOM, L.pa + (L.M - SKB_HEADROOM - SKB_TAILROOM), L.ka,
+        o = skb_convert(L.rec, cu, kp.skb_ifindex, L.pa + SKB_HEADROOM, L.pa + (L.M - SKB_HEADROOM - SKB_TAILROOM), L.ka,
                         L.ka + SKB_SK_SIZE + 1, R.off, n, v, load);
-    else if (R.rk == RK_SK) o = sk_convert(L.rec, R.off, n, v, load);
+    else if (R.rk == RK_SK) o = sk_convert(L.rec, cu, R.off, n, v, load);
     else o = fk_convert(L.rec, R.off, n, v, load);
     if (load) v = o.v;
     return o.st;
@@ -948,8 +949,10 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     if (lw & SKB_LOAD_FAILED) return MIMIC_ERR_CTX_LOAD;
     const uint64_t ka = *kp.skb_base + skb_leak_pre(kp, i);
     if (ka + SKB_FOOT_FIXED - 1 + lw > 0xffffffffull) return MIMIC_ERR_CTX_LOAD;  // "out of memory"
-    if (!attach_only)   // the writable state at Load (the prep kernel writes the derived words only)
+    if (!attach_only) {   // the writable state at Load (the prep kernel writes the derived words only)
         for (uint32_t q = 0; q < 8; q++) ((uint64_t *)rec)[SKB_DERIVED_Q + q] = skb_writable_word(q);
+        skb_apply_custom(*rec, (const mimic_skb_custom *)kp.skb_custom, i);
+    }
     L.rec = rec;
     L.ka = (uint32_t)ka;
     L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
@@ -959,8 +962,10 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     return 0;
 }
 
-// skb_load's tail once the record is in place (LDS slot d): entries, rooms, R1
-DEV int skb_attach(const KParams &kp, Lane &L, uint64_t &r1, uint64_t *d, uint32_t lw, uint64_t pre, uint64_t base) {
+// skb_load's tail once the record of packet i is in place (LDS slot d): a user-given sock / flow
+// keys, entries, rooms, R1
+DEV int skb_attach(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint32_t lw, uint64_t pre, uint64_t base) {
+    skb_apply_custom(*(SkbRec *)d, (const mimic_skb_custom *)kp.skb_custom, i);
     L.rec = nullptr;
     L.ka = 0;
     L.pa = 0;
@@ -991,7 +996,7 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) d[SKB_DERIVED_Q + q] = skb_writable_word(q);
     L.pkt = kp.pkt_data + po;
-    return skb_attach(kp, L, r1, d, (uint32_t)w[0], pre, base);
+    return skb_attach(kp, L, i, r1, d, (uint32_t)w[0], pre, base);
 }
 
 // skb_load for a JIT kernel that builds the record itself (no prep records: a 160-byte write and
@@ -1005,7 +1010,7 @@ DEV int skb_load_walk(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint
     skb_stage<256u>(win, threadIdx.x, pkt, len);
     SkbRec &r = *(SkbRec *)d;
     skb_init(SkbWinBytes<256u>{win, pkt, threadIdx.x}, len, r);
-    return skb_attach(kp, L, r1, d, r.len, pre, base);
+    return skb_attach(kp, L, i, r1, d, r.len, pre, base);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -26,6 +26,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/mimic_amd.h"   // mimic_skb_custom (user-given sock / flow keys)
+
 #define SKB_STRUCT_SIZE 192u     // SKBuff.Size(), emulator_linux_sk_buff.go:679-681
 #define SKB_SK_SIZE 80u          // SK.Size()
 #define SKB_FK_SIZE 40u          // FlowKeys.Size()
@@ -66,7 +68,7 @@ struct SkbRec {  // 160 bytes
     uint8_t fk_is_frag, fk_is_first_frag, fk_is_encap, fk_ip_proto;
     uint16_t fk_n_proto, fk_sport, fk_dport;
     uint32_t fk_flags, fk_flow_label;
-    uint32_t pad2;
+    uint32_t cust;             // 1 + the process's entry in the batch's mimic_skb_custom table (0: none)
 };
 
 #define SKB_TSTAMP_ZERO (-62135596800ll)   // time.Time{}.Unix()
@@ -532,8 +534,51 @@ SKB_DEV void skb_init_regs(const uint32_t *w, uint32_t *win, uint32_t t, const u
 // ---------------------------------------------------------------------------------------
 SKB_DEV uint64_t skb_to_size(uint64_t v, uint32_t n) { return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1)); }
 
-// copy(v, ip[start:start+n]); b2i(v): a slice-bounds panic past the capacity
-SKB_DEV int skb_ip_load(const SkbRec &r, uint32_t which, uint64_t start, uint32_t n, uint64_t &v) {
+// the process's user-given sock (flag MIMIC_SKB_CUSTOM_SK) or flow keys (_FLOWKEYS), or null
+SKB_DEV const mimic_skb_custom *skb_cust(const SkbRec &r, const mimic_skb_custom *cu, uint32_t flag) {
+    if (!cu || !r.cust) return nullptr;
+    const mimic_skb_custom *c = cu + (r.cust - 1);
+    return (c->flags & flag) ? c : nullptr;
+}
+
+// LinuxContextSKBuff.Load's user-given SK / FlowKeys (context_sk_buff.go:53-66) for process i,
+// after the record's writable state got its defaults: the writable SK words and the flow keys
+// start from the user's values; the record remembers the entry for the read-only SK fields
+SKB_DEV void skb_apply_custom(SkbRec &r, const mimic_skb_custom *cu, uint32_t i) {
+    if (!cu || !cu[i].flags) return;
+    const mimic_skb_custom &c = cu[i];
+    if (c.flags & MIMIC_SKB_CUSTOM_SK) {
+        r.sk_bound_dev_if = c.sk_bound_dev_if;
+        r.sk_mark = c.sk_mark;
+        r.sk_priority = c.sk_priority;
+    }
+    if (c.flags & MIMIC_SKB_CUSTOM_FLOWKEYS) {
+        r.fk_nhoff = c.fk_nhoff;
+        r.fk_thoff = c.fk_thoff;
+        r.fk_addr_proto = c.fk_addr_proto;
+        r.fk_is_frag = c.fk_is_frag;
+        r.fk_is_first_frag = c.fk_is_first_frag;
+        r.fk_is_encap = c.fk_is_encap;
+        r.fk_ip_proto = c.fk_ip_proto;
+        r.fk_n_proto = c.fk_n_proto;
+        r.fk_sport = c.fk_sport;
+        r.fk_dport = c.fk_dport;
+        r.fk_flags = c.fk_flags;
+        r.fk_flow_label = c.fk_flow_label;
+    }
+    r.cust = i + 1;
+}
+
+// copy(v, ip[start:start+n]); b2i(v): a slice-bounds panic past the capacity.  A user-given SK's
+// addresses are the bytes its UnmarshalJSON parsed (mimic_skb_custom.sk_ip)
+SKB_DEV int skb_ip_load(const SkbRec &r, const mimic_skb_custom *cu, uint32_t which, uint64_t start, uint32_t n, uint64_t &v) {
+    if (const mimic_skb_custom *c = skb_cust(r, cu, MIMIC_SKB_CUSTOM_SK)) {
+        if (start + n > c->sk_ip_len[which]) return 27;   // MIMIC_PANIC_SLICE
+        uint64_t x = 0;
+        for (uint32_t k = 0; k < n; k++) x = (x << 8) | c->sk_ip[which][(uint32_t)start + k];
+        v = x;
+        return 0;
+    }
     const SkbIP ip = r.ip[which];
     const uint64_t cap = ip.kind == 0 ? ip.n : ip.kind == 1 ? 0 : (uint64_t)(r.len & ~SKB_LOAD_FAILED) - ip.off;
     if (start + n > cap) return 27;   // MIMIC_PANIC_SLICE
@@ -548,10 +593,18 @@ SKB_DEV int skb_ip_load(const SkbRec &r, uint32_t which, uint64_t start, uint32_
 
 #define SKB_RO() do { if (!load) return 26; } while (0)   // errReadOnly -> MIMIC_ERR_CTX_ACCESS
 
-// SKBuff.convertAccess; data = skb.data, end = skb.end, ka/fa = sock / flow-keys addresses
-SKB_DEV int skb_convert_(SkbRec &r, uint32_t ifindex, uint32_t data, uint32_t end, uint32_t ka, uint32_t fa,
-                         uint32_t off, uint32_t n, uint64_t &v, bool load) {
+// SKBuff.convertAccess; data = skb.data, end = skb.end, ka/fa = sock / flow-keys addresses; the
+// fields read through skb.sk come from a user-given SK when the process has one (cu)
+SKB_DEV int skb_convert_(SkbRec &r, const mimic_skb_custom *cu, uint32_t ifindex, uint32_t data, uint32_t end,
+                         uint32_t ka, uint32_t fa, uint32_t off, uint32_t n, uint64_t &v, bool load) {
     const uint64_t val = v;
+    if (off == 88 || off == 132 || off == 136) {
+        if (const mimic_skb_custom *c = skb_cust(r, cu, MIMIC_SKB_CUSTOM_SK)) {
+            SKB_RO();
+            v = skb_to_size(off == 88 ? c->sk_family : off == 132 ? c->sk_dst_port : c->sk_src_port, n);
+            return 0;
+        }
+    }
     switch (off) {
     case 0: SKB_RO(); v = skb_to_size(r.len & ~SKB_LOAD_FAILED, n); return 0;
     case 4: SKB_RO(); v = 0; return 0;                                   // pkt_type & 7 (never set)
@@ -590,16 +643,28 @@ SKB_DEV int skb_convert_(SkbRec &r, uint32_t ifindex, uint32_t data, uint32_t en
         if (load) return 27;
         return 0;
     }
-    if (off >= 92 && off < 96) { SKB_RO(); return skb_ip_load(r, 1, off - 92, n, v); }     // remote_ip4
-    if (off >= 96 && off < 100) { SKB_RO(); return skb_ip_load(r, 0, off - 96, n, v); }    // local_ip4
-    if (off >= 100 && off < 116) { SKB_RO(); return skb_ip_load(r, 3, off - 100, n, v); }  // remote_ip6
-    if (off >= 116 && off < 132) { SKB_RO(); return skb_ip_load(r, 2, off - 116, n, v); }  // local_ip6
+    if (off >= 92 && off < 96) { SKB_RO(); return skb_ip_load(r, cu, 1, off - 92, n, v); }     // remote_ip4
+    if (off >= 96 && off < 100) { SKB_RO(); return skb_ip_load(r, cu, 0, off - 96, n, v); }    // local_ip4
+    if (off >= 100 && off < 116) { SKB_RO(); return skb_ip_load(r, cu, 3, off - 100, n, v); }  // remote_ip6
+    if (off >= 116 && off < 132) { SKB_RO(); return skb_ip_load(r, cu, 2, off - 116, n, v); }  // local_ip6
     return 26;   // "invalid offset"
 }
 
-// SK.convertAccess
-SKB_DEV int sk_convert_(SkbRec &r, uint32_t off, uint32_t n, uint64_t &v, bool load) {
+// SK.convertAccess (a user-given SK's read-only fields from its table entry)
+SKB_DEV int sk_convert_(SkbRec &r, const mimic_skb_custom *cu, uint32_t off, uint32_t n, uint64_t &v, bool load) {
     const uint64_t val = v;
+    if (const mimic_skb_custom *c = skb_cust(r, cu, MIMIC_SKB_CUSTOM_SK)) {
+        switch (off) {
+        case 4: SKB_RO(); v = skb_to_size(c->sk_family, n); return 0;
+        case 8: SKB_RO(); v = skb_to_size(c->sk_type, n); return 0;
+        case 12: SKB_RO(); v = skb_to_size(c->sk_protocol, n); return 0;
+        case 44: SKB_RO(); v = skb_to_size(c->sk_src_port, n); return 0;
+        case 48: SKB_RO(); v = skb_to_size(c->sk_dst_port, n); return 0;
+        case 72: SKB_RO(); v = skb_to_size(c->sk_state, n); return 0;
+        case 76: SKB_RO(); v = skb_to_size((uint64_t)(int64_t)c->sk_rx_queue_mapping, n); return 0;
+        default: break;
+        }
+    }
     switch (off) {
     case 0: if (load) v = skb_to_size(r.sk_bound_dev_if, n); else r.sk_bound_dev_if = (uint32_t)skb_to_size(val, n); return 0;
     case 4: SKB_RO(); v = skb_to_size(r.family, n); return 0;
@@ -613,10 +678,10 @@ SKB_DEV int sk_convert_(SkbRec &r, uint32_t off, uint32_t n, uint64_t &v, bool l
     case 76: SKB_RO(); v = 0; return 0;                                  // rx_queue_mapping
     default: break;
     }
-    if (off >= 24 && off < 28) { SKB_RO(); return skb_ip_load(r, 0, off - 24, n, v); }
-    if (off >= 28 && off < 44) { SKB_RO(); return skb_ip_load(r, 2, off - 28, n, v); }
-    if (off >= 52 && off < 56) { SKB_RO(); return skb_ip_load(r, 1, off - 52, n, v); }
-    if (off >= 56 && off < 72) { SKB_RO(); return skb_ip_load(r, 3, (uint64_t)(uint32_t)(off - 68), n, v); }  // start wraps below 68
+    if (off >= 24 && off < 28) { SKB_RO(); return skb_ip_load(r, cu, 0, off - 24, n, v); }
+    if (off >= 28 && off < 44) { SKB_RO(); return skb_ip_load(r, cu, 2, off - 28, n, v); }
+    if (off >= 52 && off < 56) { SKB_RO(); return skb_ip_load(r, cu, 1, off - 52, n, v); }
+    if (off >= 56 && off < 72) { SKB_RO(); return skb_ip_load(r, cu, 3, (uint64_t)(uint32_t)(off - 68), n, v); }  // start wraps below 68
     return 26;
 }
 
@@ -645,16 +710,16 @@ SKB_DEV int fk_convert_(SkbRec &r, uint32_t off, uint32_t n, uint64_t &v, bool l
 #undef FK_RW
 #undef SKB_RO
 
-SKB_COLD SkbRes skb_convert(SkbRec *r, uint32_t ifindex, uint32_t data, uint32_t end, uint32_t ka, uint32_t fa,
-                            uint32_t off, uint32_t n, uint64_t v, bool load) {
+SKB_COLD SkbRes skb_convert(SkbRec *r, const mimic_skb_custom *cu, uint32_t ifindex, uint32_t data, uint32_t end,
+                            uint32_t ka, uint32_t fa, uint32_t off, uint32_t n, uint64_t v, bool load) {
     SkbRes o;
-    o.st = skb_convert_(*r, ifindex, data, end, ka, fa, off, n, v, load);
+    o.st = skb_convert_(*r, cu, ifindex, data, end, ka, fa, off, n, v, load);
     o.v = v;
     return o;
 }
-SKB_COLD SkbRes sk_convert(SkbRec *r, uint32_t off, uint32_t n, uint64_t v, bool load) {
+SKB_COLD SkbRes sk_convert(SkbRec *r, const mimic_skb_custom *cu, uint32_t off, uint32_t n, uint64_t v, bool load) {
     SkbRes o;
-    o.st = sk_convert_(*r, off, n, v, load);
+    o.st = sk_convert_(*r, cu, off, n, v, load);
     o.v = v;
     return o;
 }

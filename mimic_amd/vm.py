@@ -333,13 +333,135 @@ class NetDev:  # emulator_linux_sk_buff.go:962-964
     IFIndex: int = 0
 
 
+def _jget(obj: dict, key: str, default=None):
+    """encoding/json's field match: exact key first, then case-insensitive."""
+    if key in obj:
+        return obj[key]
+    lk = key.lower()
+    for k, v in obj.items():
+        if k.lower() == lk:
+            return v
+    return default
+
+
+def _parse_ip(text: str) -> Optional[bytes]:
+    """net.ParseIP: 16 bytes for a valid IPv4 (::ffff:a.b.c.d) or IPv6 address, else None."""
+    import ipaddress
+
+    if not text or "%" in text:
+        return None
+    try:
+        ip = ipaddress.ip_address(text)
+    except ValueError:
+        return None
+    if ip.version == 4:
+        return b"\x00" * 10 + b"\xff\xff" + ip.packed
+    return ip.packed
+
+
+@dataclass
+class SK:  # emulator_linux_sk_buff.go:698-718 (JSON "sock" of an sk_buff context)
+    """A user-given socket.  Its addresses are read through net.IP fields that only SK's
+    UnmarshalJSON fills (:721-757): ``FromJSON`` sets them as it does (make(net.IP, 4 / 16), or the
+    16 bytes of net.ParseIP); an SK made directly has nil addresses (reads panic), as a Go SK
+    literal would."""
+    BoundDevIF: int = 0
+    Family: int = 0
+    SockType: int = 0
+    Protocol: int = 0
+    Mark: int = 0
+    Priority: int = 0
+    SrcIP4: str = ""
+    SrcIP6: str = ""
+    SrcPort: int = 0
+    DstPort: int = 0
+    DstIP4: str = ""
+    DstIP6: str = ""
+    State: int = 0
+    RXQueueMapping: int = 0
+    ips: Optional[Tuple[bytes, bytes, bytes, bytes]] = None   # srcIP4, dstIP4, srcIP6, dstIP6 (None: nil)
+
+    @classmethod
+    def FromJSON(cls, obj: dict) -> "SK":
+        u = lambda k: int(_jget(obj, k, 0) or 0) & 0xFFFFFFFF   # noqa: E731
+        sk = cls(BoundDevIF=u("boundDevIF"), Family=u("family"), SockType=u("sockType"), Protocol=u("protocol"),
+                 Mark=u("mark"), Priority=u("priority"), SrcIP4=_jget(obj, "srcIP4", "") or "",
+                 SrcIP6=_jget(obj, "srcIP6", "") or "", SrcPort=u("srcPort"), DstPort=u("dstPort"),
+                 DstIP4=_jget(obj, "dstIP4", "") or "", DstIP6=_jget(obj, "dstIP6", "") or "", State=u("state"),
+                 RXQueueMapping=int(_jget(obj, "rxQueueMapping", 0) or 0))
+        # UnmarshalJSON: make(net.IP, 4 / 16), replaced by net.ParseIP's bytes when it parses
+        # (DstIP6 / SrcIP6 through To16, which keeps 16 bytes)
+        sk.ips = tuple(_parse_ip(t) or bytes(n) for t, n in ((sk.SrcIP4, 4), (sk.DstIP4, 4), (sk.SrcIP6, 16),
+                                                             (sk.DstIP6, 16)))
+        return sk
+
+
+@dataclass
+class FlowKeys:  # emulator_linux_sk_buff.go:967-982 (JSON "flowKeys" of an sk_buff context)
+    """User-given flow keys: the values the program's bpf_flow_keys start from.  SrcIPv6orIPv4 is
+    kept for the JSON surface; no access reaches it (convertAccess panics at offsets 16..31)."""
+    Nhoff: int = 0
+    Thoff: int = 0
+    AddrProto: int = 0
+    IsFrag: int = 0
+    IsFirstFrag: int = 0
+    IsEncap: int = 0
+    IPProto: int = 0
+    NProto: int = 0
+    Sport: int = 0
+    Dport: int = 0
+    SrcIPv6orIPv4: Optional[bytes] = None
+    Flags: int = 0
+    FlowLabel: int = 0
+
+    @classmethod
+    def FromJSON(cls, obj: dict) -> "FlowKeys":
+        g = lambda k, m: int(_jget(obj, k, 0) or 0) & m   # noqa: E731
+        ip = _jget(obj, "ip")
+        return cls(Nhoff=g("nhoff", 0xFFFF), Thoff=g("thoff", 0xFFFF), AddrProto=g("addrProto", 0xFFFF),
+                   IsFrag=g("isFrag", 0xFF), IsFirstFrag=g("isFirstFrag", 0xFF), IsEncap=g("isEncap", 0xFF),
+                   IPProto=g("ipProto", 0xFF), NProto=g("nProto", 0xFFFF), Sport=g("sport", 0xFFFF),
+                   Dport=g("dport", 0xFFFF), SrcIPv6orIPv4=_parse_ip(ip) if isinstance(ip, str) else None,
+                   Flags=g("flags", 0xFFFFFFFF), FlowLabel=g("flowLabel", 0xFFFFFFFF))
+
+
 @dataclass
 class LinuxContextSKBuff:  # context_sk_buff.go:20-29
-    """An sk_buff context.  The reference also accepts a user-given SK / FlowKeys (JSON "sock" /
-    "flowKeys"); this engine builds them from the packet (the reference's default) only."""
+    """An sk_buff context: the packet, the device, and optionally a user-given socket / flow keys
+    that Load puts in place of the ones SKBuffFromBytes derives (context_sk_buff.go:53-66)."""
     Packet: bytes = b""
     Dev: Optional[NetDev] = None
     Name: str = ""
+    SK: Optional["SK"] = None
+    FlowKeys: Optional["FlowKeys"] = None
+
+
+def skb_custom_record(ctx: "LinuxContextSKBuff"):
+    """The mimic_skb_custom entry (include/mimic_amd.h) of a context: a numpy record whose flags
+    are 0 when the context gives neither a socket nor flow keys."""
+    import numpy as np
+
+    r = np.zeros((), L.SKB_CUSTOM_DTYPE)
+    sk, fk = ctx.SK, ctx.FlowKeys
+    if sk is not None:
+        r["flags"] |= L.SKB_CUSTOM_SK
+        for f, v in (("sk_bound_dev_if", sk.BoundDevIF), ("sk_family", sk.Family), ("sk_type", sk.SockType),
+                     ("sk_protocol", sk.Protocol), ("sk_mark", sk.Mark), ("sk_priority", sk.Priority),
+                     ("sk_src_port", sk.SrcPort), ("sk_dst_port", sk.DstPort), ("sk_state", sk.State)):
+            r[f] = int(v) & 0xFFFFFFFF
+        r["sk_rx_queue_mapping"] = int(sk.RXQueueMapping)
+        for k, ip in enumerate(sk.ips or (None,) * 4):
+            b = bytes(ip or b"")[:16]
+            r["sk_ip_len"][k] = len(b)
+            r["sk_ip"][k][:len(b)] = np.frombuffer(b, np.uint8)
+    if fk is not None:
+        r["flags"] |= L.SKB_CUSTOM_FLOWKEYS
+        for f, v in (("fk_nhoff", fk.Nhoff), ("fk_thoff", fk.Thoff), ("fk_addr_proto", fk.AddrProto),
+                     ("fk_is_frag", fk.IsFrag), ("fk_is_first_frag", fk.IsFirstFrag), ("fk_is_encap", fk.IsEncap),
+                     ("fk_ip_proto", fk.IPProto), ("fk_n_proto", fk.NProto), ("fk_sport", fk.Sport),
+                     ("fk_dport", fk.Dport), ("fk_flags", fk.Flags), ("fk_flow_label", fk.FlowLabel)):
+            r[f] = v
+    return r
 
 
 def UnmarshalContextJSON(text: str):
@@ -348,13 +470,13 @@ def UnmarshalContextJSON(text: str):
     typ = obj.get("type")
     c = obj.get("ctx") or {}
     if typ == "sk_buff":
-        if c.get("sock") is not None or c.get("flowKeys") is not None:
-            raise MimicError("sk_buff contexts with a custom sock / flowKeys are not supported by this engine")
         pkt = c.get("packet")
         dev = c.get("dev")
+        sock, fks = _jget(c, "sock"), _jget(c, "flowKeys")
         return LinuxContextSKBuff(Packet=base64.b64decode(pkt) if pkt else b"",
                                   Dev=NetDev(int(dev.get("ifIndex", 0))) if dev is not None else None,
-                                  Name=obj.get("name", ""))
+                                  Name=obj.get("name", ""), SK=SK.FromJSON(sock) if sock is not None else None,
+                                  FlowKeys=FlowKeys.FromJSON(fks) if fks is not None else None)
     if typ != "xdp_md":
         raise MimicError(f"no context unmarshaller registered for type '{typ}'")
     pkt = c.get("packet")
@@ -664,8 +786,10 @@ class Process:
         h = C.c_void_p()
         pkt = bytes(ctx.Packet)
         if isinstance(ctx, LinuxContextSKBuff):   # its Load (leak addresses) happens here, as in NewProcess
-            _check(self.VM.h, self.VM.lib.mimic_process_new_skb(self.VM.h, self.prog_id, pkt, len(pkt),
-                                                                 ctx.Dev.IFIndex if ctx.Dev else 0, C.byref(h)),
+            cust = skb_custom_record(ctx)
+            cp = cust.ctypes.data if int(cust["flags"]) else None
+            _check(self.VM.h, self.VM.lib.mimic_process_new_skb_ctx(self.VM.h, self.prog_id, pkt, len(pkt),
+                                                                     ctx.Dev.IFIndex if ctx.Dev else 0, cp, C.byref(h)),
                    "NewProcess")
         else:
             _check(self.VM.h, self.VM.lib.mimic_process_new(self.VM.h, self.prog_id, pkt, len(pkt), ctx.Headroom,
@@ -863,9 +987,11 @@ class SKBBatch:
     32 + L + 64 bytes at pkt_off[i], the packet at +32."""
     HEADROOM, TAILROOM = 32, 64
 
-    def __init__(self, pkt_data, pkt_off, pkt_len, ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+    def __init__(self, pkt_data, pkt_off, pkt_len, ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0,
+                 custom=None):
         self.pkt_data, self.pkt_off, self.pkt_len = pkt_data, pkt_off, pkt_len
         self.ifindex, self.schedule, self.cpu, self.step_budget = ifindex, schedule, cpu, step_budget
+        self.custom = custom   # device uint8 tensor [n * sizeof(mimic_skb_custom)] or None
 
     @property
     def n(self) -> int:
@@ -888,6 +1014,7 @@ class SKBBatch:
         else:
             b.cpu = None
         b.step_budget = self.step_budget
+        b.custom = self.custom.data_ptr() if self.custom is not None else None
         self._cstruct_obj = b
         self._cstruct = C.byref(b)
         return self._cstruct
@@ -896,9 +1023,20 @@ class SKBBatch:
     def layout(cls, lengths: Sequence[int], align: int = 64):
         return XDPBatch.layout(lengths, cls.HEADROOM, cls.TAILROOM, align)
 
+    @staticmethod
+    def custom_array(contexts: Sequence["LinuxContextSKBuff"]):
+        """The mimic_skb_custom table (numpy) of a batch's contexts, or None when none gives a
+        socket or flow keys."""
+        import numpy as np
+
+        recs = np.zeros(len(contexts), L.SKB_CUSTOM_DTYPE)
+        for i, c in enumerate(contexts):
+            recs[i] = skb_custom_record(c)
+        return recs if recs["flags"].any() else None
+
     @classmethod
     def from_packets(cls, packets: Sequence[bytes], device="cuda", ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None,
-                     step_budget=0):
+                     step_budget=0, custom=None):
         import numpy as np
 
         lens = np.asarray([len(p) for p in packets], dtype=np.uint32)
@@ -907,18 +1045,28 @@ class SKBBatch:
         for i, p in enumerate(packets):
             o = int(off[i]) + cls.HEADROOM
             buf[o:o + len(p)] = np.frombuffer(bytes(p), dtype=np.uint8)
-        return cls.from_numpy(buf, off, lens, device, ifindex, schedule, cpu, step_budget)
+        return cls.from_numpy(buf, off, lens, device, ifindex, schedule, cpu, step_budget, custom)
 
     @classmethod
-    def from_numpy(cls, buf, off, lens, device="cuda", ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0):
+    def from_numpy(cls, buf, off, lens, device="cuda", ifindex=0, schedule=L.SCHED_CHUNKED, cpu=None, step_budget=0,
+                   custom=None):
+        """custom: a numpy mimic_skb_custom table (custom_array / skb_custom_record), one entry per
+        packet, or None."""
         import numpy as np
         import torch
 
         def t(a, dt):
             return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=dt))).to(device)
 
+        cu = None
+        if custom is not None:
+            ca = np.ascontiguousarray(custom)
+            if ca.dtype != L.SKB_CUSTOM_DTYPE or len(ca) != len(lens):
+                raise MimicError("custom: one mimic_skb_custom entry per packet")
+            cu = t(ca.view(np.uint8).reshape(-1), np.uint8)
         return cls(t(buf, np.uint8), t(np.asarray(off, dtype=np.uint64).view(np.int64), np.int64),
-                   t(np.asarray(lens, dtype=np.uint32).view(np.int32), np.int32), ifindex, schedule, cpu, step_budget)
+                   t(np.asarray(lens, dtype=np.uint32).view(np.int32), np.int32), ifindex, schedule, cpu, step_budget,
+                   cu)
 
     def packet_bytes(self, i: int) -> bytes:
         o = int(self.pkt_off[i].item())

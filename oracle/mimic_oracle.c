@@ -1716,10 +1716,12 @@ int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_resul
 
 /* A net.IP as the reference holds it: kind 0 = make(net.IP, n) (zeros, cap n), 1 = nil
  * (cap 0), 2 = a slice of gopacket's copy of the packet starting at byte `off` (cap = L - off;
- * Go lets s[a:b] reach up to the capacity, so reads may run past the address). */
+ * Go lets s[a:b] reach up to the capacity, so reads may run past the address), 3 = n bytes of
+ * its own (a user-given SK's address as SK.UnmarshalJSON parsed it, emulator_linux_sk_buff.go:721-757). */
 typedef struct {
     int kind;
     uint32_t off, n;
+    uint8_t own[16];
 } go_ip;
 
 typedef struct sk_state { /* SK, emulator_linux_sk_buff.go:700-720 */
@@ -1774,11 +1776,13 @@ static uint64_t be_bytes(const uint8_t *b, int n) {
 
 /* copy(v, ip[start:start+n]) then b2i: a slice-bounds panic when start+n exceeds the capacity */
 static int ip_load(const sk_state *sk, const go_ip *ip, uint64_t start, int n, uint64_t *v) {
-    uint64_t cap = ip->kind == 0 ? ip->n : ip->kind == 1 ? 0 : (uint64_t)sk->L - ip->off;
+    uint64_t cap = ip->kind == 0 || ip->kind == 3 ? ip->n : ip->kind == 1 ? 0 : (uint64_t)sk->L - ip->off;
     if (start + (uint64_t)n > cap) return ORC_PANIC_SLICE;
     uint8_t b[8] = {0};
     if (ip->kind == 2)
         for (int k = 0; k < n; k++) b[k] = sk->pkt[ip->off + start + k];
+    if (ip->kind == 3)
+        for (int k = 0; k < n; k++) b[k] = ip->own[start + k];
     *v = be_bytes(b, n);
     return 0;
 }
@@ -2081,7 +2085,17 @@ static void walk_ethernet(skb_walk *w, uint32_t o, uint32_t len) {
 }
 
 /* LinuxContextSKBuff.Load, context_sk_buff.go:42-107.  Returns 0 or ORC_ERR_CTX_LOAD. */
-static int skb_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t ifindex) {
+/* a user-given SK's net.IP: its own bytes, or nil */
+static go_ip custom_ip(const orc_skb_custom *c, int k) {
+    go_ip ip;
+    memset(&ip, 0, sizeof ip);
+    ip.kind = c->sk_ip_len[k] ? 3 : 1;
+    ip.n = c->sk_ip_len[k] > 16 ? 16 : c->sk_ip_len[k];
+    memcpy(ip.own, c->sk_ip[k], ip.n);
+    return ip;
+}
+
+static int skb_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t ifindex, const orc_skb_custom *custom) {
     orc_vm *vm = p->vm;
     skb_walk w;
     memset(&w, 0, sizeof w);
@@ -2108,6 +2122,38 @@ static int skb_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t ifinde
     sk->state = 7; /* BPF_TCP_CLOSE */
     sk->pkt = copy;
     sk->L = L;
+    /* context_sk_buff.go:53-66: a user-given SK replaces the one SKBuffFromBytes made (every
+     * field, the addresses included); user-given FlowKeys are the flow keys the program sees */
+    if (custom && (custom->flags & ORC_SKB_CUSTOM_SK)) {
+        sk->bound_dev_if = custom->sk_bound_dev_if;
+        sk->family = custom->sk_family;
+        sk->sock_type = custom->sk_type;
+        sk->protocol = custom->sk_protocol;
+        sk->mark = custom->sk_mark;
+        sk->priority = custom->sk_priority;
+        sk->src4 = custom_ip(custom, 0);
+        sk->dst4 = custom_ip(custom, 1);
+        sk->src6 = custom_ip(custom, 2);
+        sk->dst6 = custom_ip(custom, 3);
+        sk->src_port = custom->sk_src_port;
+        sk->dst_port = custom->sk_dst_port;
+        sk->state = custom->sk_state;
+        sk->rx_queue_mapping = custom->sk_rx_queue_mapping;
+    }
+    if (custom && (custom->flags & ORC_SKB_CUSTOM_FLOWKEYS)) {
+        fk->nhoff = custom->fk_nhoff;
+        fk->thoff = custom->fk_thoff;
+        fk->addr_proto = custom->fk_addr_proto;
+        fk->is_frag = custom->fk_is_frag;
+        fk->is_first_frag = custom->fk_is_first_frag;
+        fk->is_encap = custom->fk_is_encap;
+        fk->ip_proto = custom->fk_ip_proto;
+        fk->n_proto = custom->fk_n_proto;
+        fk->sport = custom->fk_sport;
+        fk->dport = custom->fk_dport;
+        fk->flags = custom->fk_flags;
+        fk->flow_label = custom->fk_flow_label;
+    }
     s->len = L;
     s->protocol = w.protocol;
     s->vlan_proto = w.vlan_proto;
@@ -2154,9 +2200,15 @@ static int skb_load(orc_proc *p, const uint8_t *pkt, uint32_t L, uint32_t ifinde
 /* NewProcess(prog, &LinuxContextSKBuff{Packet, Dev}) for single-process stepping (vm.go:198-235,
  * context_sk_buff.go:42-107): NULL (with *status) when the context does not load */
 orc_proc *orc_proc_new_skb(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t ifindex, int *status) {
+    return orc_proc_new_skb_ctx(vm, prog_id, pkt, L, ifindex, NULL, status);
+}
+
+orc_proc *orc_proc_new_skb_ctx(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t ifindex,
+                               const void *custom, int *status) {
     if (prog_id < 0 || prog_id >= vm->nprogs) return NULL;
     orc_proc *p = proc_new(vm, prog_id);
-    const int st = skb_load(p, pkt, L, ifindex);
+    const orc_skb_custom *c = (const orc_skb_custom *)custom;
+    const int st = skb_load(p, pkt, L, ifindex, c && c->flags ? c : NULL);
     if (status) *status = st;
     if (st) {
         orc_proc_free(p);
@@ -2177,7 +2229,8 @@ int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_resul
         orc_proc *p = proc_new(vm, prog_id);
         uint32_t steps = 0;
         int32_t epc = -1;
-        int st = skb_load(p, mem + 32, L, b->ifindex);
+        const orc_skb_custom *cu = b->custom && b->custom[i].flags ? &b->custom[i] : NULL;
+        int st = skb_load(p, mem + 32, L, b->ifindex, cu);
         if (!st) {
             const int cpu = b->cpu ? b->cpu[i] : 0;
             if (cpu != -1 && orc_proc_set_cpu(p, cpu)) st = ORC_ERR_NO_CPU;   /* -1: never set */

@@ -126,6 +126,9 @@ orc_proc *orc_proc_new_xdp(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t
                            int32_t ingress, int32_t rxq, int32_t egress);
 /* NewProcess with a LinuxContextSKBuff (its Load runs here); NULL + *status when it fails */
 orc_proc *orc_proc_new_skb(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t ifindex, int *status);
+/* the same with a user-given SK / FlowKeys (custom may be NULL) */
+orc_proc *orc_proc_new_skb_ctx(orc_vm *vm, int prog_id, const uint8_t *pkt, uint32_t L, uint32_t ifindex,
+                               const void *custom, int *status);
 int orc_proc_step(orc_proc *p, int32_t *err_pc);
 int64_t orc_proc_get_pc(orc_proc *p);
 int orc_proc_get_prog(orc_proc *p);
@@ -166,6 +169,24 @@ int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_resul
 /* sk_buff batches (LinuxContextSKBuff, context_sk_buff.go): packet i is pkt_len[i] bytes at
  * pkt_data + pkt_off[i] + 32; the process sees packet memory [pkt_off[i], +32+L+64) (headroom
  * 32, tailroom 64, emulator_linux_sk_buff.go:113-121), written back when write_back is set. */
+/* A user-given SK / FlowKeys of one context (LinuxContextSKBuff.SK / .FlowKeys, context_sk_buff.go:
+ * 24-26, put in place at Load :53-66): the same layout as the engine's mimic_skb_custom.  sk_ip_len
+ * = len() of the SK's srcIP4 / dstIP4 / srcIP6 / dstIP6 net.IP (0 = nil), sk_ip their bytes. */
+#define ORC_SKB_CUSTOM_SK 1u
+#define ORC_SKB_CUSTOM_FLOWKEYS 2u
+typedef struct {
+    uint32_t flags;
+    uint32_t sk_bound_dev_if, sk_family, sk_type, sk_protocol, sk_mark, sk_priority;
+    uint32_t sk_src_port, sk_dst_port, sk_state;
+    int32_t sk_rx_queue_mapping;
+    uint8_t sk_ip_len[4];
+    uint8_t sk_ip[4][16];
+    uint16_t fk_nhoff, fk_thoff, fk_addr_proto;
+    uint8_t fk_is_frag, fk_is_first_frag, fk_is_encap, fk_ip_proto;
+    uint16_t fk_n_proto, fk_sport, fk_dport;
+    uint32_t fk_flags, fk_flow_label;
+} orc_skb_custom;
+
 typedef struct {
     uint32_t n;
     uint8_t *pkt_data;
@@ -175,6 +196,7 @@ typedef struct {
     const int32_t *cpu;
     uint64_t step_budget;
     int write_back;
+    const orc_skb_custom *custom;   /* [n] or NULL: the contexts' user-given SK / FlowKeys */
 } orc_skb_batch;
 int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_results *out);
 

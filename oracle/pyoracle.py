@@ -30,7 +30,8 @@ class _Batch(C.Structure):
 
 class _SkbBatch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("pkt_data", C.c_void_p), ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p),
-                ("ifindex", C.c_uint32), ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("write_back", C.c_int)]
+                ("ifindex", C.c_uint32), ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("write_back", C.c_int),
+                ("custom", C.c_void_p)]
 
 
 class _Results(C.Structure):
@@ -75,6 +76,8 @@ def load(build: bool = True) -> C.CDLL:
         "orc_proc_call_helper": (C.c_int, [C.c_void_p, C.c_int32]),
         "orc_proc_new_xdp": (C.c_void_p, [C.c_void_p, C.c_int, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                           C.c_int32, C.c_int32, C.c_int32]),
+        "orc_proc_new_skb_ctx": (C.c_void_p, [C.c_void_p, C.c_int, C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                                              C.POINTER(C.c_int)]),
         "orc_proc_new_skb": (C.c_void_p, [C.c_void_p, C.c_int, C.c_char_p, C.c_uint32, C.c_uint32,
                                           C.POINTER(C.c_int)]),
         "orc_proc_step": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
@@ -94,12 +97,16 @@ def load(build: bool = True) -> C.CDLL:
 class OracleProcess:
     def __init__(self, vm: "OracleVM", prog_id: int, xdp=None, skb=None):
         """xdp = (packet bytes, headroom, tailroom, ingress, rxq, egress): an xdp_md context;
-        skb = (packet bytes, ifindex): an sk_buff context (Load at construction)."""
+        skb = (packet bytes, ifindex[, custom]): an sk_buff context (Load at construction); custom =
+        a numpy orc_skb_custom record (the engine's mimic_skb_custom layout) or None."""
         self.vm = vm
         if skb is not None:
-            pkt, ifindex = skb
+            pkt, ifindex = skb[0], skb[1]
+            custom = skb[2] if len(skb) > 2 else None
             st = C.c_int(0)
-            self.p = vm.lib.orc_proc_new_skb(vm.h, prog_id, bytes(pkt), len(pkt), ifindex, C.byref(st))
+            self._custom = None if custom is None else np.ascontiguousarray(custom)
+            cp = None if self._custom is None else self._custom.ctypes.data
+            self.p = vm.lib.orc_proc_new_skb_ctx(vm.h, prog_id, bytes(pkt), len(pkt), ifindex, cp, C.byref(st))
             if not self.p:
                 raise OracleError(f"sk_buff context load failed (status {st.value})")
             return
@@ -279,16 +286,20 @@ class OracleVM:
         return out
 
     def run_skb_batch(self, prog_id: int, buf: np.ndarray, off: np.ndarray, lens: np.ndarray, cpu: np.ndarray,
-                      ifindex: int = 0, step_budget: int = 0, write_back: bool = True):
+                      ifindex: int = 0, step_budget: int = 0, write_back: bool = True, custom=None):
         """Sequential sk_buff-context run: packet i is lens[i] bytes at buf[off[i] + 32:]; the
-        process's packet memory [off[i], off[i] + 96 + L) is written back if write_back."""
+        process's packet memory [off[i], off[i] + 96 + L) is written back if write_back.  custom:
+        a numpy table of orc_skb_custom records (one per packet) or None."""
         n = len(lens)
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         cpu = np.ascontiguousarray(cpu, dtype=np.int32)
+        cu = None if custom is None else np.ascontiguousarray(custom)
+        if cu is not None:
+            assert cu.dtype.itemsize == 136 and len(cu) == n
         b = _SkbBatch(n, buf.ctypes.data, off.ctypes.data, lens.ctypes.data, ifindex, cpu.ctypes.data, step_budget,
-                      int(write_back))
+                      int(write_back), None if cu is None else cu.ctypes.data)
         out = {"r0": np.zeros(n, np.uint64), "status": np.zeros(n, np.uint8), "steps": np.zeros(n, np.uint32),
                "err_pc": np.zeros(n, np.int32)}
         r = _Results(out["r0"].ctypes.data, out["status"].ctypes.data, out["steps"].ctypes.data,

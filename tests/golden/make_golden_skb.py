@@ -76,11 +76,17 @@ PKT_LLC = pad(MAC + (58).to_bytes(2, "big") + bytes.fromhex("aaaa03000000" "0800
 CASES = []
 
 
-def case(name, ref, items, packets, expect, ifindex=0):
+def case(name, ref, items, packets, expect, ifindex=0, contexts=None):
+    """contexts: per packet, the user-given part of its context JSON ({"sock": ..., "flowKeys": ...},
+    context_sk_buff.go:20-29) or None; "nilIPs": true marks an SK built as a Go literal (its net.IP
+    fields never set by SK.UnmarshalJSON: nil)."""
     raw, rel = A.assemble(items)
     assert not rel
-    CASES.append(dict(name=name, ref=ref, raw=raw.hex(), packets=[p.hex() for p in packets], ifindex=ifindex,
-                      expect=expect))
+    d = dict(name=name, ref=ref, raw=raw.hex(), packets=[p.hex() for p in packets], ifindex=ifindex, expect=expect)
+    if contexts is not None:
+        assert len(contexts) == len(packets)
+        d["contexts"] = contexts
+    CASES.append(d)
 
 
 def e(r0=None, status=OK, steps=None, err_pc=-1):
@@ -286,6 +292,95 @@ case("ldabs_into_fk", "data - 33 is the flow keys' offset 40: Load error", r6ctx
      [PKT4], [e(0, status=LDABS, steps=2, err_pc=1)])
 case("ldind_badreg", "Registers.Get(11) panics after the R6 check", r6ctx([A.raw(0x50, 0, 11, 0, 0), A.exit_()]),
      [PKT4], [e(0, status=BADREG, steps=2, err_pc=1)])
+
+# ---- user-given sock / flow keys (context_sk_buff.go:24-26, Load :53-66) --------------------------
+# A context's "sock" replaces the SK SKBuffFromBytes made -- every field, the __sk_buff fields read
+# through skb.sk included (:522-600) -- and its net.IP fields are what SK.UnmarshalJSON leaves
+# (:721-757): make(net.IP, 4 / 16) unless net.ParseIP parses the string, which returns 16 bytes
+# (::ffff:a.b.c.d for IPv4), so a user-given IPv4 address reads as zeros through the 4-byte
+# ipv4 fields.  "flowKeys" are the flow keys' starting values.
+def sock(**kw):
+    return {"sock": kw}
+
+
+def fks(**kw):
+    return {"flowKeys": kw}
+
+
+V4M = bytes(10) + b"\xff\xff"   # net.ParseIP's 16-byte form of an IPv4 address: 10 zeros, ff ff, a.b.c.d
+case("sock_family", "SK replaces skb.sk; __sk_buff->family = sk.sk.Family (:522-525)", ld_field(S["family"]),
+     [PKT4], [e(10, steps=2)], contexts=[sock(family=10)])
+case("sock_sk_family", "bpf_sock->family", via_sk(K["family"]), [PKT4], [e(10, steps=3)], contexts=[sock(family=10)])
+case("sock_type", "bpf_sock->type = SockType (:806-811)", via_sk(K["type"]), [PKT4], [e(5, steps=3)],
+     contexts=[sock(sockType=5, protocol=17)])
+case("sock_protocol", "bpf_sock->protocol (:815-820)", via_sk(K["protocol"]), [PKT4], [e(17, steps=3)],
+     contexts=[sock(sockType=5, protocol=17)])
+case("sock_state_zero", "a user SK's State is what it gives (0), not BPF_TCP_CLOSE", via_sk(K["state"]), [PKT4],
+     [e(0, steps=3)], contexts=[sock(family=2)])
+case("sock_state", "bpf_sock->state (:906-911)", via_sk(K["state"]), [PKT4], [e(10, steps=3)],
+     contexts=[sock(state=10)])
+case("sock_rxq_u32", "toSize(uint64(RXQueueMapping)) of int32 -1, asm.Word", via_sk(K["rx_queue_mapping"]), [PKT4],
+     [e(0xFFFFFFFF, steps=3)], contexts=[sock(rxQueueMapping=-1)])
+case("sock_rxq_u64", "int32 -1 sign-extends", via_sk(K["rx_queue_mapping"], 8), [PKT4], [e(-1, steps=3)],
+     contexts=[sock(rxQueueMapping=-1)])
+case("sock_local_port", "__sk_buff->local_port = sk.sk.SrcPort (:593-597)", ld_field(S["local_port"]), [PKT4],
+     [e(0xBEEF, steps=2)], contexts=[sock(srcPort=0xBEEF, dstPort=8080)])
+case("sock_remote_port", "__sk_buff->remote_port = sk.sk.DstPort (:584-588)", ld_field(S["remote_port"]), [PKT4],
+     [e(8080, steps=2)], contexts=[sock(srcPort=0xBEEF, dstPort=8080)])
+case("sock_src_port", "bpf_sock->src_port", via_sk(K["src_port"]), [PKT4], [e(0xBEEF, steps=3)],
+     contexts=[sock(srcPort=0xBEEF, dstPort=8080)])
+case("sock_dst_port", "bpf_sock->dst_port", via_sk(K["dst_port"]), [PKT4], [e(8080, steps=3)],
+     contexts=[sock(srcPort=0xBEEF, dstPort=8080)])
+case("sock_ip4_reads_zero", "ParseIP's 16-byte form: srcIP4[0:4] are zeros", ld_field(S["local_ip4"]), [PKT4],
+     [e(0, steps=2)], contexts=[sock(srcIP4="192.168.1.2")])
+case("sock_ip4_16_bytes", "srcIP4[3:11] of ::ffff:192.168.1.2 reaches the ff ff", ld_field(S["local_ip4"] + 3, 8),
+     [PKT4], [e(int.from_bytes((V4M + bytes([192, 168, 1, 2]))[3:11], "big"), steps=2)],
+     contexts=[sock(srcIP4="192.168.1.2")])
+case("sock_sk_ip4_16_bytes", "bpf_sock->src_ip4 at +3, 8 bytes", via_sk(K["src_ip4"] + 3, 8), [PKT4],
+     [e(0xFF, steps=3)], contexts=[sock(srcIP4="192.168.1.2")])
+case("sock_ip4_default_len4", "dstIP4 = make(net.IP, 4): [3:7] panics", ld_field(S["remote_ip4"] + 3), [PKT4],
+     [e(0, status=PANIC_SLICE, steps=1, err_pc=0)], contexts=[sock(family=2)])
+case("sock_ip4_unparsable", "ParseIP fails: make(net.IP, 4) stays", ld_field(S["remote_ip4"]), [PKT4],
+     [e(0, steps=2)], contexts=[sock(dstIP4="not-an-ip")])
+case("sock_ip6", "srcIP6 = ParseIP(...).To16()", ld_field(S["local_ip6"]), [PKT4], [e(0x20010DB8, steps=2)],
+     contexts=[sock(srcIP6="2001:db8::1")])
+case("sock_ip6_last", "srcIP6[12:16]", ld_field(S["local_ip6"] + 12), [PKT4], [e(1, steps=2)],
+     contexts=[sock(srcIP6="2001:db8::1")])
+case("sock_ip6_from_v4", "dstIP6 = ParseIP(\"10.0.0.1\").To16(): ::ffff:10.0.0.1", ld_field(S["remote_ip6"] + 8, 8),
+     [PKT4], [e(0x0000FFFF0A000001, steps=2)], contexts=[sock(dstIP6="10.0.0.1")])
+case("sock_sk_dst_ip6_68", "offset 68: dstIP6[0:4] of the user's address", via_sk(68), [PKT4],
+     [e(0x20010DB8, steps=3)], contexts=[sock(dstIP6="2001:db8::2")])
+case("sock_mark", "bpf_sock->mark starts at the user's value", via_sk(K["mark"]), [PKT4], [e(5, steps=3)],
+     contexts=[sock(mark=5)])
+case("sock_mark_rw", "and is writable", via_sk(K["mark"], store=0x77), [PKT4], [e(0x77, steps=4)],
+     contexts=[sock(mark=5)])
+case("sock_bound_dev_if", "bound_dev_if", via_sk(K["bound_dev_if"]), [PKT4], [e(3, steps=3)],
+     contexts=[sock(boundDevIF=3)])
+case("sock_priority", "priority", via_sk(K["priority"]), [PKT4], [e(6, steps=3)], contexts=[sock(priority=6)])
+case("sock_nil_ips", "an SK literal: its net.IP fields are nil, ip[0:4] panics", ld_field(S["local_ip4"]), [PKT4],
+     [e(0, status=PANIC_SLICE, steps=1, err_pc=0)], contexts=[dict(sock(family=2), nilIPs=True)])
+case("sock_keeps_skb_fields", "skb.len / protocol still come from the packet", ld_field(S["protocol"]), [PKT4],
+     [e(0x0800, steps=2)], contexts=[sock(family=10)])
+case("sock_mixed_batch", "per-context: a user SK, none, another user SK", ld_field(S["family"]), [PKT4, PKT4, PKT6],
+     [e(10, steps=2), e(2, steps=2), e(99, steps=2)], contexts=[sock(family=10), None, sock(family=99)])
+case("fk_user_nhoff", "FlowKeys start from the user's values (:1031-1041)", via_fk(FK["nhoff"], 2), [PKT4],
+     [e(14, steps=3)], contexts=[fks(nhoff=14, sport=4660, ipProto=6, flags=7, flowLabel=0x12345)])
+case("fk_user_sport", "sport", via_fk(FK["sport"], 2), [PKT4], [e(4660, steps=3)],
+     contexts=[fks(nhoff=14, sport=4660, ipProto=6, flags=7, flowLabel=0x12345)])
+case("fk_user_ip_proto", "ip_proto", via_fk(FK["ip_proto"], 1), [PKT4], [e(6, steps=3)],
+     contexts=[fks(nhoff=14, sport=4660, ipProto=6, flags=7, flowLabel=0x12345)])
+case("fk_user_flags", "flags", via_fk(FK["flags"], 4), [PKT4], [e(7, steps=3)],
+     contexts=[fks(nhoff=14, sport=4660, ipProto=6, flags=7, flowLabel=0x12345)])
+case("fk_user_flow_label", "flow_label", via_fk(FK["flow_label"], 4), [PKT4], [e(0x12345, steps=3)],
+     contexts=[fks(nhoff=14, sport=4660, ipProto=6, flags=7, flowLabel=0x12345)])
+case("fk_user_store", "a store replaces the user's value", via_fk(FK["sport"], 2, store=0x55), [PKT4],
+     [e(0x55, steps=6)], contexts=[fks(sport=4660)])
+case("fk_user_ip_panics", "ip[offset:...] panics whatever the user's ip", via_fk(16, 4), [PKT4],
+     [e(0, status=PANIC_SLICE, steps=2, err_pc=1)], contexts=[fks(ip="10.0.0.1")])
+case("sock_and_fk", "both: flow_keys.nhoff + __sk_buff->family",
+     [A.ldx(4, 2, 1, S["flow_keys"]), A.ldx(2, 0, 2, FK["nhoff"]), A.ldx(4, 3, 1, S["family"]),
+      A.alu64("add", 0, 3, reg=True), A.exit_()], [PKT4], [e(14 + 10, steps=5)],
+     contexts=[dict(sock(family=10), **fks(nhoff=14))])
 
 # ---- context load and the leaked-entry layout (context_sk_buff.go:42-119) -------------------------
 case("load_vxlan", "a second Ethernet layer: 'handling of multiple link layers not supported'",

@@ -220,13 +220,15 @@ def _map_readout(sc, read_values, read_hash):
 
 
 def run_oracle_skb(sc: Scenario, buf, off, lens, cpu, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
-                   splits=None):
-    """Sequential reference semantics; `splits` = indices where a new batch (same VM) starts."""
+                   splits=None, custom=None):
+    """Sequential reference semantics; `splits` = indices where a new batch (same VM) starts;
+    custom = the contexts' mimic_skb_custom table (numpy) or None."""
     vm, mids, pids = build_oracle(sc)
     buf = np.array(buf, dtype=np.uint8, copy=True)
     parts = []
     for a, b in _splits(len(lens), splits):
-        parts.append(vm.run_skb_batch(pids[entry], buf, off[a:b], lens[a:b], cpu[a:b], ifindex, step_budget))
+        parts.append(vm.run_skb_batch(pids[entry], buf, off[a:b], lens[a:b], cpu[a:b], ifindex, step_budget,
+                                      custom=None if custom is None else custom[a:b]))
     out = {k: np.concatenate([p[k] for p in parts]) for k in ("r0", "status", "steps", "err_pc")}
     out["pkt"] = buf
 
@@ -240,7 +242,7 @@ def run_oracle_skb(sc: Scenario, buf, off, lens, cpu, entry: int = 0, ifindex: i
 
 
 def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
-                   schedule=None, splits=None, device: int = 0, exec_mode: Optional[str] = None):
+                   schedule=None, splits=None, device: int = 0, exec_mode: Optional[str] = None, custom=None):
     import torch
 
     import mimic_amd as M
@@ -249,11 +251,13 @@ def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifind
     if schedule is None:
         schedule = M.SCHED_EXPLICIT
     dev = f"cuda:{device}"
-    full = M.SKBBatch.from_numpy(buf, off, lens, device=dev, ifindex=ifindex)
+    full = M.SKBBatch.from_numpy(buf, off, lens, device=dev, ifindex=ifindex, custom=custom)
+    CS = 136   # sizeof(mimic_skb_custom)
     parts = []
     for a, b in _splits(len(lens), splits):
         sub = M.SKBBatch(full.pkt_data, full.pkt_off[a:b], full.pkt_len[a:b], ifindex, schedule,
-                         None if cpu is None else np.asarray(cpu)[a:b], step_budget)
+                         None if cpu is None else np.asarray(cpu)[a:b], step_budget,
+                         None if full.custom is None else full.custom[a * CS:b * CS])
         parts.append(vm.RunSKBBatch(pids[entry], sub).numpy(b - a))
     out = {k: np.concatenate([p[k] for p in parts]) for k in ("r0", "status", "steps", "err_pc")}
     torch.cuda.synchronize(device)
@@ -287,7 +291,7 @@ def run_sequence_oracle(sc: Scenario, runs):
         if r.get("skb"):
             b = np.array(r["buf"], dtype=np.uint8, copy=True)
             o = vm.run_skb_batch(pids[r["entry"]], b, r["off"], r["lens"], r["cpu"], r.get("ifindex", 0),
-                                 r.get("step_budget", 0))
+                                 r.get("step_budget", 0), custom=r.get("custom"))
             o["pkt"] = b
             outs.append(o)
             continue
@@ -313,7 +317,7 @@ def run_sequence_engine(sc: Scenario, runs, exec_mode: Optional[str] = None, dev
     for r in runs:
         if r.get("skb"):
             sb = M.SKBBatch.from_numpy(r["buf"], r["off"], r["lens"], f"cuda:{device}", r.get("ifindex", 0),
-                                       M.SCHED_EXPLICIT, r["cpu"], r.get("step_budget", 0))
+                                       M.SCHED_EXPLICIT, r["cpu"], r.get("step_budget", 0), r.get("custom"))
             o = vm.RunSKBBatch(pids[r["entry"]], sb).numpy(len(r["lens"]))
             o["pkt"] = sb.pkt_data.cpu().numpy()
             o["last_exec"] = vm.LastExec()

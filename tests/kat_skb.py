@@ -18,9 +18,28 @@ def scenario(c):
     return Scenario(vcpus=1, progs=[("main", bytes.fromhex(c["raw"]), [])])
 
 
+def custom_table(contexts):
+    """The mimic_skb_custom table of a vector's contexts (sock / flowKeys JSON, parsed as
+    UnmarshalContextJSON parses them), or None."""
+    if not contexts:
+        return None
+    from mimic_amd import vm as V
+
+    ctxs = []
+    for cj in contexts:
+        cj = cj or {}
+        sk = V.SK.FromJSON(cj["sock"]) if cj.get("sock") is not None else None
+        if sk is not None and cj.get("nilIPs"):
+            sk.ips = None   # a Go SK literal: UnmarshalJSON never set its net.IP fields
+        fk = V.FlowKeys.FromJSON(cj["flowKeys"]) if cj.get("flowKeys") is not None else None
+        ctxs.append(V.LinuxContextSKBuff(SK=sk, FlowKeys=fk))
+    return V.SKBBatch.custom_array(ctxs)
+
+
 def inputs(c):
     buf, off, lens = skb_packets_to_buffer([bytes.fromhex(p) for p in c["packets"]])
-    return dict(buf=buf, off=off, lens=lens, cpu=np.zeros(len(lens), dtype=np.int32), ifindex=c["ifindex"])
+    return dict(buf=buf, off=off, lens=lens, cpu=np.zeros(len(lens), dtype=np.int32), ifindex=c["ifindex"],
+                custom=custom_table(c.get("contexts")))
 
 
 def check(c, out):
@@ -42,6 +61,6 @@ def jit_groups(cases, max_progs: int = 40):
             progs.append((f"k{k}", bytes.fromhex(c["raw"]), []))
             i = inputs(c)
             runs.append(dict(skb=True, entry=k, buf=i["buf"], off=i["off"], lens=i["lens"], cpu=i["cpu"],
-                             ifindex=i["ifindex"]))
+                             ifindex=i["ifindex"], custom=i["custom"]))
         out.append((Scenario(vcpus=1, progs=progs), runs, chunk))
     return out

@@ -34,9 +34,10 @@ def jit_kernels():
 def _skb_kat(c, exec_mode):
     sc = kat_skb.scenario(c)
     inp = kat_skb.inputs(c)
-    e = run_engine_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"], exec_mode=exec_mode)
+    e = run_engine_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"], exec_mode=exec_mode,
+                       custom=inp["custom"])
     kat_skb.check(c, e)
-    o = run_oracle_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"])
+    o = run_oracle_skb(sc, inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"], custom=inp["custom"])
     assert_same(o, e)
 
 
@@ -192,4 +193,37 @@ def test_process_run_skb(gpu):
     assert got[1] - got[0] == 219 + 64
     ctx = M.UnmarshalContextJSON('{"name": "x", "type": "sk_buff", "ctx": {"packet": "AAAA", "dev": {"ifIndex": 4}}}')
     assert isinstance(ctx, M.LinuxContextSKBuff) and ctx.Dev.IFIndex == 4 and ctx.Packet == b"\0\0\0"
+    vm.close()
+
+
+@pytest.mark.parametrize("name", ["sock_family", "sock_ip4_16_bytes", "sock_rxq_u64", "fk_user_flow_label", "sock_and_fk",
+                                  "sock_nil_ips", "fk_user_store"])
+def test_process_with_user_sock_and_flow_keys(gpu, name):
+    """NewProcess over an sk_buff context with a user-given sock / flow keys
+    (mimic_process_new_skb_ctx, context_sk_buff.go:53-66), run to the end: the vector's answer."""
+    import mimic_amd as M
+    from mimic_amd import vm as V
+
+    c = next(c for c in CASES if c["name"] == name)
+    table = kat_skb.custom_table(c["contexts"])
+    vm = M.NewVM(M.VMOptEmulator(M.NewLinuxEmulator()), M.VMOptSetvCPUs(1))
+    pid = vm.AddProgram(M.ProgramSpec("main", bytes.fromhex(c["raw"])))
+    for k, (pkt, ex) in enumerate(zip(c["packets"], c["expect"])):
+        cj = c["contexts"][k] or {}
+        sk = M.SK.FromJSON(cj["sock"]) if cj.get("sock") is not None else None
+        if sk is not None and cj.get("nilIPs"):
+            sk.ips = None
+        fk = M.FlowKeys.FromJSON(cj["flowKeys"]) if cj.get("flowKeys") is not None else None
+        ctx = M.LinuxContextSKBuff(Packet=bytes.fromhex(pkt), SK=sk, FlowKeys=fk, Dev=M.NetDev(c["ifindex"]))
+        assert V.skb_custom_record(ctx).tobytes() == table[k].tobytes()
+        p = vm.NewProcess(pid, ctx)
+        p.SetCPUID(0)
+        try:
+            p.Run()
+        except M.MimicError:
+            pass
+        assert p.Status == ex["status"], (name, k, p.Status)
+        if "r0" in ex and ex["status"] == 0:
+            assert p.Registers.R0 == ex["r0"], (name, k, hex(p.Registers.R0))
+        p.Cleanup()
     vm.close()

@@ -13,7 +13,8 @@ CASES = kat_skb.load_cases()
 @pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
 def test_oracle_skb_kat(c):
     inp = kat_skb.inputs(c)
-    out = run_oracle_skb(kat_skb.scenario(c), inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"])
+    out = run_oracle_skb(kat_skb.scenario(c), inp["buf"], inp["off"], inp["lens"], inp["cpu"], ifindex=inp["ifindex"],
+                         custom=inp["custom"])
     kat_skb.check(c, out)
 
 
@@ -85,3 +86,42 @@ def test_oracle_memory_indexes_match_literal_scans(monkeypatch):
         assert lit["maps"] == fast["maps"]
         if splits is None:
             assert len(set(lit["r0"].tolist())) > 1000   # addresses drift over the batch (leaks)
+
+
+def test_context_json_sock_and_flow_keys():
+    """UnmarshalContextJSON (context_sk_buff.go:8-17, :20-29) keeps a user-given "sock" and
+    "flowKeys": SK.UnmarshalJSON's address rules (net.ParseIP's 16 bytes, else make(net.IP, 4 / 16);
+    emulator_linux_sk_buff.go:721-757), encoding/json's case-insensitive field names, and the
+    mimic_skb_custom record the engine and the oracle read."""
+    import base64
+    import json
+
+    import mimic_amd as M
+    from mimic_amd import _lib as L
+
+    pkt = bytes(range(64))
+    text = json.dumps({"name": "c1", "type": "sk_buff", "ctx": {
+        "packet": base64.b64encode(pkt).decode(), "dev": {"ifIndex": 3},
+        "sock": {"family": 10, "SRCIP4": "1.2.3.4", "dstIP6": "2001:db8::7", "dstIP4": "bogus", "srcPort": 9,
+                 "rxQueueMapping": -2, "state": 1},
+        "flowKeys": {"nhoff": 14, "sport": 80, "flowLabel": 5, "ip": "10.0.0.1"}}})
+    ctx = M.UnmarshalContextJSON(text)
+    assert isinstance(ctx, M.LinuxContextSKBuff) and ctx.Packet == pkt and ctx.Dev.IFIndex == 3
+    sk, fk = ctx.SK, ctx.FlowKeys
+    assert sk.Family == 10 and sk.SrcPort == 9 and sk.RXQueueMapping == -2 and sk.State == 1
+    src4, dst4, src6, dst6 = sk.ips
+    assert src4 == bytes(10) + b"\xff\xff" + bytes([1, 2, 3, 4])        # ParseIP: 16 bytes
+    assert dst4 == bytes(4)                                              # unparsable: make(net.IP, 4)
+    assert src6 == bytes(16) and dst6 == bytes.fromhex("20010db8000000000000000000000007")
+    assert fk.Nhoff == 14 and fk.Sport == 80 and fk.FlowLabel == 5
+    r = M.vm.skb_custom_record(ctx)
+    assert r.dtype == L.SKB_CUSTOM_DTYPE and r.dtype.itemsize == 136
+    assert int(r["flags"]) == L.SKB_CUSTOM_SK | L.SKB_CUSTOM_FLOWKEYS
+    assert list(r["sk_ip_len"]) == [16, 4, 16, 16] and int(r["sk_rx_queue_mapping"]) == -2
+    assert int(r["fk_nhoff"]) == 14 and int(r["fk_flow_label"]) == 5
+    # a context without either: no record flags, no table
+    plain = M.UnmarshalContextJSON(json.dumps({"type": "sk_buff", "ctx": {"packet": base64.b64encode(pkt).decode()}}))
+    assert plain.SK is None and plain.FlowKeys is None
+    assert M.SKBBatch.custom_array([plain, plain]) is None
+    # a Go SK literal: nil addresses
+    assert int(M.vm.skb_custom_record(M.LinuxContextSKBuff(SK=M.SK(Family=2)))["sk_ip_len"].sum()) == 0
