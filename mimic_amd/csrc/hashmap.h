@@ -40,10 +40,10 @@ HDEV void h_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // the index region of one map: [records | rebuild copy | locks | freelist ring | HashCtl]
 struct HT {
     uint8_t *base;
-    uint32_t cap, rec_q, K, nlocks, fl_cap;
+    uint32_t cap, rec_q, K, nlocks, fl_cap, E;
 };
 HDEV HT h_table(uint8_t *arena, const DMap &m) {
-    return HT{arena + m.ht_dev_off, m.ht_cap, m.rec_q, m.key_size, m.nlocks, m.fl_cap};
+    return HT{arena + m.ht_dev_off, m.ht_cap, m.rec_q, m.key_size, m.nlocks, m.fl_cap, m.max_entries};
 }
 HDEV size_t h_rec_bytes(const HT &t) { return (size_t)t.cap * t.rec_q * 8; }
 HDEV uint64_t *h_rec(const HT &t, uint32_t p) { return (uint64_t *)t.base + (size_t)p * t.rec_q; }
@@ -87,9 +87,12 @@ HDEV bool h_key_eq(const uint64_t *r, const KS &ks, uint32_t K) {
     return true;
 }
 
-// lock-free lookup: slot index or -1; *pos = bucket of the key
+// lock-free lookup: slot index or -1; *pos = bucket of the key.  recheck = false in pop-only
+// launches (no program of the launch deletes): a bucket then only moves EMPTY / TOMB -> BUSY ->
+// live (or BUSY back, on E2BIG) and a live record never changes, so the state word's re-read that
+// guards against a concurrent delete + reuse is not needed (one memory round trip per hit less)
 template <class KS>
-HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos) {
+HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos, bool recheck = true) {
     const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32);
     uint32_t p = (uint32_t)h & mask;
     for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
@@ -97,7 +100,7 @@ HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos) {
         const uint64_t w = h_ld(r);
         const uint32_t s = (uint32_t)w;
         if (s == HT_EMPTY) return -1;
-        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K) && h_ld(r) == w) {
+        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K) && (!recheck || h_ld(r) == w)) {
             if (pos) *pos = p;
             return (int32_t)s;
         }
@@ -325,7 +328,9 @@ HDEV int32_t h_insert_wave(const HT &t, const KS &ks, uint64_t h, bool *inserted
 // bucket: its key live -> found; a BUSY bucket before any reusable one -> it may be k being
 // written, wait for the next round; else it tries to claim the first reusable bucket with one CAS
 // (lanes of one key race for the same bucket, one wins).  Winners take their freelist positions
-// with one head reservation for the round (lane order), write the key words and publish tag | slot
+// with one head reservation for the round (lane order; while tail is still E -- nothing was ever
+// pushed since the ring was filled with 0..E-1 -- position p holds slot p and the ring is not
+// read), write the key words and publish tag | slot
 // in the same round (a lane never waits on a lane of its own wave), or give the bucket back when
 // the freelist is spent (E2BIG).  A lone lane pops exactly as h_insert_wave does (FIFO slots).
 template <class KS>
@@ -378,17 +383,26 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
             const uint32_t k = (uint32_t)__builtin_popcountll(needm), first = (uint32_t)__builtin_ctzll(needm);
             uint32_t got = 0;
             uint64_t base = 0;
+            uint32_t ident = 0;
             if (me == first) {
+#ifdef MIMIC_MEAS_NOHEAD   // measurement only (slots collide, results wrong): no shared head counter
+                base = ((uint64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u) % (t.E > 64 ? t.E - 64 : 1);
+                got = k;
+                ident = 1;
+#else
                 base = __hip_atomic_fetch_add(&c->head, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long tl = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 got = base >= tl ? 0u : (tl - base < k ? (uint32_t)(tl - base) : k);
+                ident = tl == t.E;
+#endif
             }
             got = (uint32_t)__builtin_amdgcn_readlane((int)got, (int)first);
+            ident = (uint32_t)__builtin_amdgcn_readlane((int)ident, (int)first);
             base = h_bcast64(base, first);
             const uint32_t rank = (uint32_t)__builtin_popcountll(needm & ((1ull << me) - 1));
             if (mine && rank < got) {   // positions below tail were written before this launch
                 int32_t *f = h_ring(t) + ((base + rank) & (t.fl_cap - 1));
-                slot = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                slot = ident ? (int32_t)(base + rank) : __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }

@@ -110,6 +110,8 @@ class Gen {
         if (ka) karg = atoi(ka);
         const char *nr = getenv("MIMIC_JIT_NTRES");   // 0: per-packet results stored as plain stores
         ntres = !(nr && nr[0] == '0');
+        const char *dnr = getenv("MIMIC_JIT_DEFER_NOREGS");
+        defer_noregs = dnr ? atoi(dnr) : 0;
         const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
         skb_fields = !(sf && sf[0] == '0');
         const char *sl = getenv("MIMIC_JIT_SKBLDS");   // 0: sk_buff records read from global memory
@@ -197,6 +199,7 @@ class Gen {
     bool elide = true;         // MIMIC_JIT_ELIDE=0: no deferred stack stores
     bool window = true;        // MIMIC_JIT_WINDOW=0: no windowed early loads
     int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
+    int defer_noregs = 0;   // MIMIC_JIT_DEFER_NOREGS=1: deferral sites store no registers, 2: low halves (register census only)
     bool ntres = true;         // MIMIC_JIT_NTRES=0: r0 / status stores not non-temporal (measured 1-3 % slower)
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
@@ -312,6 +315,10 @@ class Gen {
                 d.clear();
             }
         }
+        // traffic-attribution knobs (set through MIMIC_JIT_DEFS; results are wrong with them on):
+        // no packet stores on the fast path, no fused counter adds, no per-packet result stores
+        E.line("#ifdef MIMIC_MEAS_NOPKTST\n#define PKT_ST(p_, n_, v_) ((void)(v_))\n#else\n#define PKT_ST(p_, n_, v_) st_n(p_, n_, v_)\n#endif");
+        E.line("#ifdef MIMIC_MEAS_NOATOM\n#define CNT_ADD(p_, n_, v_) ((void)(p_))\n#else\n#define CNT_ADD(p_, n_, v_) atomic_add_n(p_, n_, v_)\n#endif");
         if (spread_on) E.line("#define MIMIC_SPREAD 1");
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
@@ -601,6 +608,7 @@ class Gen {
             E.line("    { const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else
             E.line("    {");
+        E.line("#ifndef MIMIC_MEAS_NORES");
         if (nt || ntres) {
             E.line("    if (kq_.r0) st_nt(kq_.r0 + i, r0);");
             E.line("    if (kq_.status) st_nt(kq_.status + i, (uint8_t)st_);");
@@ -611,6 +619,7 @@ class Gen {
         if (census) E.line("    if (kq_.steps) st_nt(kq_.steps + i, coldn_);   // census: slow-path calls, not steps");
         else E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
         E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
+        E.line("#endif");
         E.line("    }");
         E.line("    lane_steps += steps;");
         E.line("  }");
@@ -1245,10 +1254,10 @@ class Gen {
         return "COLD_CALL(" + call + ", " + std::to_string(i) + ");";
     }
     std::string defer_text(uint32_t i) const {
-        const uint16_t m = live.at(cur_prog).at(i) | 1u | (1u << 10);
+        const uint16_t m = defer_noregs == 1 || defer_noregs == 10 + (int)cur_prog ? 0 : live.at(cur_prog).at(i) | 1u | (1u << 10);
         std::string t = "{ DeferRec *dr_ = kp.defer + g;";
         for (uint32_t r = 0; r < 11; r++)
-            if ((m >> r) & 1) t += " dr_->r[" + std::to_string(r) + "] = r" + std::to_string(r) + ";";
+            if ((m >> r) & 1) t += " dr_->r[" + std::to_string(r) + "] = " + (defer_noregs == 2 && r ? "(uint32_t)" : "") + "r" + std::to_string(r) + ";";
         return t + " DFR(" + std::to_string(i) + "u, " + std::to_string(cur_prog) + "u); }";
     }
     // Registers live into each slot (backward dataflow over every program; a tail call continues
@@ -1366,7 +1375,7 @@ class Gen {
                 E.line("    if (false) { }");
             }
         } else
-        E.line("    if (%s) { steps += 3u; atomic_add_n(L.t_ptr + (uint32_t)(ga_ - L.t_lo), %s, %s); }", cond.c_str(), N.c_str(), imm(k).c_str());
+        E.line("    if (%s) { steps += 3u; CNT_ADD(L.t_ptr + (uint32_t)(ga_ - L.t_lo), %s, %s); }", cond.c_str(), N.c_str(), imm(k).c_str());
         E.line("    else {");
         insn(p, i);
         insn(p, i + 1);
@@ -1462,7 +1471,7 @@ class Gen {
                 f.push_back({"(uint64_t)" + wo + " + " + N + " <= W_", ord("win_load(pwin_, tl_, " + wo + ", " + N + ")", n), ""});
             }
             f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord(std::string(nt ? "ld_n_nt" : "ld_n") + "(L.pkt + " + o + ", " + N + ")", n),
-                         "{ st_n(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
+                         "{ PKT_ST(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
                              (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
             // the lane's cached per-CPU row (analyze_vc): every access inside the row while the
             // cache is valid is served here, so memory and registers never disagree

@@ -750,7 +750,7 @@ DEV HelperOut helper_lookup(const KParams &kp, const Lane &L, uint64_t r1, uint6
     const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
     const HT t = h_table(kp.arena, m);
     const uint64_t h = h_hash(ks, m.key_size);
-    const int32_t idx = HASH_RO(kp) ? h_find_ro(t, ks, h) : h_find(t, ks, h, nullptr);
+    const int32_t idx = HASH_RO(kp) ? h_find_ro(t, ks, h) : h_find(t, ks, h, nullptr, !HASH_POPONLY(kp));
     o.r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
     o.set_r0 = true;
     if (idx >= 0) {
@@ -790,12 +790,15 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
     const KeyPriv ks = key_fetch(kp, L, K, m.key_size);
     const uint64_t h = h_hash(ks, m.key_size);
     const HT t = h_table(kp.arena, m);
-    int32_t idx = h_find(t, ks, h, nullptr);
+    // pop-only launches: h_insert_nolock's own walk finds a present key (no separate probe first)
+    const bool nolock = HASH_POPONLY(kp) && MIMIC_HASH_NOLOCK;
+    int32_t idx = nolock ? -1 : h_find(t, ks, h, nullptr);
     bool inserted = false;
-    if (idx < 0) {
+    if (nolock) {
+        idx = h_insert_nolock(t, ks, h, &inserted);
+    } else if (idx < 0) {
         // a new key: find-or-insert under its stripe lock, the wave's lanes in lock rounds
-        idx = HASH_POPONLY(kp) ? (MIMIC_HASH_NOLOCK ? h_insert_nolock(t, ks, h, &inserted) : h_insert_wave(t, ks, h, &inserted, true))
-                               : h_insert_wave(t, ks, h, &inserted, false);
+        idx = HASH_POPONLY(kp) ? h_insert_wave(t, ks, h, &inserted, true) : h_insert_wave(t, ks, h, &inserted, false);
     }
     if (idx < 0) {
         o.r0 = 7; // syscall.E2BIG: the freelist is empty
@@ -1191,7 +1194,7 @@ DEV bool hash_lookup_fast(const KParams &kp, Lane &L, uint32_t mid, uint64_t r1,
     ks.w3 = K > 24 ? stack_load(kp, L, ko + 24, K - 24) : 0;
     const HT t = h_table(kp.arena, m);
     const uint64_t h = h_hash(ks, K);
-    const int32_t idx = HASH_RO(kp) ? h_find_ro(t, ks, h) : h_find(t, ks, h, nullptr);
+    const int32_t idx = HASH_RO(kp) ? h_find_ro(t, ks, h) : h_find(t, ks, h, nullptr, !HASH_POPONLY(kp));
     r0 = idx < 0 ? 0 : hash_value_addr(m, L.cpu, (uint32_t)idx);
     if (idx >= 0) {
         L.t_lo = hash_value_addr(m, L.cpu, 0);

@@ -9,7 +9,7 @@ bench line times:
   cfg 4  flowtrack shard, 2 097 152 IMIX, E = 131 072, V = 262 144, interleaved
          per packet r0 / status exact, key -> value map exact (slots and the found / inserted
          path of a packet depend on which vCPU of a flow ran first, as in processPool)
-  cfg 5  sk_buff 5-program tail-call chain, 1 048 576 IMIX, V = 65 536, interleaved
+  cfg 5  sk_buff 5-program tail-call chain, 1 048 576 IMIX, V = 131 072, interleaved
          exact: per packet r0 / status / steps / err_pc, packet memory, every map
 
 Per-CPU maps make vCPUs independent, so the cfg-3 oracle runs in host threads, each one a VM

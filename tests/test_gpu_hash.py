@@ -326,3 +326,40 @@ def test_host_updates_run_on_the_host_image(gpu):
     assert fm.Lookup(newk) != 0 and fm.Delete(newk) == 0 and fm.Lookup(newk) == 0
     vm.close()
     ovm.close()
+
+
+def test_pop_only_launch_after_host_deletes_pops_the_pushed_slots(gpu):
+    """A pop-only launch after host deletes: the freelist's tail has moved past E, so its next
+    positions hold the freed slots in delete order, not position = slot (hashmap.h reads the ring
+    only then).  One vCPU runs every packet: each new flow takes exactly the slot the oracle's
+    FIFO freelist gives it (emulator_linux_map_hash.go:179-186, 244-250)."""
+    import mimic_amd as M
+
+    E = 400
+    p = W.prog_flowtrack(max_entries=E)
+    sc = _sc(p, 4)
+    buf, off, lens = W.make_packets(3000, **W.IMIX, seed=21)
+    keys = [bytes(k) for k in W.flow_keys_np(buf, off, lens)]
+    first = list(dict.fromkeys(keys))
+    ovm, omids, opids = build_oracle(sc)
+    vm, maps, pids = build_engine(sc)
+    fm, om = maps["flows"], omids["flows"]
+    rng = np.random.default_rng(5)
+    host = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(120)]
+    for k in host:   # slots 0..119
+        assert fm.Update(k, k[:8]) == ovm.map_update(om, k, k[:8], 0, 0) == 0
+    for k in host[::3] + first[:5]:   # frees 40 slots out of order (absent keys delete nothing)
+        fm.Delete(k)
+        ovm.lib.orc_map_delete(ovm.h, om, k)
+    assert sorted(fm.Entries()) == sorted(ovm.map_entries(om))
+    n = len(lens)
+    cpu = np.zeros(n, dtype=np.int32)
+    o = ovm.run_xdp_batch(opids[0], buf, off, lens, cpu, write_back=False)
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", cpu=cpu, schedule=M.SCHED_EXPLICIT)
+    e = vm.RunXDPBatch(pids[0], batch).numpy(n)
+    for k in ("r0", "status"):
+        assert np.array_equal(np.asarray(o[k]).astype(np.int64), np.asarray(e[k]).astype(np.int64)), k
+    assert sorted(fm.Entries()) == sorted(ovm.map_entries(om))
+    assert fm.Values(0) == ovm.map_values(om, 0)
+    vm.close()
+    ovm.close()

@@ -5,13 +5,16 @@ Input (tools/profile.sh): under DIR, one rocprofv3 output directory per pass:
   kt_<cfg>     --kernel-trace --stats            (kernel time)
   fetch_<cfg>  --pmc FETCH_SIZE                  (HBM read bytes, KiB per dispatch)
   write_<cfg>  --pmc WRITE_SIZE                  (HBM write bytes, KiB per dispatch)
+  req_<cfg>    --pmc TCC_EA0_RDREQ{,_32B,_64B,_128B}_sum   (read requests by size)
   sq_<cfg>     --pmc SQ_* + GRBM_GUI_ACTIVE      (instruction mix, VALU busy)
 Per-dispatch values are averaged over the engine kernel's dispatches of the bench's timed region:
 the first --skip dispatches (the bench's warmup; for cfg 4 the first one inserts every flow) are
 left out.  FETCH_SIZE is
 also reported doubled (MI355X_MICROARCH.md: on gfx950 it counts 1/2 of wide streaming reads);
 `bytes_per_launch` = doubled FETCH + WRITE, an upper estimate for this kernel's mixed-width
-loads.  The summary is keyed to the kernel source hash, packets and vCPUs of the run, which is
+loads.  With the request-size pass, read bytes are counted exactly instead
+(32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B, when those three partition RDREQ) and
+`bytes_per_launch` is that + WRITE.  The summary is keyed to the kernel source hash, packets and vCPUs of the run, which is
 how bench.py finds it.
 """
 import argparse
@@ -114,6 +117,7 @@ def main():
     fetch = counters(os.path.join(a.dir, f"fetch_{nm}"), a.kernel, a.skip, a.keep).get("FETCH_SIZE")
     write = counters(os.path.join(a.dir, f"write_{nm}"), a.kernel, a.skip, a.keep).get("WRITE_SIZE")
     sq = counters(os.path.join(a.dir, f"sq_{nm}"), a.kernel, a.skip, a.keep)
+    req = counters(os.path.join(a.dir, f"req_{nm}"), a.kernel, a.skip, a.keep)
     out = {"config": c, "round": a.tag, "kernel": a.kernel,
            "kernel_src_hash": bench.kernel_src_hash_of(c, vcpus if a.spread else 0), "spread": a.spread,
            "packets": n, "vcpus": vcpus, "batches": a.batches or bench.default_batches(c, n),
@@ -126,6 +130,19 @@ def main():
         out["correction"] = ("FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 FETCH_SIZE counts 1/2 of wide "
                              "streaming reads); this kernel mixes 8-B and narrower loads, so true read bytes lie "
                              "between the raw and the doubled value")
+    if req and fetch is not None and write is not None:
+        g = lambda k: req.get(f"TCC_EA0_RDREQ{k}_sum", req.get(f"TCC_EA0_RDREQ{k}", 0.0))
+        n_all, n32, n64, n128 = g(""), g("_32B"), g("_64B"), g("_128B")
+        out["read_requests_per_launch"] = {"all": n_all, "32B": n32, "64B": n64, "128B": n128}
+        rest = n_all - n32 - n64 - n128
+        if n_all and abs(rest) <= 0.01 * n_all:   # the sizes partition the requests: exact read bytes
+            rd = 32 * n32 + 64 * n64 + 128 * n128
+            out["read_bytes_per_launch"] = int(rd)
+            out["bytes_per_launch"] = int(rd + write * 1024)
+            out["correction"] = ("read bytes from the request counts by size (TCC_EA0_RDREQ_32B/_64B/_128B); "
+                                 "FETCH_SIZE tallies 128-byte requests at 64 B")
+        else:
+            out["read_requests_unpartitioned"] = rest
     if sq:
         out["sq_per_launch"] = sq
         waves = sq.get("SQ_WAVES") or 0
