@@ -428,7 +428,13 @@ def main(argv=None):
                          f"GPU(s) visible\n")
         return 2
     use_dist = ws > 1 or args.rccl   # the collective paths (RCCL); at world size 1 only with --rccl
+    json_out = sys.stdout
     if use_dist:
+        # RCCL writes its banner to file descriptor 1 when a communicator starts: native writes to
+        # stdout go to stderr from here on, the one JSON line to the original stdout
+        json_out = os.fdopen(os.dup(1), "w")
+        sys.stdout.flush()
+        os.dup2(2, 1)
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -576,7 +582,7 @@ def main(argv=None):
             T = host_threads()
             allc = cpu_baseline(wl, args.cpu_seconds, T) if T > 1 else one
             out["cpu_baseline"] = dict(one, all_cores=allc)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if use_dist:
         dist.destroy_process_group()
     vm.close()

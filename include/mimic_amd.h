@@ -364,8 +364,9 @@ long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots,
                               char *buf, size_t cap);
 int mimic_jit_prebuild_ctx(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind);
 /* The kernel source a VM generates when some LD_IMM64 slots name a per-CPU array whose per-vCPU
- * row is at most 32 bytes, a multiple of 8 (the lane value cache, jit.cpp analyze_vc): vc_slots
- * holds n_vc (program index, slot) pairs.  mimic_jit_source_for_ctx is this with n_vc = 0. */
+ * row is at most 128 bytes, a multiple of 8 (the lane value cache, jit.cpp analyze_vc: rows up to
+ * 32 bytes in registers, longer ones in LDS): vc_slots holds n_vc (program index, slot, E * S)
+ * triples.  mimic_jit_source_for_ctx is this with n_vc = 0. */
 long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
                          const uint32_t *vc_slots, uint32_t n_vc, char *buf, size_t cap);
 /* The spread kernel's source (mimic_set_spread): pc = (program, slot, map id) triples of the

@@ -37,8 +37,8 @@ extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStr
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
-                                     uint32_t n, SkbRec *rec, uint64_t *prefix, uint64_t *state, uint64_t init_base,
-                                     uint32_t use_init, hipStream_t st);
+                                     uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
+                                     uint64_t init_base, uint32_t use_init, hipStream_t st);
 
 namespace {
 
@@ -78,7 +78,7 @@ struct HostMap {
 // can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
 bool vc_row_ok(uint32_t family, uint32_t max_entries, uint32_t value_size) {
     const uint64_t rb = (uint64_t)max_entries * value_size;
-    return family == FAM_PERCPU_ARRAY && rb > 0 && rb <= 32 && (rb & 7) == 0;
+    return family == FAM_PERCPU_ARRAY && rb > 0 && rb <= MIMIC_VC_MAX_ROW && (rb & 7) == 0;
 }
 
 struct HostProg {
@@ -181,6 +181,7 @@ struct mimic_vm {
     // sk_buff batches (skb.h): per-packet records, their leak prefixes (skb.hip), and
     // the device word pair {next leak address, this batch's leak base}
     SkbRec *d_skb_rec = nullptr;
+    uint64_t *d_skb_drv = nullptr;   // the prep kernel's derived record words, SKB_DERIVED_Q per packet
     uint64_t *d_skb_prefix = nullptr, *d_skb_state = nullptr;
     size_t skb_cap = 0;
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
@@ -642,6 +643,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (vm->kp_side_ev) hipEventDestroy(vm->kp_side_ev);
     if (vm->s_kp) hipStreamDestroy(vm->s_kp);
     hipFree(vm->d_skb_rec);
+    hipFree(vm->d_skb_drv);
     hipFree(vm->d_skb_prefix);
     hipFree(vm->d_skb_state);
     if (vm->s_h2d) hipStreamDestroy(vm->s_h2d);
@@ -1441,11 +1443,14 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     if (n > vm->skb_cap || !vm->d_skb_state) {
         HIP_OK(vm, hipStreamSynchronize(st));
         hipFree(vm->d_skb_rec);
+        hipFree(vm->d_skb_drv);
         hipFree(vm->d_skb_prefix);
         vm->d_skb_rec = nullptr;
+        vm->d_skb_drv = nullptr;
         vm->d_skb_prefix = nullptr;
         const size_t cap = std::max<size_t>(n, 1024);
         HIP_OK(vm, hipMalloc(&vm->d_skb_rec, cap * sizeof(SkbRec)));
+        HIP_OK(vm, hipMalloc(&vm->d_skb_drv, cap * 8 * SKB_DERIVED_Q));
         // within-block prefixes, then the blocks' offsets (skb.hip)
         HIP_OK(vm, hipMalloc(&vm->d_skb_prefix, (cap + (cap >> SKB_PREP_LOG2) + 1) * 8));
         if (!vm->d_skb_state) {   // leak cursor, batch base, the prep kernel's block counter (zero)
@@ -1456,8 +1461,11 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     }
     // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
     const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
-    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, into ? into->rec : records ? vm->d_skb_rec : nullptr,
-                              into ? into->prefix : vm->d_skb_prefix, vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
+    // a batch's derived words go to the compact array (read by skb_load*), a process's into its record
+    uint64_t *out = into ? (uint64_t *)into->rec : records ? vm->d_skb_drv : nullptr;
+    const uint32_t out_q = into ? (uint32_t)(sizeof(SkbRec) / 8) : SKB_DERIVED_Q;
+    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
+                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;
     vm->skb_stream = st;
@@ -1690,13 +1698,14 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     bool jit = vm->exec_mode == MIMIC_EXEC_JIT && !step;   // stepping runs on the interpreter
     if (jit && !vm->jit_fn[ctx]) {
         std::string log;
-        std::vector<uint32_t> vc;   // LD_IMM64 slots naming a per-CPU array whose row the lane value cache can hold
+        // LD_IMM64 slots naming a per-CPU array whose row the lane value cache can hold, with its E * S
+        std::vector<std::pair<uint32_t, uint32_t>> vc;
         for (size_t s = 0; s < vm->h_all.size(); s++) {
             const DInsn &x = vm->h_all[s];
             const uint32_t mh = AUX_MAPHINT(x.aux);
             if (AUX_H(x.aux) != H_LDIMM || !mh || mh > vm->maps.size()) continue;
             const HostMap &hm = vm->maps[mh - 1];
-            if (vc_row_ok(hm.family, hm.max_entries, hm.value_size)) vc.push_back((uint32_t)s);
+            if (vc_row_ok(hm.family, hm.max_entries, hm.value_size)) vc.push_back({(uint32_t)s, hm.max_entries * hm.value_size});
         }
         if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx], &vc),
                               &vm->jit_fn[ctx], &log))
@@ -1783,6 +1792,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.ctx_kind = CTX_SKB;
         kp.skb_ifindex = skb->ifindex;
         kp.skb_rec = vm->d_skb_rec;
+        kp.skb_drv = own_recs ? nullptr : vm->d_skb_drv;
         kp.skb_prefix = vm->d_skb_prefix;
         kp.skb_base = vm->d_skb_state + 1;
         kp.skb_custom = skb->custom;
@@ -2171,11 +2181,11 @@ long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint
     std::vector<DInsn> all;
     std::vector<DProg> dp;
     build_host_tables(hp, all, dp);
-    std::vector<uint32_t> vc;
+    std::vector<std::pair<uint32_t, uint32_t>> vc;
     for (uint32_t q = 0; q < n_vc; q++) {
-        const uint32_t p = vc_slots[2 * q], s = vc_slots[2 * q + 1];
+        const uint32_t p = vc_slots[3 * q], s = vc_slots[3 * q + 1], rb = vc_slots[3 * q + 2];
         if (p >= dp.size() || s >= dp[p].n) return MIMIC_EINVAL;
-        vc.push_back(dp[p].base + s);
+        vc.push_back({dp[p].base + s, rb});
     }
     const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr, &vc);
     if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);

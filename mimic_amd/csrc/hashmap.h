@@ -385,9 +385,19 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
             uint64_t base = 0;
             uint32_t ident = 0;
             if (me == first) {
-#ifdef MIMIC_MEAS_NOHEAD   // measurement only (slots collide, results wrong): no shared head counter
+#if defined(MIMIC_MEAS_NOHEAD) || defined(MIMIC_MEAS_SPREADHEAD)
+                // measurement only (slots collide, results wrong): no shared head counter; SPREADHEAD
+                // keeps an atomic with return of the same latency on a per-wave address
                 base = ((uint64_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u) % (t.E > 64 ? t.E - 64 : 1);
+#ifdef MIMIC_MEAS_SPREADHEAD
+                base += __hip_atomic_fetch_add(&c->used_sh[32 * ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (HT_USED_SHARDS - 1))],
+                                               0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0u;
+#endif
                 got = k;
+                ident = 1;
+#elif defined(MIMIC_MEAS_NOTAIL)   // measurement only: the head atomic without the tail load
+                base = __hip_atomic_fetch_add(&c->head, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                got = base >= t.E ? 0u : (t.E - base < k ? (uint32_t)(t.E - base) : k);
                 ident = 1;
 #else
                 base = __hip_atomic_fetch_add(&c->head, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -211,8 +211,10 @@ class Gen {
     const SpreadReq *spread_req = nullptr;   // the VM's per-CPU arrays: spread mode is possible (analyze_spread)
     bool spread_on = false;
     uint32_t spread_map = 0, spread_n = 0, spread_row = 0;   // the counted map, counter width, E * S
-    std::set<uint32_t> vc_ok;  // LD_IMM64 slots (kernel-wide) naming a per-CPU array whose row can be cached
+    std::map<uint32_t, uint32_t> vc_ok;  // LD_IMM64 slots (kernel-wide) naming a per-CPU array whose row can be cached -> E * S
     uint32_t vc_slot = 0;      // the LD_IMM64 slot (kernel-wide index) whose map hint names the cached map
+    uint32_t vc_rb = 0;        // its row bytes
+    bool vc_lds = false;       // the row is longer than four registers: an LDS slot per lane
     // The cross-packet window prefetch (analyze_xpf): the entry program `prog` makes its first
     // window of early loads at slot `hp` from register `base` = data + `off` - lo; the window's
     // bytes lie at data offset `off` .. off + 8 * words of the packet.
@@ -365,9 +367,12 @@ class Gen {
         else
             E.line("#define COLD_CALL(call_, pc_) do { VC_FLUSH(); SPILL(); call_; FILL(); if (sp_.st) TERM(sp_.st, pc_); } while (0)");
         // defer mode: the site stored the live registers; the rest is the lane's (defer_finish)
-        E.line("#define DFR(pc_, prog_) do { VC_FLUSH(); dr_->pc = (int32_t)(pc_); dr_->prog = (prog_); dr_->steps = steps - 1u; goto L_defer; } while (0)");
+        // (the lane value cache is written back once, at L_defer: not inlined at every site)
+        E.line("#define DFR(pc_, prog_) do { dr_->pc = (int32_t)(pc_); dr_->prog = (prog_); dr_->steps = steps - 1u; goto L_defer; } while (0)");
         // a cold path may read or write the cached row in memory: write it back and stop caching
-        if (vc_on)
+        if (vc_on && vc_lds)
+            E.line("#define VC_FLUSH() do { if (vcd_) { lvc_writeback(vcp_, vcb_, lvt_); vcd_ = 0u; } vcv_ = 0u; } while (0)");
+        else if (vc_on)
             E.line("#define VC_FLUSH() do { if (vcd_) { vc_writeback(vcp_, vcb_, vc0_, vc1_, vc2_, vc3_); vcd_ = 0u; } vcv_ = 0u; } while (0)");
         else
             E.line("#define VC_FLUSH() do { } while (0)");
@@ -439,9 +444,20 @@ class Gen {
         }
         if (vc_on) {
             // the lane's own row of the per-CPU array the hint names (analyze_vc)
-            E.line("  uint64_t vc0_ = 0, vc1_ = 0, vc2_ = 0, vc3_ = 0; uint32_t vcv_ = 0u, vcd_ = 0u, vclo_ = 0u, vcb_ = 0u; uint8_t *vcp_ = nullptr;");
-            E.line("  { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", vc_slot);
-            E.line("    if (mh_) vc_open(kp, cget(kp.maps, mh_ - 1u), L.cpu, vcp_, vclo_, vcb_, vcv_, vc0_, vc1_, vc2_, vc3_); }");
+            if (vc_lds) {
+                // rows over 32 bytes: the lane's row in its LDS slot, dword d at lvc_[d * 256 + thread]
+                // (two spare dwords: an unaligned read at the row's end stays in the array)
+                E.line("  __shared__ uint32_t lvc_[(%uu / 4u + 2u) * 256u];", vc_rb);
+                E.line("  uint32_t *const lvt_ = lvc_ + threadIdx.x;");
+                E.line("  constexpr uint32_t vcb_ = %uu;   // the row's bytes", vc_rb);
+                E.line("  uint32_t vcv_ = 0u, vcd_ = 0u, vclo_ = 0u; uint8_t *vcp_ = nullptr;");
+                E.line("  { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", vc_slot);
+                E.line("    if (mh_) lvc_open(kp, cget(kp.maps, mh_ - 1u), L.cpu, vcb_, vcp_, vclo_, vcv_, lvt_); }");
+            } else {
+                E.line("  uint64_t vc0_ = 0, vc1_ = 0, vc2_ = 0, vc3_ = 0; uint32_t vcv_ = 0u, vcd_ = 0u, vclo_ = 0u, vcb_ = 0u; uint8_t *vcp_ = nullptr;");
+                E.line("  { const uint32_t mh_ = AUX_MAPHINT(cget(kp.insns, %uu).aux);", vc_slot);
+                E.line("    if (mh_) vc_open(kp, cget(kp.maps, mh_ - 1u), L.cpu, vcp_, vclo_, vcb_, vcv_, vc0_, vc1_, vc2_, vc3_); }");
+            }
         }
         E.line("  uint32_t ex_begin = 0, ex_count = 0;");
         E.line("  if (kp.sched == SCHED_EXPLICIT) { ex_begin = *gp(kp.sched_start + g); ex_count = *gp(kp.sched_start + g + 1) - ex_begin; }");
@@ -600,6 +616,7 @@ class Gen {
         E.line("    TERM(MIMIC_ERR_ENGINE_HELPER, -1);");
         if (defer_mode) {
             E.line("  L_defer:");
+            E.line("    VC_FLUSH();");
             E.line("    defer_finish(kp, L, g, i, j, lane_steps);");
             E.line("    break;");
         }
@@ -1017,6 +1034,8 @@ class Gen {
                 if (j >= 0 && vc_ok.count(p.base + (uint32_t)j)) {
                     vc_on = true;
                     vc_slot = p.base + (uint32_t)j;
+                    vc_rb = vc_ok.at(vc_slot);
+                    vc_lds = vc_rb > 32;
                     return;
                 }
             }
@@ -1364,6 +1383,13 @@ class Gen {
         E.line("    // %u..%u: counter increment of r%u (dead after): one atomic add in the lookup's value region", i, i + 2, d);
         E.line("    ga_ = %s;", addr(b, insn_off(ld)).c_str());
         std::string cond = "(uint64_t)(uint32_t)(ga_ - L.t_lo) + " + N + " < L.t_n && !((uintptr_t)(L.t_ptr + (uint32_t)(ga_ - L.t_lo)) & (" + N + " - 1u))";
+        if (vc_on && vc_lds) {
+            // an aligned counter in the lane's LDS row: one LDS read-modify-write (the row is the
+            // lane's own vCPU's: no other lane touches it)
+            E.line("    if (vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + %s <= vcb_ && !((ga_ - vclo_) & 3u)) { steps += 3u; lvc_add(lvt_, ga_ - vclo_, %s, %s); vcd_ = 1u; }",
+                   N.c_str(), N.c_str(), imm(k).c_str());
+            E.line("    else");
+        }
         if (vc_on) cond = "!(vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + " + N + " <= vcb_) && " + cond;
         if (spread_on) {
             // a counter of this packet's vCPU row in the spread map: into the block's table (or one
@@ -1475,7 +1501,11 @@ class Gen {
                              (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
             // the lane's cached per-CPU row (analyze_vc): every access inside the row while the
             // cache is valid is served here, so memory and registers never disagree
-            if (vc_on)
+            if (vc_on && vc_lds)
+                f.push_back({"vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + " + N + " <= vcb_",
+                             "lvc_load(lvt_, ga_ - vclo_, " + N + ")",
+                             "{ lvc_store(lvt_, ga_ - vclo_, " + N + ", " + v + "); vcd_ = 1u; }"});
+            else if (vc_on)
                 f.push_back({"vcv_ && (uint64_t)(uint32_t)(ga_ - vclo_) + " + N + " <= vcb_",
                              "vc_load(vc0_, vc1_, vc2_, vc3_, ga_ - vclo_, " + N + ")",
                              "{ vc_store(vc0_, vc1_, vc2_, vc3_, ga_ - vclo_, " + N + ", " + v + "); vcd_ = 1u; }"});
@@ -1953,12 +1983,14 @@ std::map<CacheKey, hipFunction_t> g_cache;
 }  // namespace
 
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
-                             JitInfo *info, const std::vector<uint32_t> *vc_slots, bool no_early_loads,
+                             JitInfo *info, const std::vector<std::pair<uint32_t, uint32_t>> *vc_slots, bool no_early_loads,
                              const SpreadReq *spread) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
     Gen g(v, ctx_kind);
-    if (vc_slots) g.vc_ok.insert(vc_slots->begin(), vc_slots->end());
+    if (vc_slots)
+        for (auto &v : *vc_slots)
+            if (v.second > 0 && v.second <= MIMIC_VC_MAX_ROW && !(v.second & 7)) g.vc_ok[v.first] = v.second;
     if (no_early_loads) g.speculate = 0;
     g.spread_req = spread;
     std::string src = g.source();

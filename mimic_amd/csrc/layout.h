@@ -218,6 +218,9 @@ struct KParams {
     uint32_t *spread_bad;
     // sk_buff batches: the user-given sock / flow keys (mimic_skb_custom [n], packet-indexed), or null
     const void *skb_custom;
+    // sk_buff batches: the prep kernel's derived record words, SKB_DERIVED_Q per packet with no gaps
+    // (skb.hip), or null (a stepped process's own record holds them)
+    const uint64_t *skb_drv;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

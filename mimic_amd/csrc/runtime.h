@@ -655,6 +655,60 @@ DEV void vc_writeback(uint8_t *p, uint32_t nb, uint64_t w0, uint64_t w1, uint64_
     if (nb > 24) d[3] = w3;
 }
 
+// The LDS form of the lane value cache, for rows of 40..MIMIC_VC_MAX_ROW bytes (jit.cpp vc_lds):
+// the lane's row in its LDS slot `c` (dword d at c[d * 256], the block's lanes interleaved, so a
+// wave's same-offset access hits 64 consecutive banks).  Same semantics as the register form:
+// little-endian like the arena, any size / alignment inside the row.
+#define LVC_T 256u
+DEV void lvc_open(const KParams &kp, const DMap &m, int32_t cpu, uint32_t rb, uint8_t *&p, uint32_t &lo, uint32_t &valid,
+                  uint32_t *c) {
+    if (m.family != FAM_PERCPU_ARRAY || cpu < 0 || (uint32_t)cpu >= m.ncpu || (uint64_t)m.max_entries * m.value_size != rb) return;
+    uint8_t *q = array_value_ptr(kp, m, cpu, 0);
+    if ((uintptr_t)q & 7) return;
+    p = q;
+    lo = m.backing_addr + (cpu > 0 ? (uint32_t)cpu * m.addr_period : 0u);
+    const GAS uint64_t *s = (const GAS uint64_t *)q;
+    for (uint32_t w = 0; w < rb / 8; w++) {
+        const uint64_t v = s[w];
+        c[(2 * w) * LVC_T] = (uint32_t)v;
+        c[(2 * w + 1) * LVC_T] = (uint32_t)(v >> 32);
+    }
+    valid = 1u;
+}
+DEV void lvc_writeback(uint8_t *p, uint32_t nb, const uint32_t *c) {
+    GAS uint64_t *d = (GAS uint64_t *)p;
+    for (uint32_t w = 0; w < nb / 8; w++) d[w] = (uint64_t)c[(2 * w) * LVC_T] | ((uint64_t)c[(2 * w + 1) * LVC_T] << 32);
+}
+DEV uint64_t lvc_load(const uint32_t *c, uint32_t o, uint32_t n) {
+    const uint32_t d = o >> 2, sh = (o & 3) * 8;
+    uint64_t v = ((uint64_t)c[d * LVC_T] | ((uint64_t)c[(d + 1) * LVC_T] << 32)) >> sh;
+    if (sh && 8 * n + sh > 64) v |= (uint64_t)c[(d + 2) * LVC_T] << (64 - sh);
+    return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
+}
+DEV void lvc_store(uint32_t *c, uint32_t o, uint32_t n, uint64_t v) {
+    if (!(o & 3) && (n == 4 || n == 8)) {
+        c[(o >> 2) * LVC_T] = (uint32_t)v;
+        if (n == 8) c[((o >> 2) + 1) * LVC_T] = (uint32_t)(v >> 32);
+        return;
+    }
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t b = o + k, s = (b & 3) * 8;
+        uint32_t &w = c[(b >> 2) * LVC_T];
+        w = (w & ~(0xffu << s)) | (((uint32_t)(v >> (8 * k)) & 0xffu) << s);
+    }
+}
+// a fused counter increment (4 or 8 bytes at a 4-byte aligned offset o)
+DEV void lvc_add(uint32_t *c, uint32_t o, uint32_t n, uint64_t k) {
+    uint32_t *w = c + (o >> 2) * LVC_T;
+    if (n == 4) {
+        w[0] += (uint32_t)k;
+        return;
+    }
+    const uint64_t x = ((uint64_t)w[0] | ((uint64_t)w[LVC_T] << 32)) + k;
+    w[0] = (uint32_t)x;
+    w[LVC_T] = (uint32_t)(x >> 32);
+}
+
 // memmove of n bytes from a VM region into the arena (map update, emulator_linux_map_array.go:112)
 DEV void copy_into(const KParams &kp, const Lane &L, const Ref &src, uint8_t *dst, uint32_t n) {
     bool backward = (src.rk == RK_GLOBAL || src.rk == RK_BEPKT) && src.ptr + src.off < dst && dst < src.ptr + src.off + n;
@@ -907,6 +961,16 @@ DEV int ld_abs(const KParams &kp, const Lane &L, uint64_t r6, uint32_t x, uint32
 // are read first and written only when some byte is not zero already (a program stored there in
 // an earlier run of the buffer, or the caller's bytes): the common case writes nothing, and the
 // reads share their lines with the packet's first bytes and travel with the header loads.
+DEV void skb_rooms_zero(uint8_t *pkt, uint32_t lw) {
+    typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
+    const u64x2u z = {0, 0};
+    GAS u64x2u *hw = (GAS u64x2u *)pkt, *tw = (GAS u64x2u *)(pkt + SKB_HEADROOM + lw);
+    hw[0] = z;
+    hw[1] = z;
+    for (uint32_t q = 0; q < SKB_TAILROOM / 16; q++) tw[q] = z;
+}
+// the rooms flag of a record the prep kernel built (skb.h SKB_DIRTY_Q)
+DEV bool skb_rec_dirty(const SkbRec &r) { return r.ip[0].pad[0] != 0; }
 DEV void skb_rooms_clear(uint8_t *pkt, uint32_t lw) {
 #if defined(MIMIC_ROOMS_MODE) && MIMIC_ROOMS_MODE == 2   // measurement only (MIMIC_JIT_ROOMS=2): rooms untouched
     return;
@@ -944,6 +1008,8 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     SkbRec *rec = kp.skb_rec + i;
     L.pkt = kp.pkt_data + kp.pkt_off[i];
     if (!kp.skb_rec_built && !attach_only) skb_init(SkbBytes{L.pkt + SKB_HEADROOM}, kp.pkt_len[i], *rec);
+    else if (kp.skb_drv && !attach_only)   // the prep kernel's derived words into the record
+        for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) ((uint64_t *)rec)[q] = kp.skb_drv[(size_t)i * SKB_DERIVED_Q + q];
     const uint32_t lw = rec->len;
     L.rec = nullptr;
     L.ka = 0;
@@ -960,14 +1026,19 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     L.ka = (uint32_t)ka;
     L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
     L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
-    if (!attach_only) skb_rooms_clear(L.pkt, lw);
+    if (!attach_only) {
+        if (!kp.skb_rec_built) skb_rooms_clear(L.pkt, lw);
+        else if (skb_rec_dirty(*rec)) skb_rooms_zero(L.pkt, lw);
+    }
     r1 = kp.static_next + kp.stack_size + 1;
     return 0;
 }
 
 // skb_load's tail once the record of packet i is in place (LDS slot d): a user-given sock / flow
 // keys, entries, rooms, R1
-DEV int skb_attach(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint32_t lw, uint64_t pre, uint64_t base) {
+// dirty: the record's rooms flag (1 / 0), or -1 when no prep kernel looked (read the rooms here)
+DEV int skb_attach(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint32_t lw, uint64_t pre, uint64_t base,
+                   int dirty) {
     skb_apply_custom(*(SkbRec *)d, (const mimic_skb_custom *)kp.skb_custom, i);
     L.rec = nullptr;
     L.ka = 0;
@@ -980,7 +1051,8 @@ DEV int skb_attach(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_
     L.ka = (uint32_t)ka;
     L.pa = L.ka + SKB_SK_SIZE + 1 + SKB_FK_SIZE + 1;
     L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
-    skb_rooms_clear(L.pkt, lw);
+    if (dirty < 0) skb_rooms_clear(L.pkt, lw);
+    else if (dirty) skb_rooms_zero(L.pkt, lw);
     r1 = kp.static_next + kp.stack_size + 1;
     return 0;
 }
@@ -989,17 +1061,24 @@ DEV int skb_attach(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_
 // the packet offset and the leak prefix are loaded together (one memory round trip, not the
 // record length first and the rest after it), then the record goes to LDS.
 DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d) {
-    const GAS uint64_t *s = (const GAS uint64_t *)(kp.skb_rec + i);
+    // the packet's derived words: 96 contiguous bytes of the prep kernel's compact array (consecutive
+    // lanes, consecutive records), six 16-byte loads
+    typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
+    const GAS u64x2a *s = (const GAS u64x2a *)(kp.skb_drv + (size_t)i * SKB_DERIVED_Q);
     uint64_t w[SKB_DERIVED_Q];
 #pragma unroll
-    for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) w[q] = s[q];
+    for (uint32_t q = 0; q < SKB_DERIVED_Q / 2; q++) {
+        const u64x2a v = s[q];
+        w[2 * q] = v.x;
+        w[2 * q + 1] = v.y;
+    }
     const uint64_t po = kp.pkt_off[i], pre = skb_leak_pre(kp, i), base = *kp.skb_base;
 #pragma unroll
     for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) d[q] = w[q];
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) d[SKB_DERIVED_Q + q] = skb_writable_word(q);
     L.pkt = kp.pkt_data + po;
-    return skb_attach(kp, L, i, r1, d, (uint32_t)w[0], pre, base);
+    return skb_attach(kp, L, i, r1, d, (uint32_t)w[0], pre, base, (int)((w[SKB_DIRTY_Q] >> SKB_DIRTY_SHIFT) & 1u));
 }
 
 // skb_load for a JIT kernel that builds the record itself (no prep records: a 160-byte write and
@@ -1013,7 +1092,7 @@ DEV int skb_load_walk(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint
     skb_stage<256u>(win, threadIdx.x, pkt, len);
     SkbRec &r = *(SkbRec *)d;
     skb_init(SkbWinBytes<256u>{win, pkt, threadIdx.x}, len, r);
-    return skb_attach(kp, L, i, r1, d, r.len, pre, base);
+    return skb_attach(kp, L, i, r1, d, r.len, pre, base, -1);
 }
 
 // ---------------------------------------------------------------------------------------

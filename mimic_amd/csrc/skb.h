@@ -45,7 +45,7 @@
 // 2 = gopacket's packet copy from byte `off` (cap = L - off: Go slices may read past n)
 struct SkbIP {
     uint32_t off;
-    uint8_t kind, n, pad[2];
+    uint8_t kind, n, pad[2];   // ip[0].pad[0]: the prep kernel's rooms flag (SKB_DIRTY_Q)
 };
 
 struct SkbRec {  // 160 bytes
@@ -78,6 +78,14 @@ struct SkbRec {  // 160 bytes
 // (skb_load: in HBM; the JIT: in its LDS slot).
 #define SKB_DERIVED_Q 12u
 static_assert(__builtin_offsetof(SkbRec, mark) == 8 * SKB_DERIVED_Q, "writable state follows the derived words");
+// The prep kernel also finds whether the packet memory's headroom or tailroom holds a non-zero byte
+// (Load hands the program zeroed rooms, context_sk_buff.go:110-119): a spare byte of the derived
+// words, ip[0].pad[0] (word SKB_DIRTY_Q, bit SKB_DIRTY_SHIFT), so whoever loads the process knows
+// without reading the rooms itself (a dependent round trip on every process's critical path).
+#define SKB_DIRTY_Q 3u
+#define SKB_DIRTY_SHIFT 16u
+static_assert(__builtin_offsetof(SkbRec, ip) + __builtin_offsetof(SkbIP, pad) == 8 * SKB_DIRTY_Q + SKB_DIRTY_SHIFT / 8,
+              "the rooms flag byte");
 static_assert(__builtin_offsetof(SkbRec, tstamp) == 8 * (SKB_DERIVED_Q + 2), "tstamp is word 14");
 static_assert(sizeof(SkbRec) == 8 * (SKB_DERIVED_Q + 8), "8 writable words");
 

@@ -23,14 +23,14 @@
 #define PREP_W SKB_WIN
 #define PREP_T 256u
 
-// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them.  rec == nullptr: the
+// packet i: packet bytes at pkt_data + pkt_off[i] + 32, pkt_len[i] of them; its derived record words
+// at rec + i * rec_q.  rec == nullptr: the
 // leak prefixes only (a JIT kernel that walks the headers itself builds the records in LDS).  Only
 // the records' derived words are written (skb.h SKB_DERIVED_Q: the writable state is constant at
 // Load and set by whoever loads the process).  They leave through LDS: each thread puts its
 // words there and the block writes them with consecutive threads on consecutive 8-byte words --
 // stored one record per thread, every store instruction of a wave would touch 64 records 160
 // bytes apart.  The block's derived words (24 KiB) fit the windows' 32 KiB.
-#define PREP_RQ (sizeof(SkbRec) / 8)
 #ifdef MIMIC_PREP_PLAIN   // measurement: cached record stores
 #define PREP_ST(p, v) (*(p) = (v))
 #else   // records are streamed out: non-temporal stores
@@ -67,8 +67,8 @@ static __device__ uint64_t prep_exscan(uint64_t v, uint64_t *wtot, uint64_t *tot
 extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
-                                                                          uint32_t n, SkbRec *__restrict__ rec,
-                                                                          uint64_t *__restrict__ prefix) {
+                                                                          uint32_t n, uint64_t *__restrict__ rec,
+                                                                          uint32_t rec_q, uint64_t *__restrict__ prefix) {
     __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
     __shared__ uint64_t wtot[PREP_T / 64];
     uint32_t *win = (uint32_t *)area;
@@ -99,6 +99,13 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
 #else
         skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
 #endif
+        // the rooms flag (skb.h SKB_DIRTY_Q): any non-zero byte in the 32 bytes before the packet
+        // or the 64 after it
+        const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
+        u32x4u o = hr[0] | hr[1];
+#pragma unroll
+        for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) o |= tr[c];
+        r.ip[0].pad[0] = (o.x | o.y | o.z | o.w) ? 1u : 0u;
         f = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
     if (rec) {
@@ -106,7 +113,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
         if (live) {
             typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
             const u64x2 *rv = (const u64x2 *)&r;
-            u64x2 *o = (u64x2 *)(rec + i);
+            u64x2 *o = (u64x2 *)(rec + (size_t)i * rec_q);
 #pragma unroll
             for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) PREP_ST(o + u, rv[u]);
         }
@@ -121,13 +128,21 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
         }
         __syncthreads();
         // the block's records are contiguous in rec: 16-byte units, consecutive threads on consecutive
-        // units (the writable words between the records are not written)
+        // units.  rec_q = SKB_DERIVED_Q (a batch's compact derived-word array): the block's output is
+        // one contiguous 24 KiB run; rec_q = 20 (SkbRec records, a stepped process): the writable
+        // words between the records are not written
         const uint32_t cnt = n - i0 < PREP_T ? n - i0 : PREP_T;
-        u64x2 *dst = (u64x2 *)(rec + i0);
-        constexpr uint32_t DU = SKB_DERIVED_Q / 2, RU = sizeof(SkbRec) / 16;
-        for (uint32_t w = t; w < cnt * DU; w += PREP_T) {
-            const uint32_t k = w / DU, u = w - k * DU;
-            PREP_ST(dst + (size_t)k * RU + u, area2[w]);
+        constexpr uint32_t DU = SKB_DERIVED_Q / 2;
+        if (rec_q == SKB_DERIVED_Q) {
+            u64x2 *dst = (u64x2 *)(rec + (size_t)i0 * SKB_DERIVED_Q);
+            for (uint32_t w = t; w < cnt * DU; w += PREP_T) PREP_ST(dst + w, area2[w]);
+        } else {
+            u64x2 *dst = (u64x2 *)(rec + (size_t)i0 * rec_q);
+            const uint32_t RU = rec_q / 2;
+            for (uint32_t w = t; w < cnt * DU; w += PREP_T) {
+                const uint32_t k = w / DU, u = w - k * DU;
+                PREP_ST(dst + (size_t)k * RU + u, area2[w]);
+            }
         }
 #endif
     }
@@ -179,9 +194,9 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
 
 // the prep kernel alone (tools/prep_probe.py)
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
-                                   SkbRec *rec, uint64_t *prefix, uint64_t *state, hipStream_t st) {
+                                   uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state, hipStream_t st) {
     hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                       rec, prefix);
+                       rec, rec_q, prefix);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        0ull, 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -189,11 +204,11 @@ extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_
 
 // prefix: n + ceil(n / 256) words; state: 2 words
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
-                                     uint32_t n, SkbRec *rec, uint64_t *prefix, uint64_t *state, uint64_t init_base,
-                                     uint32_t use_init, hipStream_t st) {
+                                     uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
+                                     uint64_t init_base, uint32_t use_init, hipStream_t st) {
     if (n)
         hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                           rec, prefix);
+                           rec, rec_q, prefix);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        init_base, use_init);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -30,15 +30,15 @@ def _progs_args(raws: Sequence[bytes]):
     return bufs, arr, ns
 
 
-def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int]] = (), spread=None) -> str:
-    """vc: (program index, slot) of the LD_IMM64 slots that name a per-CPU array whose per-vCPU
-    row is at most 32 bytes, a multiple of 8 -- what a VM with those maps generates (see
+def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int, int]] = (), spread=None) -> str:
+    """vc: (program index, slot, E * S) of the LD_IMM64 slots that name a per-CPU array whose
+    per-vCPU row is at most 128 bytes, a multiple of 8 -- what a VM with those maps generates (see
     ``vc_slots``).  spread: a ``spread_spec`` -- the VM's spread kernel instead (xdp_md)."""
     if spread is not None:
         return spread_source(raws, *spread)[0]
     lib = _lib.load()
     keep, arr, ns = _progs_args(raws)
-    flat = [v for pair in vc for v in pair]
+    flat = [v for t in vc for v in t]
     vca = (C.c_uint32 * max(len(flat), 1))(*flat)
     n = lib.mimic_jit_source_vc(arr, ns, len(raws), ctx, vca, len(vc), None, 0)
     if n < 0:
@@ -48,12 +48,12 @@ def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[
     return buf.value.decode()
 
 
-def vc_slots(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict]) -> List[Tuple[int, int]]:
-    """The (program index, slot) pairs of kernel_source's ``vc`` for programs (raw, relocations
-    [(slot, map name), ...]) loaded next to ``maps`` (name, type, value_size, max_entries): the
-    LD_IMM64 slots whose constant is the object of a per-CPU array (type 6) whose row E * S is at
-    most 32 bytes and a multiple of 8.  A PseudoMapValue slot names the object only when its
-    offset is 0 (Q16: the constant is the object address + offset)."""
+def vc_slots(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict]) -> List[Tuple[int, int, int]]:
+    """The (program index, slot, E * S) triples of kernel_source's ``vc`` for programs (raw,
+    relocations [(slot, map name), ...]) loaded next to ``maps`` (name, type, value_size,
+    max_entries): the LD_IMM64 slots whose constant is the object of a per-CPU array (type 6)
+    whose row E * S is at most 128 bytes and a multiple of 8.  A PseudoMapValue slot names the
+    object only when its offset is 0 (Q16: the constant is the object address + offset)."""
     by_name = {m["name"]: m for m in maps}
     out = []
     for pi, (raw, rel) in enumerate(progs):
@@ -63,11 +63,11 @@ def vc_slots(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict]) -> L
             if m is None or m["type"] != 6:
                 continue
             rb = m["max_entries"] * m["value_size"]
-            if not (0 < rb <= 32 and rb % 8 == 0):
+            if not (0 < rb <= 128 and rb % 8 == 0):
                 continue
             src, off = raw[8 * slot + 1] >> 4, int.from_bytes(raw[8 * slot + 2:8 * slot + 4], "little", signed=True)
             if src == 1 or (src == 2 and off == 0):
-                out.append((pi, slot))
+                out.append((pi, slot, rb))
     return out
 
 

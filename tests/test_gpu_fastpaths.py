@@ -503,7 +503,10 @@ def test_fused_counter_increments(gpu, variant):
 
     sc = _inc_scenario(variant)
     src = J.kernel_source(*kernel_of(sc))
-    assert src.count("atomic_add_n(") == {0: 2, 1: 2, 2: 2, 3: 1}[variant], src
+    # the fused form: an atomic add in the lookup's value region; for the per-CPU array (a 64-byte
+    # row: the lane value cache's LDS form) an LDS add first when the row is cached
+    assert src.count("CNT_ADD(L.t_ptr") == {0: 2, 1: 2, 2: 2, 3: 1}[variant], src
+    assert src.count("lvc_add(lvt_") == {0: 2, 1: 0, 2: 2, 3: 1}[variant], src
     n = 4096
     buf, off, lens = W.make_packets(n, sizes=(14, 64), weights=(1, 3))
     cpu = W.schedule_cpu(n, sc.vcpus, "interleaved")

@@ -1,9 +1,11 @@
 """The JIT's lane value cache (jit.cpp analyze_vc): a lane's own row of a small per-CPU array is
-held in registers across its packets and written back when the lane ends.  Programs here read and
-write the row at every offset and size (aligned and not, across value boundaries, past the row
-end), call map_update on the same map (a cold path: the row is written back and the cache is
-switched off), and run on CPU IDs -1 and V (no row).  Every run compares per-packet R0 / status /
-steps / err_pc, the packet memory and every map with the oracle, bit for bit."""
+held across its packets -- in four registers up to 32 bytes, in an LDS slot per lane up to 128 --
+and written back when the lane ends.  Programs here read and write the row at every offset and
+size (aligned and not, across value boundaries, past the row end), increment counters in it (the
+fused form: an LDS add in the LDS form), call map_update on the same map (a cold path: the row is
+written back and the cache is switched off), and run on CPU IDs -1 and V (no row).  Every run
+compares per-packet R0 / status / steps / err_pc, the packet memory and every map with the oracle,
+bit for bit."""
 import numpy as np
 import pytest
 
@@ -13,8 +15,10 @@ from mimic_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
 
-# (E, S, update): rows of 32, 8, 8, 24, 32 bytes (cached), 20 bytes (not cached)
-VC_CASES = [(4, 8, False), (2, 4, False), (1, 8, False), (3, 8, True), (2, 16, True), (5, 4, False), (4, 8, True)]
+# (E, S, update): rows of 32, 8, 8, 24, 32 bytes (registers), 20 and 136 bytes (not cached), 40, 64,
+# 64, 128 bytes (LDS)
+VC_CASES = [(4, 8, False), (2, 4, False), (1, 8, False), (3, 8, True), (2, 16, True), (5, 4, False), (4, 8, True),
+            (10, 4, False), (8, 8, True), (4, 16, False), (16, 8, True), (17, 8, False)]
 
 
 def _vc_prog(E, S, update):
@@ -63,11 +67,15 @@ def _vc_prog(E, S, update):
         A.alu64("mod", 9, E * S + 2),
         A.alu64("add", 0, 9, reg=True),
         A.mov64_reg(1, 8),
-        A.alu64("and", 1, 3),
+        A.alu64("and", 1, 7),
     ]
     for k, n in enumerate((1, 2, 4)):
         items += [A.jmp("jne", 1, k, f"s{k + 1}"), A.ldx(n, 5, 0, 0), A.alu64("add", 5, 8, reg=True),
                   A.stx(n, 0, 0, 5), A.ja("done"), f"s{k + 1}"]
+    # counter increments (4 / 8 bytes, the register dead after: jit.cpp fusable_inc), aligned or not
+    for k, n in ((3, 4), (4, 8)):
+        items += [A.jmp("jne", 1, k, f"s{k + 1}"), A.ldx(n, 4, 0, 0), A.alu64("add", 4, 0x10001 * k),
+                  A.stx(n, 0, 0, 4), A.mov64_imm(5, 0x5eed + k), A.ja("done"), f"s{k + 1}"]
     items += [
         A.ldx(8, 5, 0, 0), A.alu64("add", 5, 8, reg=True), A.stx(8, 0, 0, 5),
         "done",
@@ -99,11 +107,12 @@ def test_lane_value_cache(gpu, case, sched):
 
     E, S, update = VC_CASES[case]
     sc = _vc_scenario(E, S, update)
-    cached = E * S <= 32 and E * S % 8 == 0
+    cached = E * S <= 128 and E * S % 8 == 0
     import os
 
     if os.environ.get("MIMIC_JIT_VC", "1") != "0":
-        assert ("vc_open" in J.kernel_source(*kernel_of(sc))) == cached
+        src = J.kernel_source(*kernel_of(sc))
+        assert ("vc_open(" in src) == cached and ("lvc_open(" in src) == (cached and E * S > 32)
     n = 4096
     buf, off, lens = W.make_packets(n, seed=100 + case)
     rng = np.random.default_rng(case)

@@ -138,14 +138,19 @@ def test_hot_kernels_register_budget(fn, vgprs, waves):
 
 
 def test_lane_value_cache_selection():
-    """The lane value cache is generated only for per-CPU arrays whose row fits four registers."""
+    """The lane value cache is generated for per-CPU arrays whose row is a multiple of 8 bytes: up
+    to 32 bytes in four registers, up to 128 bytes in an LDS slot per lane."""
     from mimic_amd import jit as J
 
     p = W.prog_classifier()
-    assert J.vc_slots([(p.raw, p.relocs)], p.maps) == [(0, 27)]
-    assert "vc_open" in J.kernel_source([p.raw], 0, [(0, 27)])
+    assert J.vc_slots([(p.raw, p.relocs)], p.maps) == [(0, 27, 32)]
+    src = J.kernel_source([p.raw], 0, [(0, 27, 32)])
+    assert "vc_open" in src and "lvc_open" not in src
     assert "vc_open" not in J.kernel_source([p.raw], 0, [])
-    for E, S, ok in [(4, 8, True), (2, 16, True), (1, 8, True), (5, 4, False), (8, 8, False), (3, 4, False)]:
+    lsrc = J.kernel_source([p.raw], 0, [(0, 27, 64)])
+    assert "constexpr uint32_t vcb_ = 64u;" in lsrc and "lvc_open(kp, cget(kp.maps, mh_ - 1u), L.cpu, vcb_," in lsrc and "__shared__ uint32_t lvc_[(64u / 4u + 2u) * 256u]" in lsrc
+    for E, S, ok in [(4, 8, True), (2, 16, True), (1, 8, True), (5, 4, False), (8, 8, True), (16, 8, True), (17, 8, False),
+                     (3, 4, False)]:
         m = dict(p.maps[0], max_entries=E, value_size=S)
         assert (J.vc_slots([(p.raw, p.relocs)], [m]) != []) == ok
     assert J.vc_slots([(p.raw, p.relocs)], [dict(p.maps[0], type=2)]) == []   # a plain array: shared by every lane

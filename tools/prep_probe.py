@@ -21,9 +21,9 @@ for so in sys.argv[1:] + ["norec:" + sys.argv[1]]:
     norec = so.startswith("norec:")
     lib = C.CDLL(so.split(":")[-1])
     f = lib.mimic_skb_prep_only
-    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
     s = torch.cuda.current_stream()
-    args = (d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, None if norec else rec.data_ptr(), prefix.data_ptr(),
+    args = (d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, None if norec else rec.data_ptr(), 12, prefix.data_ptr(),
             state.data_ptr(), C.c_void_p(s.cuda_stream))
     for _ in range(3):
         f(*args)

@@ -16,8 +16,9 @@ def one(spec):
     from mimic_amd import _lib
     from mimic_amd import jit as J
     from mimic_amd import workloads as W
-    progs, _, _ = W.skb_programs()
-    src = J.kernel_source([p.raw for p in progs], _lib.CTX_SKB)
+    progs, maps, _ = W.skb_programs()
+    vc = J.vc_slots([(p.raw, p.relocs) for p in progs], maps) if os.environ.get("VC", "1") == "1" else []
+    src = J.kernel_source([p.raw for p in progs], _lib.CTX_SKB, vc)
     return spec or "default", J.kernel_resources(J.code_object(src))
 
 
