@@ -38,7 +38,7 @@ extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32
                                     hipStream_t st);
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
-                                     uint64_t init_base, uint32_t use_init, hipStream_t st);
+                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, hipStream_t st);
 
 namespace {
 
@@ -1464,8 +1464,10 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     // a batch's derived words go to the compact array (read by skb_load*), a process's into its record
     uint64_t *out = into ? (uint64_t *)into->rec : records ? vm->d_skb_drv : nullptr;
     const uint32_t out_q = into ? (uint32_t)(sizeof(SkbRec) / 8) : SKB_DERIVED_Q;
+    // MIMIC_SKB_ROOMS_CHAIN=1 (measurement, JIT batches only): the chain kernel reads the rooms itself
+    static const bool rooms_chain = getenv("MIMIC_SKB_ROOMS_CHAIN") && getenv("MIMIC_SKB_ROOMS_CHAIN")[0] == '1';
     if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
-                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, st))
+                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : 1u, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;
     vm->skb_stream = st;

@@ -322,6 +322,8 @@ class Gen {
         E.line("#ifdef MIMIC_MEAS_NOPKTST\n#define PKT_ST(p_, n_, v_) ((void)(v_))\n#else\n#define PKT_ST(p_, n_, v_) st_n(p_, n_, v_)\n#endif");
         E.line("#ifdef MIMIC_MEAS_NOATOM\n#define CNT_ADD(p_, n_, v_) ((void)(p_))\n#else\n#define CNT_ADD(p_, n_, v_) atomic_add_n(p_, n_, v_)\n#endif");
         if (spread_on) E.line("#define MIMIC_SPREAD 1");
+        if (const char *rc = getenv("MIMIC_SKB_ROOMS_CHAIN"))   // measurement: see engine.cpp skb_prepare
+            if (rc[0] == '1') E.line("#define MIMIC_SKB_ROOMS_CHAIN 1");
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
         E.line("#define MIMIC_COLD_INLINE %d", cold_inline ? 1 : 0);
         {   // no program of the set updates or deletes: hash tables are read-only in every launch

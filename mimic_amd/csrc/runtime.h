@@ -1078,7 +1078,11 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) d[SKB_DERIVED_Q + q] = skb_writable_word(q);
     L.pkt = kp.pkt_data + po;
+#ifdef MIMIC_SKB_ROOMS_CHAIN   // measurement: the rooms read here (engine.cpp skb_prepare)
+    return skb_attach(kp, L, i, r1, d, (uint32_t)w[0], pre, base, -1);
+#else
     return skb_attach(kp, L, i, r1, d, (uint32_t)w[0], pre, base, (int)((w[SKB_DIRTY_Q] >> SKB_DIRTY_SHIFT) & 1u));
+#endif
 }
 
 // skb_load for a JIT kernel that builds the record itself (no prep records: a 160-byte write and

@@ -68,7 +68,8 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, uint64_t *__restrict__ rec,
-                                                                          uint32_t rec_q, uint64_t *__restrict__ prefix) {
+                                                                          uint32_t rec_q, uint64_t *__restrict__ prefix,
+                                                                          uint32_t rooms) {
     __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
     __shared__ uint64_t wtot[PREP_T / 64];
     uint32_t *win = (uint32_t *)area;
@@ -100,12 +101,15 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
         skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
 #endif
         // the rooms flag (skb.h SKB_DIRTY_Q): any non-zero byte in the 32 bytes before the packet
-        // or the 64 after it
-        const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
-        u32x4u o = hr[0] | hr[1];
+        // or the 64 after it (rooms = 0: a measurement build whose JIT kernel reads them itself)
+        r.ip[0].pad[0] = 0;
+        if (rooms) {
+            const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
+            u32x4u o = hr[0] | hr[1];
 #pragma unroll
-        for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) o |= tr[c];
-        r.ip[0].pad[0] = (o.x | o.y | o.z | o.w) ? 1u : 0u;
+            for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) o |= tr[c];
+            r.ip[0].pad[0] = (o.x | o.y | o.z | o.w) ? 1u : 0u;
+        }
         f = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
     if (rec) {
@@ -196,7 +200,7 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
                                    uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state, hipStream_t st) {
     hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                       rec, rec_q, prefix);
+                       rec, rec_q, prefix, 1u);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        0ull, 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -205,10 +209,10 @@ extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_
 // prefix: n + ceil(n / 256) words; state: 2 words
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
-                                     uint64_t init_base, uint32_t use_init, hipStream_t st) {
+                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, hipStream_t st) {
     if (n)
         hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                           rec, rec_q, prefix);
+                           rec, rec_q, prefix, rooms);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        init_base, use_init);
     return hipGetLastError() == hipSuccess ? 0 : -1;
