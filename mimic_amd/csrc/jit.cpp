@@ -110,6 +110,8 @@ class Gen {
         if (ka) karg = atoi(ka);
         const char *nr = getenv("MIMIC_JIT_NTRES");   // 0: per-packet results stored as plain stores
         ntres = !(nr && nr[0] == '0');
+        const char *cbv = getenv("MIMIC_JIT_COMBINE");
+        combine_knob = !(cbv && cbv[0] == '0');
         const char *dnr = getenv("MIMIC_JIT_DEFER_NOREGS");
         defer_noregs = dnr ? atoi(dnr) : 0;
         const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
@@ -200,6 +202,8 @@ class Gen {
     bool window = true;        // MIMIC_JIT_WINDOW=0: no windowed early loads
     int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
     int defer_noregs = 0;   // MIMIC_JIT_DEFER_NOREGS=1: deferral sites store no registers, 2: low halves (register census only)
+    bool combine_knob = true;  // MIMIC_JIT_COMBINE=0: every wave reserves freelist positions with its own add
+    bool hash_combine = false;
     bool ntres = true;         // MIMIC_JIT_NTRES=0: r0 / status stores not non-temporal (measured 1-3 % slower)
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
@@ -340,6 +344,10 @@ class Gen {
                 for (uint32_t i = 0; i < p.n; i++)
                     if (AUX_H(p.ins[i].aux) == H_CALL && (uint32_t)p.ins[i].k == 3) deletes = true;
             E.line("#define MIMIC_HASH_POPONLY %d", deletes ? 0 : 1);
+            // inline inserts of a pop-only kernel: the block's waves combine their freelist
+            // reservations (hashmap.h h_comb_reserve); zeroed in the prologue
+            hash_combine = combine_knob && writes && !deletes && cold_inline && fast_paths;
+            if (hash_combine) E.line("#define MIMIC_HASH_COMBINE 1");
         }
         E.line("#include \"runtime.h\"");
         if (spread_on) {
@@ -405,6 +413,7 @@ class Gen {
         }
         E.line("  const KParams &kp = *kpp;");
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
+        if (hash_combine) E.line("  h_comb_init();   // before any thread of the block can leave");
         if (!spread_on) E.line("  if (g >= kp.lanes) return;");
         if (stage && fast_paths) {
             E.line("  __shared__ PWin pwin_;");

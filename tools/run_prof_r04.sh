@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 end, part 1: PMC passes (kernel trace, FETCH_SIZE, WRITE_SIZE, read requests by size, SQ)
+# of every bench line's kernel at HEAD; summaries under gpurun_out/prof_r04final, copied into
+# profiles/ before part 2 (tools/run_final_r04.sh) so the lines carry their traffic.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+T=r04final
+for c in classifier parse5 flowtrack flowtrack_insert skb; do
+  CFG=$c TAG=$T timeout -k 10 600 bash tools/profile.sh || { echo "profile $c failed"; exit 1; }
+  tail -1 gpurun_out/prof_$T/summary_$c.log | cut -c1-300
+done
+CFG=classifier NAME=classifier_v256 EXTRA="--vcpus 256" SUMMARY_ARGS="--vcpus 256 --spread" TAG=$T timeout -k 10 600 bash tools/profile.sh || exit 1
