@@ -91,7 +91,10 @@ HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, ui
     uint64_t b0;
     uint32_t g0;
     if (off == 0) {   // the batch's opener
-        __builtin_amdgcn_s_sleep(2);
+#ifndef MIMIC_HCOMB_SLEEP
+#define MIMIC_HCOMB_SLEEP 2
+#endif
+        __builtin_amdgcn_s_sleep(MIMIC_HCOMB_SLEEP);
         const unsigned long long closed = __hip_atomic_exchange(&cb.word, (unsigned long long)(gen + 1u) << 32, __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint32_t total = (uint32_t)closed;
@@ -446,6 +449,11 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
         }
         const bool mine = !done && !blocked && cand != HT_EMPTY &&
                           h_cas(h_rec(t, cand), cw, ((uint64_t)tag << 32) | HT_BUSY);
+        if (mine) {   // the key words go out now: their completion overlaps the reservation's round trip
+            uint64_t *r = h_rec(t, cand);
+            const uint32_t nq = (t.K + 7) >> 3;
+            for (uint32_t q = 0; q < nq; q++) h_st(r + 1 + q, ks.word(q));
+        }
         const uint64_t needm = __ballot(mine);
         int32_t slot = -1;
         if (needm) {
@@ -494,15 +502,15 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
         if (mine) {
             uint64_t *r = h_rec(t, cand);
             if (slot >= 0) {
-                const uint32_t nq = (t.K + 7) >> 3;
-                for (uint32_t q = 0; q < nq; q++) h_st(r + 1 + q, ks.word(q));
-                h_drain();
+                h_drain();   // the key words (written above) before the record goes live
                 h_st(r, ((uint64_t)tag << 32) | (uint32_t)slot);
                 empty_used = (uint32_t)cw == HT_EMPTY;
                 idx = slot;
                 *inserted = true;
             } else {
-                h_st(r, cw);   // the freelist is spent: E2BIG, the bucket as it was
+                // the freelist is spent: E2BIG, the bucket as it was (the key words it holds now are
+                // never compared: only a live record's are)
+                h_st(r, cw);
                 idx = -1;
             }
             done = true;

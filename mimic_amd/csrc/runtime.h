@@ -1303,18 +1303,7 @@ DEV int tail_fast(const KParams &kp, const Lane &L, uint32_t mid, uint64_t r2, u
     if (r2 != (uint64_t)m.obj_addr || m.type != MIMIC_MAP_PROG_ARRAY || m.key_size != 4 || m.family != FAM_ARRAY ||
         m.value_size < 4 || (uint32_t)r3 >= m.max_entries)
         return -2;
-#ifdef MIMIC_MEAS_PASCALAR   // measurement only: the slot through the scalar cache (stale if a program writes it)
-    uint32_t pa = 0;
-    {
-        const uint32_t u_ = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r3);
-        if (__builtin_amdgcn_ballot_w64((uint32_t)r3 == u_) == __builtin_amdgcn_read_exec())
-            pa = cget((const uint32_t *)array_value_ptr(kp, m, -1, 0), u_);
-        else
-            pa = *(const GAS u32u *)array_value_ptr(kp, m, -1, (uint32_t)r3);
-    }
-#else
     const uint32_t pa = *(const GAS u32u *)array_value_ptr(kp, m, -1, (uint32_t)r3);
-#endif
     if (kp.nprogs <= 16) {   // program entries [addr, addr + 8]: compare against each (uniform loads)
         for (uint32_t k = 0; k < kp.nprogs; k++)
             if (pa - cget(kp.progs, k).addr <= 8u) return (int)k;
