@@ -148,5 +148,40 @@ def test_lane_value_cache_classifier_many_packets_per_vcpu(gpu):
 
 def jit_kernels():
     p = W.prog_classifier()
-    return [kernel_of(_vc_scenario(*c)) for c in VC_CASES] + \
+    ks = [kernel_of(_vc_scenario(*c)) for c in VC_CASES] + \
         [kernel_of(Scenario(vcpus=1, maps=p.maps, progs=[(p.name, p.raw, p.relocs)]))]
+    for E, S in ((8, 8), (16, 8)):
+        b = _vc_scenario(E, S, True)
+        ks.append(kernel_of(Scenario(vcpus=b.vcpus, maps=b.maps, progs=[_padded(b.progs[0])], map_init=b.map_init)))
+    return ks
+
+
+def _padded(prog, pad=60):
+    """The program with `pad` stack loads in front (r9 = the stack word at R10 - 8, overwritten
+    by the program later): past the JIT's 48 memory / helper sites, so its kernel defers every
+    slow path to the interpreter's resume kernel (jit.cpp defer_mode)."""
+    name, raw, rel = prog
+    pre, _ = A.assemble([A.ldx(8, 9, 10, -8)] * pad)
+    return (name, pre + raw, [(s + pad, m) for s, m in rel])
+
+
+@pytest.mark.parametrize("E,S", [(8, 8), (16, 8)])
+def test_lds_row_cache_with_deferred_slow_paths(gpu, E, S):
+    """The LDS row cache in a kernel that defers its slow paths: map_update on the cached map and
+    accesses past the row defer the lane; the row is written back once at the deferral exit, so
+    the resume kernel (interpreter) continues on the counters the JIT lane left."""
+    from mimic_amd import jit as J
+
+    base = _vc_scenario(E, S, True)
+    sc = Scenario(vcpus=base.vcpus, maps=base.maps, progs=[_padded(base.progs[0])], map_init=base.map_init)
+    src = J.kernel_source(*kernel_of(sc))
+    assert "lvc_open(" in src and "DFR(" in src and "L_defer:\n    VC_FLUSH();" in src
+    n = 4096
+    buf, off, lens = W.make_packets(n, seed=300 + E)
+    cpu = W.schedule_cpu(n, 8, "interleaved")
+    import mimic_amd as M
+
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, None, schedule=M.SCHED_INTERLEAVED, spread=0)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
