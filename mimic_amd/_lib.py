@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmimic_amd.so")
+# MIMIC_LIB=<file name>: another in-tree build of the same sources (measurement builds, A/B runs)
+LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("MIMIC_LIB", "libmimic_amd.so")))
 
 ABI_VERSION = 1
 
