@@ -163,35 +163,19 @@ HDEV bool h_key_eq(const uint64_t *r, const KS &ks, uint32_t K) {
 // launches (no program of the launch deletes): a bucket then only moves EMPTY / TOMB -> BUSY ->
 // live (or BUSY back, on E2BIG) and a live record never changes, so the state word's re-read that
 // guards against a concurrent delete + reuse is not needed (one memory round trip per hit less)
-//
-// The probe reads the state words of HT_WIN consecutive buckets at once (one round trip for a walk
-// that ends within them: at the tables' <= 1/2 load an unsuccessful linear probe visits ~2.2
-// buckets on average) and then goes through them in order.  The words are read at slightly
-// different times; states only move forward during a launch that inserts (EMPTY / TOMB -> BUSY ->
-// live; a delete turns live into TOMB), so the in-order walk over them is the walk made at the time
-// its deciding word was read -- what the one-word-at-a-time probe could have seen.
-#ifndef HT_WIN
-#define HT_WIN 2u
-#endif
 template <class KS>
 HDEV int32_t h_find(const HT &t, const KS &ks, uint64_t h, uint32_t *pos, bool recheck = true) {
     const uint32_t mask = t.cap - 1, tag = (uint32_t)(h >> 32);
     uint32_t p = (uint32_t)h & mask;
-    for (uint32_t n = 0; n < t.cap; n += HT_WIN) {
-        uint64_t w[HT_WIN];
-#pragma unroll
-        for (uint32_t j = 0; j < HT_WIN; j++) w[j] = h_ld(h_rec(t, (p + j) & mask));
-#pragma unroll
-        for (uint32_t j = 0; j < HT_WIN; j++) {
-            const uint32_t q = (p + j) & mask, s = (uint32_t)w[j];
-            const uint64_t *r = h_rec(t, q);
-            if (s == HT_EMPTY) return -1;
-            if (s < HT_BUSY && (uint32_t)(w[j] >> 32) == tag && h_key_eq(r, ks, t.K) && (!recheck || h_ld(r) == w[j])) {
-                if (pos) *pos = q;
-                return (int32_t)s;
-            }
+    for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+        const uint64_t *r = h_rec(t, p);
+        const uint64_t w = h_ld(r);
+        const uint32_t s = (uint32_t)w;
+        if (s == HT_EMPTY) return -1;
+        if (s < HT_BUSY && (uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K) && (!recheck || h_ld(r) == w)) {
+            if (pos) *pos = p;
+            return (int32_t)s;
         }
-        p = (p + HT_WIN) & mask;
     }
     return -1;
 }
@@ -435,41 +419,32 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
         uint32_t cand = HT_EMPTY;
         uint64_t cw = 0;
         bool blocked = false;
-        if (!done) {   // the walk, HT_WIN state words per round trip (see h_find)
+        if (!done) {
             uint32_t p = (uint32_t)h & mask;
-            bool end = false;
-            for (uint32_t n = 0; n < t.cap && !end; n += HT_WIN) {
-                uint64_t ww[HT_WIN];
-#pragma unroll
-                for (uint32_t j = 0; j < HT_WIN; j++) ww[j] = h_ld(h_rec(t, (p + j) & mask));
-#pragma unroll
-                for (uint32_t j = 0; j < HT_WIN; j++) {
-                    if (end) break;
-                    const uint32_t q = (p + j) & mask;
-                    const uint64_t w = ww[j];
-                    const uint32_t s = (uint32_t)w;
-                    if (s == HT_EMPTY || s == HT_TOMB) {
-                        if (cand == HT_EMPTY) {
-                            cand = q;
-                            cw = w;
-                        }
-                        if (s == HT_EMPTY) end = true;
-                        continue;
+            for (uint32_t n = 0; n < t.cap; n++, p = (p + 1) & mask) {
+                const uint64_t *r = h_rec(t, p);
+                const uint64_t w = h_ld(r);
+                const uint32_t s = (uint32_t)w;
+                if (s == HT_EMPTY || s == HT_TOMB) {
+                    if (cand == HT_EMPTY) {
+                        cand = p;
+                        cw = w;
                     }
-                    if (s == HT_BUSY) {
-                        if (cand == HT_EMPTY) {   // before any reusable bucket: possibly this key
-                            blocked = true;
-                            end = true;
-                        }
-                        continue;
-                    }
-                    if ((uint32_t)(w >> 32) == tag && h_key_eq(h_rec(t, q), ks, t.K)) {
-                        idx = (int32_t)s;
-                        done = true;
-                        end = true;
-                    }
+                    if (s == HT_EMPTY) break;
+                    continue;
                 }
-                p = (p + HT_WIN) & mask;
+                if (s == HT_BUSY) {
+                    if (cand == HT_EMPTY) {   // before any reusable bucket: possibly this key
+                        blocked = true;
+                        break;
+                    }
+                    continue;
+                }
+                if ((uint32_t)(w >> 32) == tag && h_key_eq(r, ks, t.K)) {
+                    idx = (int32_t)s;
+                    done = true;
+                    break;
+                }
             }
         }
         const bool mine = !done && !blocked && cand != HT_EMPTY &&
