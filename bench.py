@@ -293,7 +293,9 @@ def host_resident_rate(vm, pid, wl, sched, chunks: int = 0, reps: int = 5):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 100 timed steps: the barrier + synchronize around the region cost ~35 us once, 6 % of 20
+    # cfg-2 steps (26 us each) but 1 % of 100
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="classifier", choices=sorted(CONFIGS))
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")

@@ -32,7 +32,8 @@ def _fuzz(seed):
 def jit_kernels():
     ps = [W.prog_flowtrack(), W.prog_flowcount(), W.prog_flowcount(delete_every=3), W.prog_flowcount(delete_every=1),
           _prog_lookup40()]
-    return [kernel_of(_sc(p, 1)) for p in ps] + [kernel_of(_fuzz(s)[0]) for s in range(12)]
+    return [kernel_of(_sc(p, 1)) for p in ps] + [kernel_of(_fuzz(s)[0]) for s in range(12)] + \
+        [kernel_of(_sc(_prog_two_maps(), 1))]
 
 
 # Two 40-byte keys with the same first 32 bytes whose hashes (hashmap.h h_hash) share the 32-bit
@@ -363,3 +364,41 @@ def test_pop_only_launch_after_host_deletes_pops_the_pushed_slots(gpu):
     assert fm.Values(0) == ovm.map_values(om, 0)
     vm.close()
     ovm.close()
+
+
+def _prog_two_maps(E=4096):
+    """Insert-if-absent of the packet's 5-tuple into map "fa", then of the key with its first word
+    flipped into map "fb" (values: functions of the key) -- two tables whose inserting waves share
+    the block combiner's LDS (hashmap.h h_comb_reserve, one combiner per map)."""
+    from mimic_amd import asm as A
+
+    def ins(m, nxt):
+        return [A.mov64_reg(2, 10), A.alu64("add", 2, -16), A.ld_map_fd(1, m), A.call(A.FN_MAP_LOOKUP_ELEM),
+                A.jmp("jne", 0, 0, nxt),
+                A.ldx(8, 1, 10, -16), A.ldx(8, 4, 10, -8), A.alu64("mul", 1, 0x01000193), A.alu64("xor", 1, 4, reg=True),
+                A.stx(8, 10, -24, 1), A.mov64_reg(2, 10), A.alu64("add", 2, -16), A.mov64_reg(3, 10),
+                A.alu64("add", 3, -24), A.ld_map_fd(1, m), A.mov64_imm(4, 1), A.call(A.FN_MAP_UPDATE_ELEM),
+                A.jmp("jne", 0, 0, "full")]
+    items = W._flow_key_items() + ins("fa", "b") + ["b", A.ldx(4, 1, 10, -16), A.alu32("xor", 1, 0x5A5A5A5A),
+                                                     A.stx(4, 10, -16, 1)] + ins("fb", "done") + [
+        "done", A.mov64_imm(0, 2), A.exit_(), "full", A.mov64_imm(0, 7), A.exit_(), "out", A.mov64_reg(0, 7), A.exit_()]
+    raw, rel = A.assemble(items)
+    maps = [dict(name=n, type=1, key_size=16, value_size=8, max_entries=E) for n in ("fa", "fb")]
+    return W.Program("twomaps", raw, rel, maps)
+
+
+@pytest.mark.parametrize("V", [1, 512])
+def test_two_hash_maps_inserted_by_one_program(gpu, V):
+    """One program inserting into two shared hash maps, one vCPU (slots exact, FIFO) and 512 vCPUs
+    (per key exact): each map's reservations stay with its own freelist."""
+    p = _prog_two_maps()
+    sc = _sc(p, V)
+    n = 20000
+    buf, off, lens = W.make_packets(n, **W.IMIX, seed=17)
+    cpu = np.zeros(n, dtype=np.int32) if V == 1 else W.schedule_cpu(n, V, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu)
+    if V == 1:
+        assert_same(o, e)
+    else:
+        assert_same(o, e, check_pkt=False, hash_exact=False, check_steps=False)
