@@ -33,7 +33,7 @@ def jit_kernels():
     ps = [W.prog_flowtrack(), W.prog_flowcount(), W.prog_flowcount(delete_every=3), W.prog_flowcount(delete_every=1),
           _prog_lookup40()]
     return [kernel_of(_sc(p, 1)) for p in ps] + [kernel_of(_fuzz(s)[0]) for s in range(12)] + \
-        [kernel_of(_sc(_prog_two_maps(), 1))]
+        [kernel_of(_sc(_prog_two_maps(), 1)), kernel_of(_sc(_prog_two_maps(32768), 512))]
 
 
 # Two 40-byte keys with the same first 32 bytes whose hashes (hashmap.h h_hash) share the 32-bit
@@ -389,9 +389,10 @@ def _prog_two_maps(E=4096):
 
 @pytest.mark.parametrize("V", [1, 512])
 def test_two_hash_maps_inserted_by_one_program(gpu, V):
-    """One program inserting into two shared hash maps, one vCPU (slots exact, FIFO) and 512 vCPUs
-    (per key exact): each map's reservations stay with its own freelist."""
-    p = _prog_two_maps()
+    """One program inserting into two shared hash maps, one vCPU (slots exact, FIFO, E2BIG for the
+    flows past E = 4096) and 512 vCPUs (per key exact, E = 32 768 so that no flow is refused): each
+    map's reservations stay with its own freelist."""
+    p = _prog_two_maps(4096 if V == 1 else 32768)   # concurrent: no E2BIG (which flows get it is order-dependent)
     sc = _sc(p, V)
     n = 20000
     buf, off, lens = W.make_packets(n, **W.IMIX, seed=17)
