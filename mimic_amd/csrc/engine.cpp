@@ -34,6 +34,8 @@ extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st);
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
 extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st);
+extern "C" int mimic_launch_spread_reduce(const void *part, uint32_t nblocks, uint32_t lanes, uint32_t roww, uint32_t n,
+                                          uint8_t *dst, uint64_t stride, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
@@ -134,6 +136,8 @@ struct mimic_vm {
     hipFunction_t jit_fn_spread = nullptr;
     JitInfo jit_info_spread{};
     uint32_t *d_spread_bad = nullptr;
+    void *d_spread_part = nullptr;   // spread launches: the blocks' counter tables (mimic_spread_reduce_kernel)
+    uint64_t spread_part_cap = 0;
     bool spread_used = false;
     // host map operations staged for the device (flush_host): value / array writes, deduplicated
     // per arena offset (a later write to the same bytes replaces the earlier one)
@@ -626,6 +630,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_sched_pkts);
     hipFree(vm->d_lane_steps);
     hipFree(vm->d_spread_bad);
+    hipFree(vm->d_spread_part);
     hipFree(vm->d_defer);
     hipFree(vm->d_defer_any);
     hipFree(vm->d_kp);
@@ -1495,10 +1500,20 @@ static PrivPlan priv_plan(const mimic_vm *vm) {
 // set: the VM's per-CPU arrays whose values the arena keeps 8-byte aligned are the candidates; the
 // analysis names the one map the programs count into, and the kernel is then generated with an
 // LDS counter table when a block's rows fit 32 KiB.
+// packets per spread block (MIMIC_SPREAD_PPB, measurement: a multiple of 256; default 1024)
+static uint32_t spread_ppb() {
+    static const uint32_t v = [] {
+        const char *e = getenv("MIMIC_SPREAD_PPB");
+        const uint32_t x = e ? (uint32_t)atoi(e) : 0u;
+        return x >= 256 && x % 256 == 0 ? x : 1024u;
+    }();
+    return v;
+}
 static int spread_build(mimic_vm *vm) {
     if (vm->spread_state) return 0;
     vm->spread_state = -1;
     SpreadReq req;
+    req.ppb = spread_ppb();
     for (size_t s = 0; s < vm->h_all.size(); s++) {
         const DInsn &x = vm->h_all[s];
         const uint32_t mh = AUX_MAPHINT(x.aux);
@@ -1754,8 +1769,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     hipFunction_t jfn = spread ? vm->jit_fn_spread : vm->jit_fn[ctx];
     uint32_t run_lanes = lanes;
     if (spread) {
-        const SpreadReq sr0;
-        const uint32_t blocks = (uint32_t)(((uint64_t)b->n + sr0.ppb - 1) / sr0.ppb);
+        const uint32_t blocks = (uint32_t)(((uint64_t)b->n + spread_ppb() - 1) / spread_ppb());
         run_lanes = blocks * 256u;
         rc = priv_ensure(vm, q_per_lane, run_lanes, st);   // private memory (stack ...) per spread lane
         if (rc) return rc;
@@ -1776,6 +1790,22 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.lane_steps = vm->d_lane_steps;
         kp.spread_bad = vm->d_spread_bad;
         vm->spread_used = true;
+        // an LDS table that covers every lane and has no more counters than a block has packets
+        // (dense): the blocks' tables go to a buffer and one reduce kernel adds them into the map
+        // (jit.cpp spread flush).  Sparser tables keep one agent-scope add per non-zero counter.
+        kp.spread_part = nullptr;
+        if (ji.spread_rows && ji.spread_rows == cpu_lanes && ji.spread_n &&
+            (uint64_t)cpu_lanes * ji.spread_roww <= spread_ppb()) {
+            const uint64_t need = (uint64_t)blocks * ji.spread_rows * ji.spread_roww * ji.spread_n;
+            if (need > vm->spread_part_cap) {
+                HIP_OK(vm, hipStreamSynchronize(st));
+                hipFree(vm->d_spread_part);
+                vm->d_spread_part = nullptr;
+                HIP_OK(vm, hipMalloc(&vm->d_spread_part, need));
+                vm->spread_part_cap = need;
+            }
+            kp.spread_part = vm->d_spread_part;
+        }
     }
     kp.skb_rec_built = 1;
     if (skb && step && step->skb_rec) {   // a stepped sk_buff process: Load ran at NewProcess
@@ -1859,6 +1889,12 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));   // the slot is free again once this passes
         vm->kp_used[slot] = true;
+    }
+    if (jit && kp.spread_part) {   // a spread launch's block counter tables into the map
+        const DMap dm = to_dmap(vm->maps[ji.spread_map]);
+        if (mimic_launch_spread_reduce(kp.spread_part, kp.lanes / 256u, kp.cpu_lanes, ji.spread_roww, ji.spread_n,
+                                       vm->arena + dm.dev_off + (uint64_t)kp.vcpu_begin * dm.dev_stride, dm.dev_stride, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
     vm->last_lanes = run_lanes;
     vm->last_stream = st;

@@ -617,6 +617,40 @@ extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStrea
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Spread launches whose LDS table covers every vCPU lane (jit.cpp, spread flush): each block left
+// its counters in part[block][lane][counter]; thread (w, g) sums counter w over group g's blocks and
+// adds the sum into the map with one agent-scope add (groups of blocks, so the reads of a thread are
+// independent and few: nblocks / G each).  dst: the map's row of lane 0; lanes `stride` bytes apart.
+template <typename T>
+__global__ __launch_bounds__(256) void spread_reduce_kernel(const T *__restrict__ part, uint32_t nblocks, uint32_t words,
+                                                            uint32_t roww, uint32_t groups, uint8_t *dst, uint64_t stride) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)words * groups) return;
+    const uint32_t w = (uint32_t)(t % words), g = (uint32_t)(t / words);
+    const uint32_t per = (nblocks + groups - 1) / groups, b0 = g * per, b1 = b0 + per < nblocks ? b0 + per : nblocks;
+    T s = 0;
+    for (uint32_t b = b0; b < b1; b++) s += part[(size_t)b * words + w];
+    if (!s) return;
+    const uint32_t lane = w / roww, q = w - lane * roww;
+    __hip_atomic_fetch_add((T *)(dst + (size_t)lane * stride) + q, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+extern "C" int mimic_launch_spread_reduce(const void *part, uint32_t nblocks, uint32_t lanes, uint32_t roww, uint32_t n,
+                                          uint8_t *dst, uint64_t stride, hipStream_t st) {
+    const uint32_t words = lanes * roww;
+    if (!words || !nblocks) return 0;
+    uint32_t groups = (65536u + words - 1) / words;   // ~64 K threads
+    if (groups > nblocks) groups = nblocks;
+    const uint64_t threads = (uint64_t)words * groups;
+    const dim3 grid((uint32_t)((threads + 255) / 256));
+    if (n == 8)
+        hipLaunchKernelGGL(spread_reduce_kernel<uint64_t>, grid, dim3(256), 0, st, (const uint64_t *)part, nblocks, words, roww,
+                           groups, dst, stride);
+    else
+        hipLaunchKernelGGL(spread_reduce_kernel<uint32_t>, grid, dim3(256), 0, st, (const uint32_t *)part, nblocks, words, roww,
+                           groups, dst, stride);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st) {
     if (hipMemsetAsync(out, 0, (size_t)nvals * 8, st) != hipSuccess) return -1;

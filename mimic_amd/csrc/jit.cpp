@@ -655,8 +655,20 @@ class Gen {
         if (spread_on) {
             // the block's counters into the map: one agent-scope add per non-zero counter (a row's
             // counters are contiguous in the arena, so consecutive threads add consecutive words)
-            E.line("#if SPREAD_ROWS");
+            E.line("#if SPREAD_ROWS && !defined(MIMIC_MEAS_NOFLUSH)   // (measurement knob: no flush, counters wrong)");
             E.line("  __syncthreads();");
+            // a table that covers every vCPU lane (V <= packets per block): the block writes it,
+            // rotated to absolute lanes, into its slice of kp.spread_part with plain stores, and
+            // mimic_spread_reduce_kernel adds the blocks' slices into the map (one agent-scope add per
+            // counter per group of blocks, not per block: the per-block adds were 43 % of the kernel)
+            E.line("  if (kp.spread_part && kp.cpu_lanes == SPREAD_ROWS) {");
+            E.line("    spread_t *pt_ = (spread_t *)kp.spread_part + (size_t)blockIdx.x * (SPREAD_ROWS * SPREAD_ROWW);");
+            E.line("    for (uint32_t w_ = threadIdx.x; w_ < SPREAD_ROWS * SPREAD_ROWW; w_ += 256u) {");
+            E.line("      const uint32_t r_ = w_ / SPREAD_ROWW, q_ = w_ - r_ * SPREAD_ROWW;");
+            E.line("      const uint32_t lr_ = lam0_ + r_ < SPREAD_ROWS ? lam0_ + r_ : lam0_ + r_ - SPREAD_ROWS;");
+            E.line("      pt_[lr_ * SPREAD_ROWW + q_] = sacc_[w_];");
+            E.line("    }");
+            E.line("  } else");
             E.line("  for (uint32_t w_ = threadIdx.x; w_ < SPREAD_ROWS * SPREAD_ROWW; w_ += 256u) {");
             E.line("    const spread_t v_ = sacc_[w_];");
             E.line("    if (!v_) continue;");
@@ -2015,6 +2027,10 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->skb_walk = g.skb_walk;
         info->karg = g.karg != 0;
         info->spread = g.spread_on;
+        info->spread_map = g.spread_map;
+        info->spread_n = g.spread_n;
+        info->spread_roww = g.spread_n ? g.spread_row / g.spread_n : 0;
+        info->spread_rows = g.spread_on && spread ? spread->lds_rows : 0;
     }
     return src;
 }

@@ -19,6 +19,8 @@ struct JitInfo {
     bool defer;          // slow paths are deferred to the interpreter's resume kernel (launch it after)
     bool skb_walk;       // sk_buff kernel that builds its SkbRecs itself (prep: footprints only)
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
+    // spread kernels: the counted per-CPU array, counter width, counters per row, LDS table rows
+    uint32_t spread_map, spread_n, spread_roww, spread_rows;
 };
 // What a spread kernel may be built for (jit.cpp analyze_spread): the VM's per-CPU arrays.
 struct SpreadReq {

@@ -221,6 +221,9 @@ struct KParams {
     // sk_buff batches: the prep kernel's derived record words, SKB_DERIVED_Q per packet with no gaps
     // (skb.hip), or null (a stepped process's own record holds them)
     const uint64_t *skb_drv;
+    // spread launches with an LDS table covering every vCPU lane: each block's table goes here,
+    // [block][lane][counter], summed into the map by mimic_spread_reduce_kernel (interp.hip)
+    void *spread_part;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its
