@@ -1220,14 +1220,14 @@ int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
     if ((rc = skb_settle(vm)) || (rc = flush_host(vm))) return rc;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
     if (vm->last_stream && vm->last_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
-    HIP_OK(vm, hipMemsetAsync(vm->arena + m.dev_off, 0, (size_t)m.dev_stride * m.ncpu, st));
-    if (is_hash(m)) {
+    if (is_hash(m)) {   // one kernel: values, keys, index (interp.hip mimic_hash_reset_kernel)
         m.pop_dirty = false;
-        HIP_OK(vm, hipMemsetAsync(vm->arena + m.keys_dev_off, 0, (size_t)m.max_entries * m.key_size, st));
         const DMap dm = to_dmap(m);
         if (mimic_launch_hash_reset(vm->arena, &dm, st))
             return fail(vm, MIMIC_EDEVICE, "reset: %s", hipGetErrorString(hipGetLastError()));
         mirror_fresh(m);   // the image of the table the reset leaves
+    } else {
+        HIP_OK(vm, hipMemsetAsync(vm->arena + m.dev_off, 0, (size_t)m.dev_stride * m.ncpu, st));
     }
     vm->last_stream = st;
     return 0;
