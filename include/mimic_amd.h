@@ -41,6 +41,8 @@ extern "C" {
 #define MIMIC_ENOTSUP (-4)
 #define MIMIC_ENOENT (-5)
 #define MIMIC_EFAULT (-6)
+#define MIMIC_ECANCELED (-7)   /* mimic_process_run_ctx: the context was canceled ("context canceled") */
+#define MIMIC_EDEADLINE (-8)   /* mimic_process_run_ctx: its deadline passed ("context deadline exceeded") */
 
 /* Per-process status classes (one byte per packet).  Same numbering as the oracle. */
 enum mimic_status {
@@ -72,7 +74,9 @@ enum mimic_status {
     MIMIC_ERR_NO_CPU = 25,
     MIMIC_ERR_CTX_ACCESS = 26,       /* __sk_buff / bpf_sock / bpf_flow_keys field error, emulator_linux_sk_buff.go */
     MIMIC_PANIC_SLICE = 27,          /* Go slice-bounds panic in those accessors */
-    MIMIC_ERR_CTX_LOAD = 28          /* Context.Load failed (SKBuffFromBytes error, out of address space) */
+    MIMIC_ERR_CTX_LOAD = 28,         /* Context.Load failed (SKBuffFromBytes error, out of address space) */
+    MIMIC_ERR_CANCELED = 29,         /* Run's ctx was canceled: ctx.Err() = context.Canceled (vm.go:344-350) */
+    MIMIC_ERR_DEADLINE = 30          /* Run's ctx deadline passed: context.DeadlineExceeded (vm.go:344-350) */
 };
 
 /* Linux map types (ebpf.MapType). */
@@ -303,6 +307,38 @@ int mimic_process_step(mimic_process *p, uint32_t n, mimic_process_regs *out);
 /* Process.Run (vm.go:343-360): Step until exit / fatal error, or `budget` more steps (0 = the
  * default budget; a suspended process can be run or stepped again). */
 int mimic_process_run(mimic_process *p, uint64_t budget, mimic_process_regs *out);
+/* ---- Run(ctx): cancellation and deadlines (vm.go:343-360) ----------------------------------------
+ * The reference's Run checks ctx.Done() before every step and returns ctx.Err() once it is closed;
+ * a process pool job whose context is done before it starts is handed off with ctx.Err()
+ * (vm.go:548-573).  A mimic_ctx is that context: context.WithCancel(context.Background()) when
+ * timeout_ns = 0, else context.WithTimeout(.., timeout_ns) (a host timer marks it at the deadline).
+ * It is a word in pinned, device-mapped host memory that running kernels read: a batch given
+ * contexts checks packet i's context before its process's first step -- a done one ends the process
+ * there with MIMIC_ERR_CANCELED / MIMIC_ERR_DEADLINE, 0 steps, R0 = 0, err_pc = 0, its context Load
+ * done (xdp_md rooms zeroed, sk_buff entries leaked), as Run(ctx) on a done context after NewProcess.
+ * A process already running finishes (or meets its step budget): cancellation is seen per process
+ * in a batch, per launch slice in mimic_process_run_ctx.  Free a context only after the runs that use
+ * it completed. */
+typedef struct mimic_ctx mimic_ctx;
+int mimic_ctx_new(uint64_t timeout_ns, mimic_ctx **out);
+/* the CancelFunc: Err() becomes context.Canceled, unless the context is done already */
+void mimic_ctx_cancel(mimic_ctx *c);
+/* ctx.Err(): 0 = nil, 1 = context.Canceled, 2 = context.DeadlineExceeded */
+int mimic_ctx_err(const mimic_ctx *c);
+/* 1 when the word is device-visible (made with a device present; runs refuse other contexts) */
+int mimic_ctx_pinned(const mimic_ctx *c);
+void mimic_ctx_free(mimic_ctx *c);
+/* mimic_run_xdp / mimic_run_skb with contexts: ctx for every packet, or ctx_per_packet = HOST array
+ * [n] of contexts (NULL entries: context.Background()); not both.  NULL and NULL = the plain call. */
+int mimic_run_xdp_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch, const mimic_xdp_results *results,
+                      void *hip_stream, mimic_ctx *ctx, mimic_ctx *const *ctx_per_packet);
+int mimic_run_skb_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *batch, const mimic_xdp_results *results,
+                      void *hip_stream, mimic_ctx *ctx, mimic_ctx *const *ctx_per_packet);
+/* Process.Run(ctx) (vm.go:343-360): as mimic_process_run, the context checked between launch
+ * slices; a done context returns MIMIC_ECANCELED / MIMIC_EDEADLINE (text: Go's ctx.Err() string)
+ * with *out holding the suspended process (Run / Step continue it).  budget 0: no step budget. */
+int mimic_process_run_ctx(mimic_process *p, uint64_t budget, mimic_ctx *ctx, mimic_process_regs *out);
+
 /* The process's packet memory (headroom + packet + tailroom) as the program left it. */
 int mimic_process_packet(mimic_process *p, void *buf, size_t cap);
 /* Process.Cleanup (vm.go:363-374): frees the process. */

@@ -3,7 +3,7 @@
 Product path: per-program gfx950 JIT kernels (csrc/jit.cpp, hipRTC) and the hand-written batch
 interpreter (csrc/interp.hip) + C++ host engine (csrc/engine.cpp) behind the C ABI in include/mimic_amd.h, bound here with ctypes.
 """
-from .vm import (Context, ProcessPool, ProcessPoolJob, E2BIG, LinuxArrayMap, LinuxContextSKBuff, LinuxContextXDP, NetDev, SKBBatch, SK, FlowKeys, LinuxEmulator, LinuxHashMap, LinuxMap, LinuxPerCPUArrayMap,
+from .vm import (Background, Context, WithCancel, WithTimeout, ProcessPool, ProcessPoolJob, E2BIG, LinuxArrayMap, LinuxContextSKBuff, LinuxContextXDP, NetDev, SKBBatch, SK, FlowKeys, LinuxEmulator, LinuxHashMap, LinuxMap, LinuxPerCPUArrayMap,
                  LinuxPerCPUHashMap, MapSpec, MapSpecToLinuxMap, MapType, MimicError, NewLinuxEmulator, NewVM, OptMaxTailCalls, Process,
                  ProgramSpec, UnmarshalContextJSON, VM, VMOptDevice, VMOptEmulator, VMOptExecMode, VMOptSetvCPUs, VMOptShard, VMOptSpread,
                  XDPBatch, XDPResults)

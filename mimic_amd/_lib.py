@@ -22,9 +22,10 @@ STATUS_NAMES = [
     "ERR_HELPER_UNIMPLEMENTED", "ERR_HELPER_CANT_EMULATE", "ERR_LDABS", "PANIC_DIV0",
     "PANIC_SHIFT", "PANIC_BADREG", "PANIC_CALLX", "PANIC_PC", "PANIC_HELPER_NEG",
     "ERR_STEP_LIMIT", "ERR_CALL_DEPTH", "ERR_ENGINE_HELPER", "ERR_NO_CPU", "ERR_CTX_ACCESS", "PANIC_SLICE",
-    "ERR_CTX_LOAD",
+    "ERR_CTX_LOAD", "ERR_CANCELED", "ERR_DEADLINE",
 ]
 STATUS = {n: i for i, n in enumerate(STATUS_NAMES)}
+ECANCELED, EDEADLINE = -7, -8   # mimic_process_run_ctx: ctx.Err() (include/mimic_amd.h)
 
 SCHED_CHUNKED, SCHED_INTERLEAVED, SCHED_EXPLICIT = 0, 1, 2
 MAP_F_DATASEC = 1
@@ -159,6 +160,16 @@ EXPORTS = {
     "mimic_process_free": (None, [C.c_void_p]),
     "mimic_jit_code": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "mimic_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mimic_ctx_new": (C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
+    "mimic_ctx_cancel": (None, [C.c_void_p]),
+    "mimic_ctx_err": (C.c_int, [C.c_void_p]),
+    "mimic_ctx_pinned": (C.c_int, [C.c_void_p]),
+    "mimic_ctx_free": (None, [C.c_void_p]),
+    "mimic_run_xdp_ctx": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPBatch), C.POINTER(XDPResults), C.c_void_p,
+                                    C.c_void_p, C.c_void_p]),
+    "mimic_run_skb_ctx": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(SKBBatch), C.POINTER(XDPResults), C.c_void_p,
+                                    C.c_void_p, C.c_void_p]),
+    "mimic_process_run_ctx": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.POINTER(ProcessRegs)]),
     "mimic_last_steps": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }
 

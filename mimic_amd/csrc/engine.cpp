@@ -18,7 +18,10 @@
 #include <cstring>
 #include <string>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -192,7 +195,29 @@ struct mimic_vm {
     hipStream_t skb_stream = nullptr;
     bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
     hipEvent_t skb_ev = nullptr;
+    // runs with one context per packet (mimic_run_*_ctx): the packets' context word pointers
+    const uint32_t **d_cancel_pp = nullptr;
+    size_t cancel_pp_cap = 0;
 };
+
+// context.Context of Run (vm.go:343-360): a word the kernels read before each process's first step
+// (runtime.h ctx_done) and the host sets -- on cancel(), or from a timer thread at the deadline.  The
+// word is pinned, device-mapped host memory; without a device it is plain host memory (a context
+// then works on the host, and no run accepts it).
+struct mimic_ctx {
+    uint32_t *word = nullptr;     // 0 = not done, 1 = canceled, 2 = deadline exceeded (the first wins)
+    uint32_t *dword = nullptr;    // its device address (pinned only)
+    bool pinned = false;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool closing = false;
+    std::thread timer;
+};
+static void ctx_set(mimic_ctx *c, uint32_t v) {
+    uint32_t z = 0;   // Err() keeps the first reason (context.go: cancel of a done context is a no-op)
+    __atomic_compare_exchange_n(c->word, &z, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
+}
+static uint32_t ctx_get(const mimic_ctx *c) { return __atomic_load_n(c->word, __ATOMIC_SEQ_CST); }
 
 
 static int fail(mimic_vm *vm, int code, const char *fmt, ...) {
@@ -631,6 +656,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_lane_steps);
     hipFree(vm->d_spread_bad);
     hipFree(vm->d_spread_part);
+    hipFree(vm->d_cancel_pp);
     hipFree(vm->d_defer);
     hipFree(vm->d_defer_any);
     hipFree(vm->d_kp);
@@ -1385,17 +1411,42 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
     const mimic_skb_custom *skb_custom = nullptr;   // its user-given sock / flow keys (device, one entry) or null
 };
 
+struct CtxRun {      // Run(ctx) of a batch: one context for every packet, or one per packet (host array)
+    mimic_ctx *all;
+    mimic_ctx *const *per_packet;
+};
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
-                        hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr, const StepRun *step = nullptr);
+                        hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr, const StepRun *step = nullptr,
+                        const CtxRun *cx = nullptr);
 
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                   void *hip_stream) {
     return run_xdp_impl(vm, prog_id, b, res, (hipStream_t)hip_stream, 0);
 }
 
+int mimic_run_xdp_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
+                      void *hip_stream, mimic_ctx *ctx, mimic_ctx *const *ctx_per_packet) {
+    const CtxRun cx{ctx, ctx_per_packet};
+    return run_xdp_impl(vm, prog_id, b, res, (hipStream_t)hip_stream, 0, nullptr, nullptr, &cx);
+}
+
+static int run_skb_impl(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, const mimic_xdp_results *res,
+                        void *hip_stream, const CtxRun *cx);
+
 // Batch form of NewProcess(prog, &LinuxContextSKBuff{Packet, Dev}) + SetCPUID + Run + Cleanup
 int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, const mimic_xdp_results *res,
                   void *hip_stream) {
+    return run_skb_impl(vm, prog_id, sb, res, hip_stream, nullptr);
+}
+
+int mimic_run_skb_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, const mimic_xdp_results *res,
+                      void *hip_stream, mimic_ctx *ctx, mimic_ctx *const *ctx_per_packet) {
+    const CtxRun cx{ctx, ctx_per_packet};
+    return run_skb_impl(vm, prog_id, sb, res, hip_stream, &cx);
+}
+
+static int run_skb_impl(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, const mimic_xdp_results *res,
+                        void *hip_stream, const CtxRun *cx) {
     if (!vm || !sb || !res) return MIMIC_EINVAL;
     mimic_xdp_batch b{};
     b.n = sb->n;
@@ -1406,7 +1457,7 @@ int mimic_run_skb(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *sb, con
     b.cpu = sb->cpu;
     b.step_budget = sb->step_budget;
     const SkbRun r{sb->ifindex, sb->custom};
-    return run_xdp_impl(vm, prog_id, &b, res, (hipStream_t)hip_stream, 0, &r);
+    return run_xdp_impl(vm, prog_id, &b, res, (hipStream_t)hip_stream, 0, &r, nullptr, cx);
 }
 
 int mimic_skb_release(mimic_vm *vm) {
@@ -1571,10 +1622,17 @@ static int spread_check(mimic_vm *vm) {
 }
 
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
-                        hipStream_t st_in, uint64_t first_index, const SkbRun *skb, const StepRun *step) {
+                        hipStream_t st_in, uint64_t first_index, const SkbRun *skb, const StepRun *step,
+                        const CtxRun *cx) {
     if (!vm || !b || !res) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
+    if (cx && cx->all && cx->per_packet) return fail(vm, MIMIC_EINVAL, "one context for the batch or one per packet, not both");
+    if (cx && cx->all && !cx->all->pinned) return fail(vm, MIMIC_EDEVICE, "the context was made without a device");
+    if (cx && cx->per_packet)
+        for (uint32_t i = 0; i < b->n; i++)
+            if (cx->per_packet[i] && !cx->per_packet[i]->pinned)
+                return fail(vm, MIMIC_EDEVICE, "packet %u: the context was made without a device", i);
     if (!skb) {
         const int rc = skb_settle(vm);
         if (rc) return rc;
@@ -1659,6 +1717,29 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.steps = res->steps;
     kp.err_pc = res->err_pc;
     kp.lane_steps = vm->d_lane_steps;
+    if (cx && cx->all) {
+        kp.cancel = cx->all->dword;
+        kp.cancel_any = 1;
+    } else if (cx && cx->per_packet && b->n) {
+        std::vector<const uint32_t *> w(b->n);
+        bool any = false;
+        for (uint32_t i = 0; i < b->n; i++) {
+            w[i] = cx->per_packet[i] ? cx->per_packet[i]->dword : nullptr;
+            any |= w[i] != nullptr;
+        }
+        if (any) {
+            hipStreamSynchronize(st);   // an earlier launch may still read the pointer array
+            if (b->n > vm->cancel_pp_cap) {
+                hipFree(vm->d_cancel_pp);
+                vm->d_cancel_pp = nullptr;
+                HIP_OK(vm, hipMalloc(&vm->d_cancel_pp, (size_t)b->n * sizeof(void *)));
+                vm->cancel_pp_cap = b->n;
+            }
+            HIP_OK(vm, hipMemcpy(vm->d_cancel_pp, w.data(), (size_t)b->n * sizeof(void *), hipMemcpyHostToDevice));
+            kp.cancel_pp = vm->d_cancel_pp;
+            kp.cancel_any = 1;
+        }
+    }
     switch (b->schedule) {
     case MIMIC_SCHED_CHUNKED:
         kp.per_lane = lanes ? (uint32_t)(((uint64_t)b->n + lanes - 1) / lanes) : 0;
@@ -2145,6 +2226,86 @@ int mimic_process_run(mimic_process *p, uint64_t budget, mimic_process_regs *out
     if (p->h.finished) return mimic_process_step(p, 0, out);
     const int rc = process_advance(p, (uint64_t)p->h.steps + (budget ? budget : MIMIC_DEFAULT_BUDGET));
     if (rc) return rc;
+    process_regs(p, out);
+    return 0;
+}
+
+// ---- context.Context (Run(ctx), vm.go:343-360) ------------------------------------------------
+int mimic_ctx_new(uint64_t timeout_ns, mimic_ctx **out) {
+    if (!out) return MIMIC_EINVAL;
+    mimic_ctx *c = new mimic_ctx();
+    void *w = nullptr;
+    if (hipHostMalloc(&w, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+        void *d = nullptr;
+        if (hipHostGetDevicePointer(&d, w, 0) != hipSuccess) d = w;
+        c->word = (uint32_t *)w;
+        c->dword = (uint32_t *)d;
+        c->pinned = true;
+    } else {
+        (void)hipGetLastError();
+        c->word = (uint32_t *)calloc(1, 64);
+        if (!c->word) {
+            delete c;
+            return MIMIC_ENOMEM;
+        }
+    }
+    *c->word = 0;
+    if (timeout_ns) {   // context.WithTimeout: a timer sets DeadlineExceeded unless freed first
+        const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(timeout_ns);
+        c->timer = std::thread([c, until] {
+            std::unique_lock<std::mutex> lk(c->mu);
+            if (!c->cv.wait_until(lk, until, [c] { return c->closing; })) ctx_set(c, 2);
+        });
+    }
+    *out = c;
+    return 0;
+}
+
+void mimic_ctx_cancel(mimic_ctx *c) {
+    if (c) ctx_set(c, 1);
+}
+
+int mimic_ctx_err(const mimic_ctx *c) { return c ? (int)ctx_get(c) : MIMIC_EINVAL; }
+
+int mimic_ctx_pinned(const mimic_ctx *c) { return c ? (int)c->pinned : MIMIC_EINVAL; }
+
+void mimic_ctx_free(mimic_ctx *c) {
+    if (!c) return;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->closing = true;
+    }
+    c->cv.notify_all();
+    if (c->timer.joinable()) c->timer.join();
+    if (c->pinned) hipHostFree(c->word);
+    else free(c->word);
+    delete c;
+}
+
+// Process.Run(ctx): the process advances in launches of a growing number of steps and the context
+// is checked before each (the reference checks before every step, vm.go:344-349: here a cancel is
+// seen within one launch).  Done: MIMIC_ECANCELED / MIMIC_EDEADLINE (ctx.Err()) with the process
+// suspended where it stopped -- Run or Step continue it.  budget 0 with a context: no step budget
+// (the context bounds the run, as in the reference; the step counter is 32 bits).
+int mimic_process_run_ctx(mimic_process *p, uint64_t budget, mimic_ctx *ctx, mimic_process_regs *out) {
+    if (!p) return MIMIC_EINVAL;
+    if (!ctx) return mimic_process_run(p, budget, out);
+    if (p->h.finished) return mimic_process_step(p, 0, out);
+    const uint64_t end = budget ? (uint64_t)p->h.steps + budget : 0xffffffffull;
+    uint64_t slice = 4096;
+    for (;;) {
+        const uint32_t d = ctx_get(ctx);
+        if (d) {
+            process_regs(p, out);
+            return fail(p->vm, d == 1 ? MIMIC_ECANCELED : MIMIC_EDEADLINE,
+                        d == 1 ? "context canceled" : "context deadline exceeded");
+        }
+        const uint64_t to = std::min<uint64_t>(end, (uint64_t)p->h.steps + slice);
+        const int rc = process_advance(p, to);
+        if (rc) return rc;
+        if (p->h.finished || (uint64_t)p->h.steps >= end || (uint64_t)p->h.steps < to) break;
+        if (slice < (1ull << 20)) slice <<= 1;
+    }
     process_regs(p, out);
     return 0;
 }

@@ -225,6 +225,12 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         }
 
         // ---- Process.Run ------------------------------------------------------------------
+        // Run(ctx): a context already done before the first step ends the process there
+        // (vm.go:344-349).  A stepped process's context is checked by the host between launches.
+        if (MODE != MODE_STEP && kp.cancel_any && !resumed && key != KEY_DONE) {
+            const uint32_t cz = ctx_done(kp, i);
+            if (cz) TERM(MIMIC_ERR_CANCELED - 1 + (int)cz, (int32_t)(key - pbase));
+        }
         uint64_t wsteps = resumed ? steps : 0;   // wave-steps since the packets started: bounds every lane's steps
         uint32_t cand = KEY_DONE;     // speculated next key (where the first executing lane went)
         for (;;) {

@@ -597,6 +597,11 @@ class Gen {
         E.line("    int st_ = 0;");
         E.line("    int32_t epc_ = -1;");
         if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
+        // Run(ctx): a context already done when the process would take its first step ends it
+        // there (vm.go:344-349); a launch without contexts skips this on a uniform scalar test
+        E.line("#ifndef MIMIC_MEAS_NOCTX   // (measurement knob: no context check, contexts ignored)");
+        E.line("    if (kq_.cancel_any) { const uint32_t cz_ = ctx_done(kq_, i); if (cz_) TERM(MIMIC_ERR_CANCELED - 1u + cz_, 0); }");
+        E.line("#endif");
         if (dispatch_on()) {
             // one dispatch block for the entry and every tail call (see dispatch_on)
             E.line("    uint32_t cur_;   // no initializer: the TERM gotos above jump past it");

@@ -224,6 +224,13 @@ struct KParams {
     // spread launches with an LDS table covering every vCPU lane: each block's table goes here,
     // [block][lane][counter], summed into the map by mimic_spread_reduce_kernel (interp.hip)
     void *spread_part;
+    // Run(ctx) (vm.go:343-350): the contexts of the launch's processes, mimic_ctx words in pinned
+    // host memory (0 = not done, 1 = canceled, 2 = deadline exceeded).  cancel: one word for every
+    // packet; cancel_pp: one word pointer per packet (null: context.Background()).  cancel_any = 0:
+    // neither (no check at all).  Checked before each process's first step (ctx_done, runtime.h).
+    const uint32_t *cancel;
+    const uint32_t *const *cancel_pp;
+    uint32_t cancel_any;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

@@ -117,6 +117,17 @@ DEV int32_t lane_cpu(const KParams &kp, uint32_t g) {
 #endif
 template <typename T>
 DEV GAS T *gp(T *p) { return (GAS T *)p; }
+
+// Run's `select { case <-ctx.Done(): return ctx.Err() }` before a process's first step (vm.go:
+// 344-349): the state of packet i's context word -- 0 (not done), 1 (canceled), 2 (deadline
+// exceeded).  The word lives in pinned host memory that the host writes while the launch runs: a
+// system-scope load reads it past the caches (one PCIe round trip, made only when the launch was
+// given a context, KParams::cancel_any).
+DEV uint32_t ctx_done(const KParams &kp, uint32_t i) {
+    const uint32_t *w = kp.cancel_pp ? kp.cancel_pp[i] : kp.cancel;
+    if (!w) return 0u;
+    return __hip_atomic_load((GAS const uint32_t *)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 template <typename T>
 DEV const GAS T *gp(const T *p) { return (const GAS T *)p; }
 

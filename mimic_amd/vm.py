@@ -621,14 +621,20 @@ class VM:
 
     # ---- batch entry point ------------------------------------------------------------------
     def RunXDPBatch(self, prog_id: int, batch: "XDPBatch", results: Optional["XDPResults"] = None,
-                    stream=None, sync: bool = True) -> "XDPResults":
-        """N x {NewProcess, SetCPUID, Run, read R0, Cleanup} on the GPU."""
+                    stream=None, sync: bool = True, ctx: Optional["Context"] = None,
+                    ctx_per_packet: Optional[Sequence[Optional["Context"]]] = None) -> "XDPResults":
+        """N x {NewProcess, SetCPUID, Run(ctx), read R0, Cleanup} on the GPU.  ctx: one context
+        for every process, or ctx_per_packet: one each (None entries: Background)."""
         if results is None:
             results = XDPResults.empty(batch.n, batch.pkt_data.device)
         b = batch._c()
         r = results._c()
         st = stream.cuda_stream if stream is not None else None
-        rc = self.lib.mimic_run_xdp(self.h, prog_id, b, r, st)
+        if ctx is not None or ctx_per_packet is not None:
+            h, arr, _keep = _ctx_args(ctx, ctx_per_packet, batch.n)
+            rc = self.lib.mimic_run_xdp_ctx(self.h, prog_id, b, r, st, h, arr)
+        else:
+            rc = self.lib.mimic_run_xdp(self.h, prog_id, b, r, st)
         if rc:
             _check(self.h, rc, "RunXDPBatch")
         if sync:
@@ -636,12 +642,17 @@ class VM:
         return results
 
     def RunSKBBatch(self, prog_id: int, batch: "SKBBatch", results: Optional["XDPResults"] = None,
-                    stream=None, sync: bool = True) -> "XDPResults":
-        """N x {NewProcess(LinuxContextSKBuff), SetCPUID, Run, read R0, Cleanup} on the GPU."""
+                    stream=None, sync: bool = True, ctx: Optional["Context"] = None,
+                    ctx_per_packet: Optional[Sequence[Optional["Context"]]] = None) -> "XDPResults":
+        """N x {NewProcess(LinuxContextSKBuff), SetCPUID, Run(ctx), read R0, Cleanup} on the GPU."""
         if results is None:
             results = XDPResults.empty(batch.n, batch.pkt_data.device)
         st = stream.cuda_stream if stream is not None else None
-        rc = self.lib.mimic_run_skb(self.h, prog_id, batch._c(), results._c(), st)
+        if ctx is not None or ctx_per_packet is not None:
+            h, arr, _keep = _ctx_args(ctx, ctx_per_packet, batch.n)
+            rc = self.lib.mimic_run_skb_ctx(self.h, prog_id, batch._c(), results._c(), st, h, arr)
+        else:
+            rc = self.lib.mimic_run_skb(self.h, prog_id, batch._c(), results._c(), st)
         if rc:
             _check(self.h, rc, "RunSKBBatch")
         if sync:
@@ -823,17 +834,26 @@ class Process:
             raise MimicError(f"inst at PC({self.Registers.PC}): {L.STATUS_NAMES[self.Status]}")
         return self._exited
 
-    def Run(self, step_budget: int = 0) -> None:  # vm.go:343-360
+    def Run(self, step_budget: int = 0, ctx: Optional["Context"] = None) -> None:  # vm.go:343-360
         """Process.Run: run to exit (or a fatal error, or the step budget standing in for the
         context deadline).  Every register is readable afterwards (Registers.R0..R10, PC), as
         after the reference's Run (Readme.md:74-78): the process runs on the device as a
         single-lane launch that saves its whole state (mimic_process_run), continuing a process
         that Step() has started.  cpuID stays -1 when SetCPUID was never called (vm.go:214) and may
         equal V (vm.go:273): the reference runs such processes; only per-CPU map operations fail
-        in them (emulator_linux_map_array.go:236-238)."""
+        in them (emulator_linux_map_array.go:236-238).  With ctx, Run(ctx): the context is checked
+        between launch slices; once it is done Run raises MimicError(ctx.Err()) with the process
+        suspended (Run / Step continue it), and step_budget 0 means no step budget."""
         self._ensure_native()
         regs = L.ProcessRegs()
-        _check(self.VM.h, self.VM.lib.mimic_process_run(self._native, step_budget, C.byref(regs)), "Run")
+        if ctx is not None:
+            rc = self.VM.lib.mimic_process_run_ctx(self._native, step_budget, ctx._device_handle(), C.byref(regs))
+            if rc in (L.ECANCELED, L.EDEADLINE):
+                self._take(regs)
+                raise MimicError(Context._ERR[1 if rc == L.ECANCELED else 2])
+            _check(self.VM.h, rc, "Run")
+        else:
+            _check(self.VM.h, self.VM.lib.mimic_process_run(self._native, step_budget, C.byref(regs)), "Run")
         self._take(regs)
         self.ErrPC = self.Registers.PC if self.Status else -1
         self.PacketAfter = self.Packet()
@@ -1109,20 +1129,118 @@ class XDPResults:
 # ---------------------------------------------------------------------------------------------
 # ProcessPool (vm.go:468-583) on the device
 # ---------------------------------------------------------------------------------------------
-@dataclass
 class Context:
-    """The part of context.Context a job uses: cancellation and a deadline (time.monotonic())."""
-    Deadline: Optional[float] = None
-    Cancelled: bool = False
+    """context.Context as Run uses it (vm.go:343-360): Done / Err, made by Background(),
+    WithCancel() or WithTimeout().  Deadline is a time.monotonic() value.  A context given to a
+    device run is backed by a mimic_ctx (include/mimic_amd.h): a word in pinned host memory that the
+    kernels read before each process's first step, set by Cancel() or by a native timer at the
+    deadline, so a batch already running on the GPU stops starting processes once it is done."""
 
-    def Err(self) -> Optional[str]:
+    _ERR = {1: "context canceled", 2: "context deadline exceeded"}
+
+    def __init__(self, Deadline: Optional[float] = None, Cancelled: bool = False):
+        self.Deadline = Deadline
+        self.Cancelled = Cancelled
+        self._h = None
+        self._lib = None
+
+    def Cancel(self) -> None:
+        """The context's CancelFunc."""
+        self.Cancelled = True
+        if self._h is not None:
+            self._lib.mimic_ctx_cancel(self._h)
+
+    def _state(self) -> int:
         import time
 
+        if self._h is not None:
+            d = self._lib.mimic_ctx_err(self._h)
+            if d:
+                return d
         if self.Cancelled:
-            return "context canceled"
+            return 1
         if self.Deadline is not None and time.monotonic() >= self.Deadline:
-            return "context deadline exceeded"
-        return None
+            return 2
+        return 0
+
+    def Err(self) -> Optional[str]:
+        return self._ERR.get(self._state())
+
+    def Done(self) -> bool:
+        return self._state() != 0
+
+    def native(self):
+        """The mimic_ctx handle (made on first use; its state follows this context's)."""
+        import time
+
+        if self._h is None:
+            lib = L.load()
+            h = C.c_void_p()
+            ns = 0
+            if self.Deadline is not None:
+                ns = max(1, int((self.Deadline - time.monotonic()) * 1e9))
+            rc = lib.mimic_ctx_new(ns, C.byref(h))
+            if rc:
+                raise MimicError(f"context: error {rc}")
+            self._lib, self._h = lib, h
+            if self.Cancelled:   # (a passed deadline: the timer, armed at 1 ns, marks it)
+                lib.mimic_ctx_cancel(h)
+        return self._h
+
+    def _device_handle(self):
+        """The handle for a device run: the state so far carried over (a deadline already passed
+        marks the word too)."""
+        h = self.native()
+        if not self._lib.mimic_ctx_err(h) and self._state() == 2 and self.Deadline is not None:
+            # the deadline passed before the handle existed: the native timer (1 ns) marks it
+            import time
+
+            t_end = time.monotonic() + 1.0
+            while not self._lib.mimic_ctx_err(h) and time.monotonic() < t_end:
+                time.sleep(0)
+        return h
+
+    def close(self) -> None:
+        if self._h is not None:
+            self._lib.mimic_ctx_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def Background() -> Context:
+    """context.Background(): never done (a run given it checks nothing)."""
+    return Context()
+
+
+def WithCancel() -> Context:
+    """context.WithCancel(context.Background()): done once Cancel() is called."""
+    return Context()
+
+
+def WithTimeout(seconds: float) -> Context:
+    """context.WithTimeout(context.Background(), seconds)."""
+    import time
+
+    return Context(Deadline=time.monotonic() + seconds)
+
+
+def _ctx_args(ctx, ctx_per_packet, n):
+    """(handle, per-packet array, keep-alive) of a run's contexts."""
+    if ctx is not None and ctx_per_packet is not None:
+        raise MimicError("one context for the batch or one per packet, not both")
+    if ctx is not None:
+        return ctx._device_handle(), None, None
+    if ctx_per_packet is not None:
+        if len(ctx_per_packet) != n:
+            raise MimicError("one context per packet")
+        arr = (C.c_void_p * n)(*[c._device_handle() if c is not None else None for c in ctx_per_packet])
+        return None, arr, arr
+    return None, None, None
 
 
 @dataclass
@@ -1248,7 +1366,9 @@ class ProcessPool:
             for job in js:
                 p = job.Process
                 err = None
-                if p.Status:
+                if p.Status in (L.STATUS["ERR_CANCELED"], L.STATUS["ERR_DEADLINE"]):   # Run returned ctx.Err()
+                    err = MimicError(Context._ERR[p.Status - L.STATUS["ERR_CANCELED"] + 1])
+                elif p.Status:
                     err = MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[p.Status]} at PC({p.ErrPC})")
                 self._handoff(job, err)
 
@@ -1264,9 +1384,11 @@ class ProcessPool:
             # give the job addresses past its own.
             for j in js:
                 try:
-                    j.Process.Run()
-                except MimicError:
-                    if not j.Process.Status:   # not a fatal status of the program: an engine error
+                    j.Process.Run(ctx=j.Context)
+                except MimicError as ex:
+                    if str(ex) in Context._ERR.values():   # Run(ctx) returned ctx.Err()
+                        j.Process.Status = L.STATUS["ERR_CANCELED"] + (str(ex) == Context._ERR[2])
+                    elif not j.Process.Status:   # not a fatal status of the program: an engine error
                         raise
             return
         import numpy as np
@@ -1278,7 +1400,10 @@ class ProcessPool:
                                       rxq=np.array([c.RxQueueIndex for c in ctxs], np.int32),
                                       egress=np.array([c.EgressIfIndex for c in ctxs], np.int32),
                                       schedule=L.SCHED_EXPLICIT, cpu=cpus)
-        res = self.vm.RunXDPBatch(pid, batch).numpy(len(js))
+        # each job's context is checked on the device before its process's first step, so jobs
+        # whose context is done while the launch runs stop there (vm.go:548-573)
+        cpp = [j.Context for j in js] if any(j.Context is not None for j in js) else None
+        res = self.vm.RunXDPBatch(pid, batch, ctx_per_packet=cpp).numpy(len(js))
         mem = batch.pkt_data.cpu().numpy()
         offs = batch.pkt_off.cpu().numpy()
         for k, j in enumerate(js):

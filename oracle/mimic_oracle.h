@@ -57,6 +57,8 @@ enum {
                                      not implemented), emulator_linux_sk_buff.go convertAccess */
     ORC_PANIC_SLICE = 27,         /* Go slice-bounds panic inside convertAccess (cb loads, IP slices, flow_keys IP) */
     ORC_ERR_CTX_LOAD = 28,        /* NewProcess: Context.Load failed (SKBuffFromBytes error, out of memory) */
+    ORC_ERR_CANCELED = 29,        /* Run: ctx.Done() before a step, ctx.Err() = context.Canceled (vm.go:344-350) */
+    ORC_ERR_DEADLINE = 30,        /* Run: the same with context.DeadlineExceeded */
     ORC_STATUS_COUNT
 };
 
@@ -155,6 +157,10 @@ typedef struct {
     const int32_t *cpu;
     uint64_t step_budget;   /* 0 = default (1<<22) */
     int write_back;         /* copy packet memory back into pkt_data after Run */
+    /* Run(ctx) of packet i: ctx_done[i] = 0 (ctx not done: context.Background()), 1 (canceled) or
+     * 2 (deadline exceeded) -- the state ctx.Done() / ctx.Err() show before every step (vm.go:343-350).
+     * NULL = every ctx is context.Background(). */
+    const uint8_t *ctx_done;
 } orc_xdp_batch;
 
 typedef struct {
@@ -197,6 +203,7 @@ typedef struct {
     uint64_t step_budget;
     int write_back;
     const orc_skb_custom *custom;   /* [n] or NULL: the contexts' user-given SK / FlowKeys */
+    const uint8_t *ctx_done;        /* as in orc_xdp_batch */
 } orc_skb_batch;
 int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_results *out);
 

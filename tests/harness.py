@@ -114,10 +114,11 @@ def packets_to_buffer(packets: Sequence[bytes], headroom=0, tailroom=0, align: i
 
 
 def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, tailroom=0, ingress=None,
-               rxq=None, egress=None, step_budget=0):
+               rxq=None, egress=None, step_budget=0, ctx_done=None):
+    """ctx_done: per packet, the state of its Run's context (0 not done, 1 canceled, 2 deadline)."""
     vm, mids, pids = build_oracle(sc)
     out = vm.run_xdp_batch(pids[entry], buf.copy(), off, lens, cpu, headroom, tailroom, ingress, rxq, egress,
-                           step_budget)
+                           step_budget, ctx_done=ctx_done)
     out["maps"] = {}
     out["hash"] = {}
     for m in sc.maps:
@@ -133,7 +134,7 @@ def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, ta
 
 def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=0, tailroom=0, ingress=0, rxq=0,
                egress=0, step_budget=0, schedule=None, device: int = 0, exec_mode: Optional[str] = None,
-               spread: Optional[int] = None):
+               spread: Optional[int] = None, ctx=None, ctx_per_packet=None):
     import mimic_amd as M
 
     vm, maps, pids = build_engine(sc, device, exec_mode=exec_mode, spread=spread)
@@ -142,7 +143,7 @@ def run_engine(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, headroom=
     batch = M.XDPBatch.from_numpy(buf, off, lens, device=f"cuda:{device}", headroom=headroom, tailroom=tailroom,
                                   ingress=ingress, rxq=rxq, egress=egress, schedule=schedule, cpu=cpu,
                                   step_budget=step_budget)
-    res = vm.RunXDPBatch(pids[entry], batch)
+    res = vm.RunXDPBatch(pids[entry], batch, ctx=ctx, ctx_per_packet=ctx_per_packet)
     out = res.numpy(len(lens))
     out["pkt"] = batch.pkt_data.cpu().numpy()
     out["maps"] = {}
@@ -220,15 +221,16 @@ def _map_readout(sc, read_values, read_hash):
 
 
 def run_oracle_skb(sc: Scenario, buf, off, lens, cpu, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
-                   splits=None, custom=None):
+                   splits=None, custom=None, ctx_done=None):
     """Sequential reference semantics; `splits` = indices where a new batch (same VM) starts;
-    custom = the contexts' mimic_skb_custom table (numpy) or None."""
+    custom = the contexts' mimic_skb_custom table (numpy) or None; ctx_done as in run_oracle."""
     vm, mids, pids = build_oracle(sc)
     buf = np.array(buf, dtype=np.uint8, copy=True)
     parts = []
     for a, b in _splits(len(lens), splits):
         parts.append(vm.run_skb_batch(pids[entry], buf, off[a:b], lens[a:b], cpu[a:b], ifindex, step_budget,
-                                      custom=None if custom is None else custom[a:b]))
+                                      custom=None if custom is None else custom[a:b],
+                                      ctx_done=None if ctx_done is None else np.asarray(ctx_done)[a:b]))
     out = {k: np.concatenate([p[k] for p in parts]) for k in ("r0", "status", "steps", "err_pc")}
     out["pkt"] = buf
 
@@ -242,7 +244,8 @@ def run_oracle_skb(sc: Scenario, buf, off, lens, cpu, entry: int = 0, ifindex: i
 
 
 def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifindex: int = 0, step_budget: int = 0,
-                   schedule=None, splits=None, device: int = 0, exec_mode: Optional[str] = None, custom=None):
+                   schedule=None, splits=None, device: int = 0, exec_mode: Optional[str] = None, custom=None,
+                   ctx_per_packet=None):
     import torch
 
     import mimic_amd as M
@@ -258,7 +261,8 @@ def run_engine_skb(sc: Scenario, buf, off, lens, cpu=None, entry: int = 0, ifind
         sub = M.SKBBatch(full.pkt_data, full.pkt_off[a:b], full.pkt_len[a:b], ifindex, schedule,
                          None if cpu is None else np.asarray(cpu)[a:b], step_budget,
                          None if full.custom is None else full.custom[a * CS:b * CS])
-        parts.append(vm.RunSKBBatch(pids[entry], sub).numpy(b - a))
+        parts.append(vm.RunSKBBatch(pids[entry], sub, ctx_per_packet=None if ctx_per_packet is None
+                                    else ctx_per_packet[a:b]).numpy(b - a))
     out = {k: np.concatenate([p[k] for p in parts]) for k in ("r0", "status", "steps", "err_pc")}
     torch.cuda.synchronize(device)
     out["pkt"] = full.pkt_data.cpu().numpy()
