@@ -68,7 +68,7 @@ enum mimic_status {
     MIMIC_PANIC_CALLX = 19,          /* inst.go:270-273 */
     MIMIC_PANIC_PC = 20,             /* negative PC, vm.go:300 */
     MIMIC_PANIC_HELPER_NEG = 21,     /* negative helper id, emulator_linux_.go:126 */
-    MIMIC_ERR_STEP_LIMIT = 22,       /* step budget (stands for Run's ctx deadline, vm.go:344-350) */
+    MIMIC_ERR_STEP_LIMIT = 22,       /* step budget: the engine's watchdog next to Run's ctx (mimic_run_*_ctx) */
     MIMIC_ERR_CALL_DEPTH = 23,       /* > MIMIC_MAX_FRAMES nested BPF-to-BPF calls */
     MIMIC_ERR_ENGINE_HELPER = 24,    /* helper the reference emulates but this engine does not */
     MIMIC_ERR_NO_CPU = 25,
@@ -138,7 +138,7 @@ typedef struct {
     const int32_t *rx_queue_index;  int32_t rxq_all;
     const int32_t *egress_ifindex;  int32_t egress_all;
     const int32_t *cpu;         /* HOST array for MIMIC_SCHED_EXPLICIT (the engine builds the per-vCPU lists) */
-    uint64_t step_budget;       /* 0 = MIMIC default; Run's ctx deadline stand-in */
+    uint64_t step_budget;       /* 0 = MIMIC default; the per-process watchdog (contexts: mimic_run_xdp_ctx) */
 } mimic_xdp_batch;
 
 typedef struct {                /* DEVICE arrays of n entries, any may be NULL */

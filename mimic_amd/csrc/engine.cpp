@@ -132,6 +132,8 @@ struct mimic_vm {
     std::vector<DProg> h_dp;
     hipFunction_t jit_fn[2] = {nullptr, nullptr};   // per CtxKind, generated on first use
     JitInfo jit_info[2]{};
+    hipFunction_t jit_fn_cx[2] = {nullptr, nullptr};   // the same with the Run(ctx) check (launches given contexts)
+    JitInfo jit_info_cx[2]{};
     // the spread kernel (jit.cpp analyze_spread, xdp_md only): 0 not built yet, 1 built, -1 the
     // program set does not allow it; spread_bad is the device word a spread launch marks when a
     // generic access reached per-CPU memory (spread_used: some launch could have marked it)
@@ -499,6 +501,7 @@ static int upload_tables(mimic_vm *vm) {
         }
     }
     vm->jit_fn[0] = vm->jit_fn[1] = nullptr;
+    vm->jit_fn_cx[0] = vm->jit_fn_cx[1] = nullptr;
     vm->jit_fn_spread = nullptr;
     vm->spread_state = 0;
     std::vector<DInsn> all = vm->h_all;
@@ -1621,6 +1624,19 @@ static int spread_check(mimic_vm *vm) {
     return 0;
 }
 
+// LD_IMM64 slots naming a per-CPU array whose row the lane value cache can hold, with its E * S
+static std::vector<std::pair<uint32_t, uint32_t>> vc_slots_of(const mimic_vm *vm) {
+    std::vector<std::pair<uint32_t, uint32_t>> vc;
+    for (size_t s = 0; s < vm->h_all.size(); s++) {
+        const DInsn &x = vm->h_all[s];
+        const uint32_t mh = AUX_MAPHINT(x.aux);
+        if (AUX_H(x.aux) != H_LDIMM || !mh || mh > vm->maps.size()) continue;
+        const HostMap &hm = vm->maps[mh - 1];
+        if (vc_row_ok(hm.family, hm.max_entries, hm.value_size)) vc.push_back({(uint32_t)s, hm.max_entries * hm.value_size});
+    }
+    return vc;
+}
+
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                         hipStream_t st_in, uint64_t first_index, const SkbRun *skb, const StepRun *step,
                         const CtxRun *cx) {
@@ -1796,15 +1812,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     bool jit = vm->exec_mode == MIMIC_EXEC_JIT && !step;   // stepping runs on the interpreter
     if (jit && !vm->jit_fn[ctx]) {
         std::string log;
-        // LD_IMM64 slots naming a per-CPU array whose row the lane value cache can hold, with its E * S
-        std::vector<std::pair<uint32_t, uint32_t>> vc;
-        for (size_t s = 0; s < vm->h_all.size(); s++) {
-            const DInsn &x = vm->h_all[s];
-            const uint32_t mh = AUX_MAPHINT(x.aux);
-            if (AUX_H(x.aux) != H_LDIMM || !mh || mh > vm->maps.size()) continue;
-            const HostMap &hm = vm->maps[mh - 1];
-            if (vc_row_ok(hm.family, hm.max_entries, hm.value_size)) vc.push_back({(uint32_t)s, hm.max_entries * hm.value_size});
-        }
+        const std::vector<std::pair<uint32_t, uint32_t>> vc = vc_slots_of(vm);
         if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx], &vc),
                               &vm->jit_fn[ctx], &log))
             return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
@@ -1846,8 +1854,23 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             if (knob != 1 && !vm->spread_lds && cpu_lanes > 16384) spread = false;
         }
     }
-    const JitInfo &ji = spread ? vm->jit_info_spread : vm->jit_info[ctx];
-    hipFunction_t jfn = spread ? vm->jit_fn_spread : vm->jit_fn[ctx];
+    // a launch given contexts runs the variant with the per-packet Run(ctx) check, one lane per vCPU
+    const bool cxk = jit && kp.cancel_any;
+    if (cxk) {
+        spread = false;
+        if (!vm->jit_fn_cx[ctx]) {
+            const std::vector<std::pair<uint32_t, uint32_t>> vc = vc_slots_of(vm);
+            std::string log;
+            // with or without early packet loads as the VM's own kernel (the spill choice above)
+            if (mimic_jit_compile(vm->s.device,
+                                  mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info_cx[ctx], &vc,
+                                                   !vm->jit_info[ctx].early_loads, nullptr, true),
+                                  &vm->jit_fn_cx[ctx], &log))
+                return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
+        }
+    }
+    const JitInfo &ji = spread ? vm->jit_info_spread : cxk ? vm->jit_info_cx[ctx] : vm->jit_info[ctx];
+    hipFunction_t jfn = spread ? vm->jit_fn_spread : cxk ? vm->jit_fn_cx[ctx] : vm->jit_fn[ctx];
     uint32_t run_lanes = lanes;
     if (spread) {
         const uint32_t blocks = (uint32_t)(((uint64_t)b->n + spread_ppb() - 1) / spread_ppb());

@@ -213,6 +213,7 @@ class Gen {
     uint32_t lds_stack_q = 16; // MIMIC_JIT_LDSSTK=Q: LDS window over the top 8Q bytes of frame 0
     bool vc_on = false;
     const SpreadReq *spread_req = nullptr;   // the VM's per-CPU arrays: spread mode is possible (analyze_spread)
+    bool ctx_check = false;   // the kernel reads each packet's Run(ctx) context before its first step
     bool spread_on = false;
     uint32_t spread_map = 0, spread_n = 0, spread_row = 0;   // the counted map, counter width, E * S
     std::map<uint32_t, uint32_t> vc_ok;  // LD_IMM64 slots (kernel-wide) naming a per-CPU array whose row can be cached -> E * S
@@ -599,9 +600,8 @@ class Gen {
         if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
         // Run(ctx): a context already done when the process would take its first step ends it
         // there (vm.go:344-349); a launch without contexts skips this on a uniform scalar test
-        E.line("#ifndef MIMIC_MEAS_NOCTX   // (measurement knob: no context check, contexts ignored)");
-        E.line("    if (kq_.cancel_any) { const uint32_t cz_ = ctx_done(kq_, i); if (cz_) TERM(MIMIC_ERR_CANCELED - 1u + cz_, 0); }");
-        E.line("#endif");
+        // (a variant of its own, built for launches given contexts: the check costs ~2 % on cfg 2)
+        if (ctx_check) E.line("    { const uint32_t cz_ = ctx_done(kq_, i); if (cz_) TERM(MIMIC_ERR_CANCELED - 1u + cz_, 0); }");
         if (dispatch_on()) {
             // one dispatch block for the entry and every tail call (see dispatch_on)
             E.line("    uint32_t cur_;   // no initializer: the TERM gotos above jump past it");
@@ -2012,7 +2012,7 @@ std::map<CacheKey, hipFunction_t> g_cache;
 
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
                              JitInfo *info, const std::vector<std::pair<uint32_t, uint32_t>> *vc_slots, bool no_early_loads,
-                             const SpreadReq *spread) {
+                             const SpreadReq *spread, bool ctx_check) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
     Gen g(v, ctx_kind);
@@ -2021,6 +2021,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
             if (v.second > 0 && v.second <= MIMIC_VC_MAX_ROW && !(v.second & 7)) g.vc_ok[v.first] = v.second;
     if (no_early_loads) g.speculate = 0;
     g.spread_req = spread;
+    g.ctx_check = ctx_check;
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;

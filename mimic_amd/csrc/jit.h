@@ -30,6 +30,7 @@ struct SpreadReq {
     uint32_t ppb = 1024;     // packets per block
 };
 // ctx_kind: CtxKind of the batches the kernel runs
+// ctx_check: the variant for launches given Run(ctx) contexts (KParams::cancel_any)
 // vc_slots: (kernel-wide index, E * S) of the LD_IMM64 slots whose constant is the object of a
 // per-CPU array whose row the lane value cache may hold: E * S a multiple of 8, at most
 // MIMIC_VC_MAX_ROW bytes (rows up to 32 bytes in registers, longer ones in LDS)
@@ -37,7 +38,7 @@ struct SpreadReq {
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
                              JitInfo *info, const std::vector<std::pair<uint32_t, uint32_t>> *vc_slots = nullptr,
                              bool no_early_loads = false,
-                             const SpreadReq *spread = nullptr);
+                             const SpreadReq *spread = nullptr, bool ctx_check = false);
 // 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
 // batch with a smaller budget must run on the interpreter
 uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);

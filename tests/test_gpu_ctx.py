@@ -103,14 +103,15 @@ def test_per_packet_contexts(gpu, mode):
 
 
 def test_per_packet_contexts_spread(gpu):
-    """The spread kernel (a vCPU's packets on many lanes) checks each packet's context too."""
+    """A batch the spread kernel would run (a vCPU's packets on many lanes) runs with contexts on
+    the one-lane-per-vCPU variant with the context check, exactly."""
     sc = _sc_cls(7)
     buf, off, lens = W.make_packets(20000, sizes=(64, 128), weights=(1, 1))
     gone = M.WithCancel()
     gone.Cancel()
     ctxs = [gone if i % 5 == 2 else None for i in range(len(lens))]
     e = run_engine(sc, buf, off, lens, None, schedule=M.SCHED_INTERLEAVED, spread=1, ctx_per_packet=ctxs)
-    assert e["last_exec"] == "spread"
+    assert e["last_exec"] == "jit"
     cpu = W.schedule_cpu(len(lens), 7, "interleaved")
     o = run_oracle(sc, buf, off, lens, cpu, ctx_done=_states(ctxs))
     assert (e["status"][2::5] == CANCELED).all()
@@ -152,12 +153,14 @@ def test_done_while_the_batch_runs(gpu, mode, kind):
     sc = _loop_sc(V, K_LOOP)
     vm, maps, pids = build_engine(sc, exec_mode=mode)
     dev = "cuda:0"
-    # calibration: one process per lane (also builds the kernel)
+    # calibration: one process per lane, with a live context (also builds the kernel variant
+    # launches given contexts run)
     b1, o1, l1 = packets_to_buffer([bytes(64)] * V)
     cal = M.XDPBatch.from_numpy(b1, o1, l1, device=dev, schedule=M.SCHED_CHUNKED)
-    vm.RunXDPBatch(pids[0], cal)
+    live = M.WithCancel()
+    vm.RunXDPBatch(pids[0], cal, ctx=live)
     t = time.monotonic()
-    vm.RunXDPBatch(pids[0], cal)
+    vm.RunXDPBatch(pids[0], cal, ctx=live)
     t1 = time.monotonic() - t
     n = V * P
     buf, off, lens = packets_to_buffer([bytes(64)] * n)
@@ -202,12 +205,17 @@ def test_done_while_the_batch_runs_matches_the_oracle(gpu):
     vm, maps, pids = build_engine(sc)
     dev = "cuda:0"
     warm = M.XDPBatch.from_numpy(*packets_to_buffer([bytes(64)] * V), device=dev, schedule=M.SCHED_CHUNKED)
+    live = M.WithCancel()
+    vm.RunXDPBatch(pids[0], warm, ctx=live)
     t = time.monotonic()
-    vm.RunXDPBatch(pids[0], warm)
-    vm.RunXDPBatch(pids[0], warm)
+    vm.RunXDPBatch(pids[0], warm, ctx=live)
+    vm.RunXDPBatch(pids[0], warm, ctx=live)
     t1 = (time.monotonic() - t) / 2
     vm.close()
     vm, maps, pids = build_engine(sc)
+    vm.RunXDPBatch(pids[0], M.XDPBatch.from_numpy(*packets_to_buffer([bytes(64)]), device=dev), ctx=live)   # (build)
+    for c in range(V):   # the build run's count out of the way
+        maps["c"].Update((0).to_bytes(4, "little"), bytes(8), 0, c)
     batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, schedule=M.SCHED_CHUNKED)
     ctx = M.WithTimeout(0.5 * P * t1)
     res = vm.RunXDPBatch(pids[0], batch, ctx=ctx)
