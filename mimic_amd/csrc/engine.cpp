@@ -197,9 +197,11 @@ struct mimic_vm {
     hipStream_t skb_stream = nullptr;
     bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
     hipEvent_t skb_ev = nullptr;
-    // runs with one context per packet (mimic_run_*_ctx): the packets' context word pointers
+    // runs with one context per packet (mimic_run_*_ctx): the packets' context word pointers, and
+    // the stream of the last launch that reads them
     const uint32_t **d_cancel_pp = nullptr;
     size_t cancel_pp_cap = 0;
+    hipStream_t cancel_pp_stream = nullptr;
 };
 
 // context.Context of Run (vm.go:343-360): a word the kernels read before each process's first step
@@ -214,6 +216,9 @@ struct mimic_ctx {
     std::condition_variable cv;
     bool closing = false;
     std::thread timer;
+    // launches that read the word: freeing it waits for them (a kernel must never read freed
+    // host memory)
+    std::vector<hipEvent_t> uses;
 };
 static void ctx_set(mimic_ctx *c, uint32_t v) {
     uint32_t z = 0;   // Err() keeps the first reason (context.go: cancel of a done context is a no-op)
@@ -1744,7 +1749,10 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             any |= w[i] != nullptr;
         }
         if (any) {
-            hipStreamSynchronize(st);   // an earlier launch may still read the pointer array
+            // an earlier launch may still read the pointer array
+            if (vm->cancel_pp_stream) hipStreamSynchronize(vm->cancel_pp_stream);
+            hipStreamSynchronize(st);
+            vm->cancel_pp_stream = st;
             if (b->n > vm->cancel_pp_cap) {
                 hipFree(vm->d_cancel_pp);
                 vm->d_cancel_pp = nullptr;
@@ -1999,6 +2007,33 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (mimic_launch_spread_reduce(kp.spread_part, kp.lanes / 256u, kp.cpu_lanes, ji.spread_roww, ji.spread_n,
                                        vm->arena + dm.dev_off + (uint64_t)kp.vcpu_begin * dm.dev_stride, dm.dev_stride, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    }
+    if (kp.cancel_any) {   // the contexts' words are read until these launches end (mimic_ctx_free waits)
+        auto mark = [&](mimic_ctx *c) -> int {
+            std::lock_guard<std::mutex> lk(c->mu);
+            std::vector<hipEvent_t> keep;   // finished uses are dropped
+            for (hipEvent_t e : c->uses) {
+                if (hipEventQuery(e) == hipSuccess) hipEventDestroy(e);
+                else keep.push_back(e);
+            }
+            c->uses.swap(keep);
+            hipEvent_t ev = nullptr;
+            HIP_OK(vm, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIP_OK(vm, hipEventRecord(ev, st));
+            c->uses.push_back(ev);
+            return 0;
+        };
+        if (cx->all) {
+            if ((rc = mark(cx->all))) return rc;
+        } else {
+            std::vector<mimic_ctx *> u;
+            for (uint32_t i = 0; i < b->n; i++)
+                if (cx->per_packet[i]) u.push_back(cx->per_packet[i]);
+            std::sort(u.begin(), u.end());
+            u.erase(std::unique(u.begin(), u.end()), u.end());
+            for (mimic_ctx *c : u)
+                if ((rc = mark(c))) return rc;
+        }
     }
     vm->last_lanes = run_lanes;
     vm->last_stream = st;
@@ -2300,6 +2335,10 @@ void mimic_ctx_free(mimic_ctx *c) {
     }
     c->cv.notify_all();
     if (c->timer.joinable()) c->timer.join();
+    for (hipEvent_t e : c->uses) {
+        hipEventSynchronize(e);
+        hipEventDestroy(e);
+    }
     if (c->pinned) hipHostFree(c->word);
     else free(c->word);
     delete c;

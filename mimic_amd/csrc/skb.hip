@@ -95,21 +95,24 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
             w[4 * c + 2] = v.z;
             w[4 * c + 3] = v.w;
         }
-#ifdef MIMIC_PREP_NOWALK   // measurement only (tools/prep_probe.py): loads and footprints, no decode
-        r.len = w[0] == 0x12345678u ? SKB_LOAD_FAILED : L;
-#else
-        skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
-#endif
         // the rooms flag (skb.h SKB_DIRTY_Q): any non-zero byte in the 32 bytes before the packet
-        // or the 64 after it (rooms = 0: a measurement build whose JIT kernel reads them itself)
-        r.ip[0].pad[0] = 0;
+        // or the 64 after it (rooms = 0: a measurement build whose JIT kernel reads them itself).
+        // Loaded with the window, before the decode: one memory round trip per packet, not two
+        // (the headroom shares the window's first line; the tailroom is the packet's last line)
+        uint32_t dirty = 0;
         if (rooms) {
             const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
             u32x4u o = hr[0] | hr[1];
 #pragma unroll
             for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) o |= tr[c];
-            r.ip[0].pad[0] = (o.x | o.y | o.z | o.w) ? 1u : 0u;
+            dirty = (o.x | o.y | o.z | o.w) ? 1u : 0u;
         }
+#ifdef MIMIC_PREP_NOWALK   // measurement only (tools/prep_probe.py): loads and footprints, no decode
+        r.len = w[0] == 0x12345678u ? SKB_LOAD_FAILED : L;
+#else
+        skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
+#endif
+        r.ip[0].pad[0] = dirty;
         f = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
     }
     if (rec) {

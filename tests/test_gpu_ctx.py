@@ -296,3 +296,24 @@ def test_pool_jobs_with_contexts(gpu):
     assert all(got[k] == (20 + k, None) for k in range(16))
     vm.close()
     live.close()
+
+
+def test_context_freed_while_its_batch_runs(gpu):
+    """Freeing a context (mimic_ctx_free, here through the garbage collector) while a launch that
+    reads it runs waits for that launch: the kernel never reads freed host memory."""
+    import gc
+
+    V, P = 64, 16
+    sc = _loop_sc(V, K_LOOP)
+    vm, maps, pids = build_engine(sc)
+    buf, off, lens = packets_to_buffer([bytes(64)] * (V * P))
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_CHUNKED)
+    res = M.XDPResults.empty(V * P, "cuda:0")
+    ctx = M.WithCancel()
+    vm.RunXDPBatch(pids[0], batch, res, sync=False, ctx=ctx)
+    del ctx
+    gc.collect()
+    torch.cuda.synchronize()
+    e = res.numpy(V * P)
+    assert (e["status"] == 0).all() and (e["r0"] == K_LOOP).all()
+    vm.close()
