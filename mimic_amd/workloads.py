@@ -514,12 +514,13 @@ def flowtrack_value(keys: np.ndarray) -> np.ndarray:
         return (k[:, 0] * np.uint64(0x01000193)) ^ k[:, 1]
 
 
-def flow_keys_np(buf, off, lens) -> np.ndarray:
+def flow_keys_np(buf, off, lens, with_index: bool = False):
     """The 16-byte keys prog_flowtrack / prog_flowcount build (_flow_key_items), one row per
     packet that reaches the map call (IPv4 frames >= 38 bytes, IPv6 frames >= 58 bytes), as a
     structured view for np.unique.  Host-side workload arithmetic (no engine, no oracle): it
     bounds how many keys a cfg-4 batch inserts.  The key words are little-endian loads of the
-    frame bytes, stored as they were loaded, so a key's bytes are the frame's bytes."""
+    frame bytes, stored as they were loaded, so a key's bytes are the frame's bytes.
+    with_index: (keys, the packet index of each row)."""
     off = np.asarray(off, np.int64)
     L = np.asarray(lens, np.int64)
     ok = L >= 14
@@ -551,6 +552,8 @@ def flow_keys_np(buf, off, lens) -> np.ndarray:
     k[len(v4):, 1] = fold(v6, 38, 46)
     k[len(v4):, 2] = u32le(v6, 54)
     k[len(v4):, 3] = buf[off[v6] + 20]
+    if with_index:
+        return k, np.concatenate([v4, v6])
     return k
 
 

@@ -181,6 +181,18 @@ def test_cfg4_flowtrack_bench_size_per_key_exact(gpu):
     assert len(ocont) == len(econt) and len(ocont) > 100000
     assert ocont == econt, "key -> value contents differ"
     assert int((e["status"] != 0).sum()) == 0
+    # steps: which of a key's packets takes the insert path depends on the order concurrent vCPUs
+    # reach the map, so per key the multiset of step counts must agree (exactly one insert each);
+    # packets that never reach the map call agree one by one
+    k, idx = W.flow_keys_np(wl.buf, wl.off, wl.lens, with_index=True)
+    kid = np.full(n, -1, np.int64)
+    kid[idx] = np.unique(np.ascontiguousarray(k).view(np.dtype((np.void, 16))).ravel(), return_inverse=True)[1]
+    ost, est = np.asarray(o["steps"], np.int64), np.asarray(e["steps"], np.int64)
+    far = kid < 0
+    assert (ost[far] == est[far]).all()
+    at = ~far
+    oo, ee = np.lexsort((ost[at], kid[at])), np.lexsort((est[at], kid[at]))
+    assert (ost[at][oo] == est[at][ee]).all(), "per-key step multisets differ"
 
 
 def test_cfg5_skb_chain_bench_size_exact(gpu):
