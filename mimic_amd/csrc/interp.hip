@@ -234,6 +234,12 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         uint64_t wsteps = resumed ? steps : 0;   // wave-steps since the packets started: bounds every lane's steps
         uint32_t cand = KEY_DONE;     // speculated next key (where the first executing lane went)
         for (;;) {
+            // Run(ctx) while the process runs: every 4096 wave-steps each running lane reads its
+            // context again and stops before its next step once it is done (vm.go:344-349)
+            if (MODE != MODE_STEP && kp.cancel_any && (wsteps & 4095u) == 4095u && key != KEY_DONE) {
+                const uint32_t cz = ctx_done(kp, i);
+                if (cz) TERM(MIMIC_ERR_CANCELED - 1 + (int)cz, (int32_t)(key - pbase));
+            }
             const uint64_t live = __ballot(key != KEY_DONE);
             if (live == 0) break;
             uint32_t kw;

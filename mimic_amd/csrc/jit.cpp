@@ -1273,6 +1273,11 @@ class Gen {
                 if (!careful) {
                     E.line("  P%u_%u:", p.id, s);
                     if (careful_copies) E.line("    if (steps + %uu > kp.budget) goto C%u_%u;", e - s, p.id, s);
+                    // Run(ctx) inside a long process (loops, calls): a block that crosses a multiple
+                    // of 4096 steps reads the context again and stops before its first step once done
+                    if (careful_copies && ctx_check)
+                        E.line("    if (((steps + %uu) ^ steps) >> 12) { const uint32_t cz_ = ctx_done(kp, i); "
+                               "if (cz_) TERM(MIMIC_ERR_CANCELED - 1u + cz_, %u); }", e - s, s);
                 } else {
                     E.line("  C%u_%u:", p.id, s);
                 }

@@ -1556,12 +1556,12 @@ static int step(orc_proc *p, int32_t *err_pc) {
 /* Process.Run, vm.go:343-360: before every step the ctx is checked (done = 0: not done, 1:
  * canceled, 2: deadline exceeded -- Run returns ctx.Err() with the process where it stopped); the
  * step budget is the engine's watchdog */
-static int run(orc_proc *p, uint64_t budget, int done, uint32_t *steps, int32_t *err_pc) {
+static int run(orc_proc *p, uint64_t budget, int done, uint32_t done_step, uint32_t *steps, int32_t *err_pc) {
     uint64_t n = 0;
     int st;
     *err_pc = -1;
     for (;;) {
-        if (done) {   /* select { case <-done: return ctx.Err() } (vm.go:346-349) */
+        if (done && n >= done_step) {   /* select { case <-done: return ctx.Err() } (vm.go:346-349) */
             st = ORC_ERR_CANCELED - 1 + done;
             *err_pc = (int32_t)p->R.pc;
             break;
@@ -1705,7 +1705,7 @@ int orc_run_xdp_batch(orc_vm *vm, int prog_id, const orc_xdp_batch *b, orc_resul
         if (cpu != -1 && orc_proc_set_cpu(p, cpu)) {
             st = ORC_ERR_NO_CPU;
         } else {
-            st = run(p, budget, b->ctx_done ? b->ctx_done[i] : 0, &steps, &epc);
+            st = run(p, budget, b->ctx_done ? b->ctx_done[i] : 0, b->ctx_done_step ? b->ctx_done_step[i] : 0, &steps, &epc);
         }
         if (out->r0) out->r0[i] = p->R.r[0];
         if (out->status) out->status[i] = (uint8_t)st;
@@ -2241,7 +2241,7 @@ int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_resul
         if (!st) {
             const int cpu = b->cpu ? b->cpu[i] : 0;
             if (cpu != -1 && orc_proc_set_cpu(p, cpu)) st = ORC_ERR_NO_CPU;   /* -1: never set */
-            else st = run(p, budget, b->ctx_done ? b->ctx_done[i] : 0, &steps, &epc);
+            else st = run(p, budget, b->ctx_done ? b->ctx_done[i] : 0, b->ctx_done_step ? b->ctx_done_step[i] : 0, &steps, &epc);
         }
         if (out->r0) out->r0[i] = p->R.r[0];
         if (out->status) out->status[i] = (uint8_t)st;

@@ -161,6 +161,9 @@ typedef struct {
      * 2 (deadline exceeded) -- the state ctx.Done() / ctx.Err() show before every step (vm.go:343-350).
      * NULL = every ctx is context.Background(). */
     const uint8_t *ctx_done;
+    /* ctx_done_step[i]: the ctx is seen done before step ctx_done_step[i] (0: before the first);
+     * NULL = before the first.  (A cancel while a process runs, at the step the engine saw it.) */
+    const uint32_t *ctx_done_step;
 } orc_xdp_batch;
 
 typedef struct {
@@ -204,6 +207,7 @@ typedef struct {
     int write_back;
     const orc_skb_custom *custom;   /* [n] or NULL: the contexts' user-given SK / FlowKeys */
     const uint8_t *ctx_done;        /* as in orc_xdp_batch */
+    const uint32_t *ctx_done_step;  /* as in orc_xdp_batch */
 } orc_skb_batch;
 int orc_run_skb_batch(orc_vm *vm, int prog_id, const orc_skb_batch *b, orc_results *out);
 

@@ -25,13 +25,13 @@ class _Batch(C.Structure):
                 ("headroom_arr", C.c_void_p), ("headroom", C.c_uint32), ("tailroom_arr", C.c_void_p),
                 ("tailroom", C.c_uint32), ("ingress_ifindex", C.c_void_p), ("rx_queue_index", C.c_void_p),
                 ("egress_ifindex", C.c_void_p), ("cpu", C.c_void_p), ("step_budget", C.c_uint64),
-                ("write_back", C.c_int), ("ctx_done", C.c_void_p)]
+                ("write_back", C.c_int), ("ctx_done", C.c_void_p), ("ctx_done_step", C.c_void_p)]
 
 
 class _SkbBatch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("pkt_data", C.c_void_p), ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p),
                 ("ifindex", C.c_uint32), ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("write_back", C.c_int),
-                ("custom", C.c_void_p), ("ctx_done", C.c_void_p)]
+                ("custom", C.c_void_p), ("ctx_done", C.c_void_p), ("ctx_done_step", C.c_void_p)]
 
 
 class _Results(C.Structure):
@@ -244,10 +244,11 @@ class OracleVM:
 
     def run_xdp_batch(self, prog_id: int, buf: np.ndarray, off: np.ndarray, lens: np.ndarray, cpu: np.ndarray,
                       headroom=0, tailroom=0, ingress=None, rxq=None, egress=None, step_budget: int = 0,
-                      write_back: bool = True, ctx_done=None):
+                      write_back: bool = True, ctx_done=None, ctx_done_step=None):
         """Sequential reference run over a numpy packet buffer (modified in place if write_back).
         ctx_done: None, or per packet the state of its Run's ctx (0 not done, 1 canceled, 2
-        deadline exceeded; orc_xdp_batch.ctx_done)."""
+        deadline exceeded; orc_xdp_batch.ctx_done); ctx_done_step: per packet, the step before
+        which its ctx is seen done (None: before the first)."""
         n = len(lens)
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.uint64)
@@ -278,6 +279,7 @@ class OracleVM:
         b.step_budget = step_budget
         b.write_back = int(write_back)
         b.ctx_done = arr(ctx_done, np.uint8)
+        b.ctx_done_step = arr(ctx_done_step, np.uint32)
         out = {"r0": np.zeros(n, np.uint64), "status": np.zeros(n, np.uint8), "steps": np.zeros(n, np.uint32),
                "err_pc": np.zeros(n, np.int32)}
         r = _Results(out["r0"].ctypes.data, out["status"].ctypes.data, out["steps"].ctypes.data,
@@ -289,7 +291,8 @@ class OracleVM:
         return out
 
     def run_skb_batch(self, prog_id: int, buf: np.ndarray, off: np.ndarray, lens: np.ndarray, cpu: np.ndarray,
-                      ifindex: int = 0, step_budget: int = 0, write_back: bool = True, custom=None, ctx_done=None):
+                      ifindex: int = 0, step_budget: int = 0, write_back: bool = True, custom=None, ctx_done=None,
+                      ctx_done_step=None):
         """Sequential sk_buff-context run: packet i is lens[i] bytes at buf[off[i] + 32:]; the
         process's packet memory [off[i], off[i] + 96 + L) is written back if write_back.  custom:
         a numpy table of orc_skb_custom records (one per packet) or None."""
@@ -302,8 +305,10 @@ class OracleVM:
         if cu is not None:
             assert cu.dtype.itemsize == 136 and len(cu) == n
         cd = None if ctx_done is None else np.ascontiguousarray(ctx_done, dtype=np.uint8)
+        cs = None if ctx_done_step is None else np.ascontiguousarray(ctx_done_step, dtype=np.uint32)
         b = _SkbBatch(n, buf.ctypes.data, off.ctypes.data, lens.ctypes.data, ifindex, cpu.ctypes.data, step_budget,
-                      int(write_back), None if cu is None else cu.ctypes.data, None if cd is None else cd.ctypes.data)
+                      int(write_back), None if cu is None else cu.ctypes.data, None if cd is None else cd.ctypes.data,
+                      None if cs is None else cs.ctypes.data)
         out = {"r0": np.zeros(n, np.uint64), "status": np.zeros(n, np.uint8), "steps": np.zeros(n, np.uint32),
                "err_pc": np.zeros(n, np.int32)}
         r = _Results(out["r0"].ctypes.data, out["status"].ctypes.data, out["steps"].ctypes.data,

@@ -114,11 +114,11 @@ def packets_to_buffer(packets: Sequence[bytes], headroom=0, tailroom=0, align: i
 
 
 def run_oracle(sc: Scenario, buf, off, lens, cpu, entry: int = 0, headroom=0, tailroom=0, ingress=None,
-               rxq=None, egress=None, step_budget=0, ctx_done=None):
+               rxq=None, egress=None, step_budget=0, ctx_done=None, ctx_done_step=None):
     """ctx_done: per packet, the state of its Run's context (0 not done, 1 canceled, 2 deadline)."""
     vm, mids, pids = build_oracle(sc)
     out = vm.run_xdp_batch(pids[entry], buf.copy(), off, lens, cpu, headroom, tailroom, ingress, rxq, egress,
-                           step_budget, ctx_done=ctx_done)
+                           step_budget, ctx_done=ctx_done, ctx_done_step=ctx_done_step)
     out["maps"] = {}
     out["hash"] = {}
     for m in sc.maps:

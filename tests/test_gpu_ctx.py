@@ -317,3 +317,54 @@ def test_context_freed_while_its_batch_runs(gpu):
     e = res.numpy(V * P)
     assert (e["status"] == 0).all() and (e["r0"] == K_LOOP).all()
     vm.close()
+
+
+@pytest.mark.parametrize("mode,K", [("jit", 1_000_000), ("interp", 200_000)])
+def test_canceled_inside_running_processes(gpu, mode, K):
+    """A cancel while processes run their loops: each running process reads its context again
+    every 4096 steps (the JIT's context variant at block starts, the interpreter per 4096
+    wave-steps) and stops before its next step.  The oracle replays the batch with each canceled
+    process's context seen done before the step the device stopped at (orc ctx_done_step): R0,
+    status, steps, err_pc, packet memory and the per-CPU counters agree."""
+    V, P = 64, 4
+    sc = _loop_sc(V, K)
+    vm, maps, pids = build_engine(sc, exec_mode=mode)
+    dev = "cuda:0"
+    live = M.WithCancel()
+    one = M.XDPBatch.from_numpy(*packets_to_buffer([bytes(64)] * V), device=dev, schedule=M.SCHED_CHUNKED,
+                                step_budget=1 << 26)
+    vm.RunXDPBatch(pids[0], one, ctx=live)   # builds the kernel variant
+    t = time.monotonic()
+    vm.RunXDPBatch(pids[0], one, ctx=live)
+    t1 = time.monotonic() - t
+    vm.close()
+    vm, maps, pids = build_engine(sc, exec_mode=mode)
+    vm.RunXDPBatch(pids[0], M.XDPBatch.from_numpy(*packets_to_buffer([bytes(64)]), device=dev, step_budget=1 << 26),
+                   ctx=live)   # (build; its count reset below)
+    maps["c"].Update((0).to_bytes(4, "little"), bytes(8), 0, 0)
+    buf, off, lens = packets_to_buffer([bytes(64)] * (V * P))
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, schedule=M.SCHED_CHUNKED, step_budget=1 << 26)
+    ctx = M.WithCancel()
+    ctx.native()
+    res = M.XDPResults.empty(V * P, dev)
+    vm.RunXDPBatch(pids[0], batch, res, sync=False, ctx=ctx)
+    threading.Timer(0.4 * P * t1, ctx.Cancel).start()
+    torch.cuda.synchronize()
+    e = res.numpy(V * P)
+    e["pkt"] = batch.pkt_data.cpu().numpy()
+    e["maps"] = {"c": [maps["c"].Values(c) for c in range(V)]}
+    e["hash"] = {}
+    st = e["status"]
+    assert set(np.unique(st)) <= {0, CANCELED}
+    mid = (st == CANCELED) & (e["steps"] > 0)
+    assert mid.any(), (t1, (st == 0).mean())
+    assert (e["steps"][mid] < 2 * K + 20).all()
+    _suffix_per_lane(st, V, P)
+    cpu = W.schedule_cpu(V * P, V, "chunked")
+    done = (st == CANCELED).astype(np.uint8)
+    o = run_oracle(sc, buf, off, lens, cpu, step_budget=1 << 26, ctx_done=done,
+                   ctx_done_step=np.where(done > 0, e["steps"], 0).astype(np.uint32))
+    assert_same(o, e)
+    vm.close()
+    ctx.close()
+    live.close()
