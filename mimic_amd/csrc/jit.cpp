@@ -2026,7 +2026,9 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
             if (v.second > 0 && v.second <= MIMIC_VC_MAX_ROW && !(v.second & 7)) g.vc_ok[v.first] = v.second;
     if (no_early_loads) g.speculate = 0;
     g.spread_req = spread;
-    g.ctx_check = ctx_check;
+    // (MIMIC_JIT_CTXCHECK=1: the context variant from every entry point -- CPU compile tests)
+    static const bool ctx_env = getenv("MIMIC_JIT_CTXCHECK") && getenv("MIMIC_JIT_CTXCHECK")[0] == '1';
+    g.ctx_check = ctx_check || ctx_env;
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;

@@ -198,3 +198,27 @@ def test_every_gpu_test_kernel_generates():
             assert "mimic_jit_kernel" in J.kernel_source(*k)
             count += 1
     assert count > 20
+
+
+def test_context_variant_compiles():
+    """The Run(ctx) variant (launches given contexts): a check before each process's first step,
+    and in kernels with loops one at every block start that crosses a multiple of 4096 steps.
+    Generated in a child process with MIMIC_JIT_CTXCHECK=1 (the knob is read once per process)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    loop = A.assemble([A.mov64_imm(0, 0), "top", A.alu64("add", 0, 1), A.jmp("jlt", 0, 10, "top"), A.exit_()])[0]
+    straight = W.prog_classifier().raw
+    code = ("import sys, json; sys.path.insert(0, 'tests'); import test_jit_cpu as t; "
+            f"print(json.dumps([t._source([bytes.fromhex('{loop.hex()}')]), t._source([bytes.fromhex('{straight.hex()}')])]))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                         env=dict(os.environ, MIMIC_JIT_CTXCHECK="1"), check=True).stdout
+    s_loop, s_straight = json.loads(out.strip().splitlines()[-1])
+    assert s_loop.count("ctx_done(") >= 2 and ">> 12" in s_loop
+    assert s_straight.count("ctx_done(") == 1
+    assert "ctx_done(" not in _source([loop])
+    _compiles(s_loop)
+    _compiles(s_straight)
