@@ -316,9 +316,9 @@ int mimic_process_run(mimic_process *p, uint64_t budget, mimic_process_regs *out
  * contexts checks packet i's context before its process's first step -- a done one ends the process
  * there with MIMIC_ERR_CANCELED / MIMIC_ERR_DEADLINE, 0 steps, R0 = 0, err_pc = 0, its context Load
  * done (xdp_md rooms zeroed, sk_buff entries leaked), as Run(ctx) on a done context after NewProcess.
- * A process already running finishes (or meets its step budget): cancellation is seen per process
- * in a batch, per launch slice in mimic_process_run_ctx.  Free a context only after the runs that use
- * it completed. */
+ * A running process reads its context again every 4096 steps and stops before its next step once
+ * it is done (status as above, steps and registers where it stopped); mimic_process_run_ctx checks
+ * between launch slices.  mimic_ctx_free waits for the launches that read the context. */
 typedef struct mimic_ctx mimic_ctx;
 int mimic_ctx_new(uint64_t timeout_ns, mimic_ctx **out);
 /* the CancelFunc: Err() becomes context.Canceled, unless the context is done already */
