@@ -190,7 +190,14 @@ def test_done_while_the_batch_runs(gpu, mode, kind):
     _suffix_per_lane(st, V, P)
     ok = st == 0
     assert (e["r0"][ok] == K_LOOP).all() and (e["steps"][ok] == e["steps"][ok][0]).all()
-    assert (e["steps"][~ok] == 0).all() and (e["r0"][~ok] == 0).all()
+    # a lane's first stopped process may have been running (it re-reads its context every 4096
+    # steps); every later one stopped before its first step
+    steps = e["steps"].reshape(V, P).astype(np.int64)
+    for g in range(V):
+        d = np.nonzero(st.reshape(V, P)[g] != 0)[0]
+        if len(d):
+            assert (steps[g, d[0] + 1:] == 0).all() and steps[g, d[0]] < 2 * K_LOOP + 20
+    assert (e["r0"][~ok] == 0).all()
     vm.close()
     ctx.close()
 
@@ -224,7 +231,8 @@ def test_done_while_the_batch_runs_matches_the_oracle(gpu):
     e["maps"] = {"c": [maps["c"].Values(c) for c in range(V)]}
     e["hash"] = {}
     done = (e["status"] == DEADLINE).astype(np.uint8) * 2
-    o = run_oracle(sc, buf, off, lens, cpu, ctx_done=done)
+    o = run_oracle(sc, buf, off, lens, cpu, ctx_done=done,
+                   ctx_done_step=np.where(done > 0, e["steps"], 0).astype(np.uint32))
     assert_same(o, e)
     vm.close()
     ctx.close()
@@ -319,51 +327,46 @@ def test_context_freed_while_its_batch_runs(gpu):
     vm.close()
 
 
-@pytest.mark.parametrize("mode,K", [("jit", 1_000_000), ("interp", 200_000)])
+@pytest.mark.parametrize("mode,K", [("jit", 20_000_000), ("interp", 2_000_000)])
 def test_canceled_inside_running_processes(gpu, mode, K):
     """A cancel while processes run their loops: each running process reads its context again
     every 4096 steps (the JIT's context variant at block starts, the interpreter per 4096
-    wave-steps) and stops before its next step.  The oracle replays the batch with each canceled
-    process's context seen done before the step the device stopped at (orc ctx_done_step): R0,
-    status, steps, err_pc, packet memory and the per-CPU counters agree."""
-    V, P = 64, 4
+    wave-steps) and stops before its next step.  Each of the 8 lanes runs 2 processes of 2 K steps
+    (about a second each at this engine's rate for one wave), so a cancel 30 ms in lands inside
+    every lane's first one; without the in-process check the batch would run to its end (bounded).
+    The oracle replays the batch with each canceled process's context seen done before the step the
+    device stopped at (orc ctx_done_step): R0, status, steps, err_pc, packet memory and the per-CPU
+    counters agree."""
+    V, P = 8, 2
     sc = _loop_sc(V, K)
     vm, maps, pids = build_engine(sc, exec_mode=mode)
     dev = "cuda:0"
     live = M.WithCancel()
-    one = M.XDPBatch.from_numpy(*packets_to_buffer([bytes(64)] * V), device=dev, schedule=M.SCHED_CHUNKED,
-                                step_budget=1 << 26)
-    vm.RunXDPBatch(pids[0], one, ctx=live)   # builds the kernel variant
-    t = time.monotonic()
-    vm.RunXDPBatch(pids[0], one, ctx=live)
-    t1 = time.monotonic() - t
-    vm.close()
-    vm, maps, pids = build_engine(sc, exec_mode=mode)
     vm.RunXDPBatch(pids[0], M.XDPBatch.from_numpy(*packets_to_buffer([bytes(64)]), device=dev, step_budget=1 << 26),
-                   ctx=live)   # (build; its count reset below)
+                   ctx=live)   # builds the kernel variant (its count reset below)
     maps["c"].Update((0).to_bytes(4, "little"), bytes(8), 0, 0)
     buf, off, lens = packets_to_buffer([bytes(64)] * (V * P))
     batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, schedule=M.SCHED_CHUNKED, step_budget=1 << 26)
     ctx = M.WithCancel()
     ctx.native()
     res = M.XDPResults.empty(V * P, dev)
+    t = time.monotonic()
     vm.RunXDPBatch(pids[0], batch, res, sync=False, ctx=ctx)
-    threading.Timer(0.4 * P * t1, ctx.Cancel).start()
+    threading.Timer(0.03, ctx.Cancel).start()
     torch.cuda.synchronize()
+    wall = time.monotonic() - t
     e = res.numpy(V * P)
     e["pkt"] = batch.pkt_data.cpu().numpy()
     e["maps"] = {"c": [maps["c"].Values(c) for c in range(V)]}
     e["hash"] = {}
-    st = e["status"]
-    assert set(np.unique(st)) <= {0, CANCELED}
-    mid = (st == CANCELED) & (e["steps"] > 0)
-    assert mid.any(), (t1, (st == 0).mean())
-    assert (e["steps"][mid] < 2 * K + 20).all()
-    _suffix_per_lane(st, V, P)
+    st = e["status"].reshape(V, P)
+    steps = e["steps"].reshape(V, P)
+    assert (st == CANCELED).all(), (wall, st)
+    assert (steps[:, 0] > 0).all() and (steps[:, 0] < 2 * K).all() and (steps[:, 1] == 0).all(), steps
     cpu = W.schedule_cpu(V * P, V, "chunked")
-    done = (st == CANCELED).astype(np.uint8)
+    done = np.ones(V * P, np.uint8)
     o = run_oracle(sc, buf, off, lens, cpu, step_budget=1 << 26, ctx_done=done,
-                   ctx_done_step=np.where(done > 0, e["steps"], 0).astype(np.uint32))
+                   ctx_done_step=e["steps"].astype(np.uint32))
     assert_same(o, e)
     vm.close()
     ctx.close()
