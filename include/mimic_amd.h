@@ -372,6 +372,9 @@ typedef struct {
 } mimic_xdp_host_batch;
 /* chunks = number of sub-batches (0: about 16 MiB of packet memory each) */
 int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks);
+/* The same with Run(ctx): every sub-batch's kernel reads ctx (see mimic_run_xdp_ctx). */
+int mimic_run_xdp_host_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
+                           mimic_ctx *ctx);
 /* Pin / unpin host memory for DMA (hipHostRegister / hipHostUnregister). */
 int mimic_host_register(void *p, size_t bytes);
 int mimic_host_unregister(void *p);

@@ -2595,7 +2595,17 @@ static int slot_reserve(mimic_vm *vm, mimic_vm::Slot &sl, size_t bytes, size_t n
 // its packet window and its launch parameters; the kernel on the VM stream after them; its r0 /
 // status (and packet bytes) on the D2H stream after the kernel.  The host-side scan of sub-batch
 // c + 1 runs while sub-batch c's copies are in flight, so no O(n) pass precedes the first copy.
+static int run_xdp_host_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
+                             mimic_ctx *ctx);
 int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks) {
+    return run_xdp_host_impl(vm, prog_id, hb, chunks, nullptr);
+}
+int mimic_run_xdp_host_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
+                           mimic_ctx *ctx) {
+    return run_xdp_host_impl(vm, prog_id, hb, chunks, ctx);
+}
+static int run_xdp_host_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
+                             mimic_ctx *ctx) {
     if (!vm || !hb) return MIMIC_EINVAL;
     const uint32_t n = hb->n;
     if (n == 0) return 0;
@@ -2683,7 +2693,8 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
         r.r0 = sl.r0;
         r.status = sl.st;
         vm->kp_copy_stream = h2d;
-        rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a);
+        const CtxRun cx{ctx, nullptr};   // every sub-batch's kernel reads the run's context
+        rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a, nullptr, nullptr, ctx ? &cx : nullptr);
         vm->kp_copy_stream = nullptr;
         if (rc) return rc;
         t_run += std::chrono::duration<double, std::micro>(clk::now() - t2).count();

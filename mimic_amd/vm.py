@@ -666,7 +666,7 @@ class VM:
 
     def RunXDPHost(self, prog_id: int, buf, off, lens, schedule=L.SCHED_INTERLEAVED, cpu=None, headroom: int = 0,
                    tailroom: int = 0, ingress: int = 0, rxq: int = 0, egress: int = 0, step_budget: int = 0,
-                   chunks: int = 0, pkt_out=None, r0=None, status=None):
+                   chunks: int = 0, pkt_out=None, r0=None, status=None, ctx: Optional["Context"] = None):
         """A batch resident in HOST memory (numpy arrays): the engine pipelines H2D copies, the
         kernels and the D2H copies of r0/status (and of the packet memory into pkt_out).
         Returns (r0 uint64[n], status uint8[n]).  Register the arrays (HostRegister) for
@@ -690,7 +690,11 @@ class VM:
         hb.step_budget = step_budget
         hb.pkt_out = pkt_out.ctypes.data if pkt_out is not None else None
         hb.r0, hb.status = r0.ctypes.data, status.ctypes.data
-        _check(self.h, self.lib.mimic_run_xdp_host(self.h, prog_id, C.byref(hb), chunks), "RunXDPHost")
+        if ctx is not None:   # Run(ctx): every sub-batch's kernel reads the context
+            _check(self.h, self.lib.mimic_run_xdp_host_ctx(self.h, prog_id, C.byref(hb), chunks, ctx._device_handle()),
+                   "RunXDPHost")
+        else:
+            _check(self.h, self.lib.mimic_run_xdp_host(self.h, prog_id, C.byref(hb), chunks), "RunXDPHost")
         return r0, status
 
     def HostRegister(self, arr) -> None:
@@ -1238,7 +1242,11 @@ def _ctx_args(ctx, ctx_per_packet, n):
     if ctx_per_packet is not None:
         if len(ctx_per_packet) != n:
             raise MimicError("one context per packet")
-        arr = (C.c_void_p * n)(*[c._device_handle() if c is not None else None for c in ctx_per_packet])
+        hs = {}   # one handle per distinct context (a pool's jobs often share one)
+        for c in ctx_per_packet:
+            if c is not None and id(c) not in hs:
+                hs[id(c)] = c._device_handle()
+        arr = (C.c_void_p * n)(*[hs[id(c)] if c is not None else None for c in ctx_per_packet])
         return None, arr, arr
     return None, None, None
 

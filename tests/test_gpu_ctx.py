@@ -371,3 +371,28 @@ def test_canceled_inside_running_processes(gpu, mode, K):
     vm.close()
     ctx.close()
     live.close()
+
+
+def test_host_resident_batch_with_a_context(gpu):
+    """mimic_run_xdp_host_ctx: every sub-batch's kernel reads the run's context -- a live one
+    changes nothing, a canceled one ends every process before its first step."""
+    sc = _count_sc()
+    buf, off, lens = _packets(3000, seed=9)
+    cpu = W.schedule_cpu(len(lens), sc.vcpus, "interleaved")
+    results = []
+    for state in (0, 1):
+        vm, maps, pids = build_engine(sc)
+        c = M.WithCancel()
+        if state:
+            c.Cancel()
+        hbuf = buf.copy()
+        r0, st = vm.RunXDPHost(pids[0], hbuf, off, lens, schedule=M.SCHED_INTERLEAVED, headroom=8, tailroom=8,
+                               chunks=3, ctx=c)
+        o = run_oracle(sc, buf, off, lens, cpu, headroom=8, tailroom=8,
+                       ctx_done=np.full(len(lens), state, np.uint8))
+        assert (r0 == o["r0"]).all() and (st == o["status"]).all()
+        assert [maps["c"].Values(k) for k in range(sc.vcpus)] == o["maps"]["c"]
+        results.append(st)
+        vm.close()
+        c.close()
+    assert (results[0] == 0).all() and (results[1] == CANCELED).all()
