@@ -312,6 +312,13 @@ def parse_args(argv=None):
                     help="run the multi-GPU setup / readout collectives over RCCL even at world size 1 "
                          "(a one-GPU rehearsal of the N-rank path: program broadcast, counter all-reduce, "
                          "hash replica merge)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend of the N-rank path: nccl (= RCCL, tensors on the rank's GPU) or "
+                         "gloo (CPU tensors): with --one-device, N engine ranks share GPU 0, so the whole "
+                         "N-rank sequence runs on a one-GPU box")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank runs its engine on GPU 0 (a rehearsal of the N-rank path on one GPU; "
+                         "value is then not a scaling number)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="CPU rehearsal of the --gpus N launcher: gloo ranks run the setup / readout "
                          "collectives with no engine and rank 0 prints the launch facts")
@@ -331,7 +338,7 @@ def launch_ranks(args, argv) -> int:
     import socket
     import subprocess
 
-    if not args.launch_selftest:
+    if not args.launch_selftest and not args.one_device:
         import torch
 
         have = torch.cuda.device_count()
@@ -425,11 +432,16 @@ def main(argv=None):
 
     import torch
 
-    if torch.cuda.device_count() <= local:
+    gpu = 0 if args.one_device else local   # the device this rank's engine runs on
+    if torch.cuda.device_count() <= gpu:
         sys.stderr.write(f"bench.py rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} "
                          f"GPU(s) visible\n")
         return 2
-    use_dist = ws > 1 or args.rccl   # the collective paths (RCCL); at world size 1 only with --rccl
+    use_dist = ws > 1 or args.rccl   # the collective paths; at world size 1 only with --rccl
+    gloo = args.dist_backend == "gloo"
+    if gloo and args.rccl:
+        sys.stderr.write("bench.py: --rccl and --dist-backend gloo exclude each other\n")
+        return 2
     json_out = sys.stdout
     if use_dist:
         # RCCL writes its banner to file descriptor 1 when a communicator starts: native writes to
@@ -443,10 +455,14 @@ def main(argv=None):
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(ws))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(gpu)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+    dev = torch.device(f"cuda:{gpu}")
     torch.cuda.set_device(dev)
+    cdev = "cpu" if gloo else dev   # where the collectives' tensors live
 
     import mimic_amd as M
     from mimic_amd import dist as D
@@ -459,8 +475,8 @@ def main(argv=None):
     wl = Workload(args.config, n, W.SEED + rank, rank, ws)
 
     # program bytes: built on rank 0, broadcast over RCCL (the setup-time exchange)
-    raws = [D.broadcast_bytes(p.raw if rank == 0 else None, dev) if use_dist else p.raw for p in wl.progs]
-    vm, maps, pids = wl.build_vm(M, V, local, D.shard(vpg, rank), raws)
+    raws = [D.broadcast_bytes(p.raw if rank == 0 else None, cdev) if use_dist else p.raw for p in wl.progs]
+    vm, maps, pids = wl.build_vm(M, V, gpu, D.shard(vpg, rank), raws)
     pid = pids[0]
 
     sched = M.SCHED_INTERLEAVED if args.sched == "interleaved" else M.SCHED_CHUNKED
@@ -503,7 +519,7 @@ def main(argv=None):
     st = np.concatenate([res.status[:n].cpu().numpy() for _, _, res in batches])
     timed = [(args.warmup + k) % nb for k in range(args.steps)]
     if use_dist:
-        elapsed = D.allreduce_max_f64(elapsed, dev)
+        elapsed = D.allreduce_max_f64(elapsed, cdev)
 
     # sum-over-CPUs readout of the per-CPU counters (RCCL all-reduce across ranks); shared hash
     # maps: one replica per GPU, (key, value) records merged
@@ -514,12 +530,12 @@ def main(argv=None):
     if hm and not wl.skb:
         m0 = hm[0]
         mine = {k: v[0] for k, v in maps[m0["name"]].Contents().items()}
-        merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], dev, m0["max_entries"]) if use_dist else mine
+        merged = D.merge_hash_replicas(mine, m0["key_size"], m0["value_size"], cdev, m0["max_entries"]) if use_dist else mine
         hash_keys = len(merged)
     if pcm:
         b0, cnt = D.shard(vpg, rank)
         local_sum = maps[pcm[0]["name"]].SumU64(b0, b0 + cnt)
-        counters = D.allreduce_sum_u64(local_sum, dev) if use_dist else local_sum
+        counters = D.allreduce_sum_u64(local_sum, cdev) if use_dist else local_sum
 
     # eBPF instructions per batch (exact per-lane step counts): one more untimed launch of each
     # batch after the readout above
@@ -530,7 +546,7 @@ def main(argv=None):
         steps_of.append(vm.LastSteps())
     steps_timed = float(sum(steps_of[b] for b in timed))
     if use_dist:
-        steps_timed = float(D.allreduce_sum_u64([int(steps_timed)], dev)[0])
+        steps_timed = float(D.allreduce_sum_u64([int(steps_timed)], cdev)[0])
 
     if rank == 0:
         total_pkts = n * ws * args.steps
@@ -576,7 +592,9 @@ def main(argv=None):
             "hash_keys": hash_keys,
         }
         if use_dist:
-            out["collectives"] = f"rccl, world size {ws}"
+            out["collectives"] = f"{'gloo' if gloo else 'rccl'}, world size {ws}"
+        if args.one_device and ws > 1:
+            out["one_device"] = True   # N engine ranks shared GPU 0: a rehearsal, not a scaling point
         if not args.no_host_resident and ws == 1 and not wl.skb:
             out["host_resident"] = host_resident_rate(vm, pid, wl, sched)
         if not args.no_cpu_baseline and ws == 1:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIMIC_ABI_VERSION 1
+#define MIMIC_ABI_VERSION 2  /* 2: mimic_skb_batch.custom, statuses 29-30, MIMIC_EXEC_SPREAD */
 
 /* errors */
 #define MIMIC_EINVAL (-1)

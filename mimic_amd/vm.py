@@ -630,8 +630,8 @@ class VM:
         b = batch._c()
         r = results._c()
         st = stream.cuda_stream if stream is not None else None
-        if ctx is not None or ctx_per_packet is not None:
-            h, arr, _keep = _ctx_args(ctx, ctx_per_packet, batch.n)
+        h, arr, _keep = _ctx_args(ctx, ctx_per_packet, batch.n)
+        if h is not None or arr is not None:
             rc = self.lib.mimic_run_xdp_ctx(self.h, prog_id, b, r, st, h, arr)
         else:
             rc = self.lib.mimic_run_xdp(self.h, prog_id, b, r, st)
@@ -648,8 +648,8 @@ class VM:
         if results is None:
             results = XDPResults.empty(batch.n, batch.pkt_data.device)
         st = stream.cuda_stream if stream is not None else None
-        if ctx is not None or ctx_per_packet is not None:
-            h, arr, _keep = _ctx_args(ctx, ctx_per_packet, batch.n)
+        h, arr, _keep = _ctx_args(ctx, ctx_per_packet, batch.n)
+        if h is not None or arr is not None:
             rc = self.lib.mimic_run_skb_ctx(self.h, prog_id, batch._c(), results._c(), st, h, arr)
         else:
             rc = self.lib.mimic_run_skb(self.h, prog_id, batch._c(), results._c(), st)
@@ -690,6 +690,7 @@ class VM:
         hb.step_budget = step_budget
         hb.pkt_out = pkt_out.ctypes.data if pkt_out is not None else None
         hb.r0, hb.status = r0.ctypes.data, status.ctypes.data
+        ctx = _live(ctx)
         if ctx is not None:   # Run(ctx): every sub-batch's kernel reads the context
             _check(self.h, self.lib.mimic_run_xdp_host_ctx(self.h, prog_id, C.byref(hb), chunks, ctx._device_handle()),
                    "RunXDPHost")
@@ -1142,14 +1143,17 @@ class Context:
 
     _ERR = {1: "context canceled", 2: "context deadline exceeded"}
 
-    def __init__(self, Deadline: Optional[float] = None, Cancelled: bool = False):
+    def __init__(self, Deadline: Optional[float] = None, Cancelled: bool = False, _background: bool = False):
         self.Deadline = Deadline
         self.Cancelled = Cancelled
+        self._background = _background   # context.Background(): never done, nothing to check
         self._h = None
         self._lib = None
 
     def Cancel(self) -> None:
-        """The context's CancelFunc."""
+        """The context's CancelFunc (context.Background() has none)."""
+        if self._background:
+            raise MimicError("context.Background() cannot be canceled")
         self.Cancelled = True
         if self._h is not None:
             self._lib.mimic_ctx_cancel(self._h)
@@ -1217,8 +1221,14 @@ class Context:
 
 
 def Background() -> Context:
-    """context.Background(): never done (a run given it checks nothing)."""
-    return Context()
+    """context.Background(): never done.  A run given it takes the plain entry points (no pinned
+    word, no context-checking kernel variant, spread launches allowed), as if no context were given."""
+    return Context(_background=True)
+
+
+def _live(ctx: Optional[Context]) -> Optional[Context]:
+    """ctx, or None for context.Background() (which no kernel needs to read)."""
+    return None if ctx is None or ctx._background else ctx
 
 
 def WithCancel() -> Context:
@@ -1237,6 +1247,13 @@ def _ctx_args(ctx, ctx_per_packet, n):
     """(handle, per-packet array, keep-alive) of a run's contexts."""
     if ctx is not None and ctx_per_packet is not None:
         raise MimicError("one context for the batch or one per packet, not both")
+    ctx = _live(ctx)
+    if ctx_per_packet is not None:
+        if len(ctx_per_packet) != n:
+            raise MimicError("one context per packet")
+        ctx_per_packet = [_live(c) for c in ctx_per_packet]
+        if all(c is None for c in ctx_per_packet):
+            ctx_per_packet = None
     if ctx is not None:
         return ctx._device_handle(), None, None
     if ctx_per_packet is not None:

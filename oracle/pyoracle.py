@@ -9,7 +9,8 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# MIMIC_ORACLE_LIB: another build of the same source (tools/run_asan.sh: the sanitizer build)
+LIB_PATH = os.environ.get("MIMIC_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 
 
 class OracleError(RuntimeError):

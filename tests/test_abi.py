@@ -38,6 +38,9 @@ def test_abi_version():
     from mimic_amd import _lib
 
     assert _lib.load().mimic_abi_version() == _lib.ABI_VERSION
+    hdr = int(re.search(r"#define MIMIC_ABI_VERSION (\d+)", open(HDR).read()).group(1))
+    # 2: mimic_skb_batch grew `custom`, statuses 29/30, mimic_last_exec may return MIMIC_EXEC_SPREAD
+    assert hdr == _lib.ABI_VERSION == 2
 
 
 def test_status_numbering_matches_oracle():

@@ -48,7 +48,8 @@ K_LOOP = 50000
 
 
 def jit_kernels():
-    return [kernel_of(_count_sc()), kernel_of(_loop_sc(64, K_LOOP)), spread_kernel_of(_sc_cls(7))]
+    return [kernel_of(_count_sc()), kernel_of(_loop_sc(64, K_LOOP)), kernel_of(_pkt_loop_sc(64)),
+            spread_kernel_of(_sc_cls(7))]
 
 
 def _sc_cls(V):
@@ -137,69 +138,68 @@ def test_skb_per_packet_contexts(gpu):
     late.close()
 
 
-def _suffix_per_lane(status, V, P):
-    """Chunked schedule: lane g runs packets [g P, (g+1) P) in order; once a lane sees its context
-    done, every later process of the lane sees it too."""
-    st = status.reshape(V, P)
-    for g in range(V):
-        d = np.nonzero(st[g] != 0)[0]
-        if len(d):
-            assert (st[g, d[0]:] != 0).all(), f"lane {g}: {st[g]}"
+def _pkt_loop_sc(V):
+    """r7 counts to the packet's first u32 in a loop, then c[0] += 1 (per-CPU); r0 = r7."""
+    raw, rel = A.assemble([A.ldx(4, 2, 1, 0), A.ldx(4, 3, 2, 0), A.mov64_imm(7, 0), "top", A.alu64("add", 7, 1),
+                           A.jmp("jlt", 7, 3, "top", reg=True), A.st(4, 10, -4, 0), A.mov64_reg(2, 10),
+                           A.alu64("add", 2, -4), A.ld_map_fd(1, "c"), A.call(A.FN_MAP_LOOKUP_ELEM),
+                           A.jmp("jeq", 0, 0, "out"), A.ldx(8, 3, 0, 0), A.alu64("add", 3, 1), A.stx(8, 0, 0, 3),
+                           "out", A.mov64_reg(0, 7), A.exit_()])
+    return Scenario(vcpus=V, maps=[dict(name="c", type=6, key_size=4, value_size=8, max_entries=1)],
+                    progs=[("pktloop", raw, rel)])
+
+
+K_SHORT, K_LONG = 100, (1 << 31) + 5   # a long process runs >= 2^31 loop iterations: seconds on any lane
 
 
 @pytest.mark.parametrize("mode,kind", [("jit", "cancel"), ("jit", "deadline"), ("interp", "cancel")])
 def test_done_while_the_batch_runs(gpu, mode, kind):
-    V, P = 64, 48
-    sc = _loop_sc(V, K_LOOP)
+    """Each lane (chunked, P processes) first runs a short process, then long ones that cannot
+    finish before the context is done (0.5 s after the launch).  Whatever the box's speed, the
+    outcome is fixed: per lane the short process exits, the first long one stops inside its run
+    (it re-reads its context every 4096 steps), every later one stops before its first step."""
+    V, P = 64, 4
+    sc = _pkt_loop_sc(V)
     vm, maps, pids = build_engine(sc, exec_mode=mode)
     dev = "cuda:0"
-    # calibration: one process per lane, with a live context (also builds the kernel variant
-    # launches given contexts run)
-    b1, o1, l1 = packets_to_buffer([bytes(64)] * V)
-    cal = M.XDPBatch.from_numpy(b1, o1, l1, device=dev, schedule=M.SCHED_CHUNKED)
+    k = np.full((V, P), K_LONG, np.uint32)
+    k[:, 0] = K_SHORT
+    buf, off, lens = packets_to_buffer([int(x).to_bytes(4, "little") + bytes(60) for x in k.ravel()])
+    budget = 1 << 40
+    # the context-checking kernel variant, built and loaded before the timed launch
+    warm = M.XDPBatch.from_numpy(*packets_to_buffer([K_SHORT.to_bytes(4, "little") + bytes(60)] * V), device=dev,
+                                 schedule=M.SCHED_CHUNKED, step_budget=budget)
     live = M.WithCancel()
-    vm.RunXDPBatch(pids[0], cal, ctx=live)
-    t = time.monotonic()
-    vm.RunXDPBatch(pids[0], cal, ctx=live)
-    t1 = time.monotonic() - t
-    n = V * P
-    buf, off, lens = packets_to_buffer([bytes(64)] * n)
-    batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, schedule=M.SCHED_CHUNKED)
-    after = 0.45 * P * t1
+    vm.RunXDPBatch(pids[0], warm, ctx=live)
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device=dev, schedule=M.SCHED_CHUNKED, step_budget=budget)
     if kind == "cancel":
         ctx = M.WithCancel()
         ctx.native()
-        timer = threading.Timer(after, ctx.Cancel)
+        timer = threading.Timer(0.5, ctx.Cancel)
     else:
-        ctx = M.WithTimeout(after)
+        ctx = M.WithTimeout(0.5)
         ctx.native()
         timer = None
-    res = M.XDPResults.empty(n, dev)
-    t = time.monotonic()
+    res = M.XDPResults.empty(V * P, dev)
     vm.RunXDPBatch(pids[0], batch, res, sync=False, ctx=ctx)
     if timer is not None:
         timer.start()
     torch.cuda.synchronize()
-    wall = time.monotonic() - t
-    e = res.numpy(n)
+    e = res.numpy(V * P)
     want = CANCELED if kind == "cancel" else DEADLINE
-    st = e["status"]
-    assert set(np.unique(st)) <= {0, want}
-    assert (st == 0).any() and (st == want).any(), (t1, after, wall, (st == 0).mean())
-    assert wall < 0.9 * P * t1 + 0.5
-    _suffix_per_lane(st, V, P)
-    ok = st == 0
-    assert (e["r0"][ok] == K_LOOP).all() and (e["steps"][ok] == e["steps"][ok][0]).all()
-    # a lane's first stopped process may have been running (it re-reads its context every 4096
-    # steps); every later one stopped before its first step
+    st = e["status"].reshape(V, P)
     steps = e["steps"].reshape(V, P).astype(np.int64)
-    for g in range(V):
-        d = np.nonzero(st.reshape(V, P)[g] != 0)[0]
-        if len(d):
-            assert (steps[g, d[0] + 1:] == 0).all() and steps[g, d[0]] < 2 * K_LOOP + 20
-    assert (e["r0"][~ok] == 0).all()
+    r0 = e["r0"].reshape(V, P)
+    assert (st[:, 0] == 0).all() and (r0[:, 0] == K_SHORT).all()
+    assert (steps[:, 0] == steps[0, 0]).all()
+    assert (st[:, 1:] == want).all()
+    assert ((steps[:, 1] > 2 * K_SHORT) & (steps[:, 1] < 2 * K_LONG)).all()   # stopped inside its run
+    assert (steps[:, 2:] == 0).all() and (r0[:, 1:] == 0).all()
+    # only the short processes counted
+    assert all(int(np.frombuffer(maps["c"].Values(c), np.uint64)[0]) == 2 for c in range(V))
     vm.close()
     ctx.close()
+    live.close()
 
 
 def test_done_while_the_batch_runs_matches_the_oracle(gpu):
