@@ -338,6 +338,14 @@ int mimic_run_skb_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *bat
  * slices; a done context returns MIMIC_ECANCELED / MIMIC_EDEADLINE (text: Go's ctx.Err() string)
  * with *out holding the suspended process (Run / Step continue it).  budget 0: no step budget. */
 int mimic_process_run_ctx(mimic_process *p, uint64_t budget, mimic_ctx *ctx, mimic_process_regs *out);
+/* processPool's workers (vm.go:548-573): n x Process.Run(ctx) of fresh (never stepped or run) sk_buff
+ * processes of one VM, program and ifindex, as ONE device launch instead of one launch per process.
+ * Each process keeps the sock / flow-keys / packet addresses its Load reserved at NewProcess and runs
+ * on its SetCPUID vCPU (-1 and V allowed); a vCPU's processes run in array order.  ctxs: HOST array
+ * [n] of contexts (NULL entries, or ctxs NULL: Background), no step budget.  Afterwards every process
+ * is finished: out[i] (optional, [n]) and the process hold R0, status, steps; a batch lane keeps no
+ * R1-R10 (zero) and pc is the failing instruction or -1.  Not in the reference API. */
+int mimic_process_run_many(mimic_process *const *ps, uint32_t n, mimic_ctx *const *ctxs, mimic_process_regs *out);
 
 /* The process's packet memory (headroom + packet + tailroom) as the program left it. */
 int mimic_process_packet(mimic_process *p, void *buf, size_t cap);

@@ -41,9 +41,11 @@ extern "C" int mimic_launch_spread_reduce(const void *part, uint32_t nblocks, ui
                                           uint8_t *dst, uint64_t stride, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
                                     hipStream_t st);
+extern "C" int mimic_launch_skb_gather(const uint8_t *const *mem, uint32_t n, uint64_t *drv, uint64_t *prefix,
+                                       mimic_skb_custom *cust, const uint8_t *has_cust, hipStream_t st);
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
-                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, hipStream_t st);
+                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse, hipStream_t st);
 
 namespace {
 
@@ -193,6 +195,10 @@ struct mimic_vm {
     uint64_t *d_skb_drv = nullptr;   // the prep kernel's derived record words, SKB_DERIVED_Q per packet
     uint64_t *d_skb_prefix = nullptr, *d_skb_state = nullptr;
     size_t skb_cap = 0;
+    // mimic_process_run_many: the gathered descriptors, records, prefixes, custom entries and results
+    // of the processes of one launch (one allocation, grown as needed)
+    uint8_t *d_many = nullptr;
+    size_t many_cap = 0;
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
     hipStream_t skb_stream = nullptr;
     bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
@@ -684,6 +690,7 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_skb_rec);
     hipFree(vm->d_skb_drv);
     hipFree(vm->d_skb_prefix);
+    hipFree(vm->d_many);
     hipFree(vm->d_skb_state);
     if (vm->s_h2d) hipStreamDestroy(vm->s_h2d);
     if (vm->s_h2d2) hipStreamDestroy(vm->s_h2d2);
@@ -1407,6 +1414,9 @@ int mimic_mem_load(mimic_vm *vm, uint32_t addr, int32_t size, uint64_t *out) {
 struct SkbRun {     // the sk_buff part of a batch (mimic_run_skb)
     uint32_t ifindex;
     const mimic_skb_custom *custom;   // device, [n] or null
+    // processes whose Load ran at NewProcess (mimic_process_run_many): their derived record words,
+    // absolute leak addresses (+ flags) and a zero base, gathered -- no prep kernel for this batch
+    const uint64_t *pre_drv = nullptr, *pre_prefix = nullptr, *pre_base = nullptr;
 };
 struct StepRun {    // a stepped single process (mimic_process_*): its state, private memory and budget
     StepState *state;
@@ -1498,12 +1508,33 @@ struct SkbInto {
     SkbRec *rec;
     uint64_t *prefix;   // 2 words (skb.h skb_leak_pre)
 };
+static int skb_ensure(mimic_vm *vm, uint32_t n, hipStream_t st);
 static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, const SkbInto *into = nullptr,
-                       bool records = true) {
+                       bool records = true, bool sparse = false) {
     const uint32_t n = b->n;
     if (vm->skb_stream && vm->skb_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
     // batches released on a stream the caller may have destroyed since: ordered through their event
     if (vm->skb_release_pending) HIP_OK(vm, hipStreamWaitEvent(st, vm->skb_ev, 0));
+    int rc0 = skb_ensure(vm, n, st);
+    if (rc0) return rc0;
+    // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
+    const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
+    // a batch's derived words go to the compact array (read by skb_load*), a process's into its record
+    uint64_t *out = into ? (uint64_t *)into->rec : records ? vm->d_skb_drv : nullptr;
+    const uint32_t out_q = into ? (uint32_t)(sizeof(SkbRec) / 8) : SKB_DERIVED_Q;
+    // MIMIC_SKB_ROOMS_CHAIN=1 (measurement, JIT batches only): the chain kernel reads the rooms itself
+    static const bool rooms_chain = getenv("MIMIC_SKB_ROOMS_CHAIN") && getenv("MIMIC_SKB_ROOMS_CHAIN")[0] == '1';
+    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
+                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : 1u,
+                              (sparse && !into) ? 1u : 0u, st))
+        return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
+    if (n) vm->skb_leaked = true;
+    vm->skb_stream = st;
+    return 0;
+}
+
+// the VM's sk_buff batch arrays for n packets (records, derived words, prefixes) and its leak state
+static int skb_ensure(mimic_vm *vm, uint32_t n, hipStream_t st) {
     if (n > vm->skb_cap || !vm->d_skb_state) {
         HIP_OK(vm, hipStreamSynchronize(st));
         hipFree(vm->d_skb_rec);
@@ -1523,18 +1554,6 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
         }
         vm->skb_cap = cap;
     }
-    // the first leak follows the stack and sk_buff entries: St + S + 1 + 193
-    const uint64_t init = (uint64_t)vm->next_addr + stack_size(vm) + 1 + SKB_STRUCT_SIZE + 1;
-    // a batch's derived words go to the compact array (read by skb_load*), a process's into its record
-    uint64_t *out = into ? (uint64_t *)into->rec : records ? vm->d_skb_drv : nullptr;
-    const uint32_t out_q = into ? (uint32_t)(sizeof(SkbRec) / 8) : SKB_DERIVED_Q;
-    // MIMIC_SKB_ROOMS_CHAIN=1 (measurement, JIT batches only): the chain kernel reads the rooms itself
-    static const bool rooms_chain = getenv("MIMIC_SKB_ROOMS_CHAIN") && getenv("MIMIC_SKB_ROOMS_CHAIN")[0] == '1';
-    if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
-                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : 1u, st))
-        return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
-    if (n) vm->skb_leaked = true;
-    vm->skb_stream = st;
     return 0;
 }
 
@@ -1927,12 +1946,24 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.skb_prefix = step->skb_prefix;
         kp.skb_base = step->skb_base;
         kp.skb_custom = step->skb_custom;
-    } else if (skb) {
-        // a JIT kernel that walks the headers itself needs the footprints only
-        const bool own_recs = jit && ji.skb_walk;
-        rc = skb_prepare(vm, b, st, nullptr, !own_recs);
+    } else if (skb && skb->pre_drv) {   // processes loaded at NewProcess (mimic_process_run_many)
+        rc = skb_ensure(vm, b->n, st);   // kp.skb_rec: where deferred lanes and the interpreter keep records
         if (rc) return rc;
-        kp.skb_rec_built = own_recs ? 0u : 1u;
+        kp.ctx_kind = CTX_SKB;
+        kp.skb_ifindex = skb->ifindex;
+        kp.skb_rec = vm->d_skb_rec;
+        kp.skb_drv = skb->pre_drv;
+        kp.skb_prefix = skb->pre_prefix;
+        kp.skb_base = skb->pre_base;
+        kp.skb_custom = skb->custom;
+        vm->skb_stream = st;
+    } else if (skb) {
+        // a JIT kernel that walks the headers itself needs the footprints only; one that derives the
+        // common frames' records itself (skb_load_fast): exception records only
+        const bool own_recs = jit && ji.skb_walk, sparse = jit && ji.skb_fast;
+        rc = skb_prepare(vm, b, st, nullptr, !own_recs, sparse);
+        if (rc) return rc;
+        kp.skb_rec_built = own_recs ? 0u : sparse ? 2u : 1u;
         kp.ctx_kind = CTX_SKB;
         kp.skb_ifindex = skb->ifindex;
         kp.skb_rec = vm->d_skb_rec;
@@ -2369,6 +2400,115 @@ int mimic_process_run_ctx(mimic_process *p, uint64_t budget, mimic_ctx *ctx, mim
         if (slice < (1ull << 20)) slice <<= 1;
     }
     process_regs(p, out);
+    return 0;
+}
+
+// n x Process.Run(ctx) of fresh sk_buff processes of one VM, program and ifindex as ONE launch
+// (processPool's workers, vm.go:548-573): each process keeps the addresses its Load reserved at
+// NewProcess (gathered from its own record, mimic_launch_skb_gather) and runs on vCPU p->cpu in
+// array order; a vCPU's processes run in that order.  No step budget (Run(ctx) with ctxs, or
+// Background).  Afterwards each process is finished: R0, status, steps in out[i] (and its host
+// state); registers R1-R10 and the PC are not kept by a batch lane (out[i].r[1..10] = 0, pc = the
+// failing instruction or -1).  Packet memory is the process's own (mimic_process_packet).
+int mimic_process_run_many(mimic_process *const *ps, uint32_t n, mimic_ctx *const *ctxs, mimic_process_regs *out) {
+    if (!ps || !n) return n ? MIMIC_EINVAL : 0;
+    mimic_vm *vm = ps[0] ? ps[0]->vm : nullptr;
+    if (!vm) return MIMIC_EINVAL;
+    const uint32_t prog = ps[0]->prog, ifindex = ps[0]->ifindex;
+    uint8_t *lo = nullptr;
+    bool any_cust = false;
+    for (uint32_t i = 0; i < n; i++) {
+        const mimic_process *p = ps[i];
+        if (!p || p->vm != vm) return fail(vm, MIMIC_EINVAL, "process %u: not a process of this VM", i);
+        if (!p->skb) return fail(vm, MIMIC_ENOTSUP, "process %u: not an sk_buff process", i);
+        if (p->prog != prog || p->ifindex != ifindex)
+            return fail(vm, MIMIC_EINVAL, "process %u: one program and one interface per launch", i);
+        if (p->h.started) return fail(vm, MIMIC_EINVAL, "process %u: already started (Run / Step it instead)", i);
+        if (!lo || p->d_pkt < lo) lo = p->d_pkt;
+        any_cust |= p->skb_custom;
+    }
+    hipSetDevice(vm->s.device);
+    hipStream_t st = vm->stream;
+    const uint32_t nb = (n + 255) / 256;
+    // one device block: pkt_off | pkt_len | mem pointers | drv | prefix | base | has_cust | custom | results
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_off = 0, o_len = o_off + al((size_t)n * 8), o_mem = o_len + al((size_t)n * 4),
+                 o_drv = o_mem + al((size_t)n * 8), o_pre = o_drv + al((size_t)n * 8 * SKB_DERIVED_Q),
+                 o_base = o_pre + al(((size_t)n + nb) * 8), o_hc = o_base + 256, o_cu = o_hc + al(n),
+                 o_r0 = o_cu + (any_cust ? al((size_t)n * sizeof(mimic_skb_custom)) : 0), o_st = o_r0 + al((size_t)n * 8),
+                 o_steps = o_st + al(n), o_epc = o_steps + al((size_t)n * 4), total = o_epc + al((size_t)n * 4);
+    if (total > vm->many_cap) {
+        HIP_OK(vm, hipStreamSynchronize(st));
+        hipFree(vm->d_many);
+        vm->d_many = nullptr;
+        HIP_OK(vm, hipMalloc(&vm->d_many, total));
+        vm->many_cap = total;
+    }
+    uint8_t *D = vm->d_many;
+    std::vector<uint8_t> host(o_drv);   // the host-made part: offsets, lengths, record pointers
+    std::vector<int32_t> cpu(n);
+    std::vector<uint8_t> hc(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const mimic_process *p = ps[i];
+        const uint64_t off = (uint64_t)(p->d_pkt - lo);
+        const uint32_t len = p->len;
+        const uint8_t *m = p->d_skbmem;
+        memcpy(host.data() + o_off + 8 * (size_t)i, &off, 8);
+        memcpy(host.data() + o_len + 4 * (size_t)i, &len, 4);
+        memcpy(host.data() + o_mem + 8 * (size_t)i, &m, 8);
+        cpu[i] = p->cpu;
+        hc[i] = p->skb_custom ? 1 : 0;
+    }
+    HIP_OK(vm, hipMemcpyAsync(D, host.data(), o_drv, hipMemcpyHostToDevice, st));
+    HIP_OK(vm, hipMemsetAsync(D + o_base, 0, 8, st));
+    if (any_cust) HIP_OK(vm, hipMemcpyAsync(D + o_hc, hc.data(), n, hipMemcpyHostToDevice, st));
+    if (mimic_launch_skb_gather((const uint8_t *const *)(D + o_mem), n, (uint64_t *)(D + o_drv), (uint64_t *)(D + o_pre),
+                                any_cust ? (mimic_skb_custom *)(D + o_cu) : nullptr, D + o_hc, st))
+        return fail(vm, MIMIC_EDEVICE, "gather: %s", hipGetErrorString(hipGetLastError()));
+    mimic_xdp_batch b{};
+    b.n = n;
+    b.schedule = MIMIC_SCHED_EXPLICIT;
+    b.pkt_data = lo;
+    b.pkt_off = (const uint64_t *)(D + o_off);
+    b.pkt_len = (const uint32_t *)(D + o_len);
+    b.cpu = cpu.data();
+    b.step_budget = ~0ull >> 1;   // Run(ctx): no budget
+    mimic_xdp_results r{};
+    r.r0 = (uint64_t *)(D + o_r0);
+    r.status = D + o_st;
+    r.steps = (uint32_t *)(D + o_steps);
+    r.err_pc = (int32_t *)(D + o_epc);
+    SkbRun skr{ifindex, any_cust ? (const mimic_skb_custom *)(D + o_cu) : nullptr};
+    skr.pre_drv = (const uint64_t *)(D + o_drv);
+    skr.pre_prefix = (const uint64_t *)(D + o_pre);
+    skr.pre_base = (const uint64_t *)(D + o_base);
+    CtxRun cx{nullptr, ctxs};
+    int rc = run_xdp_impl(vm, prog, &b, &r, st, 0, &skr, nullptr, ctxs ? &cx : nullptr);
+    if (rc) return rc;
+    std::vector<uint8_t> res(total - o_r0);
+    HIP_OK(vm, hipMemcpyAsync(res.data(), D + o_r0, res.size(), hipMemcpyDeviceToHost, st));
+    HIP_OK(vm, hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n; i++) {
+        mimic_process *p = ps[i];
+        uint64_t r0;
+        uint32_t steps;
+        int32_t epc;
+        memcpy(&r0, res.data() + 8 * (size_t)i, 8);
+        memcpy(&steps, res.data() + (o_steps - o_r0) + 4 * (size_t)i, 4);
+        memcpy(&epc, res.data() + (o_epc - o_r0) + 4 * (size_t)i, 4);
+        const uint8_t status = res[(o_st - o_r0) + i];
+        memset(p->h.r, 0, sizeof p->h.r);
+        p->h.r[0] = r0;
+        p->h.pc = status ? epc : -1;
+        p->h.prog = prog;
+        p->h.steps = steps;
+        p->h.status = status;
+        p->h.started = 1;
+        p->h.finished = 1;
+        p->static_next = vm->next_addr;
+        p->arena = vm->arena;
+        process_regs(p, out ? out + i : nullptr);
+    }
     return 0;
 }
 

@@ -120,6 +120,10 @@ class Gen {
         skb_lds_knob = !(sl && sl[0] == '0');
         const char *sw = getenv("MIMIC_JIT_SKBWALK");   // 1: the kernel builds its sk_buff records (measured slower)
         skb_walk_knob = sw && sw[0] == '1';
+        const char *sfa = getenv("MIMIC_JIT_SKBFAST");   // 1: common frames' records derived in the kernel
+        skb_fast_knob = sfa && sfa[0] == '1';
+        const char *stc = getenv("MIMIC_JIT_SKBTOUCH");   // 0: no next-descriptor prefetch / header touch
+        skb_touch_knob = stc ? (uint32_t)atoi(stc) : 0u;   // 1: prefetch + touch, 2: the offset prefetch only
         const char *sml = getenv("MIMIC_JIT_SMLDS");
         sm_lds_knob = !(sml && sml[0] == '0');
         const char *ic = getenv("MIMIC_JIT_INC");   // 0: counter increments as three slots
@@ -189,6 +193,17 @@ class Gen {
     // V = 128K -- the walk on the chain's critical path costs more than the record round trip)
     bool skb_walk_knob = false;
     bool skb_walk = false;
+    // the kernel derives the record of every frame skb_fast takes from the packet's first bytes
+    // (skb_load_fast); the prep kernel writes records for the other frames only (sparse prep)
+    bool skb_fast_knob = false;   // (measured slower on MI355X: DESIGN.md 6.1)
+    bool skb_fast = false;
+    // sk_buff kernels (prep records in LDS), MIMIC_JIT_SKBTOUCH=1/2: the next packet's offset is loaded
+    // while the current one runs, and (1) a packet's header lines are touched when its record load is
+    // issued, so the programs' LD_ABS / direct packet loads find them in L2.  Off: the cfg-5 chain sits
+    // at 255 VGPRs, and either form takes it to 256 + 2 AGPRs -- one wave per SIMD, 0.22 -> 0.36 ms
+    // (profiles/r05/)
+    uint32_t skb_touch_knob = 0;
+    bool skb_touch = false;
     bool inc_knob = true;      // MIMIC_JIT_INC=0: no fused counter increments (fusable_inc)
     bool sm_lds_knob = true;   // MIMIC_JIT_SMLDS=0: stack validity masks in VGPRs in defer mode too
     static constexpr uint32_t kSrecQ = 21;   // 8-byte words per LDS record slot (SkbRec is 20)
@@ -425,6 +440,7 @@ class Gen {
         // words: lanes reading the same field hit different banks); nothing reads them back
         if (skb_lds) E.line("  __shared__ uint64_t srec_[%uu * 256u];", kSrecQ);
         skb_walk = skb_lds && skb_walk_knob;
+        skb_fast = skb_lds && !skb_walk && skb_fast_knob;
         if (skb_walk) E.line("  __shared__ uint32_t swin_[(SKB_WIN / 4u) * 256u];   // header windows (skb_load_walk)");
         E.line("  Lane L;");
         E.line("  Spill sp_;");
@@ -486,6 +502,11 @@ class Gen {
         // length are loaded while packet j runs (they travel with packet j's first loads), which
         // takes one dependent HBM round trip off every packet after the first.
         const bool pf = ctx == CTX_XDP && prefetch;
+        skb_touch = ctx == CTX_SKB && skb_lds && !skb_walk && !skb_fast && skb_touch_knob != 0 && !spread_on;
+        if (skb_touch) {
+            E.line("  uint64_t noff_ = 0;   // the next packet's offset (skb_touch)");
+            E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) noff_ = *gp(kp.pkt_off + n_); }");
+        }
         if (!spec_use.empty() && !spread_on) analyze_xpf();
         if (pf && xpf.on) {
             // descriptors two packets ahead, the window one packet ahead (analyze_xpf)
@@ -555,7 +576,22 @@ class Gen {
             E.line("    uint64_t r1 = 0;");
             if (skb_walk)   // the process's SkbRec built in this lane's LDS slot: every field access reads LDS
                 E.line("    const int ls_ = skb_load_walk(kp, L, i, r1, srec_ + %uu * threadIdx.x, swin_);", kSrecQ);
-            else if (skb_lds)   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
+            else if (skb_fast)   // derived here from the header bytes (exception frames: the prep's words), into the LDS slot
+                E.line("    const int ls_ = skb_load_fast(kp, L, i, r1, srec_ + %uu * threadIdx.x, *gp(kq_.pkt_off + i), *gp(kq_.pkt_len + i), *gp(kq_.skb_prefix + i));", kSrecQ);
+            else if (skb_touch) {
+                E.line("    const uint64_t poff_ = noff_;");
+                E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) noff_ = *gp(kp.pkt_off + n_); }");
+                // two dwords: packet bytes 14 and 38 (the Ethernet / IP / transport headers span at most
+                // two 64-byte halves of a 128-byte line whatever the slot's alignment); consumed at the
+                // packet's end, so the wait for them is long past
+                if (skb_touch_knob == 1) {
+                    E.line("    const uint32_t th0_ = *gp((const uint32_t *)(kq_.pkt_data + poff_ + SKB_HEADROOM + 12u));");
+                    E.line("    const uint32_t th1_ = *gp((const uint32_t *)(kq_.pkt_data + poff_ + SKB_HEADROOM + 36u));");
+                }
+                E.line("    const int ls_ = skb_load_lds_po(kp, L, i, r1, srec_ + %uu * threadIdx.x, poff_);", kSrecQ);
+                // consumed where the record's own wait already covers them (issued before it)
+                if (skb_touch_knob == 1) E.line("    asm volatile(\"\" :: \"v\"(th0_), \"v\"(th1_));");
+            } else if (skb_lds)   // the process's SkbRec into this lane's LDS slot: every field access reads LDS
                 E.line("    const int ls_ = skb_load_lds(kp, L, i, r1, srec_ + %uu * threadIdx.x);", kSrecQ);
             else
                 E.line("    const int ls_ = skb_load(kp, L, i, r1);");
@@ -1082,8 +1118,13 @@ class Gen {
     // the base of a fused increment -- nothing else (no load or store through it, no store of it,
     // no helper argument).  Allowed helpers: map_lookup_elem on that per-CPU array (R1 an
     // LD_IMM64 of its object in the block) and get_smp_processor_id; no tail calls, BPF-to-BPF
-    // calls or loops (no budget checks).  What the analysis cannot see -- an address the program
-    // computes into per-CPU memory -- reaches resolve(), which marks the launch (SPREAD_GUARD).
+    // calls or loops (no budget checks).  Every other load or store must go through a base the
+    // analysis can place (base provenance, `u` below): derived from R1 (the xdp_md context), R10 (the
+    // stack) or a packet pointer loaded from the context's data / data_end / data_meta fields.  A
+    // base built from an LD_IMM64 constant, loaded from memory, returned by a helper or computed from
+    // scalars alone may address per-CPU memory (memory_controller.go:117-145 resolves any address),
+    // so such a program set runs one lane per vCPU.  resolve()'s SPREAD_GUARD stays as an internal
+    // assertion of this analysis.
     bool analyze_spread() {
         if (!spread_req || ctx != CTX_XDP || !fast_paths || !cold_inline || careful_copies || any_local || any_tail ||
             stage || census || !inc_knob || live.empty())
@@ -1095,16 +1136,25 @@ class Gen {
             const std::vector<uint32_t> Lb = leaders(p);
             std::map<uint32_t, size_t> blk;
             for (size_t b = 0; b < Lb.size(); b++) blk[Lb[b]] = b;
-            std::vector<uint16_t> in(Lb.size(), 0);
+            // may-sets per register (bit r): t = may hold a value pointer of the spread map's
+            // lookup; u = may be an address of unknown provenance; nc = may not be the context pointer
+            constexpr uint16_t ALLR = 0x7ff;
+            std::vector<uint16_t> in(Lb.size(), 0), in_u(Lb.size(), 0), in_nc(Lb.size(), 0);
             std::vector<bool> seen(Lb.size(), false);
             seen[0] = true;
+            in_u[0] = (uint16_t)(ALLR & ~((1u << 1) | (1u << 10)));
+            in_nc[0] = (uint16_t)(ALLR & ~(1u << 1));
             for (bool changed = true; changed;) {
                 changed = false;
                 for (size_t b = 0; b < Lb.size(); b++) {
                     if (!seen[b]) continue;
                     const uint32_t s0 = Lb[b], e = b + 1 < Lb.size() ? Lb[b + 1] : p.n;
-                    uint16_t t = in[b];
+                    uint16_t t = in[b], u = in_u[b], nc = in_nc[b];
                     auto tn = [&](uint32_t r) { return r <= 10 && ((t >> r) & 1); };
+                    auto un = [&](uint32_t r) { return r > 10 || ((u >> r) & 1); };
+                    auto setb = [](uint16_t &m, uint32_t r, bool v) {
+                        if (r <= 10) m = v ? (uint16_t)(m | (1u << r)) : (uint16_t)(m & ~(1u << r));
+                    };
                     for (uint32_t i = s0; i < e; i++) {
                         const DInsn &x = p.ins[i];
                         const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x), op = insn_op(x);
@@ -1117,10 +1167,17 @@ class Gen {
                             const bool mov = (op & 0xf0) == 0xb0;
                             const bool v = (X && tn(sr)) || (!mov && tn(d));
                             t = v ? (uint16_t)(t | (1u << d)) : (uint16_t)(t & ~(1u << d));
+                            // provenance: a move copies it (an immediate has none); arithmetic keeps the
+                            // pointer operand's (pointer + scalar), scalars alone have none
+                            if (mov) setb(u, d, !X || un(sr));
+                            else setb(u, d, un(d) && (!X || un(sr)));
+                            setb(nc, d, !mov || !X || ((nc >> sr) & 1));
                             break;
                         }
-                        case H_LDIMM:
+                        case H_LDIMM:   // a constant (map object, map value address, number): no provenance
                             if (d <= 10) t &= (uint16_t)~(1u << d);
+                            setb(u, d, true);
+                            setb(nc, d, true);
                             break;
                         case H_LDX:
                             if (tn(sr)) {   // through a value pointer: a fused increment, nothing else
@@ -1129,17 +1186,27 @@ class Gen {
                                 if (n && n != w) return false;
                                 n = w;
                                 t &= (uint16_t)~(1u << d);   // the counter register, dead after the store
+                                setb(u, d, true);
+                                setb(nc, d, true);
                                 i += 2;
                                 break;
                             }
+                            if (un(sr)) return false;   // a base of unknown provenance
                             if (d <= 10) t &= (uint16_t)~(1u << d);
+                            // the xdp_md packet pointers (data, data_end, data_meta: context_xdp_md.go:
+                            // 117-133) keep a provenance; any other loaded value has none
+                            setb(u, d, !(sr <= 10 && !((nc >> sr) & 1) && (insn_off(x) == 0 || insn_off(x) == 4 || insn_off(x) == 8)));
+                            setb(nc, d, true);
                             break;
                         case H_ST: case H_STX:
                             if (tn(d)) return false;                  // a store through a value pointer
                             if (h == H_STX && tn(sr)) return false;   // a value pointer stored to memory
+                            if (un(d)) return false;                  // a base of unknown provenance
                             break;
                         case H_CALL: {
                             const uint32_t k = (uint32_t)x.k;
+                            u |= 0x3f;   // R0 - R5 after a helper: a result or clobbered
+                            nc |= 0x3f;
                             if (k == 8) {   // get_smp_processor_id: R0 = the packet's vCPU
                                 t &= (uint16_t)~1u;
                                 break;
@@ -1158,7 +1225,13 @@ class Gen {
                         }
                         case H_SLOW:
                             if ((op & 7) == 1) return false;   // an LDX error form (generic load)
+                            // ST / STX class forms (atomics ...): a store through dst
+                            if (((op & 7) == 2 || (op & 7) == 3) && (tn(d) || un(d))) return false;
                             if (d <= 10) t = (tn(d) || (X && tn(sr))) ? (uint16_t)(t | (1u << d)) : (uint16_t)(t & ~(1u << d));
+                            if ((op & 7) == 0 || (op & 7) == 4 || (op & 7) == 7) {   // LD / ALU forms: no provenance kept
+                                setb(u, d, true);
+                                setb(nc, d, true);
+                            }
                             break;
                         default:   // LD_ABS / LD_IND, BPF-to-BPF
                             return false;
@@ -1172,10 +1245,13 @@ class Gen {
                     for (int64_t sx : succ) {
                         auto it = blk.find((uint32_t)sx);
                         if (it == blk.end()) continue;
-                        const uint16_t nin = (uint16_t)(in[it->second] | t);
-                        if (!seen[it->second] || nin != in[it->second]) {
-                            in[it->second] = nin;
-                            seen[it->second] = true;
+                        const size_t q = it->second;
+                        const uint16_t nin = (uint16_t)(in[q] | t), nu = (uint16_t)(in_u[q] | u), nn = (uint16_t)(in_nc[q] | nc);
+                        if (!seen[q] || nin != in[q] || nu != in_u[q] || nn != in_nc[q]) {
+                            in[q] = nin;
+                            in_u[q] = nu;
+                            in_nc[q] = nn;
+                            seen[q] = true;
                             changed = true;
                         }
                     }
@@ -2038,6 +2114,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->cold_inline = g.cold_inline;
         info->defer = g.defer_mode;
         info->skb_walk = g.skb_walk;
+        info->skb_fast = g.skb_fast;
         info->karg = g.karg != 0;
         info->spread = g.spread_on;
         info->spread_map = g.spread_map;

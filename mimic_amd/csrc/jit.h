@@ -18,6 +18,7 @@ struct JitInfo {
     bool karg;           // the kernel takes KParams by value (kernarg segment), not a device copy
     bool defer;          // slow paths are deferred to the interpreter's resume kernel (launch it after)
     bool skb_walk;       // sk_buff kernel that builds its SkbRecs itself (prep: footprints only)
+    bool skb_fast;       // sk_buff kernel that derives the records of common frames itself (sparse prep)
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
     // spread kernels: the counted per-CPU array, counter width, counters per row, LDS table rows
     uint32_t spread_map, spread_n, spread_roww, spread_rows;

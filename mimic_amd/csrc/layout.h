@@ -210,7 +210,9 @@ struct KParams {
     uint32_t *defer_any;
     uint32_t defer_epoch;
     // sk_buff batches: 1 when the prep kernel wrote every packet's SkbRec; 0 when the JIT kernel
-    // builds them itself (skb_load_walk) -- then the interpreter builds the ones it needs
+    // builds them itself (skb_load_walk) -- then the interpreter builds the ones it needs; 2 when
+    // the prep wrote the derived words of the frames skb_fast rejects only (skb_prefix flag
+    // SKB_PFX_EXC, skb.h) and the JIT kernel derives the rest (skb_load_fast)
     uint32_t skb_rec_built;
     // spread launches (jit.cpp analyze_spread): a vCPU's packets run on many lanes; a generic
     // access that reaches per-CPU map memory would break that mode's exactness and sets *spread_bad

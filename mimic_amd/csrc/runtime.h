@@ -1012,13 +1012,18 @@ static_assert(SKB_HEADROOM == 32 && SKB_TAILROOM == 64, "skb_rooms_clear covers 
 // them in LDS) the record is built here first, unless `attach_only` (a process the resume kernel
 // re-attaches: its record, rooms and packet are what the JIT lane left).
 // packet i's leak prefix: within its prep block + the block's offset (skb.hip)
+// (the word's top bits are the prep kernel's flags, skb.h SKB_PFX_*)
 DEV uint64_t skb_leak_pre(const KParams &kp, uint32_t i) {
-    return kp.skb_prefix[i] + kp.skb_prefix[kp.n + (i >> SKB_PREP_LOG2)];
+    return (kp.skb_prefix[i] & SKB_PFX_MASK) + kp.skb_prefix[kp.n + (i >> SKB_PREP_LOG2)];
 }
 DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool attach_only = false) {
     SkbRec *rec = kp.skb_rec + i;
     L.pkt = kp.pkt_data + kp.pkt_off[i];
-    if (!kp.skb_rec_built && !attach_only) skb_init(SkbBytes{L.pkt + SKB_HEADROOM}, kp.pkt_len[i], *rec);
+    const uint64_t pf = kp.skb_rec_built ? kp.skb_prefix[i] : 0ull;
+    // a sparse prep (skb_rec_built == 2) left derived words for the frames skb_fast rejects only:
+    // the others are decoded here from the packet bytes (the same record)
+    if ((!kp.skb_rec_built || (kp.skb_rec_built == 2 && !(pf & SKB_PFX_EXC))) && !attach_only)
+        skb_init(SkbBytes{L.pkt + SKB_HEADROOM}, kp.pkt_len[i], *rec);
     else if (kp.skb_drv && !attach_only)   // the prep kernel's derived words into the record
         for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) ((uint64_t *)rec)[q] = kp.skb_drv[(size_t)i * SKB_DERIVED_Q + q];
     const uint32_t lw = rec->len;
@@ -1039,7 +1044,7 @@ DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool atta
     L.M = SKB_HEADROOM + lw + SKB_TAILROOM;
     if (!attach_only) {
         if (!kp.skb_rec_built) skb_rooms_clear(L.pkt, lw);
-        else if (skb_rec_dirty(*rec)) skb_rooms_zero(L.pkt, lw);
+        else if (pf & SKB_PFX_DIRTY) skb_rooms_zero(L.pkt, lw);
     }
     r1 = kp.static_next + kp.stack_size + 1;
     return 0;
@@ -1071,7 +1076,12 @@ DEV int skb_attach(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_
 // skb_load for a JIT kernel that keeps the process's SkbRec in an LDS slot `d`: the record's words,
 // the packet offset and the leak prefix are loaded together (one memory round trip, not the
 // record length first and the rest after it), then the record goes to LDS.
+DEV int skb_load_lds_po(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint64_t po);
 DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d) {
+    return skb_load_lds_po(kp, L, i, r1, d, kp.pkt_off[i]);
+}
+// the same with packet i's offset given (loaded ahead by the caller)
+DEV int skb_load_lds_po(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint64_t po) {
     // the packet's derived words: 96 contiguous bytes of the prep kernel's compact array (consecutive
     // lanes, consecutive records), six 16-byte loads
     typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
@@ -1083,7 +1093,7 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
         w[2 * q] = v.x;
         w[2 * q + 1] = v.y;
     }
-    const uint64_t po = kp.pkt_off[i], pre = skb_leak_pre(kp, i), base = *kp.skb_base;
+    const uint64_t pre = skb_leak_pre(kp, i), base = *kp.skb_base;
 #pragma unroll
     for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) d[q] = w[q];
 #pragma unroll
@@ -1094,6 +1104,52 @@ DEV int skb_load_lds(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint6
 #else
     return skb_attach(kp, L, i, r1, d, (uint32_t)w[0], pre, base, (int)((w[SKB_DIRTY_Q] >> SKB_DIRTY_SHIFT) & 1u));
 #endif
+}
+
+// skb_load for a JIT kernel after a sparse prep (skb_rec_built == 2): the record of a common frame is
+// derived here, from the packet's first SKB_WIN bytes, straight into the LDS slot `d` (skb_fast_rec);
+// only a frame skb_fast does not take has its derived words in skb_drv (SKB_PFX_EXC).  The prep's
+// 96-byte record per packet is neither written nor read back: the header bytes this loads are the
+// ones the programs' early loads fetch next.  po / len: packet i's descriptor, pw: its prefix word
+// (the caller may have loaded them ahead).
+DEV int skb_load_fast(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, uint64_t *d, uint64_t po, uint32_t len,
+                      uint64_t pw) {
+    const uint64_t pre = (pw & SKB_PFX_MASK) + kp.skb_prefix[kp.n + (i >> SKB_PREP_LOG2)], base = *kp.skb_base;
+    L.pkt = kp.pkt_data + po;
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));   // any pkt_off
+    const GAS u32x4u *pk = (const GAS u32x4u *)(L.pkt + SKB_HEADROOM);
+    uint32_t w[SKB_WIN / 4];
+#pragma unroll
+    for (uint32_t c = 0; c < SKB_WIN / 16; c++) {   // chunks that start inside the packet
+        u32x4u v = {0u, 0u, 0u, 0u};
+        if (16 * c < len) v = pk[c];
+        w[4 * c] = v.x;
+        w[4 * c + 1] = v.y;
+        w[4 * c + 2] = v.z;
+        w[4 * c + 3] = v.w;
+    }
+    uint32_t lw;
+    if (pw & SKB_PFX_EXC) {
+        typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
+        const GAS u64x2a *s = (const GAS u64x2a *)(kp.skb_drv + (size_t)i * SKB_DERIVED_Q);
+        lw = (uint32_t)s[0].x;
+#pragma unroll
+        for (uint32_t q = 0; q < SKB_DERIVED_Q / 2; q++) {
+            const u64x2a v = s[q];
+            d[2 * q] = v.x;
+            d[2 * q + 1] = v.y;
+        }
+    } else {
+        SkbRec r;
+        skb_fast_rec(w, len, r);
+        const uint64_t *rw = (const uint64_t *)&r;
+#pragma unroll
+        for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) d[q] = rw[q];
+        lw = len;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) d[SKB_DERIVED_Q + q] = skb_writable_word(q);
+    return skb_attach(kp, L, i, r1, d, lw, pre, base, (pw & SKB_PFX_DIRTY) ? 1 : 0);
 }
 
 // skb_load for a JIT kernel that builds the record itself (no prep records: a 160-byte write and

@@ -40,6 +40,14 @@
 #define SKB_PREP_LOG2 8u
 #define SKB_SNAP 40u
 #define SKB_REC_BYTES 160u
+// flags in packet i's within-block leak prefix word (skb.hip; skb_leak_pre masks them off):
+//   EXC   the frame is one skb_fast does not take; with a sparse prep (KParams::skb_rec_built == 2)
+//         only such frames have their derived words in skb_drv, every other frame's record is built
+//         by whoever loads the process, from the packet's first bytes (skb_fast_rec);
+//   DIRTY the packet memory's headroom or tailroom holds a non-zero byte (Load zeroes them)
+#define SKB_PFX_EXC (1ull << 63)
+#define SKB_PFX_DIRTY (1ull << 62)
+#define SKB_PFX_MASK ((1ull << 62) - 1ull)
 
 // net.IP as the reference holds it: kind 0 = make(net.IP, n) (zeros, cap n), 1 = nil,
 // 2 = gopacket's packet copy from byte `off` (cap = L - off: Go slices may read past n)
@@ -513,27 +521,34 @@ SKB_DEV void skb_snap_regs(const uint32_t *w, uint32_t L, SkbRec &r) {
 #undef SKW8
 #undef SKW16
 
-// skb_init over the packet's first SKB_WIN bytes in registers (w), the general walk through the
-// block's LDS window (win, column t) for the frames skb_fast does not take
-template <uint32_t T>
-SKB_DEV void skb_init_regs(const uint32_t *w, uint32_t *win, uint32_t t, const uint8_t *pkt, uint32_t L, SkbRec &r) {
+// the whole record (skb_init) of a frame skb_fast takes, from its first SKB_WIN bytes in registers;
+// false (r partly written) for the frames the general walk must decode
+SKB_DEV bool skb_fast_rec(const uint32_t *w, uint32_t L, SkbRec &r) {
     skb_rec_reset(r);
-    if (skb_fast(w, L, r)) {
-        r.len = L;
-        const uint32_t b = skb_snap_base(r);
-        r.snap_base = b;
-        if (b == 26) skb_snap_regs<26>(w, L, r);
-        else if (b == 22) skb_snap_regs<22>(w, L, r);
-        else skb_snap_regs<0>(w, L, r);
-        return;
-    }
+    if (!skb_fast(w, L, r)) return false;
+    r.len = L;
+    const uint32_t b = skb_snap_base(r);
+    r.snap_base = b;
+    if (b == 26) skb_snap_regs<26>(w, L, r);
+    else if (b == 22) skb_snap_regs<22>(w, L, r);
+    else skb_snap_regs<0>(w, L, r);
+    return true;
+}
+
+// skb_init over the packet's first SKB_WIN bytes in registers (w), the general walk through the
+// block's LDS window (win, column t) for the frames skb_fast does not take.  Returns whether
+// skb_fast took the frame.
+template <uint32_t T>
+SKB_DEV bool skb_init_regs(const uint32_t *w, uint32_t *win, uint32_t t, const uint8_t *pkt, uint32_t L, SkbRec &r) {
+    if (skb_fast_rec(w, L, r)) return true;
 #ifdef MIMIC_PREP_FAST_ONLY   // measurement only (tools/prep_probe.py): no general walk
     r.len = L;
-    return;
+    return false;
 #endif
 #pragma unroll
     for (uint32_t q = 0; q < SKB_WIN / 4; q++) win[q * T + t] = w[q];
     skb_init(SkbWinBytes<T>{win, pkt, t}, L, r);
+    return false;
 }
 
 // ---------------------------------------------------------------------------------------

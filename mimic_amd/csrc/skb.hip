@@ -69,7 +69,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, uint64_t *__restrict__ rec,
                                                                           uint32_t rec_q, uint64_t *__restrict__ prefix,
-                                                                          uint32_t rooms) {
+                                                                          uint32_t rooms, uint32_t sparse) {
     __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
     __shared__ uint64_t wtot[PREP_T / 64];
     uint32_t *win = (uint32_t *)area;
@@ -78,6 +78,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     const bool live = i < n;
     SkbRec r;
     uint64_t f = 0;   // the leak footprint
+    uint64_t flags = 0;   // skb.h SKB_PFX_*
     if (live) {
         const uint32_t L = pkt_len[i];
         const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
@@ -109,13 +110,29 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
         }
 #ifdef MIMIC_PREP_NOWALK   // measurement only (tools/prep_probe.py): loads and footprints, no decode
         r.len = w[0] == 0x12345678u ? SKB_LOAD_FAILED : L;
+        const bool fast = true;
 #else
-        skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
+        const bool fast = skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
 #endif
         r.ip[0].pad[0] = dirty;
         f = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
+        flags = (dirty ? SKB_PFX_DIRTY : 0ull) | (fast ? 0ull : SKB_PFX_EXC);
     }
-    if (rec) {
+    if (rec && sparse) {
+        // sparse: only the frames skb_fast does not take leave their derived words (the loader builds
+        // every other record itself from the packet's first bytes, skb.h skb_fast_rec): few threads
+        // store, each its own 96 bytes
+        if (live && (flags & SKB_PFX_EXC)) {
+            typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+            const uint64_t *rw = (const uint64_t *)&r;
+            u64x2 *o = (u64x2 *)(rec + (size_t)i * rec_q);
+#pragma unroll
+            for (uint32_t u = 0; u < SKB_DERIVED_Q / 2; u++) {
+                const u64x2 v = {rw[2 * u], rw[2 * u + 1]};
+                o[u] = v;
+            }
+        }
+    } else if (rec) {
 #ifdef MIMIC_PREP_DIRECT   // measurement: each thread writes its own derived words (16-byte stores)
         if (live) {
             typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -156,7 +173,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     // the leak prefix within the block, and the block's sum (mimic_skb_blocks_kernel scans those)
     uint64_t bsum;
     const uint64_t ex = prep_exscan(f, wtot, &bsum);
-    if (live) prefix[i] = ex;
+    if (live) prefix[i] = ex | flags;
     if (t == 0) prefix[n + blockIdx.x] = bsum;
 }
 
@@ -203,20 +220,54 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
                                    uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state, hipStream_t st) {
     hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                       rec, rec_q, prefix, 1u);
+                       rec, rec_q, prefix, 1u, 0u);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        0ull, 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// prefix: n + ceil(n / 256) words; state: 2 words
+// prefix: n + ceil(n / 256) words; state: 2 words.  sparse: derived words for the frames skb_fast
+// does not take only (SKB_PFX_EXC), every packet's flags in its prefix word
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
-                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, hipStream_t st) {
+                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse, hipStream_t st) {
     if (n)
         hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
-                           rec, rec_q, prefix, rooms);
+                           rec, rec_q, prefix, rooms, sparse);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        init_base, use_init);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// mimic_process_run_many: processes whose LinuxContextSKBuff.Load ran at NewProcess, each with its
+// own device block (engine.cpp mimic_process::d_skbmem: SkbRec | prefix word | block word | base |
+// mimic_skb_custom), as one batch: derived words into drv (SKB_DERIVED_Q per process), the absolute
+// leak address of process i (base + prefix, the prep flags kept) into prefix[i], zero block offsets
+// after them, and the user-given sock / flow keys (has_cust[i]) into cust.  The batch's leak base is
+// then 0 and skb_leak_pre gives every process the addresses its own Load reserved.
+extern "C" __global__ __launch_bounds__(256) void mimic_skb_gather_kernel(const uint8_t *const *__restrict__ mem, uint32_t n,
+                                                                         uint64_t *__restrict__ drv, uint64_t *__restrict__ prefix,
+                                                                         mimic_skb_custom *__restrict__ cust,
+                                                                         const uint8_t *__restrict__ has_cust) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t nb = (n + PREP_T - 1) / PREP_T;
+    if (i < nb) prefix[n + i] = 0;
+    if (i >= n) return;
+    const uint64_t *r = (const uint64_t *)mem[i];
+#pragma unroll
+    for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) drv[(size_t)i * SKB_DERIVED_Q + q] = r[q];
+    const uint64_t *px = (const uint64_t *)(mem[i] + sizeof(SkbRec));
+    const uint64_t p0 = px[0];
+    prefix[i] = (px[2] + (p0 & SKB_PFX_MASK) + px[1]) | (p0 & ~SKB_PFX_MASK);
+    if (cust) {
+        if (has_cust[i]) cust[i] = *(const mimic_skb_custom *)(mem[i] + sizeof(SkbRec) + 24);
+        else cust[i].flags = 0;
+    }
+}
+
+extern "C" int mimic_launch_skb_gather(const uint8_t *const *mem, uint32_t n, uint64_t *drv, uint64_t *prefix,
+                                       mimic_skb_custom *cust, const uint8_t *has_cust, hipStream_t st) {
+    const uint32_t nb = (n + PREP_T - 1) / PREP_T, m = n > nb ? n : nb;
+    if (m) hipLaunchKernelGGL(mimic_skb_gather_kernel, dim3((m + 255) / 256), dim3(256), 0, st, mem, n, drv, prefix, cust, has_cust);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -659,6 +659,31 @@ class VM:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
         return results
 
+    def RunProcesses(self, procs: Sequence["Process"], ctxs: Optional[Sequence[Optional["Context"]]] = None) -> None:
+        """processPool's workers for fresh sk_buff processes: Run(ctx) of every process as ONE device
+        launch (mimic_process_run_many), each with the leak addresses its NewProcess reserved and on
+        its SetCPUID vCPU.  Afterwards each process has R0, Status, Steps and ErrPC (registers R1-R10
+        are not kept by a batch lane); a fatal status is left in Status (not raised)."""
+        n = len(procs)
+        if not n:
+            return
+        for p in procs:
+            p._ensure_native()
+        arr = (C.c_void_p * n)(*[p._native for p in procs])
+        cx = None
+        if ctxs is not None and any(_live(c) is not None for c in ctxs):
+            hs = {}
+            for c in ctxs:
+                if _live(c) is not None and id(c) not in hs:
+                    hs[id(c)] = c._device_handle()
+            cx = (C.c_void_p * n)(*[hs[id(c)] if _live(c) is not None else None for c in ctxs])
+        regs = (L.ProcessRegs * n)()
+        _check(self.h, self.lib.mimic_process_run_many(arr, n, cx, regs), "RunProcesses")
+        for p, r in zip(procs, regs):
+            p._take(r)
+            p._started = True
+            p.ErrPC = int(r.pc) if p.Status else -1
+
     def SKBRelease(self) -> None:
         """Forget the sock / flow-keys / packet entries earlier sk_buff processes leaked (a fresh
         VM with the same maps and programs)."""
@@ -778,6 +803,7 @@ class Process:
         self.PacketAfter: Optional[bytes] = None
         self._native = None
         self._exited = False
+        self._started = False   # stepped or run at least once
         self.Registers.R10 = vm.StackAddress() + vm.settings.stack_frame_size   # vm.go:224
         if isinstance(ctx, LinuxContextSKBuff):
             self._ensure_native()
@@ -829,6 +855,7 @@ class Process:
         A fatal error raises MimicError (the reference returns it), after which the process is
         terminated."""
         self._ensure_native()
+        self._started = True
         regs = L.ProcessRegs()
         rc = self.VM.lib.mimic_process_step(self._native, 1, C.byref(regs))
         if rc < 0:
@@ -850,6 +877,7 @@ class Process:
         between launch slices; once it is done Run raises MimicError(ctx.Err()) with the process
         suspended (Run / Step continue it), and step_budget 0 means no step budget."""
         self._ensure_native()
+        self._started = True
         regs = L.ProcessRegs()
         if ctx is not None:
             rc = self.VM.lib.mimic_process_run_ctx(self._native, step_budget, ctx._device_handle(), C.byref(regs))
@@ -1361,8 +1389,8 @@ class ProcessPool:
         when the round-robin counter wraps inside the batch and a vCPU would get a job of a second
         group, the jobs so far run first."""
         V = self.vm.settings.vcpus
-        groups: Dict[Tuple[int, bool], list] = {}
-        owner: Dict[int, Tuple[int, bool]] = {}   # vCPU -> the group its jobs of this segment are in
+        groups: Dict[Tuple[int, bool, int], list] = {}
+        owner: Dict[int, Tuple[int, bool, int]] = {}   # vCPU -> the group its jobs of this segment are in
         for job in jobs:
             err = job.Context.Err() if job.Context is not None else None
             if err is not None:
@@ -1370,7 +1398,9 @@ class ProcessPool:
                 continue
             cpu = self._next_cpu
             skb = isinstance(job.Process.Context, LinuxContextSKBuff)
-            key = (job.Process.prog_id, skb)
+            # (sk_buff launches run one interface each: __sk_buff.ifindex is a launch parameter)
+            ifx = (job.Process.Context.Dev.IFIndex if job.Process.Context.Dev else 0) if skb else 0
+            key = (job.Process.prog_id, skb, ifx)
             if owner.get(cpu, key) != key:
                 self._run_groups(groups)
                 groups, owner = {}, {}
@@ -1381,7 +1411,7 @@ class ProcessPool:
         self._run_groups(groups)
 
     def _run_groups(self, groups) -> None:
-        for (pid, skb), js in groups.items():
+        for (pid, skb, _ifx), js in groups.items():
             try:
                 self._launch(pid, skb, js)
             except MimicError as ex:
@@ -1404,10 +1434,20 @@ class ProcessPool:
         if skb:
             # An sk_buff process ran its context Load at NewProcess (its sock / flow keys / packet
             # took the VM's next leak addresses then, context_sk_buff.go:110-119), and the pool
-            # worker only calls Run (vm.go:570): each job runs on the device process NewProcess
-            # made (mimic_process_run), in enqueue order -- a batch launch would Load again and
-            # give the job addresses past its own.
-            for j in js:
+            # worker only calls Run (vm.go:570).  The fresh processes of the group run as ONE launch
+            # on the device processes NewProcess made, each with the addresses its Load reserved
+            # (mimic_process_run_many); one a caller already stepped continues on its own.
+            # (the group's jobs keep their order: fresh runs before a started job go first)
+            fresh = []
+            for j in js + [None]:
+                if j is not None and not j.Process._started:
+                    fresh.append(j)
+                    continue
+                if fresh:
+                    self.vm.RunProcesses([f.Process for f in fresh], [f.Context for f in fresh])
+                    fresh = []
+                if j is None:
+                    break
                 try:
                     j.Process.Run(ctx=j.Context)
                 except MimicError as ex:

@@ -196,3 +196,65 @@ def test_pool_keeps_enqueue_order_per_vcpu_across_programs(gpu):
         val[c] = val[c] + 1 if k == 0 else val[c] * 3
         assert got[i][0] == val[c], (i, got[i], val)
     vm.close()
+
+
+def test_pool_skb_chain_jobs_batched_like_the_oracle(gpu):
+    """cfg 5's tail-call chain through the pool: 3 000 sk_buff jobs (NewProcess each, so every Load
+    reserves its own leak addresses in enqueue order) run as micro-batched launches of the
+    processes NewProcess made (mimic_process_run_many).  Every job's R0 / status / steps, its
+    packet memory, and every per-CPU counter equal the oracle running the same jobs in order on the
+    vCPUs the pool gave them (round robin); a few processes stepped before they are enqueued run
+    on their own and still agree."""
+    from harness import run_oracle_skb
+
+    V = 16
+    buf, off, lens = W.make_skb_packets(3000, **W.IMIX, variety=0.2, seed=8)
+    progs, maps, pa = W.skb_programs()
+    init = [("flows", k, v, 0) for k, v in W.skb_flow_keys(buf, off, lens)]
+    sc = Scenario(vcpus=V, maps=maps, progs=[(p.name, p.raw, p.relocs) for p in progs], prog_array=pa, map_init=init)
+    vm, mp, pids = build_engine(sc, ctx=1)
+    procs, keep = [], []
+    for i, (o_, n_) in enumerate(zip(off, lens)):
+        try:   # NewProcess returns the context's Load error (vm.go:226-229): those jobs never exist
+            procs.append(vm.NewProcess(pids[0], M.LinuxContextSKBuff(Packet=bytes(buf[int(o_) + 32:int(o_) + 32 + int(n_)]),
+                                                                    Dev=M.NetDev(IFIndex=3))))
+            keep.append(i)
+        except M.MimicError as ex:
+            assert "ERR_CTX_LOAD" in str(ex)
+    assert 2500 < len(keep) < 3000
+    off, lens = off[keep], lens[keep]
+    pk = procs
+    for k in (5, 77):   # stepped first: these continue on their own device process
+        procs[k].SetCPUID(k % V)
+        procs[k].Step()
+    pool = vm.GetProcessPool()
+    pool.max_batch = 1024
+    pool.Start(len(pk))
+    got = {}
+    mu = threading.Lock()
+
+    def handoff(proc, err):
+        with mu:
+            got[proc.idx] = (proc.Registers.R0, proc.CPUID(), proc.Status, proc.Steps, proc.Packet())
+        proc.Cleanup()
+
+    for i, p in enumerate(procs):
+        p.idx = i
+        pool.Enqueue(M.ProcessPoolJob(p, None, handoff))
+    pool.Stop()
+    t0 = time.time()
+    while len(got) < len(pk) and time.time() - t0 < 60:
+        time.sleep(0.01)
+    assert len(got) == len(pk)
+    cpu = np.array([got[i][1] for i in range(len(pk))], np.int32)
+    assert (cpu == np.arange(len(pk)) % V).all()
+    o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=3)
+    assert [got[i][0] for i in range(len(pk))] == [int(x) for x in o["r0"]]
+    assert [got[i][2] for i in range(len(pk))] == [int(x) for x in o["status"]]
+    assert [got[i][3] for i in range(len(pk))] == [int(x) for x in o["steps"]]
+    for i in range(0, len(pk), 7):
+        o_ = int(off[i])
+        assert got[i][4] == bytes(o["pkt"][o_:o_ + 32 + int(lens[i]) + 64]), i
+    for c in range(V):
+        assert mp["stats"].Values(c) == o["maps"]["stats"][c], c
+    vm.close()

@@ -37,6 +37,28 @@ def _counter_prog(size=8, leak=False):
                      [dict(name="c", type=6, key_size=4, value_size=size, max_entries=4)])
 
 
+def _peek_sc(V):
+    """The classifier plus a program that bumps per-CPU counter[1], then reads the same counter back
+    through a computed address: get_smp_processor_id * the row period + an LD_IMM64 constant (the
+    addresses from the oracle's layout, which is the engine's: layout_* KATs).  Its R0 counts the
+    vCPU's packets in order, so it is exact only when a vCPU's packets run in order."""
+    from harness import build_oracle
+
+    p = W.prog_classifier()
+    base = Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    ovm, mids, _ = build_oracle(base)
+    a0 = ovm.map_lookup(mids["verdicts"], (1).to_bytes(4, "little"), 0)[1]
+    period = ovm.map_lookup(mids["verdicts"], (1).to_bytes(4, "little"), 1)[1] - a0
+    ovm.close()
+    assert a0 and period > 0
+    raw, rel = A.assemble([
+        A.st(4, 10, -4, 1), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, "verdicts"),
+        A.call(A.FN_MAP_LOOKUP_ELEM), A.jmp("jeq", 0, 0, 3), A.ldx(8, 1, 0, 0), A.alu64("add", 1, 1), A.stx(8, 0, 0, 1),
+        A.call(A.FN_GET_SMP_PROCESSOR_ID), A.alu64("mul", 0, period), A.ld_imm64(3, a0), A.alu64("add", 3, 0, reg=True),
+        A.ldx(8, 0, 3, 0), A.exit_()])
+    return Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs), ("peek", raw, list(rel))])
+
+
 def jit_kernels():
     out = []
     for V in (1, 7, 256, 1000, 4096):
@@ -46,6 +68,7 @@ def jit_kernels():
     out.append(spread_kernel_of(_sc(_counter_prog(4), 256)))
     out.append(spread_kernel_of(_sc(W.prog_classifier(), 128)))
     out.append(kernel_of(_sc(_counter_prog(8, leak=True), 1)))
+    out.append(kernel_of(_peek_sc(128)))
     return out
 
 
@@ -167,24 +190,19 @@ def test_host_resident_sub_batches(gpu):
     vm.close()
 
 
-def test_computed_address_into_per_cpu_memory_fails_loudly(gpu):
-    """An address the program computes (an LD_IMM64 constant) into the counters: the analysis
-    cannot see it, the generic load reaches resolve(), and the launch is reported as an engine
-    error instead of returning a result that depends on the lanes' interleaving."""
-    p = W.prog_classifier()
+def test_computed_address_into_per_cpu_memory_runs_exact(gpu):
+    """An address the program computes (an LD_IMM64 constant) into the per-CPU counters: the base
+    has no provenance the spread analysis can place, so under the default policy the program set
+    runs one lane per vCPU and the result is the oracle's (memory_controller.go:117-145 resolves any
+    address); SPREAD_GUARD is never reached."""
     V = 128
-    sc = _sc(p, V)
-    vm, maps, pids = build_engine(sc)
-    addr = maps["verdicts"].Lookup((1).to_bytes(4, "little"), 3)
-    assert addr
-    raw, rel = A.assemble([
-        A.st(4, 10, -4, 1), A.mov64_reg(2, 10), A.alu64("add", 2, -4), A.ld_map_fd(1, "verdicts"),
-        A.call(A.FN_MAP_LOOKUP_ELEM), A.jmp("jeq", 0, 0, 3), A.ldx(8, 1, 0, 0), A.alu64("add", 1, 1), A.stx(8, 0, 0, 1),
-        A.ld_imm64(3, addr), A.ldx(8, 0, 3, 0), A.exit_()])
-    pid = vm.AddProgram(M.ProgramSpec("peek", raw, list(rel)))
+    sc = _peek_sc(V)
     n = 50000
     buf, off, lens = W.make_packets(n, seed=13)
-    batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
-    with pytest.raises(M.MimicError, match="spread launch"):
-        vm.RunXDPBatch(pid, batch)
-    vm.close()
+    cpu = W.schedule_cpu(n, V, "interleaved")
+    o = run_oracle(sc, buf, off, lens, cpu, entry=1)
+    e = run_engine(sc, buf, off, lens, None, entry=1, schedule=M.SCHED_INTERLEAVED)
+    assert e["last_exec"] == "jit"
+    assert_same(o, e)
+    # R0 counts each vCPU's packets in order: 1, 2, 3 ... (a spread launch would interleave them)
+    assert sorted(set(np.asarray(o["r0"]).tolist())) == list(range(1, -(-n // V) + 1))

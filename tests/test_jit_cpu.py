@@ -84,10 +84,17 @@ def test_skb_chain_register_budget():
     """cfg 5's five-program chain with deferred slow paths: no call left in the kernel, so no
     scratch (the Spill record and the call ABI's saves were 240 bytes per lane) and at least two
     waves per SIMD (it was 380 VGPRs + AGPRs at one wave with called slow paths)."""
-    progs, _, _ = W.skb_programs()
+    from mimic_amd import jit as J
+
+    progs, maps, _ = W.skb_programs()
     r = _resources([p.raw for p in progs], _lib.CTX_SKB)
     assert r["vgpr_total"] <= 256 and r["waves_per_simd"] >= 2, r
     assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["agpr"] == 0, r
+    # the kernel the cfg-5 bench runs (the per-CPU stats row in the LDS value cache): it sits at the
+    # edge -- one more live value spills into AGPRs and halves the waves (0.22 -> 0.36 ms, DESIGN 6.1)
+    vc = J.vc_slots([(p.raw, p.relocs) for p in progs], maps)
+    r = _resources([p.raw for p in progs], _lib.CTX_SKB, vc)
+    assert r["vgpr_total"] <= 256 and r["waves_per_simd"] >= 2 and r["agpr"] == 0, r
 
 
 def test_defer_sites_store_live_registers_only():

@@ -83,6 +83,31 @@ def test_rejected_forms():
     assert not _allowed(tail)
 
 
+def test_base_provenance():
+    """Loads and stores outside the fused increment must go through a base derived from R1 (the
+    context), R10 (the stack) or a packet pointer; anything else may address per-CPU memory
+    (memory_controller.go:117-145 resolves any address), so the program set runs one lane per vCPU."""
+    cnt = _lookup() + [A.jmp("jeq", 0, 0, 3)] + _inc()
+    tail = [A.mov64_imm(0, 2), A.exit_()]
+    # packet pointers from the context (data / data_end), arithmetic on them, the stack: accepted
+    pkt = [A.mov64_reg(6, 1), A.ldx(4, 2, 6, 0), A.ldx(4, 3, 6, 4), A.mov64_reg(4, 2), A.alu64("add", 4, 14),
+           A.jmp("jgt", 4, 3, 2), A.ldx(1, 5, 2, 12), A.stx(1, 2, 0, 5)]
+    assert _allowed(pkt + cnt + tail)
+    assert _allowed([A.ldx(4, 2, 1, 16), A.stx(4, 10, -8, 2), A.ldx(4, 3, 10, -8)] + cnt + tail)
+    # an LD_IMM64 constant as a base (the round-4 guard case), a pointer loaded from memory, a
+    # context scalar (ingress_ifindex), a helper's clobbered argument register: rejected
+    assert not _allowed(cnt + [A.ld_imm64(3, 0x10000), A.ldx(8, 0, 3, 0), A.exit_()])
+    assert not _allowed(cnt + [A.ld_imm64(3, 0x10000), A.st(8, 3, 0, 1)] + tail)
+    assert not _allowed([A.stx(8, 10, -8, 1), A.ldx(8, 6, 10, -8), A.ldx(4, 2, 6, 0)] + cnt + tail)
+    assert not _allowed([A.ldx(4, 6, 1, 12), A.ldx(4, 2, 6, 0)] + cnt + tail)
+    assert not _allowed([A.mov64_reg(6, 1)] + cnt + [A.ldx(4, 2, 1, 0)] + tail)
+    # scalars alone (an immediate moved into a register, then arithmetic)
+    assert not _allowed(cnt + [A.mov64_imm(3, 0x10000), A.alu64("add", 3, 8), A.ldx(8, 0, 3, 0), A.exit_()])
+    # a base that is the context on one path and a constant on the other
+    assert not _allowed([A.mov64_reg(6, 1), A.ldx(4, 2, 1, 12), A.jmp("jeq", 2, 0, 1), A.ld_imm64(6, 0x10000),
+                         A.ldx(4, 3, 6, 0)] + cnt + tail)
+
+
 def test_lds_table_or_atomics():
     """The block's counter table lives in LDS when min(1024, V) rows fit 32 KiB, else every
     increment is an agent-scope atomic into the map (spread_spec mirrors engine.cpp spread_build)."""
