@@ -56,12 +56,23 @@ namespace {
 // device round trip; the image goes to the device in one upload before the device next uses the
 // map (flush_host).  valid: the image equals or is newer than the device's (a launch that may
 // write the table makes it stale: the next host operation downloads it again); dirty: newer.
+//
+// After such a launch the image is fetched on demand: the counters at once, bucket
+// records and freelist positions a page at a time when an operation first reads them, everything
+// left in one copy per region once an operation sequence has faulted MIRROR_BULK pages.  Host
+// writes (records, ring positions, keys, values) are staged as arena writes (stage_write) and the
+// counters once at flush: a few Updates between two batches move a few pages down and a few
+// hundred bytes up, not the whole index both ways.
+#define MIRROR_PAGE 8192u   // bytes of records / ring per fetch
+#define MIRROR_BULK 32u     // faults after which the rest of the index comes in one copy per region
 struct HashMirror {
     bool valid = false, dirty = false;
     std::vector<uint64_t> rec;
     std::vector<int32_t> ring;
     HashCtl ctl{};
-    std::vector<uint8_t> keys;
+    std::vector<uint8_t> rec_pg, ring_pg;   // per page: 1 = on the host
+    bool all = true;                        // every page on the host
+    uint32_t faults = 0;
 };
 
 struct HostMap {
@@ -938,13 +949,17 @@ static void mirror_fresh(const HostMap &m) {
     x.ctl.head = 0;
     x.ctl.tail = m.max_entries;
     x.ctl.avail = (int32_t)m.max_entries;
-    x.keys.assign((size_t)m.max_entries * m.key_size, 0);
+    x.rec_pg.assign(((size_t)m.ht_cap * m.rec_q * 8 + MIRROR_PAGE - 1) / MIRROR_PAGE, 1);
+    x.ring_pg.assign(((size_t)m.fl_cap * 4 + MIRROR_PAGE - 1) / MIRROR_PAGE, 1);
+    x.all = true;
+    x.faults = 0;
     x.valid = true;
     x.dirty = false;
 }
 
-// the device's table into the image (after the last batch), head / avail normalised as
-// mimic_hash_normalize_kernel would (a pop-only launch may leave head past tail)
+// the device's table as the image's source (after the last batch): the counters now, head / avail
+// normalised as mimic_hash_normalize_kernel would (a pop-only launch may leave head past tail);
+// records and ring pages when first read (mirror_page)
 static int mirror_ensure(mimic_vm *vm, const HostMap &m) {
     HashMirror &x = *m.mir;
     if (x.valid) return 0;
@@ -954,12 +969,11 @@ static int mirror_ensure(mimic_vm *vm, const HostMap &m) {
     ht_offsets(m, &rb, &fo, &co);
     x.rec.resize((size_t)m.ht_cap * m.rec_q);
     x.ring.resize(m.fl_cap);
-    x.keys.resize((size_t)m.max_entries * m.key_size);
-    const uint8_t *base = vm->arena + m.ht_dev_off;
-    HIP_OK(vm, hipMemcpy(x.rec.data(), base, rb, hipMemcpyDeviceToHost));
-    HIP_OK(vm, hipMemcpy(x.ring.data(), base + fo, (size_t)m.fl_cap * 4, hipMemcpyDeviceToHost));
-    HIP_OK(vm, hipMemcpy(&x.ctl, base + co, sizeof(HashCtl), hipMemcpyDeviceToHost));
-    if (!x.keys.empty()) HIP_OK(vm, hipMemcpy(x.keys.data(), vm->arena + m.keys_dev_off, x.keys.size(), hipMemcpyDeviceToHost));
+    x.rec_pg.assign((rb + MIRROR_PAGE - 1) / MIRROR_PAGE, 0);
+    x.ring_pg.assign(((size_t)m.fl_cap * 4 + MIRROR_PAGE - 1) / MIRROR_PAGE, 0);
+    x.all = false;
+    x.faults = 0;
+    HIP_OK(vm, hipMemcpy(&x.ctl, vm->arena + m.ht_dev_off + co, sizeof(HashCtl), hipMemcpyDeviceToHost));
     if (x.ctl.head > x.ctl.tail) x.ctl.head = x.ctl.tail;
     x.ctl.avail = (int32_t)(x.ctl.tail - x.ctl.head);
     x.valid = true;
@@ -967,7 +981,56 @@ static int mirror_ensure(mimic_vm *vm, const HostMap &m) {
     return 0;
 }
 
-// a host write of n bytes at arena offset off, applied before the device next reads the arena
+// byte range [lo, hi) of a region (records at 0, ring at fo) on the host: the missing pages of it
+// come down (all of both regions once the operations have faulted MIRROR_BULK times)
+static int mirror_pages(mimic_vm *vm, const HostMap &m, bool ring, uint64_t lo, uint64_t hi) {
+    HashMirror &x = *m.mir;
+    if (x.all) return 0;
+    uint64_t rb, fo, co;
+    ht_offsets(m, &rb, &fo, &co);
+    const uint8_t *base = vm->arena + m.ht_dev_off;
+    std::vector<uint8_t> &pg = ring ? x.ring_pg : x.rec_pg;
+    const uint64_t size = ring ? (uint64_t)m.fl_cap * 4 : rb;
+    uint8_t *host = ring ? (uint8_t *)x.ring.data() : (uint8_t *)x.rec.data();
+    for (uint64_t q = lo / MIRROR_PAGE; q * MIRROR_PAGE < hi; q++) {
+        if (pg[q]) continue;
+        if (++x.faults > MIRROR_BULK) {   // the rest of both regions at once
+            for (int reg = 0; reg < 2; reg++) {
+                std::vector<uint8_t> &pp = reg ? x.ring_pg : x.rec_pg;
+                uint8_t *h = reg ? (uint8_t *)x.ring.data() : (uint8_t *)x.rec.data();
+                const uint64_t sz = reg ? (uint64_t)m.fl_cap * 4 : rb, off = reg ? fo : 0;
+                for (size_t a = 0; a < pp.size();) {   // runs of absent pages
+                    if (pp[a]) { a++; continue; }
+                    size_t b = a;
+                    while (b < pp.size() && !pp[b]) b++;
+                    const uint64_t s0 = (uint64_t)a * MIRROR_PAGE, s1 = std::min<uint64_t>((uint64_t)b * MIRROR_PAGE, sz);
+                    HIP_OK(vm, hipMemcpy(h + s0, base + off + s0, s1 - s0, hipMemcpyDeviceToHost));
+                    for (size_t c = a; c < b; c++) pp[c] = 1;
+                    a = b;
+                }
+            }
+            x.all = true;
+            return 0;
+        }
+        const uint64_t s0 = q * MIRROR_PAGE, s1 = std::min<uint64_t>(s0 + MIRROR_PAGE, size);
+        HIP_OK(vm, hipMemcpy(host + s0, base + (ring ? fo : 0) + s0, s1 - s0, hipMemcpyDeviceToHost));
+        pg[q] = 1;
+    }
+    return 0;
+}
+// bucket record p / ring position at, on the host
+static int mirror_rec(mimic_vm *vm, const HostMap &m, uint32_t p) {
+    const uint64_t b = (uint64_t)p * m.rec_q * 8;
+    return mirror_pages(vm, m, false, b, b + (uint64_t)m.rec_q * 8);
+}
+static int mirror_ring(mimic_vm *vm, const HostMap &m, uint64_t at) {
+    const uint64_t b = (at & (m.fl_cap - 1)) * 4;
+    return mirror_pages(vm, m, true, b, b + 4);
+}
+
+// a host write of n bytes at arena offset off, applied before the device next reads the arena.
+// The writes of one flush land in parallel (one scatter launch): a later write of the same offset
+// and size replaces the earlier one; callers never stage two writes of different sizes that overlap.
 static void stage_write(mimic_vm *vm, uint64_t off, const void *src, uint32_t n) {
     if (!n) return;
     auto it = vm->pend_at.find(off);
@@ -990,16 +1053,12 @@ static int flush_host(mimic_vm *vm) {
     if (!vm->host_dirty) return 0;
     int rc = settle(vm);
     if (rc) return rc;
-    for (auto &m : vm->maps) {
+    for (auto &m : vm->maps) {   // the records, ring positions and keys went out as staged writes
         if (!m.mir || !m.mir->dirty) continue;
         HashMirror &x = *m.mir;
         uint64_t rb, fo, co;
         ht_offsets(m, &rb, &fo, &co);
-        uint8_t *base = vm->arena + m.ht_dev_off;
-        HIP_OK(vm, hipMemcpy(base, x.rec.data(), rb, hipMemcpyHostToDevice));
-        HIP_OK(vm, hipMemcpy(base + fo, x.ring.data(), (size_t)m.fl_cap * 4, hipMemcpyHostToDevice));
-        HIP_OK(vm, hipMemcpy(base + co, &x.ctl, sizeof(HashCtl), hipMemcpyHostToDevice));
-        if (!x.keys.empty()) HIP_OK(vm, hipMemcpy(vm->arena + m.keys_dev_off, x.keys.data(), x.keys.size(), hipMemcpyHostToDevice));
+        stage_write(vm, m.ht_dev_off + co, &x.ctl, sizeof(HashCtl));
         x.dirty = false;
         m.pop_dirty = false;   // the uploaded counters are normalised
     }
@@ -1040,12 +1099,15 @@ static int flush_host(mimic_vm *vm) {
 // the sequential hash algorithm on the image (hashmap.h h_find / h_probe_held / h_place_held /
 // h_fl_pop / h_fl_push with one thread): slot of the key or -1; *pos = its bucket, *freep = the
 // first reusable bucket on its probe path
-static int32_t mh_probe(const HostMap &m, const KeyBytes &ks, uint64_t h, uint32_t *pos, uint32_t *freep) {
+// (MH_FAULT: a page could not be fetched; the error is the VM's)
+#define MH_FAULT (-2)
+static int32_t mh_probe(mimic_vm *vm, const HostMap &m, const KeyBytes &ks, uint64_t h, uint32_t *pos, uint32_t *freep) {
     const HashMirror &x = *m.mir;
     const uint32_t mask = m.ht_cap - 1, tag = (uint32_t)(h >> 32), nq = (m.key_size + 7) >> 3;
     uint32_t p = (uint32_t)h & mask;
     *freep = HT_EMPTY;
     for (uint32_t n = 0; n < m.ht_cap; n++, p = (p + 1) & mask) {
+        if (mirror_rec(vm, m, p)) return MH_FAULT;
         const uint64_t *r = &x.rec[(size_t)p * m.rec_q];
         const uint32_t st = (uint32_t)r[0];
         if (st == HT_EMPTY) {
@@ -1074,19 +1136,26 @@ static int mh_update(mimic_vm *vm, const HostMap &m, const void *key, const void
     const KeyBytes ks{(const uint8_t *)key, m.key_size};
     const uint64_t h = h_hash(ks, m.key_size);
     uint32_t pos = 0, freep = HT_EMPTY;
-    int32_t idx = mh_probe(m, ks, h, &pos, &freep);
+    int32_t idx = mh_probe(vm, m, ks, h, &pos, &freep);
+    if (idx == MH_FAULT) return MIMIC_EDEVICE;
     if (idx < 0) {
         if (x.ctl.avail <= 0) return 7;   // the freelist is empty: syscall.E2BIG
+        const uint64_t at = x.ctl.head;
+        if (mirror_ring(vm, m, at) || mirror_rec(vm, m, freep)) return MIMIC_EDEVICE;
         x.ctl.avail--;
-        const uint64_t at = x.ctl.head++;
+        x.ctl.head++;
         int32_t &f = x.ring[at & (m.fl_cap - 1)];
         idx = f;
         f = -1;
+        uint64_t rb, fo, co;
+        ht_offsets(m, &rb, &fo, &co);
+        stage_write(vm, m.ht_dev_off + fo + (at & (m.fl_cap - 1)) * 4, &f, 4);
         uint64_t *r = &x.rec[(size_t)freep * m.rec_q];
         if ((uint32_t)r[0] == HT_EMPTY) x.ctl.used0++;
         for (uint32_t q = 0; q * 8 < m.key_size; q++) r[1 + q] = ks.word(q);
         r[0] = ((uint64_t)(uint32_t)(h >> 32) << 32) | (uint32_t)idx;
-        memcpy(x.keys.data() + (size_t)idx * m.key_size, key, m.key_size);   // keys.Write (:188-192)
+        stage_write(vm, m.ht_dev_off + (uint64_t)freep * m.rec_q * 8, r, m.rec_q * 8);
+        stage_write(vm, m.keys_dev_off + (uint64_t)idx * m.key_size, key, m.key_size);   // keys.Write (:188-192)
         x.dirty = true;
         vm->host_dirty = true;
     }
@@ -1097,21 +1166,30 @@ static int mh_update(mimic_vm *vm, const HostMap &m, const void *key, const void
 }
 
 // LinuxHashMap.Delete :225-255 on the image (an absent key is no error)
-static void mh_delete(mimic_vm *vm, const HostMap &m, const void *key) {
+static int mh_delete(mimic_vm *vm, const HostMap &m, const void *key) {
     HashMirror &x = *m.mir;
     const KeyBytes ks{(const uint8_t *)key, m.key_size};
     const uint64_t h = h_hash(ks, m.key_size);
     uint32_t pos = 0, freep;
-    const int32_t idx = mh_probe(m, ks, h, &pos, &freep);
-    if (idx < 0) return;
+    const int32_t idx = mh_probe(vm, m, ks, h, &pos, &freep);
+    if (idx == MH_FAULT) return MIMIC_EDEVICE;
+    if (idx < 0) return 0;
+    const uint64_t at = x.ctl.tail;
+    if (mirror_ring(vm, m, at)) return MIMIC_EDEVICE;
     uint64_t &w = x.rec[(size_t)pos * m.rec_q];
     w = (w & ~0xffffffffull) | HT_TOMB;
-    const uint64_t at = x.ctl.tail++;
+    x.ctl.tail++;
     x.ring[at & (m.fl_cap - 1)] = idx;   // the freelist's tail (:244-250)
+    uint64_t rb, fo, co;
+    ht_offsets(m, &rb, &fo, &co);
+    // (the whole record, as inserts stage it: stage_write merges writes of one offset and size only)
+    stage_write(vm, m.ht_dev_off + (uint64_t)pos * m.rec_q * 8, &w, m.rec_q * 8);
+    stage_write(vm, m.ht_dev_off + fo + (at & (m.fl_cap - 1)) * 4, &idx, 4);
     x.ctl.avail++;
     x.dirty = true;
     vm->host_dirty = true;
     m.may_tomb = true;
+    return 0;
 }
 
 // LinuxArrayMap.Update / LinuxPerCPUArrayMap.Update (emulator_linux_map_array.go:97-113, 244-250),
@@ -1169,7 +1247,8 @@ int mimic_map_lookup(mimic_vm *vm, uint32_t id, const void *key, int32_t cpu, ui
         if ((rc = mirror_ensure(vm, m))) return rc;
         const KeyBytes ks{(const uint8_t *)key, m.key_size};
         uint32_t pos = 0, freep;
-        const int32_t slot = mh_probe(m, ks, h_hash(ks, m.key_size), &pos, &freep);
+        const int32_t slot = mh_probe(vm, m, ks, h_hash(ks, m.key_size), &pos, &freep);
+        if (slot == MH_FAULT) return MIMIC_EDEVICE;
         *addr_out = slot < 0 ? 0 : b + (uint32_t)slot * m.value_size;
         return 0;
     }
@@ -1189,14 +1268,14 @@ int mimic_map_delete(mimic_vm *vm, uint32_t id, const void *key) {
     const HostMap &m = vm->maps[id];
     if (!is_hash(m)) return fail(vm, MIMIC_EINVAL, "can't delete from given LinuxMap");
     if ((rc = mirror_ensure(vm, m))) return rc;
-    mh_delete(vm, m, key);
-    return 0;
+    return mh_delete(vm, m, key);
 }
 
 // live (key, slot) pairs of a hash map in table order
 static int hash_entries(mimic_vm *vm, const HostMap &m, uint8_t *keys, int32_t *slots, size_t cap_entries,
                         uint32_t *n_out) {
     int rc = mirror_ensure(vm, m);
+    if (!rc) rc = mirror_pages(vm, m, false, 0, (uint64_t)m.ht_cap * m.rec_q * 8);   // every record
     if (rc) return rc;
     const std::vector<uint64_t> &rec = m.mir->rec;
     uint32_t n = 0;

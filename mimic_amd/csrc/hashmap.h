@@ -54,20 +54,23 @@ HDEV HT h_table(uint8_t *arena, const DMap &m) {
 // agent-scope add to the map's `head`; those same-address atomics serialise at the memory side
 // (cfg 4's inserting launch: 0.42 ms, 0.32 ms with the add spread over 16 addresses).  Here the
 // waves of a block that reserve at about the same time share one add: the first to arrive opens a
-// batch (`word`: generation << 32 | positions requested so far), waits ~128 cycles for others to
-// add their counts, closes it, reserves the total with one add and publishes base and count in
-// LDS; the others take their share at the offset their add returned.  The batch's positions are
-// contiguous and ordered by arrival -- a valid order of pops, as if those waves had popped one
-// after another -- and a lone wave gets exactly what a direct add gives (FIFO slots of sequential
-// runs unchanged).  Nobody waits on a joiner, so the protocol cannot deadlock; 16 result slots.
+// batch (`word`: generation << 48 | mask of the joined waves << 32 | positions requested so far),
+// waits ~128 cycles for others to add their counts, closes it, reserves the total with one add and
+// hands base and count to each wave of the batch through that wave's own mailbox; the others take
+// their share at the offset their add returned.  The batch's positions are contiguous and ordered
+// by arrival -- a valid order of pops, as if those waves had popped one after another -- and a lone
+// wave gets exactly what a direct add gives (FIFO slots of sequential runs unchanged).  A wave is
+// in at most one batch at a time and only the opener of that batch writes its mailbox, which the
+// wave clears after reading: no mailbox is overwritten before it is read, whatever the timing.
+// Nobody waits on a joiner, so the protocol cannot deadlock.
 #define HCOMB_MAPS 4u
-#define HCOMB_SLOTS 16u
+#define HCOMB_WAVES 16u   // waves per block (1024 threads at most)
 struct HComb {
     unsigned long long word;
     uint32_t owner;                     // the map (HT::tag) this combiner serves in this block
-    uint32_t ready[HCOMB_SLOTS];        // generation + 1 once base / got of that batch are published
-    uint32_t got[HCOMB_SLOTS];          // positions below tail (bit 31: tail == E, the ring untouched)
-    unsigned long long base[HCOMB_SLOTS];
+    uint32_t ready[HCOMB_WAVES];        // per wave: generation + 1 once its batch's base / got are there (0: read)
+    uint32_t got[HCOMB_WAVES];          // positions below tail (bit 31: tail == E, the ring untouched)
+    unsigned long long base[HCOMB_WAVES];
 };
 static __shared__ HComb h_comb_[HCOMB_MAPS];
 // zeroed by every thread of the block before any of them can insert (the JIT prologue)
@@ -76,7 +79,7 @@ HDEV void h_comb_init() {
     for (uint32_t q = threadIdx.x; q < sizeof(h_comb_) / 4; q += blockDim.x) w[q] = 0;
     __syncthreads();
 }
-// k positions for the calling wave (one lane): *base, *got (positions below tail), *ident
+// k (>= 1) positions for the calling wave (one lane): *base, *got (positions below tail), *ident
 HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, uint32_t *got, uint32_t *ident) {
     HComb &cb = h_comb_[(t.tag >> 4) & (HCOMB_MAPS - 1)];
     uint32_t own = __hip_atomic_load(&cb.owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -86,29 +89,35 @@ HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, ui
         own = __hip_atomic_load(&cb.owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (own != t.tag) return false;   // another map holds this combiner: reserve directly
-    const unsigned long long old = __hip_atomic_fetch_add(&cb.word, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t gen = (uint32_t)(old >> 32), off = (uint32_t)old, s = gen & (HCOMB_SLOTS - 1);
+    const uint32_t wid = threadIdx.x >> 6;
+    const unsigned long long old = __hip_atomic_fetch_add(&cb.word, (1ull << (32 + wid)) + k, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t gen = (uint32_t)(old >> 48), off = (uint32_t)old, joined = (uint32_t)(old >> 32) & 0xffffu;
     uint64_t b0;
     uint32_t g0;
-    if (off == 0) {   // the batch's opener
+    if (joined == 0) {   // the batch's opener
 #ifndef MIMIC_HCOMB_SLEEP
 #define MIMIC_HCOMB_SLEEP 2
 #endif
         __builtin_amdgcn_s_sleep(MIMIC_HCOMB_SLEEP);
-        const unsigned long long closed = __hip_atomic_exchange(&cb.word, (unsigned long long)(gen + 1u) << 32, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t total = (uint32_t)closed;
+        const unsigned long long closed = __hip_atomic_exchange(&cb.word, (unsigned long long)((gen + 1u) & 0xffffu) << 48,
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t total = (uint32_t)closed, mask = (uint32_t)(closed >> 32) & 0xffffu & ~(1u << wid);
         b0 = __hip_atomic_fetch_add(&c->head, (unsigned long long)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tl = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         g0 = (b0 >= tl ? 0u : (tl - b0 < total ? (uint32_t)(tl - b0) : total)) | (tl == t.E ? 0x80000000u : 0u);
-        cb.base[s] = b0;
-        cb.got[s] = g0;
-        __hip_atomic_store(&cb.ready[s], gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t m = mask; m; m &= m - 1) {
+            const uint32_t w = (uint32_t)__builtin_ctz(m);
+            cb.base[w] = b0;
+            cb.got[w] = g0;
+            __hip_atomic_store(&cb.ready[w], gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     } else {
-        while (__hip_atomic_load(&cb.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != gen + 1u)
+        while (__hip_atomic_load(&cb.ready[wid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != gen + 1u)
             __builtin_amdgcn_s_sleep(1);
-        b0 = cb.base[s];
-        g0 = cb.got[s];
+        b0 = cb.base[wid];
+        g0 = cb.got[wid];
+        __hip_atomic_store(&cb.ready[wid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     *ident = g0 >> 31;
     g0 &= 0x7fffffffu;

@@ -98,6 +98,8 @@ class Gen {
         prefetch = !(pfv && pfv[0] == '0');
         const char *xv = getenv("MIMIC_JIT_XPF");   // 1: next-packet header window prefetch
         xpf_knob = xv && xv[0] == '1';
+        const char *lpv = getenv("MIMIC_JIT_LPF");   // 1: lane-start prefetch of the first packets' windows
+        lpf_knob = lpv && lpv[0] == '1';
         const char *lq = getenv("MIMIC_JIT_LDSSTK");   // 8-byte words of the LDS stack window (0: none)
         if (lq) lds_stack_q = (uint32_t)std::min(32, std::max(0, atoi(lq)));
         const char *dv = getenv("MIMIC_JIT_DISPATCH");   // 0: a jump table at every tail-call site
@@ -134,6 +136,8 @@ class Gen {
         tail_inline = !(ti && ti[0] == '0');
         const char *ce = getenv("MIMIC_JIT_CENSUS");   // 1: per-packet slow-path call counts in place of steps
         census = ce && ce[0] == '1';
+        const char *mt = getenv("MIMIC_JIT_MEMTIME");   // 1: per-packet start / end clocks in place of steps / err_pc
+        memtime = mt && mt[0] == '1';
         const char *el = getenv("MIMIC_JIT_ELIDE");   // 0: forwarded key stores are always made
         elide = !(el && el[0] == '0');
         const char *wnd = getenv("MIMIC_JIT_WINDOW");   // 0: early loads one by one
@@ -213,6 +217,9 @@ class Gen {
     bool hash_fast = true;     // MIMIC_JIT_HASH=0: no inline hash-map lookups
     bool tail_inline = true;   // MIMIC_JIT_TAIL=0: no inline tail calls
     bool census = false;       // MIMIC_JIT_CENSUS=1: diagnostics (tools/cold_census.py)
+    // MIMIC_JIT_MEMTIME=1 (measurement only, tools/memtime.py): s_memrealtime (100 MHz) when each
+    // packet's process starts (err_pc) and when its results are stored (steps)
+    bool memtime = false;
     bool elide = true;         // MIMIC_JIT_ELIDE=0: no deferred stack stores
     bool window = true;        // MIMIC_JIT_WINDOW=0: no windowed early loads
     int speculate = 8;         // MIMIC_JIT_SPEC=N: at most N early packet loads per region (0: none)
@@ -224,6 +231,18 @@ class Gen {
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
     bool prefetch = true;      // MIMIC_JIT_PREFETCH=0: no next-packet descriptor prefetch
     bool xpf_knob = false;     // MIMIC_JIT_XPF=1: next-packet header window prefetch (measured slower)
+    // Lane prefetch (analyze_xpf's window, lpf_safe): when a lane starts, the descriptors and the
+    // entry program's early window of its first kLpfD packets are loaded at once and parked in LDS,
+    // so the packets then run without a dependent HBM round trip each (one lane's packets are
+    // independent but for per-CPU state, which the programs keep in the lane value cache or in
+    // memory they do not prefetch).  Only for program sets that never store into packet memory.
+    // Off by default: cfg 2 measured 25.6 -> 32.0 us per launch (the lanes' prologue burst of 1 M
+    // descriptor and window loads delays every first packet; tools/memtime.py), the
+    // chunked schedule 38.9 -> 36.8 us, cfg 3 / cfg 4 unchanged.
+    bool lpf_knob = false;
+    bool lpf_on = false;
+    bool lds_stack_on = false;
+    static constexpr uint32_t kLpfD = 4;
     bool vc_knob = true;       // MIMIC_JIT_VC=0: no lane value cache (analyze_vc)
     uint32_t lds_stack_q = 16; // MIMIC_JIT_LDSSTK=Q: LDS window over the top 8Q bytes of frame 0
     bool vc_on = false;
@@ -325,6 +344,7 @@ class Gen {
                     if ((h == H_ST || h == H_STX) && insn_dst(x) == 10 && !elided.count({p.id, i})) any = true;
                 }
             if (any) E.line("#define MIMIC_LDS_STACK_Q %u", lds_stack_q);
+            lds_stack_on = any;
         }
         if (defer_mode && sm_lds_knob) E.line("#define MIMIC_SM_LDS 1");
         if (const char *rm = getenv("MIMIC_JIT_ROOMS")) E.line("#define MIMIC_ROOMS_MODE %d", atoi(rm));   // measurement knob
@@ -508,7 +528,41 @@ class Gen {
             E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) noff_ = *gp(kp.pkt_off + n_); }");
         }
         if (!spec_use.empty() && !spread_on) analyze_xpf();
-        if (pf && xpf.on) {
+        // (LDS budget: 4 blocks of 256 lanes per CU with the window alone; no other LDS user)
+        lpf_on = pf && xpf.on && lpf_knob && !xpf_knob && !spread_on && !stage && !vc_lds && !lds_stack_on && !defer_mode &&
+                 !hash_combine && lpf_safe();
+        if (!lpf_on && !xpf_knob) xpf.on = false;   // (the one-packet-ahead form only on request)
+        if (lpf_on) {
+            const uint32_t D = kLpfD, XW = xpf.words;
+            E.line("  // lane prefetch: packets 0..%u of the lane, descriptors + P%u slot %u window (data + %u, %u words)", D - 1,
+                   xpf.prog, xpf.hp, (uint32_t)xpf.off, XW);
+            E.line("  __shared__ uint64_t lpfo_[%uu * 256u];", D);
+            E.line("  __shared__ uint32_t lpfl_[%uu * 256u];", D);
+            E.line("  __shared__ uint64_t lpfw_[%uu * 256u];", D * XW);
+            E.line("  uint32_t lpf_n_ = 0u, xc_ok_ = 0u;");
+            E.line("  if (kp.entry_prog == %uu && !kp.headroom_arr && !kp.tailroom_arr && kp.headroom == 0u && kp.tailroom == 0u) {", xpf.prog);
+            for (uint32_t d = 0; d < D; d++) {
+                E.line("    const uint32_t lx%u_ = pkt_index(kp, g, %uu, ex_begin, ex_count);", d, d);
+                E.line("    uint64_t lo%u_ = 0; uint32_t ll%u_ = 0;", d, d);
+                E.line("    if (lx%u_ != NO_PKT) { lo%u_ = *gp(kp.pkt_off + lx%u_); ll%u_ = *gp(kp.pkt_len + lx%u_); }", d, d, d, d, d);
+            }
+            for (uint32_t d = 0; d < D; d++) {
+                for (uint32_t q = 0; q < XW; q++) E.line("    uint64_t lw%u_%u_ = 0;", d, q);
+                E.line("    const bool lk%u_ = lx%u_ != NO_PKT && %uu <= ll%u_;", d, d, (uint32_t)xpf.off + 8 * XW, d);
+                E.line("    if (lk%u_) {", d);
+                E.line("      const uint8_t *xp_ = kp.pkt_data + lo%u_ + %uu;", d, (uint32_t)xpf.off);
+                for (uint32_t q = 0; q < XW; q++) E.line("      lw%u_%u_ = ld_n(xp_ + %uu, 8u);", d, q, 8 * q);
+                E.line("    }");
+            }
+            for (uint32_t d = 0; d < D; d++) {
+                E.line("    lpfo_[%uu * 256u + threadIdx.x] = lo%u_;", d, d);
+                E.line("    lpfl_[%uu * 256u + threadIdx.x] = ll%u_ | (lk%u_ ? 0x80000000u : 0u);", d, d, d);
+                for (uint32_t q = 0; q < XW; q++) E.line("    lpfw_[%uu * 256u + threadIdx.x] = lw%u_%u_;", d * XW + q, d, q);
+            }
+            E.line("    lpf_n_ = lx0_ == NO_PKT ? 0u : lx1_ == NO_PKT ? 1u : lx2_ == NO_PKT ? 2u : lx3_ == NO_PKT ? 3u : 4u;");
+            E.line("  }");
+            static_assert(kLpfD == 4, "the lpf_n_ line above");
+        } else if (pf && xpf.on) {
             // descriptors two packets ahead, the window one packet ahead (analyze_xpf)
             E.line("  const bool xpf_on_ = kp.entry_prog == %uu && !kp.headroom_arr;   // P%u slot %u window, data + %u, %u words",
                    xpf.prog, xpf.prog, xpf.hp, (uint32_t)xpf.off, xpf.words);
@@ -537,7 +591,20 @@ class Gen {
             E.line("    else if (kp.sched == SCHED_INTERLEAVED) { const uint64_t ii = (uint64_t)j * kp.lanes + (g >= kp.sched_shift ? g - kp.sched_shift : g + kp.lanes - kp.sched_shift); if (ii >= kp.n) break; i = (uint32_t)ii; }");
             E.line("    else { if (j >= ex_count) break; i = ld_nt(kp.sched_pkts + ex_begin + j); }");
         }
-        if (pf && xpf.on) {
+        if (lpf_on) {
+            E.line("    uint64_t poff_; uint32_t plen_;");
+            for (uint32_t q = 0; q < xpf.words; q++) E.line("    uint64_t xc%u_ = 0;", q);
+            E.line("    if (j < lpf_n_) {   // parked in LDS when the lane started");
+            E.line("      poff_ = lpfo_[j * 256u + threadIdx.x];");
+            E.line("      const uint32_t lw_ = lpfl_[j * 256u + threadIdx.x];");
+            E.line("      plen_ = lw_ & 0x7fffffffu;");
+            E.line("      xc_ok_ = lw_ >> 31;");
+            for (uint32_t q = 0; q < xpf.words; q++)
+                E.line("      if (xc_ok_) xc%u_ = lpfw_[(j * %uu + %uu) * 256u + threadIdx.x];", q, xpf.words, q);
+            E.line("    } else {");
+            E.line("      poff_ = *gp(kp.pkt_off + i); plen_ = *gp(kp.pkt_len + i); xc_ok_ = 0u;");
+            E.line("    }");
+        } else if (pf && xpf.on) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             E.line("    xc_ok_ = xn_ok_;");
             for (uint32_t q = 0; q < xpf.words; q++) E.line("    const uint64_t xc%u_ = xn%u_;", q, q);
@@ -551,6 +618,7 @@ class Gen {
             else if (spread_on) E.line("    { const uint32_t n_ = i + 256u; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
+        if (memtime) E.line("    const uint32_t mt0_ = (uint32_t)__builtin_amdgcn_s_memrealtime();");
         // fields used once per packet are read through an opaque copy of the parameter pointer:
         // loaded where used instead of hoisted out of the packet loop into SGPRs
         if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
@@ -686,8 +754,10 @@ class Gen {
             E.line("    if (kq_.status) *gp(kq_.status + i) = (uint8_t)st_;");
         }
         if (census) E.line("    if (kq_.steps) st_nt(kq_.steps + i, coldn_);   // census: slow-path calls, not steps");
+        else if (memtime) E.line("    if (kq_.steps) st_nt(kq_.steps + i, (uint32_t)__builtin_amdgcn_s_memrealtime());");
         else E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
-        E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
+        if (memtime) E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, (int32_t)mt0_);");
+        else E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
         E.line("#endif");
         E.line("    }");
         E.line("    lane_steps += steps;");
@@ -985,8 +1055,90 @@ class Gen {
     // zeroed at packet start); a packet too short, a per-packet headroom array or another entry
     // program takes the normal window code.  Any jump or call to slot 0 disables it; a tail call
     // clears the flag, so only the packet's own first pass through slot 0 uses the words.
+    // Lane prefetch is exact when no packet's bytes can change between the lane's start and the
+    // packet's own run: no program of the set stores through a base that may be a packet pointer.
+    // Every store (ST / STX / atomics) must go through R10 (+ a constant) or through a map value
+    // pointer a lookup just returned; helpers other than map lookup / update / delete,
+    // get_smp_processor_id and tail calls, and BPF-to-BPF calls, turn it off.
+    bool lpf_safe() const {
+        for (auto &p : P) {
+            if (!p.n) continue;
+            const std::vector<uint32_t> Lb = leaders(p);
+            std::map<uint32_t, size_t> blk;
+            for (size_t b = 0; b < Lb.size(); b++) blk[Lb[b]] = b;
+            // per register: bit r of `ns` = may be something other than a stack or map-value pointer
+            constexpr uint16_t ALLR = 0x7ff;
+            std::vector<uint16_t> in(Lb.size(), 0);
+            std::vector<bool> seen(Lb.size(), false);
+            seen[0] = true;
+            in[0] = (uint16_t)(ALLR & ~(1u << 10));
+            for (bool changed = true; changed;) {
+                changed = false;
+                for (size_t b = 0; b < Lb.size(); b++) {
+                    if (!seen[b]) continue;
+                    const uint32_t s0 = Lb[b], e = b + 1 < Lb.size() ? Lb[b + 1] : p.n;
+                    uint16_t ns = in[b];
+                    auto bad = [&](uint32_t r) { return r > 10 || ((ns >> r) & 1); };
+                    auto setb = [&](uint32_t r, bool v) {
+                        if (r <= 10) ns = v ? (uint16_t)(ns | (1u << r)) : (uint16_t)(ns & ~(1u << r));
+                    };
+                    for (uint32_t i = s0; i < e; i++) {
+                        const DInsn &x = p.ins[i];
+                        const uint32_t h = AUX_H(x.aux), d = insn_dst(x), sr = insn_src(x), op = insn_op(x);
+                        const bool X = (x.aux & AUX_X) != 0;
+                        switch (h) {
+                        case H_NOP: case H_JA: case H_JCC: case H_EXIT: case H_ERR:
+                            break;
+                        case H_ALU64: {   // a pointer moved, or moved by a constant, stays one
+                            const uint32_t alu = op & 0xf0;
+                            if (alu == 0xb0) setb(d, !X || bad(sr));
+                            else if ((alu == 0x00 || alu == 0x10) && !X) setb(d, bad(d));
+                            else setb(d, true);
+                            break;
+                        }
+                        case H_ALU32: case H_LDIMM: case H_LDX:
+                            setb(d, true);
+                            break;
+                        case H_ST: case H_STX:
+                            if (bad(d)) return false;
+                            break;
+                        case H_CALL: {
+                            const uint32_t k = (uint32_t)x.k;
+                            if (k != 1 && k != 2 && k != 3 && k != 8 && k != 12) return false;
+                            ns |= 0x3f;
+                            if (k == 1) ns &= (uint16_t)~1u;   // R0: a map value pointer (or 0)
+                            break;
+                        }
+                        case H_SLOW:
+                            if (((op & 7) == 2 || (op & 7) == 3) && bad(d)) return false;
+                            if ((op & 7) == 0 || (op & 7) == 1 || (op & 7) == 4 || (op & 7) == 7) setb(d, true);
+                            break;
+                        default:   // BPF-to-BPF calls, LD_ABS / LD_IND
+                            return false;
+                        }
+                    }
+                    const DInsn &last = p.ins[e - 1];
+                    const uint32_t lh = AUX_H(last.aux);
+                    std::vector<int64_t> succ;
+                    if ((!ends_block(last) || lh == H_JCC) && (last.aux & AUX_FALL_OK)) succ.push_back(e);
+                    if ((lh == H_JA || lh == H_JCC) && (last.aux & AUX_JT_OK)) succ.push_back(jump_target(last, e - 1));
+                    for (int64_t sx : succ) {
+                        auto it = blk.find((uint32_t)sx);
+                        if (it == blk.end()) continue;
+                        const uint16_t nin = (uint16_t)(in[it->second] | ns);
+                        if (!seen[it->second] || nin != in[it->second]) {
+                            in[it->second] = nin;
+                            seen[it->second] = true;
+                            changed = true;
+                        }
+                    }
+                }
+            }
+        }
+        return true;
+    }
     void analyze_xpf() {
-        if (!xpf_knob || ctx != CTX_XDP || !prefetch || !window || stage || !fast_paths) return;
+        if (!(xpf_knob || lpf_knob) || ctx != CTX_XDP || !prefetch || !window || stage || !fast_paths) return;
         for (auto &p : P) {
             if (p.n == 0) continue;
             bool to0 = false;

@@ -392,6 +392,92 @@ def test_cross_packet_window_prefetch(gpu, case, room, sched, monkeypatch):
     assert len(set(o["r0"].tolist())) > 100
 
 
+@pytest.mark.parametrize("case", [0, 1])
+@pytest.mark.parametrize("room", ["none", "uniform", "per_packet"])
+@pytest.mark.parametrize("sched", ["interleaved", "chunked", "explicit"])
+@pytest.mark.parametrize("V", [400, 700])
+def test_lane_prefetch(gpu, case, room, sched, V, monkeypatch):
+    """Lane prefetch (jit.cpp lpf_on, MIMIC_JIT_LPF=1: off by default, measured slower on cfg 2; for
+    xdp_md program sets that never store into packet memory): a lane's first 4 packets' descriptors and early windows are loaded when the lane
+    starts and parked in LDS.  Every schedule, rooms (prefetch off at run time), short packets
+    (window past the packet), lanes with fewer and with more than 4 packets (V = 700 / 400; fewer
+    than 8 packets per vCPU, so no spread launch): oracle-exact.  The
+    windowed program of XPF_CASES without the packet store (case 0: window at data + 12, case 1:
+    data + 26)."""
+    monkeypatch.setenv("MIMIC_JIT_LPF", "1")
+    items_c = XPF_CASES[case][0]
+    sc = Scenario(vcpus=V, maps=[dict(name="c", type=6, key_size=4, value_size=8, max_entries=4)],
+                  progs=[_lpf_prog(items_c)])
+    import mimic_amd as M
+    from mimic_amd import jit as J
+
+    assert "lpf_n_" in J.kernel_source(*kernel_of(sc))
+    n = 3000
+    rng = np.random.default_rng(case + 7)
+    headroom = {"none": 0, "uniform": 16, "per_packet": rng.integers(0, 4, n) * 8}[room]
+    tailroom = 8 if room == "uniform" else 0
+    pkts = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in rng.choice([20, 36, 40, 41, 60, 64, 128], n)]
+    buf, off, lens = packets_to_buffer(pkts, headroom, tailroom)
+    mode = {"interleaved": M.SCHED_INTERLEAVED, "chunked": M.SCHED_CHUNKED, "explicit": M.SCHED_EXPLICIT}[sched]
+    cpu = rng.integers(0, V, n).astype(np.int32) if sched == "explicit" else W.schedule_cpu(n, V, sched)
+    o = run_oracle(sc, buf, off, lens, cpu, headroom=headroom, tailroom=tailroom)
+    e = run_engine(sc, buf, off, lens, cpu if sched == "explicit" else None, headroom=headroom, tailroom=tailroom,
+                   schedule=mode)
+    assert_same(o, e)
+    assert e["last_exec"] == "jit"
+    assert len(set(o["r0"].tolist())) > 100
+
+
+def test_lane_prefetch_needs_packet_memory_untouched(monkeypatch):
+    """A program set that may store into packet memory (a store through a packet pointer, or
+    through a base the analysis cannot place) gets no lane prefetch."""
+    from mimic_amd import jit as J
+
+    monkeypatch.setenv("MIMIC_JIT_LPF", "1")
+    sc = _xpf_scenario(0, True)
+    assert "lpf_n_" not in J.kernel_source(*kernel_of(sc))   # _xpf_prog(tail) stores into the packet
+    assert "lpf_n_" in J.kernel_source(*kernel_of(Scenario(vcpus=8, maps=[dict(name="c", type=6, key_size=4,
+                                                                                value_size=8, max_entries=4)],
+                                                            progs=[_lpf_prog(0)])))
+
+
+def _lpf_prog(c):
+    """Reads a window of packet bytes at data + 12 + c (early loads), folds them into R0 and a
+    per-CPU counter[r0 & 3] += 1; no store into the packet."""
+    items = [
+        A.mov64_reg(6, 1),
+        A.ldx(4, 2, 6, 0),
+        A.ldx(4, 3, 6, 4),
+        A.mov64_reg(4, 2),
+        A.alu64("add", 4, 24 + c),
+        A.jmp("jgt", 4, 3, "out", reg=True),
+        A.ldx(2, 7, 2, 12 + c),
+        A.ldx(4, 8, 2, 14 + c),
+        A.ldx(1, 9, 2, 21 + c),
+        A.alu64("lsh", 8, 8),
+        A.alu64("xor", 7, 8, reg=True),
+        A.alu64("add", 7, 9, reg=True),
+        A.mov64_reg(5, 7),
+        A.alu64("and", 5, 3),
+        A.stx(4, 10, -4, 5),
+        A.mov64_reg(2, 10),
+        A.alu64("add", 2, -4),
+        A.ld_map_fd(1, "c"),
+        A.call(A.FN_MAP_LOOKUP_ELEM),
+        A.jmp("jeq", 0, 0, 3),
+        A.ldx(8, 1, 0, 0),
+        A.alu64("add", 1, 1),
+        A.stx(8, 0, 0, 1),
+        A.mov64_reg(0, 7),
+        A.exit_(),
+        "out",
+        A.mov64_imm(0, 2),
+        A.exit_(),
+    ]
+    raw, rel = A.assemble(items)
+    return ("lpf", raw, rel)
+
+
 # ---------------------------------------------------------------------------------------------
 # LDS stack window (runtime.h, MIMIC_LDS_STACK_Q): frame 0's top 128 bytes live in LDS, the rest
 # of the stack in HBM.  Stores and loads of every size at offsets around the window's lower edge

@@ -403,3 +403,44 @@ def test_two_hash_maps_inserted_by_one_program(gpu, V):
         assert_same(o, e)
     else:
         assert_same(o, e, check_pkt=False, hash_exact=False, check_steps=False)
+
+
+@pytest.mark.parametrize("host_ops", [6, 400])
+def test_launches_and_host_ops_interleaved(gpu, host_ops):
+    """launch -> host Update / Delete / Lookup -> launch, five rounds, on a 20 000-entry table
+    (the host image is fetched on demand after a launch -- a few pages for a few
+    operations, the rest in one copy once they fault MIRROR_BULK pages -- and only the touched
+    records, ring positions, keys and the counters go back).  One vCPU, so every slot, tombstone
+    and freelist position is the oracle's; the table is compared after every round."""
+    p = W.prog_flowcount(max_entries=20000, delete_every=3)
+    sc = _sc(p, 1)
+    m = p.maps[0]
+    ovm, omids, opids = build_oracle(sc)
+    evm, emaps, epids = build_engine(sc)
+    om, em = omids[m["name"]], emaps[m["name"]]
+    import mimic_amd as M
+
+    rng = np.random.default_rng(host_ops)
+    for rnd in range(5):
+        buf, off, lens = W.make_packets(6000, **W.IMIX, seed=100 + rnd)
+        cpu = np.zeros(len(lens), np.int32)
+        o = ovm.run_xdp_batch(opids[0], buf.copy(), off, lens, cpu, write_back=False)
+        b = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_EXPLICIT, cpu=cpu)
+        e = evm.RunXDPBatch(epids[0], b).numpy(len(lens))
+        assert np.array_equal(np.asarray(o["r0"]).astype(np.int64), np.asarray(e["r0"]).astype(np.int64)), rnd
+        keys = [k for k, _ in ovm.map_entries(om)]
+        for step in range(host_ops):
+            op = rng.random()
+            key = keys[int(rng.integers(0, len(keys)))] if keys and op < 0.6 else bytes(rng.integers(0, 256, m["key_size"], dtype=np.uint8))
+            if op < 0.3:
+                assert em.Lookup(key, 0) == ovm.map_lookup(om, key, 0)[1], (rnd, step)
+            elif op < 0.6:
+                assert em.Delete(key) == 0
+                assert ovm.lib.orc_map_delete(ovm.h, om, key) == 0
+            else:
+                val = bytes(rng.integers(0, 256, m["value_size"], dtype=np.uint8))
+                assert em.Update(key, val, 0, 0) == ovm.map_update(om, key, val, 0, 0), (rnd, step)
+        assert sorted(em.Entries()) == sorted(ovm.map_entries(om)), rnd
+        assert em.Values(0) == ovm.map_values(om, 0), rnd
+    evm.close()
+    ovm.close()
