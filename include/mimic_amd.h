@@ -341,11 +341,15 @@ int mimic_process_run_ctx(mimic_process *p, uint64_t budget, mimic_ctx *ctx, mim
 /* processPool's workers (vm.go:548-573): n x Process.Run(ctx) of fresh (never stepped or run) sk_buff
  * processes of one VM, program and ifindex, as ONE device launch instead of one launch per process.
  * Each process keeps the sock / flow-keys / packet addresses its Load reserved at NewProcess and runs
- * on its SetCPUID vCPU (-1 and V allowed); a vCPU's processes run in array order.  ctxs: HOST array
- * [n] of contexts (NULL entries, or ctxs NULL: Background), no step budget.  Afterwards every process
- * is finished: out[i] (optional, [n]) and the process hold R0, status, steps; a batch lane keeps no
- * R1-R10 (zero) and pc is the failing instruction or -1.  Not in the reference API. */
-int mimic_process_run_many(mimic_process *const *ps, uint32_t n, mimic_ctx *const *ctxs, mimic_process_regs *out);
+ * on its SetCPUID vCPU (-1 and V allowed; cpus: HOST array [n] that sets them first, or NULL); a
+ * vCPU's processes run in array order.  ctxs: HOST array [n] of contexts (NULL entries, or ctxs NULL:
+ * Background), no step budget.  Afterwards every process is finished: out[i] (optional, [n]) and the
+ * process hold R0, status, steps; a batch lane keeps no R1-R10 (zero) and pc is the failing
+ * instruction or -1.  Not in the reference API. */
+int mimic_process_run_many(mimic_process *const *ps, uint32_t n, const int32_t *cpus, mimic_ctx *const *ctxs,
+                           mimic_process_regs *out);
+/* n x Process.Cleanup with one wait for the VM's stream (NULL entries skipped). */
+void mimic_process_free_many(mimic_process *const *ps, uint32_t n);
 
 /* The process's packet memory (headroom + packet + tailroom) as the program left it. */
 int mimic_process_packet(mimic_process *p, void *buf, size_t cap);

@@ -210,6 +210,10 @@ struct mimic_vm {
     // of the processes of one launch (one allocation, grown as needed)
     uint8_t *d_many = nullptr;
     size_t many_cap = 0;
+    // single processes' device blocks (proc_alloc): freed blocks are kept per power-of-two size and
+    // handed to the next NewProcess, so a process costs no hipMalloc / hipFree once the VM is warm
+    std::map<size_t, std::vector<uint8_t *>> blk_free;
+    size_t blk_cached = 0;
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
     hipStream_t skb_stream = nullptr;
     bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
@@ -670,6 +674,8 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (!vm) return;
     hipSetDevice(vm->s.device);
     if (vm->stream) hipStreamSynchronize(vm->stream);
+    for (auto &c : vm->blk_free)
+        for (uint8_t *b : c.second) hipFree(b);
     hipFree(vm->arena);
     hipFree(vm->d_insns);
     hipFree(vm->d_progs);
@@ -2177,19 +2183,43 @@ struct mimic_process {
     bool skb_custom = false;          // a user-given sock / flow keys after the base word
     uint32_t ifindex = 0;
     uint8_t *d_skbmem = nullptr;      // SkbRec | prefix (2 words) | base | mimic_skb_custom
+    // every buffer above but d_priv is carved from one block (proc_alloc); d_priv is a block of its own
+    uint8_t *blk = nullptr;
+    size_t blk_size = 0, priv_size = 0;
 };
 
+// device blocks of single processes, from the VM's cache (one hipMalloc per size class ever)
+static size_t blk_class(size_t n) {
+    size_t c = 1024;
+    while (c < n) c <<= 1;
+    return c;
+}
+static uint8_t *proc_alloc(mimic_vm *vm, size_t n, size_t *cls) {
+    const size_t c = blk_class(n);
+    *cls = c;
+    auto it = vm->blk_free.find(c);
+    if (it != vm->blk_free.end() && !it->second.empty()) {
+        uint8_t *b = it->second.back();
+        it->second.pop_back();
+        vm->blk_cached -= c;
+        return b;
+    }
+    uint8_t *b = nullptr;
+    return hipMalloc(&b, c) == hipSuccess ? b : nullptr;
+}
+static void proc_free(mimic_vm *vm, uint8_t *b, size_t cls) {
+    if (!b) return;
+    if (vm->blk_cached + cls > (256ull << 20)) {   // keep at most 256 MiB of free blocks
+        hipFree(b);
+        return;
+    }
+    vm->blk_free[cls].push_back(b);
+    vm->blk_cached += cls;
+}
 static void process_release(mimic_process *p) {
-    hipFree(p->d_pkt);
-    hipFree(p->d_off);
-    hipFree(p->d_len);
-    hipFree(p->d_r0);
-    hipFree(p->d_st);
-    hipFree(p->d_steps);
-    hipFree(p->d_epc);
-    hipFree(p->d_state);
-    hipFree(p->d_priv);
-    hipFree(p->d_skbmem);
+    proc_free(p->vm, p->blk, p->blk_size);
+    proc_free(p->vm, p->d_priv, p->priv_size);
+    p->blk = p->d_priv = nullptr;
 }
 
 static void process_regs(const mimic_process *p, mimic_process_regs *out) {
@@ -2219,10 +2249,10 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     p->static_next = vm->next_addr;
     p->arena = vm->arena;
     if ((uint64_t)pp.q_per_lane * 8 > p->priv_bytes) {
-        hipFree(p->d_priv);
-        p->d_priv = nullptr;
+        proc_free(vm, p->d_priv, p->priv_size);
         p->priv_bytes = (uint64_t)pp.q_per_lane * 8;
-        HIP_OK(vm, hipMalloc(&p->d_priv, p->priv_bytes));
+        p->d_priv = proc_alloc(vm, p->priv_bytes, &p->priv_size);
+        if (!p->d_priv) return fail(vm, MIMIC_ENOMEM, "process private memory");
     }
     StepState st = p->h;
     st.cpu = p->cpu;
@@ -2289,19 +2319,30 @@ static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint
     p->egress = egress_ifindex;
     memset(&p->h, 0, sizeof p->h);
     const uint64_t M = (uint64_t)headroom + len + tailroom;
-    const uint64_t zero = 0;
-    hipError_t e = hipMalloc(&p->d_pkt, std::max<uint64_t>(M, 1));
-    if (e == hipSuccess) e = hipMemset(p->d_pkt, 0, std::max<uint64_t>(M, 1));
-    if (e == hipSuccess && len) e = hipMemcpy(p->d_pkt + headroom, packet, len, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_off, 8);
-    if (e == hipSuccess) e = hipMemcpy(p->d_off, &zero, 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_len, 4);
-    if (e == hipSuccess) e = hipMemcpy(p->d_len, &len, 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_r0, 8);
-    if (e == hipSuccess) e = hipMalloc(&p->d_st, 1);
-    if (e == hipSuccess) e = hipMalloc(&p->d_steps, 4);
-    if (e == hipSuccess) e = hipMalloc(&p->d_epc, 4);
-    if (e == hipSuccess) e = hipMalloc(&p->d_state, sizeof(StepState));
+    // one block: StepState | r0 | status | steps | err_pc | off | len | sk_buff memory | packet memory,
+    // its head and the packet memory written by one copy
+    const size_t o_state = 0, o_r0 = (sizeof(StepState) + 63) & ~(size_t)63, o_st = o_r0 + 8, o_steps = o_r0 + 16,
+                 o_epc = o_r0 + 20, o_off = o_r0 + 24, o_len = o_r0 + 32, o_skb = (o_len + 4 + 63) & ~(size_t)63,
+                 o_pkt = (o_skb + sizeof(SkbRec) + 24 + sizeof(mimic_skb_custom) + 63) & ~(size_t)63, total = o_pkt + std::max<uint64_t>(M, 1);
+    p->blk = proc_alloc(vm, total, &p->blk_size);
+    if (!p->blk) {
+        delete p;
+        return fail(vm, MIMIC_ENOMEM, "process memory");
+    }
+    uint8_t *b = p->blk;
+    p->d_state = (StepState *)(b + o_state);
+    p->d_r0 = (uint64_t *)(b + o_r0);
+    p->d_st = b + o_st;
+    p->d_steps = (uint32_t *)(b + o_steps);
+    p->d_epc = (int32_t *)(b + o_epc);
+    p->d_off = (uint64_t *)(b + o_off);
+    p->d_len = (uint32_t *)(b + o_len);
+    p->d_skbmem = b + o_skb;
+    p->d_pkt = b + o_pkt;
+    std::vector<uint8_t> img(total, 0);   // descriptor (off 0, len) and the packet memory, rooms zero
+    memcpy(img.data() + o_len, &len, 4);
+    if (len) memcpy(img.data() + o_pkt + headroom, packet, len);
+    const hipError_t e = hipMemcpy(b + o_off, img.data() + o_off, total - o_off, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         process_release(p);
         delete p;
@@ -2322,17 +2363,14 @@ int mimic_process_new_skb_ctx(mimic_vm *vm, uint32_t prog_id, const void *packet
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     // the packet memory is SKB_HEADROOM + len + SKB_TAILROOM with the frame at +SKB_HEADROOM
     // (context_sk_buff.go:42-107), run by the interpreter's stepping kernel as a one-packet batch
-    int rc = process_make(vm, prog_id, nullptr, 0, SKB_HEADROOM, SKB_TAILROOM + len, 0, 0, 0, out);
+    int rc = process_make(vm, prog_id, packet, len, SKB_HEADROOM, SKB_TAILROOM, 0, 0, 0, out);
     if (rc) return rc;
     mimic_process *p = *out;
     p->skb = true;
     p->ifindex = ifindex;
     p->len = len;
     p->T = SKB_TAILROOM;
-    hipError_t e = hipSuccess;
-    if (len) e = hipMemcpy(p->d_pkt + SKB_HEADROOM, packet, len, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_len, &len, 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_skbmem, sizeof(SkbRec) + 24 + sizeof(mimic_skb_custom));
+    hipError_t e = hipSuccess;   // (process_make placed the packet at +headroom and wrote len)
     p->skb_custom = custom && custom->flags;
     if (e == hipSuccess && p->skb_custom)
         e = hipMemcpy(p->d_skbmem + sizeof(SkbRec) + 24, custom, sizeof(mimic_skb_custom), hipMemcpyHostToDevice);
@@ -2489,7 +2527,8 @@ int mimic_process_run_ctx(mimic_process *p, uint64_t budget, mimic_ctx *ctx, mim
 // Background).  Afterwards each process is finished: R0, status, steps in out[i] (and its host
 // state); registers R1-R10 and the PC are not kept by a batch lane (out[i].r[1..10] = 0, pc = the
 // failing instruction or -1).  Packet memory is the process's own (mimic_process_packet).
-int mimic_process_run_many(mimic_process *const *ps, uint32_t n, mimic_ctx *const *ctxs, mimic_process_regs *out) {
+int mimic_process_run_many(mimic_process *const *ps, uint32_t n, const int32_t *cpus, mimic_ctx *const *ctxs,
+                           mimic_process_regs *out) {
     if (!ps || !n) return n ? MIMIC_EINVAL : 0;
     mimic_vm *vm = ps[0] ? ps[0]->vm : nullptr;
     if (!vm) return MIMIC_EINVAL;
@@ -2497,8 +2536,12 @@ int mimic_process_run_many(mimic_process *const *ps, uint32_t n, mimic_ctx *cons
     uint8_t *lo = nullptr;
     bool any_cust = false;
     for (uint32_t i = 0; i < n; i++) {
-        const mimic_process *p = ps[i];
+        mimic_process *p = ps[i];
         if (!p || p->vm != vm) return fail(vm, MIMIC_EINVAL, "process %u: not a process of this VM", i);
+        if (cpus) {   // SetCPUID (vm.go:268-283) of each process first
+            if (cpus[i] < 0 || cpus[i] > vm->s.vcpus) return fail(vm, MIMIC_EINVAL, "process %u: not a valid CPU ID", i);
+            p->cpu = cpus[i];
+        }
         if (!p->skb) return fail(vm, MIMIC_ENOTSUP, "process %u: not an sk_buff process", i);
         if (p->prog != prog || p->ifindex != ifindex)
             return fail(vm, MIMIC_EINVAL, "process %u: one program and one interface per launch", i);
@@ -2606,6 +2649,21 @@ void mimic_process_free(mimic_process *p) {
     hipStreamSynchronize(p->vm->stream);
     process_release(p);
     delete p;
+}
+
+void mimic_process_free_many(mimic_process *const *ps, uint32_t n) {
+    mimic_vm *last = nullptr;
+    for (uint32_t i = 0; i < n; i++) {
+        mimic_process *p = ps[i];
+        if (!p) continue;
+        if (p->vm != last) {   // one wait per VM for the launches that may use the memory
+            last = p->vm;
+            hipSetDevice(last->s.device);
+            hipStreamSynchronize(last->stream);
+        }
+        process_release(p);
+        delete p;
+    }
 }
 
 int mimic_sync(mimic_vm *vm, void *hip_stream) {

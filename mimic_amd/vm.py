@@ -659,7 +659,16 @@ class VM:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
         return results
 
-    def RunProcesses(self, procs: Sequence["Process"], ctxs: Optional[Sequence[Optional["Context"]]] = None) -> None:
+    def CleanupProcesses(self, procs: Sequence["Process"]) -> None:
+        """Process.Cleanup of many processes (one wait for the VM's stream)."""
+        nat = [p._native for p in procs if p._native is not None]
+        if nat and getattr(self, "h", None):
+            self.lib.mimic_process_free_many((C.c_void_p * len(nat))(*nat), len(nat))
+        for p in procs:
+            p._native = None
+
+    def RunProcesses(self, procs: Sequence["Process"], ctxs: Optional[Sequence[Optional["Context"]]] = None,
+                     cpus: Optional[Sequence[int]] = None) -> None:
         """processPool's workers for fresh sk_buff processes: Run(ctx) of every process as ONE device
         launch (mimic_process_run_many), each with the leak addresses its NewProcess reserved and on
         its SetCPUID vCPU.  Afterwards each process has R0, Status, Steps and ErrPC (registers R1-R10
@@ -678,11 +687,21 @@ class VM:
                     hs[id(c)] = c._device_handle()
             cx = (C.c_void_p * n)(*[hs[id(c)] if _live(c) is not None else None for c in ctxs])
         regs = (L.ProcessRegs * n)()
-        _check(self.h, self.lib.mimic_process_run_many(arr, n, cx, regs), "RunProcesses")
-        for p, r in zip(procs, regs):
-            p._take(r)
+        ca = None
+        if cpus is not None:
+            import numpy as np
+
+            ca = np.ascontiguousarray(cpus, dtype=np.int32)
+        _check(self.h, self.lib.mimic_process_run_many(arr, n, ca.ctypes.data if ca is not None else None, cx, regs),
+               "RunProcesses")
+        for p, r in zip(procs, regs):   # what a batch lane keeps: R0, status, steps (R1-R10 zero)
+            st = int(r.status)
+            p.Registers.R0 = int(r.r[0])
+            p.Steps = int(r.steps)
+            p.Status = st
+            p._exited = True
             p._started = True
-            p.ErrPC = int(r.pc) if p.Status else -1
+            p.ErrPC = int(r.pc) if st else -1
 
     def SKBRelease(self) -> None:
         """Forget the sock / flow-keys / packet entries earlier sk_buff processes leaked (a fresh
@@ -1404,7 +1423,10 @@ class ProcessPool:
             if owner.get(cpu, key) != key:
                 self._run_groups(groups)
                 groups, owner = {}, {}
-            job.Process.SetCPUID(cpu)
+            if skb and not job.Process._started:
+                job.Process.cpuID = cpu   # its native SetCPUID goes with the launch (RunProcesses cpus)
+            else:
+                job.Process.SetCPUID(cpu)
             self._next_cpu = (cpu + 1) % V
             owner[cpu] = key
             groups.setdefault(key, []).append(job)
@@ -1418,6 +1440,7 @@ class ProcessPool:
                 for job in js:
                     self._handoff(job, ex)
                 continue
+            done = []   # jobs without a handoff: cleaned up together (one stream wait)
             for job in js:
                 p = job.Process
                 err = None
@@ -1425,7 +1448,11 @@ class ProcessPool:
                     err = MimicError(Context._ERR[p.Status - L.STATUS["ERR_CANCELED"] + 1])
                 elif p.Status:
                     err = MimicError(f"process encountered a fatal error: {L.STATUS_NAMES[p.Status]} at PC({p.ErrPC})")
-                self._handoff(job, err)
+                if job.Handoff is None:
+                    done.append(p)
+                else:
+                    self._handoff(job, err)
+            self.vm.CleanupProcesses(done)
 
     def _launch(self, pid: int, skb: bool, js) -> None:
         dev = f"cuda:{self.vm.settings.device}"
@@ -1444,7 +1471,8 @@ class ProcessPool:
                     fresh.append(j)
                     continue
                 if fresh:
-                    self.vm.RunProcesses([f.Process for f in fresh], [f.Context for f in fresh])
+                    self.vm.RunProcesses([f.Process for f in fresh], [f.Context for f in fresh],
+                                         [f.Process.cpuID for f in fresh])
                     fresh = []
                 if j is None:
                     break
