@@ -398,8 +398,10 @@ int mimic_exec_mode(const mimic_vm *vm);
  * increment through one per-CPU array lookup, a vCPU's packets may run on many lanes (the final
  * counters are sums; each packet's R0 / status / steps depend on its own bytes only).
  * mode -1: default (env MIMIC_SPREAD, else when a batch has >= 8 packets per vCPU), 0: never,
- * 1: whenever the programs allow it.  mimic_sync / mimic_last_steps fail if a spread launch
- * reached per-CPU memory outside a fused increment. */
+ * 1: whenever the programs allow it.  Every generic load / store of such a program set must go
+ * through a base the analysis can place (derived from R1, R10 or a packet pointer), else the set runs
+ * one lane per vCPU.  (mimic_sync / mimic_last_steps would fail if a spread launch still reached
+ * per-CPU memory outside a fused increment: an internal assertion.) */
 int mimic_set_spread(mimic_vm *vm, int32_t mode);
 /* The kernel the last batch ran on (a JIT VM runs batches whose step budget is below its
  * loop-free kernels' step bound on the interpreter). */

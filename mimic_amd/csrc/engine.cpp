@@ -1723,8 +1723,9 @@ static int priv_ensure(mimic_vm *vm, uint32_t q_per_lane, uint32_t lanes, hipStr
     return 0;
 }
 
-// a spread launch marked per-CPU memory touched outside fused increments: its results may not be
-// the reference's, which is reported as an engine error (the stream has been synchronized)
+// a spread launch marked per-CPU memory touched outside fused increments (an internal assertion:
+// jit.cpp analyze_spread's base provenance keeps such program sets off spread kernels): its
+// results may not be the reference's, which is reported as an engine error (stream synchronized)
 static int spread_check(mimic_vm *vm) {
     if (!vm->spread_used || !vm->d_spread_bad) return 0;
     uint32_t f = 0;

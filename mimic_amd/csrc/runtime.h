@@ -394,8 +394,10 @@ DEV void xdp_store(const KParams &kp, Lane &L, uint32_t o, uint32_t n, uint64_t 
 
 // Spread kernels (MIMIC_SPREAD, jit.cpp analyze_spread) run one vCPU's packets on many lanes:
 // exact only while per-CPU map memory is touched by fused counter increments alone.  The
-// generator proves that for every access it can see; a generic access that still resolves into
-// per-CPU memory (an address the program computed) marks the launch instead of passing silently.
+// generator proves that for every access (base provenance: a generic load or store whose base it
+// cannot place keeps the program set on one lane per vCPU), so this is an internal assertion of
+// that analysis: a generic access that still resolved into per-CPU memory marks the launch, which
+// the engine reports as an engine error instead of passing silently.
 #ifdef MIMIC_SPREAD
 #define SPREAD_GUARD(kp) do { if ((kp).spread_bad) *gp((kp).spread_bad) = 1u; } while (0)
 #else
@@ -863,7 +865,13 @@ DEV HelperOut helper_update(const KParams &kp, const Lane &L, uint64_t r1, uint6
         idx = h_insert_nolock(t, ks, h, &inserted);
     } else if (idx < 0) {
         // a new key: find-or-insert under its stripe lock, the wave's lanes in lock rounds
+        // (with MIMIC_HASH_NOLOCK a pop-only launch never gets here: one locked form, not two, is
+        // compiled in -- the interpreter's register budget)
+#if MIMIC_HASH_NOLOCK
+        idx = h_insert_wave(t, ks, h, &inserted, false);
+#else
         idx = HASH_POPONLY(kp) ? h_insert_wave(t, ks, h, &inserted, true) : h_insert_wave(t, ks, h, &inserted, false);
+#endif
     }
     if (idx < 0) {
         o.r0 = 7; // syscall.E2BIG: the freelist is empty

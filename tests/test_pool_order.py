@@ -13,13 +13,15 @@ class _Proc:
         self.Context = M.LinuxContextSKBuff() if skb else M.LinuxContextXDP()
         self.cpuID = -1
         self.Status = 0
+        self._started = False
 
     def SetCPUID(self, c):
         self.cpuID = c
 
 
 def _pool(V):
-    pool = ProcessPool(SimpleNamespace(settings=SimpleNamespace(vcpus=V)))
+    cleaned = []
+    pool = ProcessPool(SimpleNamespace(settings=SimpleNamespace(vcpus=V), CleanupProcesses=cleaned.extend))
     launches = []
     pool._launch = lambda pid, skb, js: launches.append([(j.Process.prog_id, skb, j.Process.cpuID, j.idx) for j in js])
     pool._handoff = lambda job, err: None

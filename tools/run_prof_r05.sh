@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-5 end, part 1: PMC passes (kernel trace, FETCH_SIZE, WRITE_SIZE, read requests by size, SQ) of the
+# bench lines' kernels at HEAD; summaries under gpurun_out/prof_$T, copied into profiles/ before part 2
+# (tools/run_final_r05.sh) so the bench lines carry their traffic.
+#   T=r05 CONFIGS="classifier skb" bash tools/run_prof_r05.sh
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+T=${T:-r05}
+for c in ${CONFIGS:-classifier classifier_v256 skb parse5 flowtrack flowtrack_insert}; do
+  if [ $c = classifier_v256 ]; then
+    CFG=classifier NAME=classifier_v256 EXTRA="--vcpus 256" SUMMARY_ARGS="--vcpus 256 --spread" TAG=$T timeout -k 10 600 bash tools/profile.sh || exit 1
+  else
+    CFG=$c TAG=$T timeout -k 10 600 bash tools/profile.sh || { echo "profile $c failed"; exit 1; }
+  fi
+  tail -1 gpurun_out/prof_$T/summary_$c.log | cut -c1-300
+done
