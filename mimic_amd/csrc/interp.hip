@@ -171,7 +171,7 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         if (resumed) {
         } else if (i != 0xffffffffu && kp.ctx_kind == CTX_SKB) {   // LinuxContextSKBuff.Load (skb.h)
             uint64_t r1 = 0;
-            const int ls = skb_load(kp, L, i, r1, resume_here);
+            const int ls = skb_load<MODE == MODE_RESUME>(kp, L, i, r1, resume_here);
             REG(10) = kp.static_next + kp.frame_size;
             if (ls) {
                 TERM(ls, -1);

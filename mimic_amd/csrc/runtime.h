@@ -1024,15 +1024,20 @@ static_assert(SKB_HEADROOM == 32 && SKB_TAILROOM == 64, "skb_rooms_clear covers 
 DEV uint64_t skb_leak_pre(const KParams &kp, uint32_t i) {
     return (kp.skb_prefix[i] & SKB_PFX_MASK) + kp.skb_prefix[kp.n + (i >> SKB_PREP_LOG2)];
 }
+// DECODE = false: a kernel only ever launched after a full prep (skb_rec_built == 1: the batch
+// interpreter and the Step kernel, engine.cpp run_xdp_impl) leaves SKBuffFromBytes out -- inlined it
+// is the largest register peak of the interpreter body (22 of its spilled VGPRs)
+template <bool DECODE = true>
 DEV int skb_load(const KParams &kp, Lane &L, uint32_t i, uint64_t &r1, bool attach_only = false) {
     SkbRec *rec = kp.skb_rec + i;
     L.pkt = kp.pkt_data + kp.pkt_off[i];
     const uint64_t pf = kp.skb_rec_built ? kp.skb_prefix[i] : 0ull;
     // a sparse prep (skb_rec_built == 2) left derived words for the frames skb_fast rejects only:
     // the others are decoded here from the packet bytes (the same record)
-    if ((!kp.skb_rec_built || (kp.skb_rec_built == 2 && !(pf & SKB_PFX_EXC))) && !attach_only)
+    if ((!kp.skb_rec_built || (kp.skb_rec_built == 2 && !(pf & SKB_PFX_EXC))) && !attach_only) {
+        if (!DECODE) return MIMIC_ERR_ENGINE_HELPER;   // not launched so (engine invariant); loud if it were
         skb_init(SkbBytes{L.pkt + SKB_HEADROOM}, kp.pkt_len[i], *rec);
-    else if (kp.skb_drv && !attach_only)   // the prep kernel's derived words into the record
+    } else if (kp.skb_drv && !attach_only)   // the prep kernel's derived words into the record
         for (uint32_t q = 0; q < SKB_DERIVED_Q; q++) ((uint64_t *)rec)[q] = kp.skb_drv[(size_t)i * SKB_DERIVED_Q + q];
     const uint32_t lw = rec->len;
     L.rec = nullptr;

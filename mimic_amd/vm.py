@@ -686,22 +686,24 @@ class VM:
                 if _live(c) is not None and id(c) not in hs:
                     hs[id(c)] = c._device_handle()
             cx = (C.c_void_p * n)(*[hs[id(c)] if _live(c) is not None else None for c in ctxs])
+        import numpy as np
+
         regs = (L.ProcessRegs * n)()
         ca = None
         if cpus is not None:
-            import numpy as np
-
             ca = np.ascontiguousarray(cpus, dtype=np.int32)
         _check(self.h, self.lib.mimic_process_run_many(arr, n, ca.ctypes.data if ca is not None else None, cx, regs),
                "RunProcesses")
-        for p, r in zip(procs, regs):   # what a batch lane keeps: R0, status, steps (R1-R10 zero)
-            st = int(r.status)
-            p.Registers.R0 = int(r.r[0])
-            p.Steps = int(r.steps)
+        a = np.ctypeslib.as_array(regs)   # one column per field, not a ctypes access per field
+        r0, steps = a["r"][:, 0].tolist(), a["steps"].tolist()
+        sts, pcs = a["status"].tolist(), a["pc"].tolist()
+        for p, x, s, st, pc in zip(procs, r0, steps, sts, pcs):   # what a batch lane keeps: R0, status, steps
+            p.Registers.R0 = x
+            p.Steps = s
             p.Status = st
             p._exited = True
             p._started = True
-            p.ErrPC = int(r.pc) if st else -1
+            p.ErrPC = pc if st else -1
 
     def SKBRelease(self) -> None:
         """Forget the sock / flow-keys / packet entries earlier sk_buff processes leaked (a fresh

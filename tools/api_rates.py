@@ -151,11 +151,23 @@ def main():
     out["pool_skb"] = {"jobs": len(procs), "seconds": round(dt, 3), "jobs_per_s": round(len(procs) / dt, 1),
                        "newprocess_us_each": round(t_new / max(len(procs), 1) * 1e6, 1),
                        "what": "Enqueue + micro-batched launches (mimic_process_run_many); NewProcess timed apart"}
+    # the same kind of jobs through the C ABI call a Go pool would make per micro-batch
+    # (mimic_process_run_many + mimic_process_free_many), without the Python pool's per-job work
+    procs = [q for q in (make(k) for k in range(ns)) if q is not None]
+    cpus = [k % V for k in range(len(procs))]
+    t0 = time.perf_counter()
+    for b in range(0, len(procs), 1 << 16):
+        svm.RunProcesses(procs[b:b + (1 << 16)], None, cpus[b:b + (1 << 16)])
+        svm.CleanupProcesses(procs[b:b + (1 << 16)])
+    dt = time.perf_counter() - t0
+    out["abi_run_many_skb"] = {"jobs": len(procs), "seconds": round(dt, 3), "jobs_per_s": round(len(procs) / dt, 1),
+                               "what": "mimic_process_run_many + mimic_process_free_many per 65 536 processes"}
     procs = [q for q in (make(k) for k in range(args.per_job)) if q is not None]
     dt = pool_run(procs, True)
     out["pool_skb_per_job"] = {"jobs": len(procs), "seconds": round(dt, 3), "jobs_per_s": round(len(procs) / dt, 1),
                                "what": "one Process.Run (single-lane launch + sync) + Cleanup per job"}
     out["pool_skb_batched_over_per_job"] = round(out["pool_skb"]["jobs_per_s"] / out["pool_skb_per_job"]["jobs_per_s"], 1)
+    out["abi_run_many_over_per_job"] = round(out["abi_run_many_skb"]["jobs_per_s"] / out["pool_skb_per_job"]["jobs_per_s"], 1)
     svm.close()
 
     # ---- the oracle, one thread, per process -------------------------------------------------------
