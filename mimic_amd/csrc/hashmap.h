@@ -54,23 +54,27 @@ HDEV HT h_table(uint8_t *arena, const DMap &m) {
 // agent-scope add to the map's `head`; those same-address atomics serialise at the memory side
 // (cfg 4's inserting launch: 0.42 ms, 0.32 ms with the add spread over 16 addresses).  Here the
 // waves of a block that reserve at about the same time share one add: the first to arrive opens a
-// batch (`word`: generation << 48 | mask of the joined waves << 32 | positions requested so far),
-// waits ~128 cycles for others to add their counts, closes it, reserves the total with one add and
-// hands base and count to each wave of the batch through that wave's own mailbox; the others take
-// their share at the offset their add returned.  The batch's positions are contiguous and ordered
-// by arrival -- a valid order of pops, as if those waves had popped one after another -- and a lone
-// wave gets exactly what a direct add gives (FIFO slots of sequential runs unchanged).  A wave is
-// in at most one batch at a time and only the opener of that batch writes its mailbox, which the
-// wave clears after reading: no mailbox is overwritten before it is read, whatever the timing.
-// Nobody waits on a joiner, so the protocol cannot deadlock.
+// batch (`word`: generation << 40 | waves joined << 32 | positions requested so far; a slot's
+// ready word carries the generation mod 2^23, so a block may run up to 2^23 batches per launch --
+// the combiner is zeroed by every launch), waits ~128
+// cycles for others to add their counts, closes it, reserves the total with one add and publishes
+// base and count in the batch's slot (generation mod 16); the others take their share at the offset
+// their add returned.  The batch's positions are contiguous and ordered by arrival -- a valid order
+// of pops, as if those waves had popped one after another -- and a lone wave gets exactly what a
+// direct add gives (FIFO slots of sequential runs unchanged).  A slot's ready word also counts the
+// joiners that have not read it yet (low 8 bits), and the opener of a later batch on the same
+// slot waits for that count to reach zero before it publishes: no slot is overwritten before every joiner read it, whatever the timing.
+// The waits are on joiners already past their join (they only read), so the protocol cannot deadlock.
+// (Per-wave mailboxes written in a loop by the opener, round 5's first fix, cost the cfg-4 kernel 8
+// more spilled VGPRs and its lookup-hit launch 0.126 -> 0.143 ms; this form 2 and 0.130 ms.)
 #define HCOMB_MAPS 4u
-#define HCOMB_WAVES 16u   // waves per block (1024 threads at most)
+#define HCOMB_SLOTS 16u
 struct HComb {
     unsigned long long word;
     uint32_t owner;                     // the map (HT::tag) this combiner serves in this block
-    uint32_t ready[HCOMB_WAVES];        // per wave: generation + 1 once its batch's base / got are there (0: read)
-    uint32_t got[HCOMB_WAVES];          // positions below tail (bit 31: tail == E, the ring untouched)
-    unsigned long long base[HCOMB_WAVES];
+    uint32_t ready[HCOMB_SLOTS];        // (generation + 1) << 8 | joiners yet to read, once base / got are published
+    uint32_t got[HCOMB_SLOTS];          // positions below tail (bit 31: tail == E, the ring untouched)
+    unsigned long long base[HCOMB_SLOTS];
 };
 static __shared__ HComb h_comb_[HCOMB_MAPS];
 // zeroed by every thread of the block before any of them can insert (the JIT prologue)
@@ -89,35 +93,35 @@ HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, ui
         own = __hip_atomic_load(&cb.owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (own != t.tag) return false;   // another map holds this combiner: reserve directly
-    const uint32_t wid = threadIdx.x >> 6;
-    const unsigned long long old = __hip_atomic_fetch_add(&cb.word, (1ull << (32 + wid)) + k, __ATOMIC_RELAXED,
+    const unsigned long long old = __hip_atomic_fetch_add(&cb.word, (1ull << 32) + k, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t gen = (uint32_t)(old >> 48), off = (uint32_t)old, joined = (uint32_t)(old >> 32) & 0xffffu;
+    const uint32_t gen = (uint32_t)(old >> 40), off = (uint32_t)old, s = gen & (HCOMB_SLOTS - 1);
     uint64_t b0;
     uint32_t g0;
-    if (joined == 0) {   // the batch's opener
+    if (((old >> 32) & 0xffu) == 0) {   // the batch's opener
 #ifndef MIMIC_HCOMB_SLEEP
 #define MIMIC_HCOMB_SLEEP 2
 #endif
         __builtin_amdgcn_s_sleep(MIMIC_HCOMB_SLEEP);
-        const unsigned long long closed = __hip_atomic_exchange(&cb.word, (unsigned long long)((gen + 1u) & 0xffffu) << 48,
+        const unsigned long long closed = __hip_atomic_exchange(&cb.word, (unsigned long long)((gen + 1u) & 0xffffffu) << 40,
                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t total = (uint32_t)closed, mask = (uint32_t)(closed >> 32) & 0xffffu & ~(1u << wid);
+        const uint32_t total = (uint32_t)closed, joiners = ((uint32_t)(closed >> 32) & 0xffu) - 1u;
         b0 = __hip_atomic_fetch_add(&c->head, (unsigned long long)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tl = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         g0 = (b0 >= tl ? 0u : (tl - b0 < total ? (uint32_t)(tl - b0) : total)) | (tl == t.E ? 0x80000000u : 0u);
-        for (uint32_t m = mask; m; m &= m - 1) {
-            const uint32_t w = (uint32_t)__builtin_ctz(m);
-            cb.base[w] = b0;
-            cb.got[w] = g0;
-            __hip_atomic_store(&cb.ready[w], gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (joiners) {
+            while (__hip_atomic_load(&cb.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & 0xffu)
+                __builtin_amdgcn_s_sleep(1);   // the slot's batch of 16 generations ago is still being read
+            cb.base[s] = b0;
+            cb.got[s] = g0;
+            __hip_atomic_store(&cb.ready[s], (((gen & 0x7fffffu) + 1u) << 8) | joiners, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     } else {
-        while (__hip_atomic_load(&cb.ready[wid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != gen + 1u)
+        while ((__hip_atomic_load(&cb.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 8) != (gen & 0x7fffffu) + 1u)
             __builtin_amdgcn_s_sleep(1);
-        b0 = cb.base[wid];
-        g0 = cb.got[wid];
-        __hip_atomic_store(&cb.ready[wid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        b0 = cb.base[s];
+        g0 = cb.got[s];
+        __hip_atomic_fetch_sub(&cb.ready[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     *ident = g0 >> 31;
     g0 &= 0x7fffffffu;

@@ -100,6 +100,8 @@ class Gen {
         xpf_knob = xv && xv[0] == '1';
         const char *lpv = getenv("MIMIC_JIT_LPF");   // 1: lane-start prefetch of the first packets' windows
         lpf_knob = lpv && lpv[0] == '1';
+        const char *hv = getenv("MIMIC_JIT_HINT");   // 1: [[unlikely]] on the slow-path branches (measured: no change)
+        hint_knob = hv && hv[0] == '1';
         const char *lq = getenv("MIMIC_JIT_LDSSTK");   // 8-byte words of the LDS stack window (0: none)
         if (lq) lds_stack_q = (uint32_t)std::min(32, std::max(0, atoi(lq)));
         const char *dv = getenv("MIMIC_JIT_DISPATCH");   // 0: a jump table at every tail-call site
@@ -240,6 +242,7 @@ class Gen {
     // descriptor and window loads delays every first packet; tools/memtime.py), the
     // chunked schedule 38.9 -> 36.8 us, cfg 3 / cfg 4 unchanged.
     bool lpf_knob = false;
+    bool hint_knob = false;    // MIMIC_JIT_HINT=1: slow-path branches marked [[unlikely]] (laid out after the hot code)
     bool lpf_on = false;
     bool lds_stack_on = false;
     static constexpr uint32_t kLpfD = 4;
@@ -1528,6 +1531,12 @@ class Gen {
         }
     }
 
+    // the branch prefix of a slow path: "else " (or an if's condition) gets [[unlikely]], so the
+    // compiler lays the slow path out after the hot code (branch weights) instead of between its blocks
+    std::string unl(const std::string &pre) const {
+        if (!hint_knob) return pre;
+        return pre.size() >= 5 && pre.compare(pre.size() - 5, 5, "else ") == 0 ? pre + "[[unlikely]] " : pre;
+    }
     // the slow path of slot i of the program being emitted: a call (COLD_CALL) or a deferral
     std::string cold(const std::string &call, uint32_t i) const {
         if (defer_mode) return defer_text(i);
@@ -1851,7 +1860,7 @@ class Gen {
         }
         skb_ptr_fast(i, base, off, n, true, dst, pre);
         // generic GetEntry + Load (cold, out of line)
-        E.line("%s{ %s %s = sp_.v; }", pre.c_str(), cold("cold_load(kp, sp_, ga_, " + std::to_string(n) + "u)", i).c_str(), dst.c_str());
+        E.line("%s{ %s %s = sp_.v; }", unl(pre).c_str(), cold("cold_load(kp, sp_, ga_, " + std::to_string(n) + "u)", i).c_str(), dst.c_str());
     }
 
     void store(uint32_t i, uint32_t base, int32_t off, uint32_t n, const std::string &val, bool deferred = false) {
@@ -1859,7 +1868,7 @@ class Gen {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         if (!deferred && elided.count({cur_prog, i})) {   // the write happens in the lookup's cold path
             const auto f = fast_forms(base, n, val);
-            E.line("    if (!(%s)) { %s%s }", f.at(0).cond.c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
+            E.line("    if (!(%s)) %s{ %s%s }", f.at(0).cond.c_str(), hint_knob ? "[[unlikely]] " : "", base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
                    cold("cold_store(kp, sp_, ga_, " + std::to_string(n) + "u, " + val + ")", i).c_str());
             return;
         }
@@ -1886,7 +1895,7 @@ class Gen {
         }
         skb_ptr_fast(i, base, off, n, false, val, pre);
         // generic GetEntry + Store (cold); the stack / xdp_md state it may change comes back
-        E.line("%s{ %s%s", pre.c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
+        E.line("%s{ %s%s", unl(pre).c_str(), base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
                cold("cold_store(kp, sp_, ga_, " + std::to_string(n) + "u, " + val + ")", i).c_str());
         if (stage)  // a store that reached the packet updates the window too
             E.line("      if (sp_.po) win_store_rel(pwin_, tl_, W_, sp_.po - 1u, %uu, %uu, %s); }", wb(), n, ord(val, n).c_str());
@@ -2019,7 +2028,7 @@ class Gen {
                 } else {
                     E.line("      if (!(mh_ && lookup_fast(kp, L, mh_ - 1u, r1, r2, r0))) {");
                 }
-                E.line("      if (!(%s)) %s } }", hfast.c_str(), cold("cold_lookup(kp, sp_)", i).c_str());
+                E.line("      if (!(%s)) %s%s } }", hfast.c_str(), hint_knob ? "[[unlikely]] " : "", cold("cold_lookup(kp, sp_)", i).c_str());
             } else {
                 E.line("    %s", cold("cold_lookup(kp, sp_)", i).c_str());
             }
@@ -2198,7 +2207,7 @@ void write_file_atomic(const std::string &path, const std::vector<char> &data) {
     else remove(tmp.c_str());
 }
 
-const char *const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-label", "-Wno-unused-variable"};
+const char *const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-label", "-Wno-unused-variable", "-Wno-c++20-extensions"};
 const int kNOpts = (int)(sizeof kOpts / sizeof *kOpts);
 
 // source -> gfx950 code object (hipRTC), through the disk cache when one is configured
