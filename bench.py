@@ -117,8 +117,8 @@ class Workload:
             self.map_init = []
         self.ctx = 1 if self.skb else 0
 
-    def kernel_src_hash(self, spread_vcpus: int = 0) -> str:
-        return kernel_src_hash_of(self.name, spread_vcpus)
+    def kernel_src_hash(self, spread_vcpus: int = 0, own: bool = False) -> str:
+        return kernel_src_hash_of(self.name, spread_vcpus, own)
 
     def build_vm(self, M, V, device, shard, raws):
         emu = M.NewLinuxEmulator()
@@ -136,10 +136,10 @@ class Workload:
         return vm, maps, pids
 
 
-def kernel_src_hash_of(cfg_name: str, spread_vcpus: int = 0) -> str:
+def kernel_src_hash_of(cfg_name: str, spread_vcpus: int = 0, own: bool = False) -> str:
     """sha256 (16 hex) of the JIT kernel source the config's programs generate (spread_vcpus > 0:
-    the spread kernel a VM of that many vCPUs per engine builds): the key that ties a committed
-    rocprofv3 summary to the exact kernel it measured."""
+    the spread kernel a VM of that many vCPUs per engine builds; own: its owned form): the key that
+    ties a committed rocprofv3 summary to the exact kernel it measured."""
     from mimic_amd import jit as J
     from mimic_amd import workloads as W
 
@@ -151,7 +151,7 @@ def kernel_src_hash_of(cfg_name: str, spread_vcpus: int = 0) -> str:
     if spread_vcpus:
         maps = progs[0].maps
         src = J.kernel_source([p.raw for p in progs], ctx, (),
-                              J.spread_spec([(p.raw, p.relocs) for p in progs], maps, spread_vcpus))
+                              J.spread_spec([(p.raw, p.relocs) for p in progs], maps, spread_vcpus, own=own))
     else:
         src = J.kernel_source([p.raw for p in progs], ctx)
     h = hashlib.sha256(src.encode())
@@ -556,7 +556,7 @@ def main(argv=None):
                   for b in timed) / len(timed)
         achieved = alg / avg_launch_s
         kernel = "mimic_jit_kernel" if vm.LastExec() in ("jit", "spread") else "mimic_xdp_kernel"
-        src_hash = wl.kernel_src_hash(vpg if vm.LastExec() == "spread" else 0)
+        src_hash = wl.kernel_src_hash(vpg if vm.LastExec() in ("spread", "spread_own") else 0, vm.LastExec() == "spread_own")
         prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched)
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",

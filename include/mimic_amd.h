@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MIMIC_ABI_VERSION 2  /* 2: mimic_skb_batch.custom, statuses 29-30, MIMIC_EXEC_SPREAD */
+#define MIMIC_ABI_VERSION 3  /* 2: mimic_skb_batch.custom, statuses 29-30, MIMIC_EXEC_SPREAD; 3: MIMIC_EXEC_SPREAD_OWN */
 
 /* errors */
 #define MIMIC_EINVAL (-1)
@@ -110,6 +110,7 @@ typedef struct {
 #define MIMIC_EXEC_INTERP 1   /* the batch interpreter kernel (interp.hip) */
 #define MIMIC_EXEC_JIT 2      /* per-program-set kernels generated from the loaded programs, hipRTC-compiled */
 #define MIMIC_EXEC_SPREAD 3   /* mimic_last_exec only: the JIT's spread kernel (a vCPU's packets on many lanes) */
+#define MIMIC_EXEC_SPREAD_OWN 4   /* mimic_last_exec only: its owned form (a block runs every packet of its vCPUs) */
 
 typedef struct {
     const char *name;

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MIMIC_LIB=<file name>: another in-tree build of the same sources (measurement builds, A/B runs)
 LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("MIMIC_LIB", "libmimic_amd.so")))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # status codes (enum mimic_status)
 STATUS_NAMES = [

@@ -153,6 +153,11 @@ struct mimic_vm {
     int spread_state = 0;
     hipFunction_t jit_fn_spread = nullptr;
     JitInfo jit_info_spread{};
+    // the owned form of the spread kernel (SpreadReq::own): state as spread_state; its LDS table rows
+    int spread_own_state = 0;
+    hipFunction_t jit_fn_spread_own = nullptr;
+    JitInfo jit_info_spread_own{};
+    uint32_t spread_own_rows = 0;
     uint32_t *d_spread_bad = nullptr;
     void *d_spread_part = nullptr;   // spread launches: the blocks' counter tables (mimic_spread_reduce_kernel)
     uint64_t spread_part_cap = 0;
@@ -530,6 +535,8 @@ static int upload_tables(mimic_vm *vm) {
     vm->jit_fn_cx[0] = vm->jit_fn_cx[1] = nullptr;
     vm->jit_fn_spread = nullptr;
     vm->spread_state = 0;
+    vm->jit_fn_spread_own = nullptr;
+    vm->spread_own_state = 0;
     std::vector<DInsn> all = vm->h_all;
     std::vector<DProg> dp = vm->h_dp;
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
@@ -1708,6 +1715,52 @@ static int spread_build(mimic_vm *vm) {
     return 0;
 }
 
+// lanes the one-lane JIT kernel holds resident at its 4-wave budget: CUs x 4 SIMDs x 4 waves x 64
+static uint32_t chip_lanes(mimic_vm *vm) {
+    static int cus = 0;
+    if (!cus) {
+        hipDeviceProp_t pr;
+        cus = hipGetDeviceProperties(&pr, vm->s.device) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
+    }
+    return (uint32_t)cus * 4u * 4u * 64u;
+}
+
+// The owned form (jit.cpp, SpreadReq::own): built once per program set when the programs allow a
+// spread kernel; its LDS table holds up to 128 rows of the counted map's row (32 KiB at most), so a
+// batch with P packets per vCPU can use it when 256 / P rows fit.
+static int spread_build_own(mimic_vm *vm) {
+    if (vm->spread_own_state) return 0;
+    vm->spread_own_state = -1;
+    SpreadReq req;
+    req.own = true;
+    for (size_t s = 0; s < vm->h_all.size(); s++) {
+        const DInsn &x = vm->h_all[s];
+        const uint32_t mh = AUX_MAPHINT(x.aux);
+        if (AUX_H(x.aux) != H_LDIMM || !mh || mh > vm->maps.size()) continue;
+        const HostMap &hm = vm->maps[mh - 1];
+        const DMap dm = to_dmap(hm);
+        if (hm.family != FAM_PERCPU_ARRAY || (dm.dev_off & 7) || (dm.dev_stride & 7)) continue;
+        req.slot_map[(uint32_t)s] = mh - 1;
+        req.shape[mh - 1] = {hm.max_entries * hm.value_size, hm.value_size};
+    }
+    if (req.slot_map.empty()) return 0;
+    uint32_t row = 0;
+    for (auto &kv : req.shape) row = std::max(row, kv.second.first);
+    if (!row) return 0;
+    req.lds_rows = std::min<uint32_t>(128u, 32768u / row);
+    if (req.lds_rows < 2) return 0;
+    JitInfo info{};
+    const std::string src = mimic_jit_source(vm->h_dp, vm->h_all, CTX_XDP, &info, nullptr, false, &req);
+    if (!info.spread || !info.spread_own) return 0;
+    std::string log;
+    if (mimic_jit_compile(vm->s.device, src, &vm->jit_fn_spread_own, &log))
+        return fail(vm, MIMIC_EDEVICE, "JIT build failed (owned spread kernel): %s", log.c_str());
+    vm->jit_info_spread_own = info;
+    vm->spread_own_rows = req.lds_rows;
+    vm->spread_own_state = 1;
+    return 0;
+}
+
 // The VM's private memory for `lanes` lanes of q_per_lane qwords, qword-interleaved with stride
 // vm->priv_lanes >= lanes (a launch with fewer lanes uses the larger stride as it is)
 static int priv_ensure(mimic_vm *vm, uint32_t q_per_lane, uint32_t lanes, hipStream_t st) {
@@ -1954,11 +2007,27 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     // every vCPU has many packets (the one-lane-per-vCPU kernel would run them as one serial chain
     // per lane, e.g. V = runtime.NumCPU(), vm.go:64).  MIMIC_SPREAD=0: never; =1: whenever the
     // program set allows it; default: when n >= 8 V.
-    bool spread = false;
+    bool spread = false, own = false;
     if (jit && !skb && b->n > 0 && (b->schedule == MIMIC_SCHED_CHUNKED || b->schedule == MIMIC_SCHED_INTERLEAVED)) {
         const char *sv = getenv("MIMIC_SPREAD");
         const int knob = vm->spread_mode >= 0 ? vm->spread_mode : sv && *sv ? atoi(sv) : -1;
-        if (knob == 1 || (knob != 0 && (uint64_t)b->n >= 8ull * cpu_lanes)) {
+        // the owned form, for batches of 2..256 packets per vCPU.  By default for 2..16 packets per
+        // vCPU when the one-lane kernel would not fill the chip (fewer vCPU lanes than 4 waves on
+        // every SIMD): classifier, 1.2-1.9x the one-lane kernel at V = 16 K..131 K and P = 4, 1.4x the
+        // LDS-table spread at V = 65 536, P = 16; slower than the one-lane kernel at V = 262 144 and
+        // than the table spread from P = 64 (its table rows then take many increments each;
+        // profiles/r05/r05u/).  MIMIC_SPREAD_OWN=1: whenever it applies, =0: never.
+        const char *ov = getenv("MIMIC_SPREAD_OWN");
+        const int own_knob = ov && *ov ? atoi(ov) : -1;
+        const bool own_pref = own_knob == 1 || (own_knob != 0 && cpu_lanes < chip_lanes(vm) && kp.per_lane <= 16);
+        if (knob != 0 && own_pref && kp.per_lane >= 2 && kp.per_lane <= 256) {
+            rc = spread_build_own(vm);
+            if (rc) return rc;
+            own = vm->spread_own_state > 0 && 256u / kp.per_lane <= vm->spread_own_rows &&
+                  mimic_jit_step_bound(vm->jit_info_spread_own, kp.max_tail_calls) <= kp.budget;
+            spread = own;
+        }
+        if (!own && (knob == 1 || (knob != 0 && (uint64_t)b->n >= 8ull * cpu_lanes))) {
             rc = spread_build(vm);
             if (rc) return rc;
             spread = vm->spread_state > 0 && mimic_jit_step_bound(vm->jit_info_spread, kp.max_tail_calls) <= kp.budget;
@@ -1970,7 +2039,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     // a launch given contexts runs the variant with the per-packet Run(ctx) check, one lane per vCPU
     const bool cxk = jit && kp.cancel_any;
     if (cxk) {
-        spread = false;
+        spread = own = false;
         if (!vm->jit_fn_cx[ctx]) {
             const std::vector<std::pair<uint32_t, uint32_t>> vc = vc_slots_of(vm);
             std::string log;
@@ -1982,11 +2051,13 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
                 return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
         }
     }
-    const JitInfo &ji = spread ? vm->jit_info_spread : cxk ? vm->jit_info_cx[ctx] : vm->jit_info[ctx];
-    hipFunction_t jfn = spread ? vm->jit_fn_spread : cxk ? vm->jit_fn_cx[ctx] : vm->jit_fn[ctx];
+    const JitInfo &ji = own ? vm->jit_info_spread_own : spread ? vm->jit_info_spread : cxk ? vm->jit_info_cx[ctx] : vm->jit_info[ctx];
+    hipFunction_t jfn = own ? vm->jit_fn_spread_own : spread ? vm->jit_fn_spread : cxk ? vm->jit_fn_cx[ctx] : vm->jit_fn[ctx];
     uint32_t run_lanes = lanes;
     if (spread) {
-        const uint32_t blocks = (uint32_t)(((uint64_t)b->n + spread_ppb() - 1) / spread_ppb());
+        // owned: 256 / P vCPU lanes per block
+        const uint32_t blocks = own ? (cpu_lanes + 256u / kp.per_lane - 1) / (256u / kp.per_lane)
+                                    : (uint32_t)(((uint64_t)b->n + spread_ppb() - 1) / spread_ppb());
         run_lanes = blocks * 256u;
         rc = priv_ensure(vm, q_per_lane, run_lanes, st);   // private memory (stack ...) per spread lane
         if (rc) return rc;
@@ -2011,7 +2082,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         // (dense): the blocks' tables go to a buffer and one reduce kernel adds them into the map
         // (jit.cpp spread flush).  Sparser tables keep one agent-scope add per non-zero counter.
         kp.spread_part = nullptr;
-        if (ji.spread_rows && ji.spread_rows == cpu_lanes && ji.spread_n &&
+        if (!own && ji.spread_rows && ji.spread_rows == cpu_lanes && ji.spread_n &&
             (uint64_t)cpu_lanes * ji.spread_roww <= spread_ppb()) {
             const uint64_t need = (uint64_t)blocks * ji.spread_rows * ji.spread_roww * ji.spread_n;
             if (need > vm->spread_part_cap) {
@@ -2083,7 +2154,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (mimic_launch_hash_rebuild(vm->arena, &dm, 0, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     }
-    vm->last_exec = jit ? (spread ? MIMIC_EXEC_SPREAD : MIMIC_EXEC_JIT) : MIMIC_EXEC_INTERP;
+    vm->last_exec = jit ? (own ? MIMIC_EXEC_SPREAD_OWN : spread ? MIMIC_EXEC_SPREAD : MIMIC_EXEC_JIT) : MIMIC_EXEC_INTERP;
     if (jit && ji.defer) {   // the lanes' suspended processes (DeferRec) and the launch's marker
         if (lanes > vm->defer_cap || !vm->d_defer_any) {
             hipStreamSynchronize(st);
@@ -2753,7 +2824,8 @@ long mimic_jit_source_spread(const void *const *progs, const uint32_t *n_slots, 
         req.slot_map[dp[p].base + sl] = pc[3 * q + 2];
     }
     for (uint32_t q = 0; q < n_shapes; q++) req.shape[shapes[3 * q]] = {shapes[3 * q + 1], shapes[3 * q + 2]};
-    req.lds_rows = lds_rows;
+    req.lds_rows = lds_rows & 0x7fffffffu;
+    req.own = (lds_rows >> 31) != 0;   // bit 31: the owned form (spread_build_own)
     JitInfo info{};
     const std::string src = mimic_jit_source(dp, all, MIMIC_CTX_XDP, &info, nullptr, false, &req);
     if (spread_out) *spread_out = info.spread ? 1 : 0;

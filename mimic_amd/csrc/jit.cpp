@@ -252,6 +252,7 @@ class Gen {
     const SpreadReq *spread_req = nullptr;   // the VM's per-CPU arrays: spread mode is possible (analyze_spread)
     bool ctx_check = false;   // the kernel reads each packet's Run(ctx) context before its first step
     bool spread_on = false;
+    bool spread_own = false;   // the owned form (SpreadReq::own): every packet of a block's vCPUs in the block
     uint32_t spread_map = 0, spread_n = 0, spread_row = 0;   // the counted map, counter width, E * S
     std::map<uint32_t, uint32_t> vc_ok;  // LD_IMM64 slots (kernel-wide) naming a per-CPU array whose row can be cached -> E * S
     uint32_t vc_slot = 0;      // the LD_IMM64 slot (kernel-wide index) whose map hint names the cached map
@@ -332,6 +333,7 @@ class Gen {
         if (speculate && fast_paths && !stage && !all_leaders)
             for (auto &p : P) analyze_spec(p);
         spread_on = analyze_spread();
+        spread_own = spread_on && spread_req->own;
         if (spread_on) vc_on = false;   // no lane owns a vCPU's row in a spread kernel
         // the LDS stack window (runtime.h) when some stack store is made for real (not deferred
         // into a cold path, analyze_elide).  Measured: cfg 4 0.197 -> 0.179 ms per launch; the
@@ -365,6 +367,7 @@ class Gen {
         E.line("#ifdef MIMIC_MEAS_NOPKTST\n#define PKT_ST(p_, n_, v_) ((void)(v_))\n#else\n#define PKT_ST(p_, n_, v_) st_n(p_, n_, v_)\n#endif");
         E.line("#ifdef MIMIC_MEAS_NOATOM\n#define CNT_ADD(p_, n_, v_) ((void)(p_))\n#else\n#define CNT_ADD(p_, n_, v_) atomic_add_n(p_, n_, v_)\n#endif");
         if (spread_on) E.line("#define MIMIC_SPREAD 1");
+        if (spread_own) E.line("#define MIMIC_SPREAD_OWN 1");
         if (const char *rc = getenv("MIMIC_SKB_ROOMS_CHAIN"))   // measurement: see engine.cpp skb_prepare
             if (rc[0] == '1') E.line("#define MIMIC_SKB_ROOMS_CHAIN 1");
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
@@ -472,7 +475,32 @@ class Gen {
             E.line("#define COLD_CALL_K(k_, call_, pc_) do { coldn_ += 1u << (k_); COLD_CALL(call_, pc_); } while (0)");
         }
         E.line("  L.lane = g;");
-        if (spread_on) {
+        if (spread_own) {
+            // Owned spread: block b runs every packet of vCPU lanes [b * R, b * R + R), R = 256 / P
+            // (P = packets per lane): thread t the j-th packet (j = t / R) of lane b * R + t % R, so
+            // a wave's lanes take consecutive lanes' j-th packets (consecutive descriptors, packets
+            // and results).  Fused increments add into the block's LDS table, one row per lane; the
+            // block then adds its rows into the map with plain read-modify-writes: no other block
+            // touches those vCPUs' rows in this launch.
+            E.line("  const uint32_t oP_ = kp.per_lane, oR_ = 256u / oP_;");
+            E.line("  const uint32_t orow_ = threadIdx.x %% oR_, oj_ = threadIdx.x / oR_, olane_ = blockIdx.x * oR_ + orow_;");
+            E.line("  uint32_t oi_ = NO_PKT;");
+            E.line("  if (oj_ < oP_ && olane_ < kp.cpu_lanes) {");
+            E.line("    const uint64_t ii_ = kp.sched == SCHED_CHUNKED ? (uint64_t)olane_ * oP_ + oj_ :");
+            E.line("        (uint64_t)oj_ * kp.cpu_lanes + (olane_ >= kp.sched_shift ? olane_ - kp.sched_shift : olane_ + kp.cpu_lanes - kp.sched_shift);");
+            E.line("    if (ii_ < kp.n) oi_ = (uint32_t)ii_;");
+            E.line("  }");
+            E.line("  const DMap SM_ = cget(kp.maps, SPREAD_MAP);");
+            E.line("  __shared__ spread_t sacc_[SPREAD_ROWS * SPREAD_ROWW];");
+            E.line("  for (uint32_t w_ = threadIdx.x; w_ < SPREAD_ROWS * SPREAD_ROWW; w_ += 256u) sacc_[w_] = 0;");
+            E.line("  __syncthreads();");
+            E.line("  uint32_t srow_ = orow_, sbase_ = 0;");
+            // the row words this thread adds into at the end, loaded now (their round trip overlaps
+            // the packet's): word threadIdx.x of the block's rows (R * SPREAD_ROWW <= 256 words)
+            E.line("  const bool ofw_ = threadIdx.x < oR_ * SPREAD_ROWW && blockIdx.x * oR_ + threadIdx.x / SPREAD_ROWW < kp.cpu_lanes;");
+            E.line("  GAS spread_t *const ofd_ = (GAS spread_t *)(kp.arena + SM_.dev_off + (size_t)(kp.vcpu_begin + blockIdx.x * oR_ + threadIdx.x / SPREAD_ROWW) * SM_.dev_stride) + threadIdx.x %% SPREAD_ROWW;");
+            E.line("  const spread_t ofv_ = ofw_ ? *ofd_ : (spread_t)0;");
+        } else if (spread_on) {
             // Spread: block b runs packets [b * SPREAD_PPB, +SPREAD_PPB) of the batch, thread t the
             // ones at t, t + 256, ... (consecutive threads, consecutive packets); each packet's
             // vCPU comes from the schedule.  Fused increments add into the block's LDS table, one
@@ -578,12 +606,18 @@ class Gen {
             E.line("  if (nidx2_ != NO_PKT) { noff2_ = *gp(kp.pkt_off + nidx2_); nlen2_ = *gp(kp.pkt_len + nidx2_); }");
         } else if (pf) {
             E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
-            if (spread_on)
+            if (spread_own)
+                E.line("  if (oi_ != NO_PKT) { noff_ = *gp(kp.pkt_off + oi_); nlen_ = *gp(kp.pkt_len + oi_); }");
+            else if (spread_on)
                 E.line("  { const uint32_t n_ = blo_ + threadIdx.x; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else
                 E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
-        if (spread_on) {
+        if (spread_own) {
+            E.line("  for (uint32_t j = 0; j < 1u; j++) {   // the thread's one packet");
+            E.line("    const uint32_t i = oi_;");
+            E.line("    if (i == NO_PKT) break;");
+        } else if (spread_on) {
             E.line("  for (uint32_t j = 0; j < SPREAD_PPB / 256u; j++) {");
             E.line("    const uint32_t i = blo_ + j * 256u + threadIdx.x;");
             E.line("    if (i >= bhi_) break;");
@@ -618,6 +652,7 @@ class Gen {
         } else if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
+            else if (spread_own) { }   // one packet per thread: nothing ahead
             else if (spread_on) E.line("    { const uint32_t n_ = i + 256u; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
@@ -626,7 +661,10 @@ class Gen {
         // loaded where used instead of hoisted out of the packet loop into SGPRs
         if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else E.line("    const KParams &kq_ = kp;");
-        if (spread_on) {   // this packet's vCPU (the schedule's lane for it) and its row of the spread map
+        if (spread_own) {   // the thread's vCPU and its row of the spread map
+            E.line("    L.cpu = (int32_t)(kp.vcpu_begin + olane_);");
+            E.line("    sbase_ = SM_.backing_addr + (uint32_t)L.cpu * SM_.addr_period;");
+        } else if (spread_on) {   // this packet's vCPU (the schedule's lane for it) and its row of the spread map
             E.line("    { if (kp.sched == SCHED_CHUNKED) lam_ = i / kp.per_lane;");
             E.line("      else if (j) { lam_ += lstep_; if (lam_ >= kp.cpu_lanes) lam_ -= kp.cpu_lanes; }");
             E.line("      L.cpu = (int32_t)(kp.vcpu_begin + lam_);");
@@ -766,7 +804,20 @@ class Gen {
         E.line("    lane_steps += steps;");
         E.line("  }");
         if (vc_on) E.line("  VC_FLUSH();");
-        if (spread_on) {
+        if (spread_own) {
+            // the block's rows into the map: plain read-modify-writes (the block owns these vCPUs)
+            E.line("#if !defined(MIMIC_MEAS_NOFLUSH)   // (measurement knob: no flush, counters wrong)");
+            E.line("  __syncthreads();");
+            E.line("  if (ofw_ && sacc_[threadIdx.x]) *ofd_ = ofv_ + sacc_[threadIdx.x];");
+            E.line("  for (uint32_t w_ = threadIdx.x + 256u; w_ < oR_ * SPREAD_ROWW; w_ += 256u) {   // rows past 256 words");
+            E.line("    const spread_t v_ = sacc_[w_];");
+            E.line("    if (!v_) continue;");
+            E.line("    const uint32_t r_ = w_ / SPREAD_ROWW, q_ = w_ - r_ * SPREAD_ROWW;");
+            E.line("    GAS spread_t *d_ = (GAS spread_t *)(kp.arena + SM_.dev_off + (size_t)(kp.vcpu_begin + blockIdx.x * oR_ + r_) * SM_.dev_stride) + q_;");
+            E.line("    *d_ += v_;");
+            E.line("  }");
+            E.line("#endif");
+        } else if (spread_on) {
             // the block's counters into the map: one agent-scope add per non-zero counter (a row's
             // counters are contiguous in the arena, so consecutive threads add consecutive words)
             E.line("#if SPREAD_ROWS && !defined(MIMIC_MEAS_NOFLUSH)   // (measurement knob: no flush, counters wrong)");
@@ -2278,6 +2329,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->skb_fast = g.skb_fast;
         info->karg = g.karg != 0;
         info->spread = g.spread_on;
+        info->spread_own = g.spread_own;
         info->spread_map = g.spread_map;
         info->spread_n = g.spread_n;
         info->spread_roww = g.spread_n ? g.spread_row / g.spread_n : 0;

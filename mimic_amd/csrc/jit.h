@@ -20,6 +20,7 @@ struct JitInfo {
     bool skb_walk;       // sk_buff kernel that builds its SkbRecs itself (prep: footprints only)
     bool skb_fast;       // sk_buff kernel that derives the records of common frames itself (sparse prep)
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
+    bool spread_own;     // ... in its owned form: a block runs every packet of its vCPUs (SpreadReq::own)
     // spread kernels: the counted per-CPU array, counter width, counters per row, LDS table rows
     uint32_t spread_map, spread_n, spread_roww, spread_rows;
 };
@@ -29,6 +30,9 @@ struct SpreadReq {
     std::map<uint32_t, std::pair<uint32_t, uint32_t>> shape;   // map id -> (E * S, S)
     uint32_t lds_rows = 0;   // rows of a block's LDS counter table (0: agent-scope atomics into the map)
     uint32_t ppb = 1024;     // packets per block
+    // owned form: block b runs all P = KParams::per_lane packets of vCPU lanes [b * 256 / P, +256 / P)
+    // (2 <= P <= 256), its counters into an LDS table it then adds into the rows it alone owns
+    bool own = false;
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // ctx_check: the variant for launches given Run(ctx) contexts (KParams::cancel_any)

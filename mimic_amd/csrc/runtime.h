@@ -662,10 +662,17 @@ DEV void vc_open(const KParams &kp, const DMap &m, int32_t cpu, uint8_t *&p, uin
 }
 DEV void vc_writeback(uint8_t *p, uint32_t nb, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
     GAS uint64_t *d = (GAS uint64_t *)p;
+#ifdef MIMIC_VC_NT   // measurement: the row streamed out (non-temporal stores)
+    __builtin_nontemporal_store(w0, d);
+    if (nb > 8) __builtin_nontemporal_store(w1, d + 1);
+    if (nb > 16) __builtin_nontemporal_store(w2, d + 2);
+    if (nb > 24) __builtin_nontemporal_store(w3, d + 3);
+#else
     d[0] = w0;
     if (nb > 8) d[1] = w1;
     if (nb > 16) d[2] = w2;
     if (nb > 24) d[3] = w3;
+#endif
 }
 
 // The LDS form of the lane value cache, for rows of 40..MIMIC_VC_MAX_ROW bytes (jit.cpp vc_lds):

@@ -71,12 +71,14 @@ def vc_slots(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict]) -> L
     return out
 
 
-def spread_spec(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict], vcpus: int, ppb: int = 1024):
+def spread_spec(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict], vcpus: int, ppb: int = 1024,
+                own: bool = False):
     """What the engine's spread_build() generates the spread kernel from, for programs (raw,
     relocations) loaded next to ``maps`` (created in this order: map id = index) on a VM with
     ``vcpus`` vCPUs: (pc, shapes, lds_rows) -- the (program, slot, map id) of every LD_IMM64 slot
     naming a per-CPU array's object, those maps' (id, E * S, S), and the LDS table's rows
-    (min(ppb, V) when that many rows of the largest such row fit 32 KiB, else 0)."""
+    (min(ppb, V) when that many rows of the largest such row fit 32 KiB, else 0).  own: the owned
+    form's (spread_build_own: min(128, 32 KiB / row) rows, bit 31 set)."""
     by_name = {m["name"]: (i, m) for i, m in enumerate(maps)}
     pc, shapes = [], {}
     for pi, (raw, rel) in enumerate(progs):
@@ -90,6 +92,8 @@ def spread_spec(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict], v
                 pc.append((pi, slot, mid))
                 shapes[mid] = (mid, m["max_entries"] * m["value_size"], m["value_size"])
     row = max((s[1] for s in shapes.values()), default=0)
+    if own:
+        return pc, list(shapes.values()), (min(128, 32768 // row) if row else 0) | (1 << 31)
     rows = min(ppb, vcpus)
     return pc, list(shapes.values()), rows if rows * row <= 32768 else 0
 

@@ -762,7 +762,7 @@ class VM:
 
     def LastExec(self) -> str:
         """The kernel the last batch ran on."""
-        return {0: "none", 1: "interp", 2: "jit", 3: "spread"}[self.lib.mimic_last_exec(self.h)]
+        return {0: "none", 1: "interp", 2: "jit", 3: "spread", 4: "spread_own"}[self.lib.mimic_last_exec(self.h)]
 
     def SetSpread(self, mode: int) -> None:
         """Spread launches (mimic_set_spread): -1 default policy, 0 never, 1 whenever allowed."""

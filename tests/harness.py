@@ -66,12 +66,13 @@ def kernel_of(sc: Scenario, ctx: int = 0):
     return [raw for _, raw, _ in sc.progs], ctx, J.vc_slots([(raw, rel) for _, raw, rel in sc.progs], sc.maps)
 
 
-def spread_kernel_of(sc: Scenario):
-    """The spread kernel a scenario's VM builds (jit.spread_spec): for the session prewarm."""
+def spread_kernel_of(sc: Scenario, own: bool = False):
+    """The spread kernel a scenario's VM builds (jit.spread_spec; own: its owned form): for the
+    session prewarm."""
     from mimic_amd import jit as J
 
     progs = [(raw, rel) for _, raw, rel in sc.progs]
-    return [raw for _, raw, _ in sc.progs], 0, (), J.spread_spec(progs, sc.maps, sc.vcpus)
+    return [raw for _, raw, _ in sc.progs], 0, (), J.spread_spec(progs, sc.maps, sc.vcpus, own=own)
 
 
 def build_engine(sc: Scenario, device: int = 0, shard=None, ctx: int = 0, exec_mode: Optional[str] = None,

@@ -130,3 +130,26 @@ def test_spread_kernels_compile_within_budget(fn, V):
     assert res["scratch"] == 0 and res["vgpr_spill"] == 0, res
     assert res["waves_per_simd"] >= 4, res
     assert res["lds"] == (spec[2] * (p.maps[0]["max_entries"] * p.maps[0]["value_size"]) if spec[2] else 0), res
+
+
+@pytest.mark.parametrize("fn,rows", [("prog_classifier", 128), ("prog_parse5", 16)])
+def test_owned_form_compiles_within_budget(fn, rows):
+    """The owned form (every packet of a block's vCPUs in the block, jit.cpp spread_own): the same
+    analysis, an LDS table of min(128, 32 KiB / row) rows, no scratch, 4 waves per SIMD."""
+    p = getattr(W, fn)()
+    sc = Scenario(vcpus=262144, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+    raws, _, _, spec = spread_kernel_of(sc, own=True)
+    assert spec[2] == rows | (1 << 31)
+    src, ok = J.spread_source(raws, *spec)
+    assert ok and "#define MIMIC_SPREAD_OWN 1" in src and f"#define SPREAD_ROWS {rows}u" in src
+    r = J.kernel_resources(J.code_object(src))
+    assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 4, r
+
+
+def test_owned_form_refuses_what_spread_refuses():
+    items = _lookup() + [A.jmp("jeq", 0, 0, 3), A.ldx(8, 1, 0, 0), A.mov64_reg(0, 1), A.exit_(), A.mov64_imm(0, 2), A.exit_()]
+    raw, rel = A.assemble(items)
+    sc = Scenario(vcpus=4096, maps=[PCPU], progs=[("p", raw, rel)])
+    raws, _, _, spec = spread_kernel_of(sc, own=True)
+    src, ok = J.spread_source(raws, *spec)
+    assert not ok and "MIMIC_SPREAD_OWN" not in src
