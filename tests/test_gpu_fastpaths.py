@@ -386,7 +386,7 @@ def test_cross_packet_window_prefetch(gpu, case, room, sched, monkeypatch):
     cpu = rng.integers(0, 8, n).astype(np.int32) if sched == "explicit" else W.schedule_cpu(n, 8, sched)
     o = run_oracle(sc, buf, off, lens, cpu, headroom=headroom, tailroom=tailroom)
     e = run_engine(sc, buf, off, lens, cpu if sched == "explicit" else None, headroom=headroom, tailroom=tailroom,
-                   schedule=mode)
+                   schedule=mode, spread=0)
     assert_same(o, e)
     assert e["last_exec"] == "jit"
     assert len(set(o["r0"].tolist())) > 100
@@ -422,7 +422,7 @@ def test_lane_prefetch(gpu, case, room, sched, V, monkeypatch):
     cpu = rng.integers(0, V, n).astype(np.int32) if sched == "explicit" else W.schedule_cpu(n, V, sched)
     o = run_oracle(sc, buf, off, lens, cpu, headroom=headroom, tailroom=tailroom)
     e = run_engine(sc, buf, off, lens, cpu if sched == "explicit" else None, headroom=headroom, tailroom=tailroom,
-                   schedule=mode)
+                   schedule=mode, spread=0)
     assert_same(o, e)
     assert e["last_exec"] == "jit"
     assert len(set(o["r0"].tolist())) > 100
