@@ -12,6 +12,7 @@ for c in classifier parse5 flowtrack flowtrack_insert skb pass8; do
 done
 $B --config classifier --vcpus 256 > $D/bench_classifier_v256.json 2> $D/bench_classifier_v256.err || exit 1
 $B --config parse5 --vcpus 256 --steps 5 --warmup 1 > $D/bench_parse5_v256.json 2> $D/bench_parse5_v256.err || exit 1
+$B --config classifier --vcpus 65536 > $D/bench_classifier_v64k.json 2> $D/bench_classifier_v64k.err || exit 1   # owned spread (16 per vCPU)
 $B --config classifier --sched chunked > $D/bench_classifier_chunked.json 2> $D/bench_classifier_chunked.err || exit 1
 $B --config flowtrack --rccl > $D/bench_flowtrack_rccl.json 2> $D/bench_flowtrack_rccl.err || exit 1
 for c in classifier flowtrack; do   # the N-rank path at N = 2, both engines on GPU 0, gloo collectives
