@@ -4,12 +4,17 @@
 # rehearsal of the N-GPU path on one GPU, and the reference-shaped API rates.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 T=${T:-r05final}
-TAG=$T bash tools/run_driver.sh || exit 1
 D=gpurun_out/$T
 B="timeout -k 10 300 python -u bench.py --no-host-resident --no-cpu-baseline"
+# PART=1: driver tiers + one bench line per config; PART=2: the other bench lines, N-rank rehearsal, API rates
+if [ "${PART:-1}" = 1 ]; then
+TAG=$T bash tools/run_driver.sh || exit 1
 for c in classifier parse5 flowtrack flowtrack_insert skb pass8; do
   $B --config $c > $D/bench_$c.json 2> $D/bench_$c.err || { tail -20 $D/bench_$c.err; exit 1; }
 done
+fi
+if [ "${PART:-2}" = 2 ]; then
+mkdir -p $D
 $B --config classifier --vcpus 256 > $D/bench_classifier_v256.json 2> $D/bench_classifier_v256.err || exit 1
 $B --config parse5 --vcpus 256 --steps 5 --warmup 1 > $D/bench_parse5_v256.json 2> $D/bench_parse5_v256.err || exit 1
 $B --config classifier --vcpus 65536 > $D/bench_classifier_v64k.json 2> $D/bench_classifier_v64k.err || exit 1   # owned spread (16 per vCPU)
@@ -18,5 +23,6 @@ $B --config flowtrack --rccl > $D/bench_flowtrack_rccl.json 2> $D/bench_flowtrac
 for c in classifier flowtrack; do   # the N-rank path at N = 2, both engines on GPU 0, gloo collectives
   $B --gpus 2 --dist-backend gloo --one-device --config $c --steps 20 > $D/bench_${c}_2rank.json 2> $D/bench_${c}_2rank.err || { tail -20 $D/bench_${c}_2rank.err; exit 1; }
 done
-for f in $D/bench_*.json; do python3 -c "import json; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print('$(basename $f)', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['frac'], r.get('frac_on_traffic'), r.get('traffic_over_algorithmic'), d['config']['engine'], d['n_gpus'])"; done
 timeout -k 10 600 python tools/api_rates.py > $D/api_rates.json 2> $D/api_rates.err && cat $D/api_rates.json
+fi
+for f in $D/bench_*.json; do python3 -c "import json; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print('$(basename $f)', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['frac'], r.get('frac_on_traffic'), r.get('traffic_over_algorithmic'), d['config']['engine'], d['n_gpus'])"; done
