@@ -144,6 +144,10 @@ def main():
         pool.Stop()
         return time.perf_counter() - t0
 
+    # the batched launches run the chain's JIT kernel: built (or read from the cache) before timing
+    warm = [q for q in (make(k) for k in range(64)) if q is not None]
+    svm.RunProcesses(warm, None, [k % V for k in range(len(warm))])
+    svm.CleanupProcesses(warm)
     t0 = time.perf_counter()
     procs = [q for q in (make(k) for k in range(ns)) if q is not None]
     t_new = time.perf_counter() - t0
@@ -153,15 +157,18 @@ def main():
                        "what": "Enqueue + micro-batched launches (mimic_process_run_many); NewProcess timed apart"}
     # the same kind of jobs through the C ABI call a Go pool would make per micro-batch
     # (mimic_process_run_many + mimic_process_free_many), without the Python pool's per-job work
-    procs = [q for q in (make(k) for k in range(ns)) if q is not None]
-    cpus = [k % V for k in range(len(procs))]
-    t0 = time.perf_counter()
-    for b in range(0, len(procs), 1 << 16):
-        svm.RunProcesses(procs[b:b + (1 << 16)], None, cpus[b:b + (1 << 16)])
-        svm.CleanupProcesses(procs[b:b + (1 << 16)])
-    dt = time.perf_counter() - t0
-    out["abi_run_many_skb"] = {"jobs": len(procs), "seconds": round(dt, 3), "jobs_per_s": round(len(procs) / dt, 1),
-                               "what": "mimic_process_run_many + mimic_process_free_many per 65 536 processes"}
+    rates = []
+    for _ in range(3):   # three rounds of fresh processes: the median
+        procs = [q for q in (make(k) for k in range(ns)) if q is not None]
+        cpus = [k % V for k in range(len(procs))]
+        t0 = time.perf_counter()
+        for b in range(0, len(procs), 1 << 16):
+            svm.RunProcesses(procs[b:b + (1 << 16)], None, cpus[b:b + (1 << 16)])
+            svm.CleanupProcesses(procs[b:b + (1 << 16)])
+        rates.append(len(procs) / (time.perf_counter() - t0))
+    out["abi_run_many_skb"] = {"jobs": len(procs), "jobs_per_s": round(sorted(rates)[1], 1),
+                               "rounds_jobs_per_s": [round(r, 1) for r in rates],
+                               "what": "mimic_process_run_many + mimic_process_free_many per 65 536 processes (median of 3)"}
     procs = [q for q in (make(k) for k in range(args.per_job)) if q is not None]
     dt = pool_run(procs, True)
     out["pool_skb_per_job"] = {"jobs": len(procs), "seconds": round(dt, 3), "jobs_per_s": round(len(procs) / dt, 1),
