@@ -91,6 +91,39 @@ def main():
                        "what": "NewProcess + Enqueue per job from one Python thread, Stop() waits for all"}
     vm.close()
 
+    # ---- host map operations between launches (launch -> Update -> launch) ---------------
+    # cfg 4's table (E = 131 072, 16-byte keys): every launch may write it, so the host image pages in
+    # on demand after each (engine.cpp HashMirror); the host ops themselves are timed
+    fp = W.prog_flowtrack()
+    fsc = Scenario(vcpus=4096, maps=fp.maps, progs=[(fp.name, fp.raw, fp.relocs)])
+    fvm, fmaps, fpids = build_engine(fsc)
+    fb, fo, fl = W.make_packets(65536, **W.IMIX, seed=17)
+    fbatch = M.XDPBatch.from_numpy(fb, fo, fl, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+    fvm.RunXDPBatch(fpids[0], fbatch)
+    ops = {"update_new_key": [], "lookup": [], "update_then_lookup_4": []}
+    rng = np.random.default_rng(23)
+    for it in range(60):
+        fvm.RunXDPBatch(fpids[0], fbatch)   # may write the table: the host image is stale after it
+        key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        t0 = time.perf_counter()
+        fmaps["flows"].Update(key, (it).to_bytes(8, "little"), 0)
+        ops["update_new_key"].append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        fmaps["flows"].Lookup(key)
+        ops["lookup"].append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        for q in range(4):
+            k2 = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+            fmaps["flows"].Update(k2, b"\0" * 8, 0)
+            fmaps["flows"].Lookup(k2)
+        ops["update_then_lookup_4"].append(time.perf_counter() - t0)
+    out["host_ops_after_launch"] = {k: {"median_us": round(float(np.median(v[5:])) * 1e6, 1),
+                                        "p90_us": round(float(np.percentile(v[5:], 90)) * 1e6, 1)} for k, v in ops.items()}
+    out["host_ops_after_launch"]["what"] = ("cfg-4 table (E = 131 072, 16-byte keys) written by a 65 536-packet launch "
+                                            "before each round: the first Update after the launch, a Lookup, then 4 more "
+                                            "Update + Lookup pairs (Python calls through the C ABI)")
+    fvm.close()
+
     # ---- sk_buff processes of the cfg-5 chain ------------------------------------------------------
     progs, smaps, pa = W.skb_programs()
     ns = args.skb_jobs
