@@ -388,6 +388,10 @@ int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batc
 /* The same with Run(ctx): every sub-batch's kernel reads ctx (see mimic_run_xdp_ctx). */
 int mimic_run_xdp_host_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
                            mimic_ctx *ctx);
+/* The same with one context per packet (ctx_per_packet[i], NULL: none) -- processPool's jobs each
+ * carry their own ctx (vm.go:548-573); the contexts' words go to the device once per call. */
+int mimic_run_xdp_host_ctx_pp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
+                              mimic_ctx *const *ctx_per_packet);
 /* Pin / unpin host memory for DMA (hipHostRegister / hipHostUnregister). */
 int mimic_host_register(void *p, size_t bytes);
 int mimic_host_unregister(void *p);

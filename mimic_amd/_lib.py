@@ -173,6 +173,7 @@ EXPORTS = {
     "mimic_process_run_many": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(ProcessRegs)]),
     "mimic_process_free_many": (None, [C.c_void_p, C.c_uint32]),
     "mimic_run_xdp_host_ctx": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPHostBatch), C.c_uint32, C.c_void_p]),
+    "mimic_run_xdp_host_ctx_pp": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPHostBatch), C.c_uint32, C.c_void_p]),
     "mimic_last_steps": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }
 

@@ -1524,6 +1524,9 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
 struct CtxRun {      // Run(ctx) of a batch: one context for every packet, or one per packet (host array)
     mimic_ctx *all;
     mimic_ctx *const *per_packet;
+    // per_packet's context words already on the device (the host pipeline uploads the whole batch's
+    // array once; a sub-batch points into it): no per-launch upload
+    const uint32_t *const *dev_pp = nullptr;
 };
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                         hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr, const StepRun *step = nullptr,
@@ -1898,6 +1901,9 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.lane_steps = vm->d_lane_steps;
     if (cx && cx->all) {
         kp.cancel = cx->all->dword;
+        kp.cancel_any = 1;
+    } else if (cx && cx->dev_pp && b->n) {
+        kp.cancel_pp = cx->dev_pp;
         kp.cancel_any = 1;
     } else if (cx && cx->per_packet && b->n) {
         std::vector<const uint32_t *> w(b->n);
@@ -2946,16 +2952,20 @@ static int slot_reserve(mimic_vm *vm, mimic_vm::Slot &sl, size_t bytes, size_t n
 // status (and packet bytes) on the D2H stream after the kernel.  The host-side scan of sub-batch
 // c + 1 runs while sub-batch c's copies are in flight, so no O(n) pass precedes the first copy.
 static int run_xdp_host_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
-                             mimic_ctx *ctx);
+                             mimic_ctx *ctx, mimic_ctx *const *ctx_per_packet);
 int mimic_run_xdp_host(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks) {
-    return run_xdp_host_impl(vm, prog_id, hb, chunks, nullptr);
+    return run_xdp_host_impl(vm, prog_id, hb, chunks, nullptr, nullptr);
 }
 int mimic_run_xdp_host_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
                            mimic_ctx *ctx) {
-    return run_xdp_host_impl(vm, prog_id, hb, chunks, ctx);
+    return run_xdp_host_impl(vm, prog_id, hb, chunks, ctx, nullptr);
+}
+int mimic_run_xdp_host_ctx_pp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
+                              mimic_ctx *const *ctx_per_packet) {
+    return run_xdp_host_impl(vm, prog_id, hb, chunks, nullptr, ctx_per_packet);
 }
 static int run_xdp_host_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_host_batch *hb, uint32_t chunks,
-                             mimic_ctx *ctx) {
+                             mimic_ctx *ctx, mimic_ctx *const *ctx_pp) {
     if (!vm || !hb) return MIMIC_EINVAL;
     const uint32_t n = hb->n;
     if (n == 0) return 0;
@@ -2989,6 +2999,28 @@ static int run_xdp_host_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_hos
         sched = MIMIC_SCHED_EXPLICIT;
     }
     if (sched == MIMIC_SCHED_EXPLICIT && !cpu) return fail(vm, MIMIC_EINVAL, "explicit schedule needs cpu[]");
+    // one context per packet: the whole batch's context words go to the device once, before the
+    // pipeline (each sub-batch's kernels read their slice; the array is 8 bytes per packet)
+    bool pp_any = false;
+    if (ctx_pp) {
+        std::vector<const uint32_t *> w(n);
+        for (uint32_t i = 0; i < n; i++) {
+            w[i] = ctx_pp[i] ? ctx_pp[i]->dword : nullptr;
+            pp_any |= w[i] != nullptr;
+        }
+        if (pp_any) {
+            if (vm->cancel_pp_stream) HIP_OK(vm, hipStreamSynchronize(vm->cancel_pp_stream));   // earlier readers
+            HIP_OK(vm, hipStreamSynchronize(vm->stream));
+            vm->cancel_pp_stream = vm->stream;
+            if (n > vm->cancel_pp_cap) {
+                hipFree(vm->d_cancel_pp);
+                vm->d_cancel_pp = nullptr;
+                HIP_OK(vm, hipMalloc(&vm->d_cancel_pp, (size_t)n * sizeof(void *)));
+                vm->cancel_pp_cap = n;
+            }
+            HIP_OK(vm, hipMemcpy(vm->d_cancel_pp, w.data(), (size_t)n * sizeof(void *), hipMemcpyHostToDevice));
+        }
+    }
     if (!vm->s_h2d) {
         HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_h2d, hipStreamNonBlocking));
         HIP_OK(vm, hipStreamCreateWithFlags(&vm->s_h2d2, hipStreamNonBlocking));
@@ -3043,8 +3075,9 @@ static int run_xdp_host_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_hos
         r.r0 = sl.r0;
         r.status = sl.st;
         vm->kp_copy_stream = h2d;
-        const CtxRun cx{ctx, nullptr};   // every sub-batch's kernel reads the run's context
-        rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a, nullptr, nullptr, ctx ? &cx : nullptr);
+        // every sub-batch's kernel reads the run's context, or its packets' slice of the per-packet words
+        const CtxRun cx{ctx, pp_any ? ctx_pp + a : nullptr, pp_any ? vm->d_cancel_pp + a : nullptr};
+        rc = run_xdp_impl(vm, prog_id, &b, &r, vm->stream, a, nullptr, nullptr, ctx || pp_any ? &cx : nullptr);
         vm->kp_copy_stream = nullptr;
         if (rc) return rc;
         t_run += std::chrono::duration<double, std::micro>(clk::now() - t2).count();

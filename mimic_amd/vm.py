@@ -712,11 +712,13 @@ class VM:
 
     def RunXDPHost(self, prog_id: int, buf, off, lens, schedule=L.SCHED_INTERLEAVED, cpu=None, headroom: int = 0,
                    tailroom: int = 0, ingress: int = 0, rxq: int = 0, egress: int = 0, step_budget: int = 0,
-                   chunks: int = 0, pkt_out=None, r0=None, status=None, ctx: Optional["Context"] = None):
+                   chunks: int = 0, pkt_out=None, r0=None, status=None, ctx: Optional["Context"] = None,
+                   ctx_per_packet: Optional[Sequence[Optional["Context"]]] = None):
         """A batch resident in HOST memory (numpy arrays): the engine pipelines H2D copies, the
         kernels and the D2H copies of r0/status (and of the packet memory into pkt_out).
         Returns (r0 uint64[n], status uint8[n]).  Register the arrays (HostRegister) for
-        asynchronous copies."""
+        asynchronous copies.  Run(ctx): one context for the batch, or one per packet
+        (ctx_per_packet, as processPool's jobs carry theirs)."""
         import numpy as np
 
         n = len(lens)
@@ -736,10 +738,11 @@ class VM:
         hb.step_budget = step_budget
         hb.pkt_out = pkt_out.ctypes.data if pkt_out is not None else None
         hb.r0, hb.status = r0.ctypes.data, status.ctypes.data
-        ctx = _live(ctx)
-        if ctx is not None:   # Run(ctx): every sub-batch's kernel reads the context
-            _check(self.h, self.lib.mimic_run_xdp_host_ctx(self.h, prog_id, C.byref(hb), chunks, ctx._device_handle()),
-                   "RunXDPHost")
+        h, arr, _keep = _ctx_args(ctx, ctx_per_packet, n)
+        if h is not None:   # Run(ctx): every sub-batch's kernel reads the context
+            _check(self.h, self.lib.mimic_run_xdp_host_ctx(self.h, prog_id, C.byref(hb), chunks, h), "RunXDPHost")
+        elif arr is not None:   # one context per packet
+            _check(self.h, self.lib.mimic_run_xdp_host_ctx_pp(self.h, prog_id, C.byref(hb), chunks, arr), "RunXDPHost")
         else:
             _check(self.h, self.lib.mimic_run_xdp_host(self.h, prog_id, C.byref(hb), chunks), "RunXDPHost")
         return r0, status

@@ -396,3 +396,41 @@ def test_host_resident_batch_with_a_context(gpu):
         vm.close()
         c.close()
     assert (results[0] == 0).all() and (results[1] == CANCELED).all()
+
+
+@pytest.mark.parametrize("sched", ["interleaved", "explicit"])
+def test_host_resident_per_packet_contexts(gpu, sched):
+    """mimic_run_xdp_host_ctx_pp: Background, live, canceled and past-deadline contexts per packet
+    (processPool's jobs each carry theirs, vm.go:548-573) across 5 sub-batches; the oracle replays
+    the states, packet bytes (pkt_out) and counters included."""
+    sc = _count_sc()
+    buf, off, lens = _packets(3000, seed=10)
+    n = len(lens)
+    rng = np.random.default_rng(5)
+    cpu = rng.integers(0, sc.vcpus, n).astype(np.int32) if sched == "explicit" else W.schedule_cpu(n, sc.vcpus, sched)
+    live, gone, late = M.WithCancel(), M.WithCancel(), M.WithTimeout(0.0)
+    gone.Cancel()
+    ctxs = [[None, live, gone, late, M.Background()][k] for k in rng.integers(0, 5, n)]
+    done = _states([None if c is not None and getattr(c, "_background", False) else c for c in ctxs])
+    assert set(np.unique(done)) == {0, 1, 2}
+    vm, maps, pids = build_engine(sc)
+    hbuf, out = buf.copy(), np.zeros_like(buf)
+    mode = M.SCHED_EXPLICIT if sched == "explicit" else M.SCHED_INTERLEAVED
+    r0, st = vm.RunXDPHost(pids[0], hbuf, off, lens, schedule=mode, cpu=cpu if sched == "explicit" else None,
+                           headroom=8, tailroom=8, chunks=5, pkt_out=out, ctx_per_packet=ctxs)
+    o = run_oracle(sc, buf, off, lens, cpu, headroom=8, tailroom=8, ctx_done=done)
+    assert (r0 == o["r0"]).all() and (st == o["status"]).all()
+    assert (st[done == 1] == CANCELED).all() and (st[done == 2] == DEADLINE).all()
+    from harness import build_oracle
+
+    ovm, _, opids = build_oracle(sc)   # the packet memory the oracle leaves (a process that ran stored a byte)
+    obuf = buf.copy()
+    ovm.run_xdp_batch(opids[0], obuf, off, lens, cpu, 8, 8, None, None, None, 0, ctx_done=done)
+    ovm.close()
+    for i in range(n):
+        a, L = int(off[i]), int(lens[i])
+        assert out[a:a + 16 + L].tobytes() == obuf[a:a + 16 + L].tobytes(), i
+    assert [maps["c"].Values(k) for k in range(sc.vcpus)] == o["maps"]["c"]
+    vm.close()
+    for c in (live, gone, late):
+        c.close()
