@@ -1619,8 +1619,10 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     const uint32_t out_q = into ? (uint32_t)(sizeof(SkbRec) / 8) : SKB_DERIVED_Q;
     // MIMIC_SKB_ROOMS_CHAIN=1 (measurement, JIT batches only): the chain kernel reads the rooms itself
     static const bool rooms_chain = getenv("MIMIC_SKB_ROOMS_CHAIN") && getenv("MIMIC_SKB_ROOMS_CHAIN")[0] == '1';
+    // MIMIC_SKB_ROOMS_ZERO=1: the prep zeroes every loaded packet's rooms without reading them
+    static const bool rooms_zero = getenv("MIMIC_SKB_ROOMS_ZERO") && getenv("MIMIC_SKB_ROOMS_ZERO")[0] == '1';
     if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
-                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : 1u,
+                              vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : rooms_zero ? 2u : 1u,
                               (sparse && !into) ? 1u : 0u, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;

@@ -64,7 +64,7 @@ static __device__ uint64_t prep_exscan(uint64_t v, uint64_t *wtot, uint64_t *tot
 }
 
 // prefix: n + ceil(n / PREP_T) words (within-block prefixes, then the blocks' sums)
-extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const uint8_t *__restrict__ pkt_data,
+extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(uint8_t *__restrict__ pkt_data,
                                                                           const uint64_t *__restrict__ pkt_off,
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, uint64_t *__restrict__ rec,
@@ -81,32 +81,49 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
     uint64_t flags = 0;   // skb.h SKB_PFX_*
     if (live) {
         const uint32_t L = pkt_len[i];
-        const uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
+        uint8_t *pkt = pkt_data + pkt_off[i] + SKB_HEADROOM;
         // the first SKB_WIN bytes into registers (16-byte chunks that start inside the packet; one may
         // run into the 64-byte tailroom); common frames decode from there (skb_fast), the rest
         // through this thread's LDS window
         typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-        uint32_t w[SKB_WIN / 4];
+        // every chunk is loaded (a chunk past the packet's start reloads chunk 0, which is always
+        // inside the packet memory) and zeroed after: no branch between the loads, so they issue
+        // back to back and the decode waits once (a conditional load per chunk made the compiler wait
+        // for the first two chunks before issuing the rest: two round trips)
+        u32x4u v[SKB_WIN / 16];
 #pragma unroll
-        for (uint32_t c = 0; c < SKB_WIN / 16; c++) {
-            u32x4u v = {0, 0, 0, 0};
-            if (16 * c < L) v = *(const u32x4u *)(pkt + 16 * c);
-            w[4 * c] = v.x;
-            w[4 * c + 1] = v.y;
-            w[4 * c + 2] = v.z;
-            w[4 * c + 3] = v.w;
-        }
+        for (uint32_t c = 0; c < SKB_WIN / 16; c++) v[c] = *(const u32x4u *)(pkt + (16 * c < L ? 16 * c : 0u));
         // the rooms flag (skb.h SKB_DIRTY_Q): any non-zero byte in the 32 bytes before the packet
         // or the 64 after it (rooms = 0: a measurement build whose JIT kernel reads them itself).
         // Loaded with the window, before the decode: one memory round trip per packet, not two
-        // (the headroom shares the window's first line; the tailroom is the packet's last line)
-        uint32_t dirty = 0;
-        if (rooms) {
-            const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
-            u32x4u o = hr[0] | hr[1];
+        // (the headroom shares the window's first line; the tailroom is the packet's last line).
+        // Issued after the window and OR-ed after the decode: loads complete in order, so the
+        // decode waits for the window only and runs while the tail line is still on its way
+        // (measured: the rooms read cost 28 of the prep's 93 us when it was consumed first).
+#ifdef MIMIC_PREP_NOROOMS   // measurement only (tools/prep_probe.py): the rooms not read (flag always clean)
+        rooms = 0;
+#endif
+        // (rooms 0 / 1: loaded whatever `rooms` says, one straight-line load sequence for the wait
+        // counter; rooms 2: not read, zeroed below)
+        const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
+        u32x4u rh0 = {0, 0, 0, 0}, rh1 = rh0, rt[SKB_TAILROOM / 16];
+        if (rooms != 2) {
+            rh0 = hr[0];
+            rh1 = hr[1];
 #pragma unroll
-            for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) o |= tr[c];
-            dirty = (o.x | o.y | o.z | o.w) ? 1u : 0u;
+            for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) rt[c] = tr[c];
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) rt[c] = rh0;
+        }
+        uint32_t w[SKB_WIN / 4];
+#pragma unroll
+        for (uint32_t c = 0; c < SKB_WIN / 16; c++) {
+            const bool in = 16 * c < L;
+            w[4 * c] = in ? v[c].x : 0u;
+            w[4 * c + 1] = in ? v[c].y : 0u;
+            w[4 * c + 2] = in ? v[c].z : 0u;
+            w[4 * c + 3] = in ? v[c].w : 0u;
         }
 #ifdef MIMIC_PREP_NOWALK   // measurement only (tools/prep_probe.py): loads and footprints, no decode
         r.len = w[0] == 0x12345678u ? SKB_LOAD_FAILED : L;
@@ -114,6 +131,19 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(const
 #else
         const bool fast = skb_init_regs<PREP_T>(w, win, t, pkt, L, r);
 #endif
+        u32x4u o = rh0 | rh1;
+#pragma unroll
+        for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) o |= rt[c];
+        const uint32_t dirty = rooms == 1 && (o.x | o.y | o.z | o.w) ? 1u : 0u;
+        if (rooms == 2 && !(r.len & SKB_LOAD_FAILED)) {   // Load's zeroed rooms, written without a look
+            typedef uint32_t u32x4w __attribute__((ext_vector_type(4), aligned(1)));
+            const u32x4w z = {0, 0, 0, 0};
+            u32x4w *hw = (u32x4w *)(pkt - SKB_HEADROOM), *tw = (u32x4w *)(pkt + L);
+            hw[0] = z;
+            hw[1] = z;
+#pragma unroll
+            for (uint32_t c = 0; c < SKB_TAILROOM / 16; c++) tw[c] = z;
+        }
         r.ip[0].pad[0] = dirty;
         f = (r.len & SKB_LOAD_FAILED) ? 0ull : (uint64_t)SKB_FOOT_FIXED + L;
         flags = (dirty ? SKB_PFX_DIRTY : 0ull) | (fast ? 0ull : SKB_PFX_EXC);
@@ -219,7 +249,7 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
 // the prep kernel alone (tools/prep_probe.py)
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
                                    uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state, hipStream_t st) {
-    hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
+    hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
                        rec, rec_q, prefix, 1u, 0u);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        0ull, 0u);
@@ -232,7 +262,7 @@ extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pk
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
                                      uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse, hipStream_t st) {
     if (n)
-        hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, pkt_data, pkt_off, pkt_len, n,
+        hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
                            rec, rec_q, prefix, rooms, sparse);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        init_base, use_init);
