@@ -403,7 +403,10 @@ int mimic_exec_mode(const mimic_vm *vm);
  * increment through one per-CPU array lookup, a vCPU's packets may run on many lanes (the final
  * counters are sums; each packet's R0 / status / steps depend on its own bytes only).
  * mode -1: default (env MIMIC_SPREAD, else when a batch has >= 8 packets per vCPU), 0: never,
- * 1: whenever the programs allow it.  Every generic load / store of such a program set must go
+ * 1: whenever the programs allow it.  The owned form (MIMIC_EXEC_SPREAD_OWN: a workgroup runs every
+ * packet of its vCPUs and adds into rows only it touches) takes batches of 2..16 packets per vCPU
+ * with fewer vCPUs than the lanes the one-lane kernel holds resident (env MIMIC_SPREAD_OWN=1: 2..256
+ * packets whatever V, =0: never).  Every generic load / store of such a program set must go
  * through a base the analysis can place (derived from R1, R10 or a packet pointer), else the set runs
  * one lane per vCPU.  (mimic_sync / mimic_last_steps would fail if a spread launch still reached
  * per-CPU memory outside a fused increment: an internal assertion.) */
@@ -429,7 +432,8 @@ long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint
                          const uint32_t *vc_slots, uint32_t n_vc, char *buf, size_t cap);
 /* The spread kernel's source (mimic_set_spread): pc = (program, slot, map id) triples of the
  * LD_IMM64 slots naming a per-CPU array's object, shapes = (map id, E * S, S) triples, lds_rows =
- * rows of a block's LDS counter table (min(1024, V) when rows * E * S <= 32 KiB, else 0).
+ * rows of a block's LDS counter table (min(1024, V) when rows * E * S <= 32 KiB, else 0); bit 31 of
+ * lds_rows set: the owned form's source (its rows: min(128, 32 KiB / (E * S))).
  * *spread_out = 1 when the programs allow a spread kernel. */
 long mimic_jit_source_spread(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, const uint32_t *pc,
                              uint32_t n_pc, const uint32_t *shapes, uint32_t n_shapes, uint32_t lds_rows,
