@@ -1738,6 +1738,10 @@ static int spread_build_own(mimic_vm *vm) {
     vm->spread_own_state = -1;
     SpreadReq req;
     req.own = true;
+    // packets per thread (MIMIC_SPREAD_OWN_Q, measurement: 1, 2 or 4)
+    const char *qv = getenv("MIMIC_SPREAD_OWN_Q");
+    const uint32_t q = qv ? (uint32_t)atoi(qv) : 1u;
+    req.own_q = q == 2 || q == 4 ? q : 1u;
     for (size_t s = 0; s < vm->h_all.size(); s++) {
         const DInsn &x = vm->h_all[s];
         const uint32_t mh = AUX_MAPHINT(x.aux);
@@ -2031,7 +2035,9 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         if (knob != 0 && own_pref && kp.per_lane >= 2 && kp.per_lane <= 256) {
             rc = spread_build_own(vm);
             if (rc) return rc;
-            own = vm->spread_own_state > 0 && 256u / kp.per_lane <= vm->spread_own_rows &&
+            const uint32_t oq = vm->jit_info_spread_own.spread_own_q ? vm->jit_info_spread_own.spread_own_q : 1u;
+            own = vm->spread_own_state > 0 && kp.per_lane % oq == 0 && 256u * oq / kp.per_lane <= vm->spread_own_rows &&
+                  256u * oq / kp.per_lane >= 1u &&
                   mimic_jit_step_bound(vm->jit_info_spread_own, kp.max_tail_calls) <= kp.budget;
             spread = own;
         }
@@ -2064,7 +2070,8 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     uint32_t run_lanes = lanes;
     if (spread) {
         // owned: 256 / P vCPU lanes per block
-        const uint32_t blocks = own ? (cpu_lanes + 256u / kp.per_lane - 1) / (256u / kp.per_lane)
+        const uint32_t orows = own ? 256u / (kp.per_lane / ji.spread_own_q) : 1u;
+        const uint32_t blocks = own ? (cpu_lanes + orows - 1) / orows
                                     : (uint32_t)(((uint64_t)b->n + spread_ppb() - 1) / spread_ppb());
         run_lanes = blocks * 256u;
         rc = priv_ensure(vm, q_per_lane, run_lanes, st);   // private memory (stack ...) per spread lane
