@@ -1738,10 +1738,6 @@ static int spread_build_own(mimic_vm *vm) {
     vm->spread_own_state = -1;
     SpreadReq req;
     req.own = true;
-    // packets per thread (MIMIC_SPREAD_OWN_Q, measurement: 1, 2 or 4)
-    const char *qv = getenv("MIMIC_SPREAD_OWN_Q");
-    const uint32_t q = qv ? (uint32_t)atoi(qv) : 1u;
-    req.own_q = q == 2 || q == 4 ? q : 1u;
     for (size_t s = 0; s < vm->h_all.size(); s++) {
         const DInsn &x = vm->h_all[s];
         const uint32_t mh = AUX_MAPHINT(x.aux);
@@ -1756,7 +1752,7 @@ static int spread_build_own(mimic_vm *vm) {
     uint32_t row = 0;
     for (auto &kv : req.shape) row = std::max(row, kv.second.first);
     if (!row) return 0;
-    req.lds_rows = std::min<uint32_t>(128u, 32768u / row);
+    req.lds_rows = std::min<uint32_t>(256u, 32768u / row);
     if (req.lds_rows < 2) return 0;
     JitInfo info{};
     const std::string src = mimic_jit_source(vm->h_dp, vm->h_all, CTX_XDP, &info, nullptr, false, &req);
@@ -2023,21 +2019,25 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     if (jit && !skb && b->n > 0 && (b->schedule == MIMIC_SCHED_CHUNKED || b->schedule == MIMIC_SCHED_INTERLEAVED)) {
         const char *sv = getenv("MIMIC_SPREAD");
         const int knob = vm->spread_mode >= 0 ? vm->spread_mode : sv && *sv ? atoi(sv) : -1;
-        // the owned form, for batches of 2..256 packets per vCPU.  By default for 2..16 packets per
-        // vCPU when the one-lane kernel would not fill the chip (fewer vCPU lanes than 4 waves on
-        // every SIMD): classifier, 1.2-1.9x the one-lane kernel at V = 16 K..131 K and P = 4, 1.4x the
-        // LDS-table spread at V = 65 536, P = 16; slower than the one-lane kernel at V = 262 144 and
-        // than the table spread from P = 64 (its table rows then take many increments each;
-        // profiles/r05/r05u/).  MIMIC_SPREAD_OWN=1: whenever it applies, =0: never.
+        // the owned form, for batches of 2..256 packets per vCPU (Q packets per thread, below): by
+        // default whenever the programs and the table allow it -- classifier at V = 262 144 (cfg 2)
+        // 25.0 vs 25.7 us, parse5 at V = 262 144 (cfg 3) 0.74 vs 1.03 ms, V = 16 384 with 64 packets
+        // per vCPU 2x the table spread (profiles/r05/).  MIMIC_SPREAD_OWN=0: never.
         const char *ov = getenv("MIMIC_SPREAD_OWN");
-        const int own_knob = ov && *ov ? atoi(ov) : -1;
-        const bool own_pref = own_knob == 1 || (own_knob != 0 && cpu_lanes < chip_lanes(vm) && kp.per_lane <= 16);
+        const bool own_pref = !(ov && ov[0] == '0');
         if (knob != 0 && own_pref && kp.per_lane >= 2 && kp.per_lane <= 256) {
             rc = spread_build_own(vm);
             if (rc) return rc;
-            const uint32_t oq = vm->jit_info_spread_own.spread_own_q ? vm->jit_info_spread_own.spread_own_q : 1u;
-            own = vm->spread_own_state > 0 && kp.per_lane % oq == 0 && 256u * oq / kp.per_lane <= vm->spread_own_rows &&
-                  256u * oq / kp.per_lane >= 1u &&
+            // Q packets per thread: enough threads to fill the chip about once (fewer, longer threads
+            // measured faster: V = 131 072, P = 4: 17.6 us at Q = 1, 15.5 at Q = 2), a divisor of P
+            // whose 256 Q / P rows fit the table (MIMIC_SPREAD_OWN_Q: a fixed Q, measurement)
+            const uint32_t P = kp.per_lane, cl = chip_lanes(vm);
+            const char *qv = getenv("MIMIC_SPREAD_OWN_Q");
+            uint32_t q = qv && *qv ? (uint32_t)atoi(qv) : (uint32_t)std::max<uint64_t>(1, ((uint64_t)b->n + cl - 1) / cl);
+            q = std::max<uint32_t>(1, std::min(q, P));
+            while (q > 1 && (P % q || 256u * q / P > vm->spread_own_rows)) q--;
+            kp.own_q = q;
+            own = vm->spread_own_state > 0 && P % q == 0 && 256u * q / P <= vm->spread_own_rows && 256u * q / P >= 1u &&
                   mimic_jit_step_bound(vm->jit_info_spread_own, kp.max_tail_calls) <= kp.budget;
             spread = own;
         }
@@ -2070,7 +2070,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     uint32_t run_lanes = lanes;
     if (spread) {
         // owned: 256 / P vCPU lanes per block
-        const uint32_t orows = own ? 256u / (kp.per_lane / ji.spread_own_q) : 1u;
+        const uint32_t orows = own ? 256u / (kp.per_lane / kp.own_q) : 1u;
         const uint32_t blocks = own ? (cpu_lanes + orows - 1) / orows
                                     : (uint32_t)(((uint64_t)b->n + spread_ppb() - 1) / spread_ppb());
         run_lanes = blocks * 256u;

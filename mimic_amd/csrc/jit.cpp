@@ -367,10 +367,7 @@ class Gen {
         E.line("#ifdef MIMIC_MEAS_NOPKTST\n#define PKT_ST(p_, n_, v_) ((void)(v_))\n#else\n#define PKT_ST(p_, n_, v_) st_n(p_, n_, v_)\n#endif");
         E.line("#ifdef MIMIC_MEAS_NOATOM\n#define CNT_ADD(p_, n_, v_) ((void)(p_))\n#else\n#define CNT_ADD(p_, n_, v_) atomic_add_n(p_, n_, v_)\n#endif");
         if (spread_on) E.line("#define MIMIC_SPREAD 1");
-        if (spread_own) {
-            E.line("#define MIMIC_SPREAD_OWN 1");
-            E.line("#define SPREAD_OWN_Q %uu      // packets per thread", spread_req->own_q);
-        }
+        if (spread_own) E.line("#define MIMIC_SPREAD_OWN 1");
         if (const char *rc = getenv("MIMIC_SKB_ROOMS_CHAIN"))   // measurement: see engine.cpp skb_prepare
             if (rc[0] == '1') E.line("#define MIMIC_SKB_ROOMS_CHAIN 1");
         E.line("#define MIMIC_CTX_FIXED %u", ctx);
@@ -485,8 +482,9 @@ class Gen {
             // and results).  Fused increments add into the block's LDS table, one row per lane; the
             // block then adds its rows into the map with plain read-modify-writes: no other block
             // touches those vCPUs' rows in this launch.
-            // (SPREAD_OWN_Q > 1: R = 256 Q / P lanes, thread t their packets j, j + P / Q, ... in order)
-            E.line("  const uint32_t oP_ = kp.per_lane, oS_ = oP_ / SPREAD_OWN_Q, oR_ = 256u / oS_;");
+            // Q = KParams::own_q packets per thread: R = 256 Q / P lanes, thread t their packets j,
+            // j + P / Q, ... in order (the engine picks Q so that the launch about fills the chip once)
+            E.line("  const uint32_t oP_ = kp.per_lane, oQ_ = kp.own_q, oS_ = oP_ / oQ_, oR_ = 256u / oS_;");
             E.line("  const uint32_t orow_ = threadIdx.x %% oR_, oj_ = threadIdx.x / oR_, olane_ = blockIdx.x * oR_ + orow_;");
             E.line("  const uint32_t osh_ = olane_ >= kp.sched_shift ? olane_ - kp.sched_shift : olane_ + kp.cpu_lanes - kp.sched_shift;");
             E.line("#define OWN_IDX(jj_) ((oj_ < oS_ && olane_ < kp.cpu_lanes && (kp.sched == SCHED_CHUNKED ? (uint64_t)olane_ * oP_ + (jj_) : (uint64_t)(jj_) * kp.cpu_lanes + osh_) < kp.n) ? (uint32_t)(kp.sched == SCHED_CHUNKED ? (uint64_t)olane_ * oP_ + (jj_) : (uint64_t)(jj_) * kp.cpu_lanes + osh_) : NO_PKT)");
@@ -615,7 +613,7 @@ class Gen {
                 E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
         if (spread_own) {
-            E.line("  for (uint32_t j = 0; j < SPREAD_OWN_Q; j++) {   // the thread's packets of its lane, in order");
+            E.line("  for (uint32_t j = 0; j < oQ_; j++) {   // the thread's packets of its lane, in order");
             E.line("    const uint32_t i = j ? OWN_IDX(oj_ + j * oS_) : oi_;");
             E.line("    if (i == NO_PKT) break;");
         } else if (spread_on) {
@@ -653,7 +651,7 @@ class Gen {
         } else if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
-            else if (spread_own) E.line("    if (j + 1u < SPREAD_OWN_Q) { const uint32_t n_ = OWN_IDX(oj_ + (j + 1u) * oS_); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+            else if (spread_own) E.line("    if (j + 1u < oQ_) { const uint32_t n_ = OWN_IDX(oj_ + (j + 1u) * oS_); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else if (spread_on) E.line("    { const uint32_t n_ = i + 256u; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
@@ -2331,7 +2329,6 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->karg = g.karg != 0;
         info->spread = g.spread_on;
         info->spread_own = g.spread_own;
-        info->spread_own_q = g.spread_own && spread ? spread->own_q : 1u;
         info->spread_map = g.spread_map;
         info->spread_n = g.spread_n;
         info->spread_roww = g.spread_n ? g.spread_row / g.spread_n : 0;

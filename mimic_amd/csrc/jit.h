@@ -21,7 +21,6 @@ struct JitInfo {
     bool skb_fast;       // sk_buff kernel that derives the records of common frames itself (sparse prep)
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
     bool spread_own;     // ... in its owned form: a block runs every packet of its vCPUs (SpreadReq::own)
-    uint32_t spread_own_q;   // owned form: packets per thread (SpreadReq::own_q)
     // spread kernels: the counted per-CPU array, counter width, counters per row, LDS table rows
     uint32_t spread_map, spread_n, spread_roww, spread_rows;
 };
@@ -34,7 +33,6 @@ struct SpreadReq {
     // owned form: block b runs all P = KParams::per_lane packets of vCPU lanes [b * 256 / P, +256 / P)
     // (2 <= P <= 256), its counters into an LDS table it then adds into the rows it alone owns
     bool own = false;
-    uint32_t own_q = 1;   // owned form: packets per thread (each a P / own_q apart), P % own_q == 0
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // ctx_check: the variant for launches given Run(ctx) contexts (KParams::cancel_any)

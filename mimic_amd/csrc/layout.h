@@ -233,6 +233,8 @@ struct KParams {
     const uint32_t *cancel;
     const uint32_t *const *cancel_pp;
     uint32_t cancel_any;
+    // owned spread launches (jit.cpp spread_own): packets per thread, a divisor of per_lane
+    uint32_t own_q;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

@@ -93,7 +93,7 @@ def spread_spec(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict], v
                 shapes[mid] = (mid, m["max_entries"] * m["value_size"], m["value_size"])
     row = max((s[1] for s in shapes.values()), default=0)
     if own:
-        return pc, list(shapes.values()), (min(128, 32768 // row) if row else 0) | (1 << 31)
+        return pc, list(shapes.values()), (min(256, 32768 // row) if row else 0) | (1 << 31)
     rows = min(ppb, vcpus)
     return pc, list(shapes.values()), rows if rows * row <= 32768 else 0
 

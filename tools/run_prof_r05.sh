@@ -9,6 +9,8 @@ T=${T:-r05}
 for c in ${CONFIGS:-classifier classifier_v256 skb parse5 flowtrack flowtrack_insert}; do
   if [ $c = classifier_v256 ]; then
     CFG=classifier NAME=classifier_v256 EXTRA="--vcpus 256" SUMMARY_ARGS="--vcpus 256 --spread" TAG=$T timeout -k 10 600 bash tools/profile.sh || exit 1
+  elif [ $c = classifier ] || [ $c = parse5 ]; then   # the owned spread form (engine spread_own)
+    CFG=$c SUMMARY_ARGS="--vcpus 262144 --own" TAG=$T timeout -k 10 600 bash tools/profile.sh || { echo "profile $c failed"; exit 1; }
   else
     CFG=$c TAG=$T timeout -k 10 600 bash tools/profile.sh || { echo "profile $c failed"; exit 1; }
   fi
