@@ -15,6 +15,13 @@ from mimic_amd import workloads as W
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _table_spread(monkeypatch):
+    """This module tests the table spread kernel: the owned form (test_gpu_spread_own.py), which
+    takes batches of up to 256 packets per vCPU by default, is kept off."""
+    monkeypatch.setenv("MIMIC_SPREAD_OWN", "0")
+
+
 def _sc(p, V):
     return Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
 
