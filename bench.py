@@ -555,7 +555,7 @@ def main(argv=None):
         alg = sum(algorithmic_bytes(batches[b][0].lens, vpg, wl.maps, wl.cfg.get("reads_packet", True))
                   for b in timed) / len(timed)
         achieved = alg / avg_launch_s
-        kernel = "mimic_jit_kernel" if vm.LastExec() in ("jit", "spread") else "mimic_xdp_kernel"
+        kernel = "mimic_jit_kernel" if vm.LastExec() in ("jit", "spread", "spread_own") else "mimic_xdp_kernel"
         src_hash = wl.kernel_src_hash(vpg if vm.LastExec() in ("spread", "spread_own") else 0, vm.LastExec() == "spread_own")
         prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched)
         out = {
