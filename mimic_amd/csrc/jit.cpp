@@ -487,8 +487,13 @@ class Gen {
             E.line("  const uint32_t oP_ = kp.per_lane, oQ_ = kp.own_q, oS_ = oP_ / oQ_, oR_ = 256u / oS_;");
             E.line("  const uint32_t orow_ = threadIdx.x %% oR_, oj_ = threadIdx.x / oR_, olane_ = blockIdx.x * oR_ + orow_;");
             E.line("  const uint32_t osh_ = olane_ >= kp.sched_shift ? olane_ - kp.sched_shift : olane_ + kp.cpu_lanes - kp.sched_shift;");
-            E.line("#define OWN_IDX(jj_) ((oj_ < oS_ && olane_ < kp.cpu_lanes && (kp.sched == SCHED_CHUNKED ? (uint64_t)olane_ * oP_ + (jj_) : (uint64_t)(jj_) * kp.cpu_lanes + osh_) < kp.n) ? (uint32_t)(kp.sched == SCHED_CHUNKED ? (uint64_t)olane_ * oP_ + (jj_) : (uint64_t)(jj_) * kp.cpu_lanes + osh_) : NO_PKT)");
-            E.line("  const uint32_t oi_ = OWN_IDX(oj_);");
+            // the thread's k-th packet.  Interleaved: packet j = oj_ + k (P / Q) of its lane.  Chunked
+            // (a lane's packets are contiguous): the block's 256 Q packets in order, thread t taking
+            // t, t + 256, ... -- consecutive threads on consecutive packets, whose lane is i / P
+            E.line("#define OWN_IDX_I(k_) ((oj_ < oS_ && olane_ < kp.cpu_lanes && (uint64_t)(oj_ + (k_) * oS_) * kp.cpu_lanes + osh_ < kp.n) ? (uint32_t)((uint64_t)(oj_ + (k_) * oS_) * kp.cpu_lanes + osh_) : NO_PKT)");
+            E.line("#define OWN_IDX_C(k_) ((threadIdx.x + 256u * (k_) < oR_ * oP_ && (uint64_t)blockIdx.x * oR_ * oP_ + threadIdx.x + 256u * (k_) < kp.n) ? (uint32_t)((uint64_t)blockIdx.x * oR_ * oP_ + threadIdx.x + 256u * (k_)) : NO_PKT)");
+            E.line("#define OWN_IDX(k_) (kp.sched == SCHED_CHUNKED ? OWN_IDX_C(k_) : OWN_IDX_I(k_))");
+            E.line("  const uint32_t oi_ = OWN_IDX(0u);");
             E.line("  const DMap SM_ = cget(kp.maps, SPREAD_MAP);");
             E.line("  __shared__ spread_t sacc_[SPREAD_ROWS * SPREAD_ROWW];");
             E.line("  for (uint32_t w_ = threadIdx.x; w_ < SPREAD_ROWS * SPREAD_ROWW; w_ += 256u) sacc_[w_] = 0;");
@@ -614,7 +619,7 @@ class Gen {
         }
         if (spread_own) {
             E.line("  for (uint32_t j = 0; j < oQ_; j++) {   // the thread's packets of its lane, in order");
-            E.line("    const uint32_t i = j ? OWN_IDX(oj_ + j * oS_) : oi_;");
+            E.line("    const uint32_t i = j ? OWN_IDX(j) : oi_;");
             E.line("    if (i == NO_PKT) break;");
         } else if (spread_on) {
             E.line("  for (uint32_t j = 0; j < SPREAD_PPB / 256u; j++) {");
@@ -651,7 +656,7 @@ class Gen {
         } else if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
-            else if (spread_own) E.line("    if (j + 1u < oQ_) { const uint32_t n_ = OWN_IDX(oj_ + (j + 1u) * oS_); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+            else if (spread_own) E.line("    if (j + 1u < oQ_) { const uint32_t n_ = OWN_IDX(j + 1u); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else if (spread_on) E.line("    { const uint32_t n_ = i + 256u; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
@@ -660,9 +665,11 @@ class Gen {
         // loaded where used instead of hoisted out of the packet loop into SGPRs
         if (kq_mode == 1) E.line("    const KParams *kqp_ = kpp; asm volatile(\"\" : \"+s\"(kqp_)); const KParams &kq_ = *kqp_;");
         else E.line("    const KParams &kq_ = kp;");
-        if (spread_own) {   // the thread's vCPU and its row of the spread map
-            E.line("    L.cpu = (int32_t)(kp.vcpu_begin + olane_);");
-            E.line("    sbase_ = SM_.backing_addr + (uint32_t)L.cpu * SM_.addr_period;");
+        if (spread_own) {   // the packet's vCPU and its row of the spread map (chunked: per packet)
+            E.line("    { const uint32_t ol_ = kp.sched == SCHED_CHUNKED ? i / oP_ : olane_;");
+            E.line("      srow_ = ol_ - blockIdx.x * oR_;");
+            E.line("      L.cpu = (int32_t)(kp.vcpu_begin + ol_);");
+            E.line("      sbase_ = SM_.backing_addr + (uint32_t)L.cpu * SM_.addr_period; }");
         } else if (spread_on) {   // this packet's vCPU (the schedule's lane for it) and its row of the spread map
             E.line("    { if (kp.sched == SCHED_CHUNKED) lam_ = i / kp.per_lane;");
             E.line("      else if (j) { lam_ += lstep_; if (lam_ >= kp.cpu_lanes) lam_ -= kp.cpu_lanes; }");
