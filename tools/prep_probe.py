@@ -1,6 +1,7 @@
 """Time mimic_skb_prep_kernel variants in isolation (tools/prep_probe.sh builds them from skb.hip with
 -D knobs): 1M IMIX sk_buff packets as the cfg-5 bench makes them, 20 launches between events."""
 import ctypes as C
+import os
 import sys
 
 import torch
@@ -8,7 +9,8 @@ import torch
 sys.path.insert(0, ".")
 from mimic_amd import workloads as W
 
-buf, off, lens = W.make_skb_packets(1 << 20, (64, 576, 1500), (7, 4, 1))
+# PREP_VARIETY: the fraction of header variants (the cfg-5 bench uses 0.05)
+buf, off, lens = W.make_skb_packets(1 << 20, (64, 576, 1500), (7, 4, 1), variety=float(os.environ.get("PREP_VARIETY", "0")))
 n = len(lens)
 dev = torch.device("cuda:0")
 d_buf = torch.from_numpy(buf).to(dev)
