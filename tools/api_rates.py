@@ -65,6 +65,36 @@ def main():
     out["process_run_xdp"] = {"us_per_call": round(dt / args.calls * 1e6, 1), "calls": args.calls,
                               "what": "NewProcess + SetCPUID + Run + Cleanup, classifier, 64 B"}
 
+    # ---- the same four calls straight through the C ABI (what a cgo binding calls; the Python
+    # mirror's Run also reads the packet back and fills its register fields) ----------------------
+    import ctypes as C
+    from mimic_amd import _lib as L
+    pr0 = vm.NewProcess(pids[0], M.LinuxContextXDP(Packet=pk[0]))
+    pr0._ensure_native()
+    prog_id, c0 = pr0.prog_id, pr0.Context
+    pr0.Cleanup()
+    lib, hv, regs = vm.lib, vm.h, L.ProcessRegs()
+
+    def one_cabi(k):
+        h = C.c_void_p()
+        if lib.mimic_process_new(hv, prog_id, pk[k], len(pk[k]), c0.Headroom, c0.Tailroom, c0.IngessIfIndex,
+                                 c0.RxQueueIndex, c0.EgressIfIndex, C.byref(h)) != 0:
+            raise RuntimeError("mimic_process_new")
+        if lib.mimic_process_set_cpu(h, k % V) != 0 or lib.mimic_process_run(h, 0, C.byref(regs)) != 0:
+            raise RuntimeError("mimic_process_set_cpu / _run")
+        r0 = int(regs.r[0])
+        lib.mimic_process_free(h)
+        return r0
+
+    for k in range(20):
+        assert one_cabi(k) == one_xdp(k)
+    t0 = time.perf_counter()
+    for k in range(args.calls):
+        one_cabi(k)
+    dt = time.perf_counter() - t0
+    out["process_run_xdp_cabi"] = {"us_per_call": round(dt / args.calls * 1e6, 1), "calls": args.calls,
+                                   "what": "mimic_process_new + _set_cpu + _run + _free through ctypes, classifier, 64 B"}
+
     # ---- ProcessPool, xdp_md jobs ------------------------------------------------------------------
     n = args.xdp_jobs
     bufx, offx, lensx = W.make_packets(n, seed=5)
