@@ -17,8 +17,10 @@
  * the reference returns gracefully as a syscall.Errno (E2BIG = 7).
  * Host pointers are host memory unless a field says DEVICE.  The engine owns all device
  * memory it allocates; the caller owns batch/result buffers.  One mimic_vm is one HIP
- * device + one command stream; calls on one vm must be serialised by the caller
- * (like the reference's single Process), distinct vms may run concurrently.
+ * device + one command stream.  Batch and map calls on one vm must be serialised by the
+ * caller; the mimic_process_* calls may come from several threads at once (processPool's
+ * workers and Handoff goroutines, vm.go:548-573, clean up while others create and run
+ * processes): the engine serialises them per vm.  Distinct vms may run concurrently.
  */
 #ifndef MIMIC_AMD_H
 #define MIMIC_AMD_H
@@ -32,7 +34,8 @@
 extern "C" {
 #endif
 
-#define MIMIC_ABI_VERSION 3  /* 2: mimic_skb_batch.custom, statuses 29-30, MIMIC_EXEC_SPREAD; 3: MIMIC_EXEC_SPREAD_OWN */
+#define MIMIC_ABI_VERSION 4  /* 2: mimic_skb_batch.custom, statuses 29-30, MIMIC_EXEC_SPREAD; 3: MIMIC_EXEC_SPREAD_OWN;
+                                4: status 31, thread-safe process calls, mimic_run_xdp_many */
 
 /* errors */
 #define MIMIC_EINVAL (-1)
@@ -76,7 +79,8 @@ enum mimic_status {
     MIMIC_PANIC_SLICE = 27,          /* Go slice-bounds panic in those accessors */
     MIMIC_ERR_CTX_LOAD = 28,         /* Context.Load failed (SKBuffFromBytes error, out of address space) */
     MIMIC_ERR_CANCELED = 29,         /* Run's ctx was canceled: ctx.Err() = context.Canceled (vm.go:344-350) */
-    MIMIC_ERR_DEADLINE = 30          /* Run's ctx deadline passed: context.DeadlineExceeded (vm.go:344-350) */
+    MIMIC_ERR_DEADLINE = 30,         /* Run's ctx deadline passed: context.DeadlineExceeded (vm.go:344-350) */
+    MIMIC_ERR_ENGINE_STATE = 31      /* engine assertion: a stepping launch found another process's state (never expected) */
 };
 
 /* Linux map types (ebpf.MapType). */
@@ -404,9 +408,9 @@ int mimic_exec_mode(const mimic_vm *vm);
  * counters are sums; each packet's R0 / status / steps depend on its own bytes only).
  * mode -1: default (env MIMIC_SPREAD, else when a batch has >= 8 packets per vCPU), 0: never,
  * 1: whenever the programs allow it.  The owned form (MIMIC_EXEC_SPREAD_OWN: a workgroup runs every
- * packet of its vCPUs and adds into rows only it touches) takes batches of 2..16 packets per vCPU
- * with fewer vCPUs than the lanes the one-lane kernel holds resident (env MIMIC_SPREAD_OWN=1: 2..256
- * packets whatever V, =0: never).  Every generic load / store of such a program set must go
+ * packet of its vCPUs and adds into rows only it touches) takes, by default, every batch of 2..256
+ * packets per vCPU, whatever V, when the counted map's rows fit its LDS table of min(256, 32 KiB / row)
+ * rows (env MIMIC_SPREAD_OWN=0: never).  Every generic load / store of such a program set must go
  * through a base the analysis can place (derived from R1, R10 or a packet pointer), else the set runs
  * one lane per vCPU.  (mimic_sync / mimic_last_steps would fail if a spread launch still reached
  * per-CPU memory outside a fused increment: an internal assertion.) */
@@ -433,7 +437,7 @@ long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint
 /* The spread kernel's source (mimic_set_spread): pc = (program, slot, map id) triples of the
  * LD_IMM64 slots naming a per-CPU array's object, shapes = (map id, E * S, S) triples, lds_rows =
  * rows of a block's LDS counter table (min(1024, V) when rows * E * S <= 32 KiB, else 0); bit 31 of
- * lds_rows set: the owned form's source (its rows: min(128, 32 KiB / (E * S))).
+ * lds_rows set: the owned form's source (its rows: min(256, 32 KiB / (E * S))).
  * *spread_out = 1 when the programs allow a spread kernel. */
 long mimic_jit_source_spread(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, const uint32_t *pc,
                              uint32_t n_pc, const uint32_t *shapes, uint32_t n_shapes, uint32_t lds_rows,

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MIMIC_LIB=<file name>: another in-tree build of the same sources (measurement builds, A/B runs)
 LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("MIMIC_LIB", "libmimic_amd.so")))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # status codes (enum mimic_status)
 STATUS_NAMES = [
@@ -22,7 +22,7 @@ STATUS_NAMES = [
     "ERR_HELPER_UNIMPLEMENTED", "ERR_HELPER_CANT_EMULATE", "ERR_LDABS", "PANIC_DIV0",
     "PANIC_SHIFT", "PANIC_BADREG", "PANIC_CALLX", "PANIC_PC", "PANIC_HELPER_NEG",
     "ERR_STEP_LIMIT", "ERR_CALL_DEPTH", "ERR_ENGINE_HELPER", "ERR_NO_CPU", "ERR_CTX_ACCESS", "PANIC_SLICE",
-    "ERR_CTX_LOAD", "ERR_CANCELED", "ERR_DEADLINE",
+    "ERR_CTX_LOAD", "ERR_CANCELED", "ERR_DEADLINE", "ERR_ENGINE_STATE",
 ]
 STATUS = {n: i for i, n in enumerate(STATUS_NAMES)}
 ECANCELED, EDEADLINE = -7, -8   # mimic_process_run_ctx: ctx.Err() (include/mimic_amd.h)

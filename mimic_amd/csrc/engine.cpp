@@ -12,10 +12,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <chrono>
 #include <condition_variable>
@@ -26,6 +28,7 @@
 #include <vector>
 
 #include "../../include/mimic_amd.h"
+#include "blkcache.h"
 #include "layout.h"
 #include "hashmap.h"
 #include "jit.h"
@@ -103,6 +106,22 @@ struct HostProg {
     std::string name;
     std::vector<DInsn> ins;
     uint32_t addr;
+};
+
+// the completion marker of a released process block's last use on the VM's stream (one event may
+// cover many blocks: mimic_process_free_many records one for the whole call)
+struct HipFence : BlkFence {
+    hipEvent_t ev = nullptr;
+    hipStream_t st = nullptr;
+    void wait() override {
+        if (hipEventSynchronize(ev) != hipSuccess) {
+            (void)hipGetLastError();
+            hipStreamSynchronize(st);
+        }
+    }
+    ~HipFence() override {
+        if (ev) hipEventDestroy(ev);
+    }
 };
 
 }  // namespace
@@ -215,10 +234,18 @@ struct mimic_vm {
     // of the processes of one launch (one allocation, grown as needed)
     uint8_t *d_many = nullptr;
     size_t many_cap = 0;
-    // single processes' device blocks (proc_alloc): freed blocks are kept per power-of-two size and
-    // handed to the next NewProcess, so a process costs no hipMalloc / hipFree once the VM is warm
-    std::map<size_t, std::vector<uint8_t *>> blk_free;
-    size_t blk_cached = 0;
+    // single processes' memory blocks (proc_alloc): freed blocks are kept per power-of-two size and
+    // handed to the next NewProcess, so a process costs no hipMalloc / hipFree once the VM is warm.
+    // A block goes back with the fence of its last use on `stream` (null when that use is known to
+    // be complete) and is handed out again only once the fence has passed; Cleanup may run on any
+    // thread (ProcessPool's Handoff, __del__, a Go finaliser ...).
+    // (blkcache.h has the rules; at most 256 MiB of free blocks are kept)
+    BlkCache blk{256ull << 20};
+    // process operations that enqueue work on `stream` (NewProcess, Run / Step, run_many, Packet)
+    // hold run_mu and number their enqueues on seq (blkcache.h SeqClock)
+    std::recursive_mutex run_mu;
+    SeqClock seq;
+    uint32_t proc_gen = 0;   // NewProcess counter: StepState::gen of each process
     bool skb_leaked = false;   // sock / flow-keys / packet entries of earlier sk_buff processes exist
     hipStream_t skb_stream = nullptr;
     bool skb_release_pending = false;   // mimic_skb_release ran: skb_ev marks the end of the released batches
@@ -681,8 +708,10 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (!vm) return;
     hipSetDevice(vm->s.device);
     if (vm->stream) hipStreamSynchronize(vm->stream);
-    for (auto &c : vm->blk_free)
-        for (uint8_t *b : c.second) hipFree(b);
+    vm->blk.drain([](Blk &b) {
+        hipFree(b.dev);
+        if (b.host) hipHostFree(b.host);
+    });
     hipFree(vm->arena);
     hipFree(vm->d_insns);
     hipFree(vm->d_progs);
@@ -1519,6 +1548,7 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
     SkbRec *skb_rec = nullptr;
     const uint64_t *skb_prefix = nullptr, *skb_base = nullptr;
     const mimic_skb_custom *skb_custom = nullptr;   // its user-given sock / flow keys (device, one entry) or null
+    uint32_t gen = 0;   // the generation its state carries (StepState::gen)
 };
 
 struct CtxRun {      // Run(ctx) of a batch: one context for every packet, or one per packet (host array)
@@ -1731,7 +1761,7 @@ static uint32_t chip_lanes(mimic_vm *vm) {
 }
 
 // The owned form (jit.cpp, SpreadReq::own): built once per program set when the programs allow a
-// spread kernel; its LDS table holds up to 128 rows of the counted map's row (32 KiB at most), so a
+// spread kernel; its LDS table holds up to 256 rows of the counted map's row (32 KiB at most), so a
 // batch with P packets per vCPU can use it when 256 / P rows fit.
 static int spread_build_own(mimic_vm *vm) {
     if (vm->spread_own_state) return 0;
@@ -1881,6 +1911,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.priv_key_q = key_q;
     kp.budget = step ? step->budget : (b->step_budget ? b->step_budget : MIMIC_DEFAULT_BUDGET);
     kp.step = step ? step->state : nullptr;
+    kp.step_gen = step ? step->gen : 0u;
     kp.n = b->n;
     kp.sched = b->schedule;
     kp.pkt_data = b->pkt_data;
@@ -2194,6 +2225,9 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         // the interpreter finishes what the kernel deferred (a wave without a deferred lane returns at once)
         if (ji.defer && mimic_launch_xdp_resume(&kp, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+    } else if (step) {   // the stepping kernel takes its parameters by value: no slot, no copy
+        if (mimic_launch_xdp(&kp, nullptr, st))
+            return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
     } else {  // launch parameters are read from a device copy
         const KParams *dkp = nullptr;
         const int slot = kp_slot(vm, kp, st, &dkp);
@@ -2245,23 +2279,36 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
 
 }  // extern "C"
 
+// A single process's memory (NewProcess, vm.go:198-235).  Its device block holds
+//   descriptor (pkt_off = 0, pkt_len) | sk_buff memory @PD_SKB: SkbRec | prefix (2 words) | base |
+//   mimic_skb_custom | packet memory @PD_PKT (headroom + len + tailroom)
+// and the pinned, device-mapped host half of the same block holds
+//   StepState @0 | one-packet results @PH_RES: r0 | status | steps | err_pc | a read-back word |
+//   the device block's upload image @PH_IMG.
+// The stepping kernel reads and writes the StepState and the results in place, so a Run / Step is
+// one launch and one host sync, and NewProcess is one asynchronous copy of the image (no sync).
+namespace {
+constexpr size_t PD_LEN = 8, PD_SKB = 64;
+constexpr size_t PD_PKT = (PD_SKB + sizeof(SkbRec) + 24 + sizeof(mimic_skb_custom) + 63) & ~(size_t)63;
+constexpr size_t PH_RES = (sizeof(StepState) + 63) & ~(size_t)63;
+constexpr size_t PH_R0 = PH_RES, PH_ST = PH_RES + 8, PH_STEPS = PH_RES + 16, PH_EPC = PH_RES + 20, PH_WORD = PH_RES + 24;
+constexpr size_t PH_IMG = PH_RES + 64;
+}  // namespace
+
 struct mimic_process {
     mimic_vm *vm = nullptr;
     uint32_t prog = 0;
     uint32_t H = 0, T = 0, len = 0;
     int32_t ingress = 0, rxq = 0, egress = 0;
-    uint8_t *d_pkt = nullptr;         // packet memory H + len + T
-    uint64_t *d_off = nullptr;        // descriptor of the one-packet batch
-    uint32_t *d_len = nullptr;
-    uint64_t *d_r0 = nullptr;
-    uint8_t *d_st = nullptr;
-    uint32_t *d_steps = nullptr;
-    int32_t *d_epc = nullptr;
-    StepState *d_state = nullptr;
-    uint8_t *d_priv = nullptr;
+    uint8_t *d_pkt = nullptr;         // packet memory H + len + T (device)
+    uint8_t *d_skbmem = nullptr;      // SkbRec | prefix (2 words) | base | mimic_skb_custom (device)
+    StepState *hs = nullptr;          // the state in the pinned host half ...
+    StepState *hs_dev = nullptr;      // ... and its device-visible address
+    uint8_t *hres = nullptr, *hres_dev = nullptr;   // the one-packet results, likewise
     uint64_t priv_bytes = 0;
     StepState h;                      // host copy after the last launch
     int32_t cpu = -1;
+    uint32_t gen = 0;                 // NewProcess number: the StepState generation its launches expect
     uint32_t static_next = 0;         // the VM's static layout the saved state's addresses assume
     uint8_t *arena = nullptr;
     // LinuxContextSKBuff processes (context_sk_buff.go): the record, leak prefix (0) and leak base
@@ -2269,44 +2316,69 @@ struct mimic_process {
     bool skb = false;
     bool skb_custom = false;          // a user-given sock / flow keys after the base word
     uint32_t ifindex = 0;
-    uint8_t *d_skbmem = nullptr;      // SkbRec | prefix (2 words) | base | mimic_skb_custom
-    // every buffer above but d_priv is carved from one block (proc_alloc); d_priv is a block of its own
-    uint8_t *blk = nullptr;
-    size_t blk_size = 0, priv_size = 0;
+    Blk mem;                          // the block above
+    Blk priv;                         // private memory (stack, frames, ...): device only
+    uint64_t last_seq = 0;            // vm->seq number of the last work enqueued that touches mem / priv
 };
 
-// device blocks of single processes, from the VM's cache (one hipMalloc per size class ever)
-static size_t blk_class(size_t n) {
-    size_t c = 1024;
-    while (c < n) c <<= 1;
-    return c;
-}
-static uint8_t *proc_alloc(mimic_vm *vm, size_t n, size_t *cls) {
-    const size_t c = blk_class(n);
-    *cls = c;
-    auto it = vm->blk_free.find(c);
-    if (it != vm->blk_free.end() && !it->second.empty()) {
-        uint8_t *b = it->second.back();
-        it->second.pop_back();
-        vm->blk_cached -= c;
-        return b;
+// blocks of single processes, from the VM's cache (one hipMalloc / hipHostMalloc per size class ever)
+static bool proc_alloc(mimic_vm *vm, size_t n, bool host, Blk *out) {
+    if (vm->blk.take(n, host, out)) return true;
+    out->cls = BlkCache::size_class(n);
+    if (hipMalloc(&out->dev, out->cls) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = Blk{};
+        return false;
     }
-    uint8_t *b = nullptr;
-    return hipMalloc(&b, c) == hipSuccess ? b : nullptr;
-}
-static void proc_free(mimic_vm *vm, uint8_t *b, size_t cls) {
-    if (!b) return;
-    if (vm->blk_cached + cls > (256ull << 20)) {   // keep at most 256 MiB of free blocks
-        hipFree(b);
-        return;
+    if (host) {
+        void *h = nullptr, *d = nullptr;
+        if (hipHostMalloc(&h, out->cls, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            hipFree(out->dev);
+            *out = Blk{};
+            return false;
+        }
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            d = h;
+        }
+        out->host = (uint8_t *)h;
+        out->hdev = (uint8_t *)d;
     }
-    vm->blk_free[cls].push_back(b);
-    vm->blk_cached += cls;
+    return true;
 }
-static void process_release(mimic_process *p) {
-    proc_free(p->vm, p->blk, p->blk_size);
-    proc_free(p->vm, p->d_priv, p->priv_size);
-    p->blk = p->d_priv = nullptr;
+// run_mu held: work touching p's memory was just enqueued on vm->stream
+static void proc_enq(mimic_process *p) { p->last_seq = p->vm->seq.next(); }
+// run_mu held: the host sync of a process operation
+static hipError_t proc_sync(mimic_vm *vm) {
+    const uint64_t upto = vm->seq.issued();
+    const hipError_t e = hipStreamSynchronize(vm->stream);
+    if (e == hipSuccess) vm->seq.complete(upto);
+    return e;
+}
+// the fence a block released now must carry: null when its last enqueue `seq` is known complete,
+// else an event behind everything enqueued on vm->stream so far
+static std::shared_ptr<BlkFence> proc_fence(mimic_vm *vm, uint64_t seq) {
+    if (vm->seq.idle(seq)) return nullptr;
+    auto f = std::make_shared<HipFence>();
+    f->st = vm->stream;
+    if (hipEventCreateWithFlags(&f->ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(f->ev, vm->stream) == hipSuccess)
+        return f;
+    (void)hipGetLastError();
+    hipStreamSynchronize(vm->stream);   // no event: wait for the stream instead
+    return nullptr;
+}
+static void proc_release_blk(mimic_vm *vm, Blk &b, const std::shared_ptr<BlkFence> &fence) {
+    if (b.dev && !vm->blk.give(b, fence)) {   // the cache is full
+        if (fence) fence->wait();
+        hipFree(b.dev);
+        if (b.host) hipHostFree(b.host);
+    }
+    b = Blk{};
+}
+static void process_release(mimic_process *p, const std::shared_ptr<BlkFence> &fence) {
+    proc_release_blk(p->vm, p->mem, fence);
+    proc_release_blk(p->vm, p->priv, fence);
 }
 
 static void process_regs(const mimic_process *p, mimic_process_regs *out) {
@@ -2320,9 +2392,13 @@ static void process_regs(const mimic_process *p, mimic_process_regs *out) {
     out->exited = p->h.finished;
 }
 
-// one launch: run the process until `budget` total steps (or exit / error), then sync its state
+// one launch: run the process until `budget` total steps (or exit / error), then one host sync.
+// The kernel restores the state from the pinned host half and saves it there (interp.hip MODE_STEP);
+// nothing else of the process is in flight then (every operation on it ends with a sync, and its
+// NewProcess upload precedes this launch on the same stream).
 static int process_advance(mimic_process *p, uint64_t budget) {
     mimic_vm *vm = p->vm;
+    std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
     hipSetDevice(vm->s.device);
     // the VM may have grown (maps / programs) since the process was made: its private plan too
     const PrivPlan pp = priv_plan(vm);
@@ -2336,31 +2412,33 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     p->static_next = vm->next_addr;
     p->arena = vm->arena;
     if ((uint64_t)pp.q_per_lane * 8 > p->priv_bytes) {
-        proc_free(vm, p->d_priv, p->priv_size);
+        proc_release_blk(vm, p->priv, proc_fence(vm, p->last_seq));
         p->priv_bytes = (uint64_t)pp.q_per_lane * 8;
-        p->d_priv = proc_alloc(vm, p->priv_bytes, &p->priv_size);
-        if (!p->d_priv) return fail(vm, MIMIC_ENOMEM, "process private memory");
+        if (!proc_alloc(vm, p->priv_bytes, false, &p->priv)) return fail(vm, MIMIC_ENOMEM, "process private memory");
     }
-    StepState st = p->h;
-    st.cpu = p->cpu;
-    HIP_OK(vm, hipMemcpy(p->d_state, &st, sizeof st, hipMemcpyHostToDevice));
+    StepState *S = p->hs;
+    *S = p->h;
+    S->cpu = p->cpu;
+    S->gen = p->gen;
+    p->hres[PH_ST - PH_RES] = 0xff;
     mimic_xdp_batch b{};
     b.n = 1;
     b.schedule = MIMIC_SCHED_CHUNKED;
     b.pkt_data = p->d_pkt;
-    b.pkt_off = p->d_off;
-    b.pkt_len = p->d_len;
+    b.pkt_off = (const uint64_t *)p->mem.dev;
+    b.pkt_len = (const uint32_t *)(p->mem.dev + PD_LEN);
     b.headroom_all = p->H;
     b.tailroom_all = p->T;
     b.ingress_all = p->ingress;
     b.rxq_all = p->rxq;
     b.egress_all = p->egress;
     mimic_xdp_results r{};
-    r.r0 = p->d_r0;
-    r.status = p->d_st;
-    r.steps = p->d_steps;
-    r.err_pc = p->d_epc;
-    StepRun sr{p->d_state, p->d_priv, p->priv_bytes, budget};
+    r.r0 = (uint64_t *)(p->hres_dev + (PH_R0 - PH_RES));
+    r.status = p->hres_dev + (PH_ST - PH_RES);
+    r.steps = (uint32_t *)(p->hres_dev + (PH_STEPS - PH_RES));
+    r.err_pc = (int32_t *)(p->hres_dev + (PH_EPC - PH_RES));
+    StepRun sr{p->hs_dev, p->priv.dev, p->priv_bytes, budget};
+    sr.gen = p->gen;
     SkbRun skr{p->ifindex};
     if (p->skb) {
         sr.skb_rec = (SkbRec *)p->d_skbmem;
@@ -2368,33 +2446,27 @@ static int process_advance(mimic_process *p, uint64_t budget) {
         sr.skb_base = (const uint64_t *)(p->d_skbmem + sizeof(SkbRec) + 16);
         if (p->skb_custom) sr.skb_custom = (const mimic_skb_custom *)(p->d_skbmem + sizeof(SkbRec) + 24);
     }
-    int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, p->skb ? &skr : nullptr, &sr);
+    const int rc = run_xdp_impl(vm, p->prog, &b, &r, vm->stream, 0, p->skb ? &skr : nullptr, &sr);
+    proc_enq(p);
+    const hipError_t e = proc_sync(vm);   // the one host sync of Run / Step
     if (rc) return rc;
-    HIP_OK(vm, hipMemcpyAsync(&p->h, p->d_state, sizeof p->h, hipMemcpyDeviceToHost, vm->stream));
-    HIP_OK(vm, hipStreamSynchronize(vm->stream));
+    if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
+    if (p->hres[PH_ST - PH_RES] == MIMIC_ERR_ENGINE_STATE || S->gen != p->gen)
+        return fail(vm, MIMIC_EDEVICE, "process: the stepping launch found another process's state (engine assertion)");
+    p->h = *S;
     return 0;
 }
 
 extern "C" {
 
+// NewProcess: the process's block, its upload image written in the pinned half and copied to the
+// device with one asynchronous copy on vm->stream (run_mu held)
 static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
                         uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
-                        mimic_process **out);
-
-int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
-                      uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
-                      mimic_process **out) {
-    if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
-    if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
-    if (vm->skb_leaked) return fail(vm, MIMIC_ENOTSUP, "xdp_md processes after sk_buff batches are not supported");
-    return process_make(vm, prog_id, packet, len, headroom, tailroom, ingress_ifindex, rx_queue_index, egress_ifindex,
-                        out);
-}
-
-static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
-                        uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
-                        mimic_process **out) {
+                        const mimic_skb_custom *custom, mimic_process **out) {
     hipSetDevice(vm->s.device);
+    const uint64_t M = (uint64_t)headroom + len + tailroom;
+    const size_t total = PD_PKT + (size_t)std::max<uint64_t>(M, 1);
     mimic_process *p = new mimic_process();
     p->vm = vm;
     p->prog = prog_id;
@@ -2404,39 +2476,48 @@ static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint
     p->ingress = ingress_ifindex;
     p->rxq = rx_queue_index;
     p->egress = egress_ifindex;
-    memset(&p->h, 0, sizeof p->h);
-    const uint64_t M = (uint64_t)headroom + len + tailroom;
-    // one block: StepState | r0 | status | steps | err_pc | off | len | sk_buff memory | packet memory,
-    // its head and the packet memory written by one copy
-    const size_t o_state = 0, o_r0 = (sizeof(StepState) + 63) & ~(size_t)63, o_st = o_r0 + 8, o_steps = o_r0 + 16,
-                 o_epc = o_r0 + 20, o_off = o_r0 + 24, o_len = o_r0 + 32, o_skb = (o_len + 4 + 63) & ~(size_t)63,
-                 o_pkt = (o_skb + sizeof(SkbRec) + 24 + sizeof(mimic_skb_custom) + 63) & ~(size_t)63, total = o_pkt + std::max<uint64_t>(M, 1);
-    p->blk = proc_alloc(vm, total, &p->blk_size);
-    if (!p->blk) {
+    if (!proc_alloc(vm, PH_IMG + total, true, &p->mem)) {
         delete p;
         return fail(vm, MIMIC_ENOMEM, "process memory");
     }
-    uint8_t *b = p->blk;
-    p->d_state = (StepState *)(b + o_state);
-    p->d_r0 = (uint64_t *)(b + o_r0);
-    p->d_st = b + o_st;
-    p->d_steps = (uint32_t *)(b + o_steps);
-    p->d_epc = (int32_t *)(b + o_epc);
-    p->d_off = (uint64_t *)(b + o_off);
-    p->d_len = (uint32_t *)(b + o_len);
-    p->d_skbmem = b + o_skb;
-    p->d_pkt = b + o_pkt;
-    std::vector<uint8_t> img(total, 0);   // descriptor (off 0, len) and the packet memory, rooms zero
-    memcpy(img.data() + o_len, &len, 4);
-    if (len) memcpy(img.data() + o_pkt + headroom, packet, len);
-    const hipError_t e = hipMemcpy(b + o_off, img.data() + o_off, total - o_off, hipMemcpyHostToDevice);
+    p->gen = ++vm->proc_gen;
+    memset(&p->h, 0, sizeof p->h);
+    p->h.gen = p->gen;
+    uint8_t *hb = p->mem.host, *db = p->mem.dev;
+    p->hs = (StepState *)hb;
+    p->hs_dev = (StepState *)p->mem.hdev;
+    p->hres = hb + PH_RES;
+    p->hres_dev = p->mem.hdev + PH_RES;
+    p->d_skbmem = db + PD_SKB;
+    p->d_pkt = db + PD_PKT;
+    // the image: descriptor (off 0, len), zeroed sk_buff memory and rooms, the packet at +headroom,
+    // a user-given sock / flow keys after the record's base word
+    uint8_t *img = hb + PH_IMG;
+    memset(img, 0, PD_PKT + headroom);
+    memcpy(img + PD_LEN, &len, 4);
+    if (custom) memcpy(img + PD_SKB + sizeof(SkbRec) + 24, custom, sizeof *custom);
+    if (len) memcpy(img + PD_PKT + headroom, packet, len);
+    memset(img + PD_PKT + headroom + len, 0, total - (PD_PKT + headroom + len));
+    const hipError_t e = hipMemcpyAsync(db, img, total, hipMemcpyHostToDevice, vm->stream);
+    proc_enq(p);
     if (e != hipSuccess) {
-        process_release(p);
+        process_release(p, proc_fence(vm, p->last_seq));
         delete p;
         return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
     }
     *out = p;
     return 0;
+}
+
+int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
+                      uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
+                      mimic_process **out) {
+    if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
+    if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
+    if (vm->skb_leaked) return fail(vm, MIMIC_ENOTSUP, "xdp_md processes after sk_buff batches are not supported");
+    return process_make(vm, prog_id, packet, len, headroom, tailroom, ingress_ifindex, rx_queue_index, egress_ifindex,
+                        nullptr, out);
 }
 
 int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
@@ -2447,42 +2528,42 @@ int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, ui
 int mimic_process_new_skb_ctx(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
                               const mimic_skb_custom *custom, mimic_process **out) {
     if (!vm || !out || (len && !packet)) return MIMIC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     // the packet memory is SKB_HEADROOM + len + SKB_TAILROOM with the frame at +SKB_HEADROOM
     // (context_sk_buff.go:42-107), run by the interpreter's stepping kernel as a one-packet batch
-    int rc = process_make(vm, prog_id, packet, len, SKB_HEADROOM, SKB_TAILROOM, 0, 0, 0, out);
+    const bool cust = custom && custom->flags;
+    int rc = process_make(vm, prog_id, packet, len, SKB_HEADROOM, SKB_TAILROOM, 0, 0, 0, cust ? custom : nullptr, out);
     if (rc) return rc;
     mimic_process *p = *out;
     p->skb = true;
     p->ifindex = ifindex;
-    p->len = len;
-    p->T = SKB_TAILROOM;
-    hipError_t e = hipSuccess;   // (process_make placed the packet at +headroom and wrote len)
-    p->skb_custom = custom && custom->flags;
-    if (e == hipSuccess && p->skb_custom)
-        e = hipMemcpy(p->d_skbmem + sizeof(SkbRec) + 24, custom, sizeof(mimic_skb_custom), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
+    p->skb_custom = cust;
+    auto drop = [&](int code, const char *what) {
         mimic_process_free(p);
         *out = nullptr;
-        return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
-    }
+        return code == MIMIC_EDEVICE && what ? fail(vm, code, "process: %s", what) : code;
+    };
     // LinuxContextSKBuff.Load now, as NewProcess does in the reference: the record and the leak
     // addresses (the VM's leak cursor moves past this process's sock / flow keys / packet)
-    if ((rc = upload_tables(vm))) return rc;
+    if ((rc = upload_tables(vm))) return drop(rc, nullptr);
     mimic_xdp_batch b{};
     b.n = 1;
     b.pkt_data = p->d_pkt;
-    b.pkt_off = p->d_off;
-    b.pkt_len = p->d_len;
+    b.pkt_off = (const uint64_t *)p->mem.dev;
+    b.pkt_len = (const uint32_t *)(p->mem.dev + PD_LEN);
     // d_skbmem: the record | its 2 prefix words | the batch base
     const SkbInto into{(SkbRec *)p->d_skbmem, (uint64_t *)(p->d_skbmem + sizeof(SkbRec))};
-    if ((rc = skb_prepare(vm, &b, vm->stream, &into))) return rc;
-    HIP_OK(vm, hipMemcpyAsync(p->d_skbmem + sizeof(SkbRec) + 16, vm->d_skb_state + 1, 8, hipMemcpyDeviceToDevice,
-                              vm->stream));
-    uint32_t lw = 0;
-    HIP_OK(vm, hipMemcpyAsync(&lw, p->d_skbmem, 4, hipMemcpyDeviceToHost, vm->stream));   // SkbRec.len
-    HIP_OK(vm, hipStreamSynchronize(vm->stream));
-    if (lw & SKB_LOAD_FAILED) {   // NewProcess returns the context's Load error (vm.go:226-229); nothing leaked
+    if ((rc = skb_prepare(vm, &b, vm->stream, &into))) return drop(rc, nullptr);
+    hipError_t e = hipMemcpyAsync(p->d_skbmem + sizeof(SkbRec) + 16, vm->d_skb_state + 1, 8, hipMemcpyDeviceToDevice,
+                                  vm->stream);
+    uint32_t *lw = (uint32_t *)(p->hres + (PH_WORD - PH_RES));   // SkbRec.len, read back into the pinned half
+    if (e == hipSuccess) e = hipMemcpyAsync(lw, p->d_skbmem, 4, hipMemcpyDeviceToHost, vm->stream);
+    proc_enq(p);
+    const hipError_t es = proc_sync(vm);
+    if (e == hipSuccess) e = es;
+    if (e != hipSuccess) return drop(MIMIC_EDEVICE, hipGetErrorString(e));
+    if (*lw & SKB_LOAD_FAILED) {   // NewProcess returns the context's Load error (vm.go:226-229); nothing leaked
         mimic_process_free(p);
         *out = nullptr;
         return fail(vm, MIMIC_EINVAL, "load context: the sk_buff context did not decode (ERR_CTX_LOAD)");
@@ -2619,16 +2700,15 @@ int mimic_process_run_many(mimic_process *const *ps, uint32_t n, const int32_t *
     if (!ps || !n) return n ? MIMIC_EINVAL : 0;
     mimic_vm *vm = ps[0] ? ps[0]->vm : nullptr;
     if (!vm) return MIMIC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
     const uint32_t prog = ps[0]->prog, ifindex = ps[0]->ifindex;
     uint8_t *lo = nullptr;
     bool any_cust = false;
+    // every process is checked before any is changed (a refused call leaves them as they were)
     for (uint32_t i = 0; i < n; i++) {
         mimic_process *p = ps[i];
         if (!p || p->vm != vm) return fail(vm, MIMIC_EINVAL, "process %u: not a process of this VM", i);
-        if (cpus) {   // SetCPUID (vm.go:268-283) of each process first
-            if (cpus[i] < 0 || cpus[i] > vm->s.vcpus) return fail(vm, MIMIC_EINVAL, "process %u: not a valid CPU ID", i);
-            p->cpu = cpus[i];
-        }
+        if (cpus && (cpus[i] < 0 || cpus[i] > vm->s.vcpus)) return fail(vm, MIMIC_EINVAL, "process %u: not a valid CPU ID", i);
         if (!p->skb) return fail(vm, MIMIC_ENOTSUP, "process %u: not an sk_buff process", i);
         if (p->prog != prog || p->ifindex != ifindex)
             return fail(vm, MIMIC_EINVAL, "process %u: one program and one interface per launch", i);
@@ -2636,8 +2716,12 @@ int mimic_process_run_many(mimic_process *const *ps, uint32_t n, const int32_t *
         if (!lo || p->d_pkt < lo) lo = p->d_pkt;
         any_cust |= p->skb_custom;
     }
+    if (cpus)   // SetCPUID (vm.go:268-283) of each process first
+        for (uint32_t i = 0; i < n; i++) ps[i]->cpu = cpus[i];
     hipSetDevice(vm->s.device);
     hipStream_t st = vm->stream;
+    const uint64_t seq = vm->seq.next();   // the launch below touches every process's memory
+    for (uint32_t i = 0; i < n; i++) ps[i]->last_seq = seq;
     const uint32_t nb = (n + 255) / 256;
     // one device block: pkt_off | pkt_len | mem pointers | drv | prefix | base | has_cust | custom | results
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -2696,7 +2780,7 @@ int mimic_process_run_many(mimic_process *const *ps, uint32_t n, const int32_t *
     if (rc) return rc;
     std::vector<uint8_t> res(total - o_r0);
     HIP_OK(vm, hipMemcpyAsync(res.data(), D + o_r0, res.size(), hipMemcpyDeviceToHost, st));
-    HIP_OK(vm, hipStreamSynchronize(st));
+    HIP_OK(vm, proc_sync(vm));
     for (uint32_t i = 0; i < n; i++) {
         mimic_process *p = ps[i];
         uint64_t r0;
@@ -2725,30 +2809,45 @@ int mimic_process_packet(mimic_process *p, void *buf, size_t cap) {
     if (!p || !buf) return MIMIC_EINVAL;
     const uint64_t M = (uint64_t)p->H + p->len + p->T;
     if (cap < M) return fail(p->vm, MIMIC_EINVAL, "buffer too small");
-    hipSetDevice(p->vm->s.device);
-    HIP_OK(p->vm, hipMemcpy(buf, p->d_pkt, M, hipMemcpyDeviceToHost));
+    mimic_vm *vm = p->vm;
+    std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
+    hipSetDevice(vm->s.device);
+    // on the process's stream: behind its NewProcess upload and its launches
+    const hipError_t e = hipMemcpyAsync(buf, p->d_pkt, M, hipMemcpyDeviceToHost, vm->stream);
+    proc_enq(p);
+    const hipError_t es = proc_sync(vm);
+    if (e != hipSuccess || es != hipSuccess) return fail(vm, MIMIC_EDEVICE, "packet: %s", hipGetErrorString(e != hipSuccess ? e : es));
     return (int)M;
 }
 
+// Process.Cleanup (vm.go:363-374): no host wait -- the blocks go back to the VM's cache with the
+// fence of their last use (none when that use is known complete, as after Run / Step)
 void mimic_process_free(mimic_process *p) {
     if (!p) return;
     hipSetDevice(p->vm->s.device);
-    hipStreamSynchronize(p->vm->stream);
-    process_release(p);
+    process_release(p, proc_fence(p->vm, p->last_seq));
     delete p;
 }
 
 void mimic_process_free_many(mimic_process *const *ps, uint32_t n) {
     mimic_vm *last = nullptr;
+    std::shared_ptr<BlkFence> f;
+    bool have = false;   // f is the fence of `last`'s stream for this call
     for (uint32_t i = 0; i < n; i++) {
         mimic_process *p = ps[i];
         if (!p) continue;
-        if (p->vm != last) {   // one wait per VM for the launches that may use the memory
+        if (p->vm != last) {
             last = p->vm;
             hipSetDevice(last->s.device);
-            hipStreamSynchronize(last->stream);
+            have = false;
+            f.reset();
         }
-        process_release(p);
+        const bool busy = !last->seq.idle(p->last_seq);
+        if (busy && !have) {   // one event for the call's blocks still in use
+            f = proc_fence(last, p->last_seq);
+            have = true;
+        }
+        process_release(p, busy ? f : nullptr);
         delete p;
     }
 }

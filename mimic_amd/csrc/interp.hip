@@ -144,8 +144,15 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
             if (STP) step_save(kp, L, RB, (st_), (epc_), steps, cur_prog); \
         } while (0)
         // Process.Step: a stepped process resumes where its last launch suspended it
-        bool resumed = false;
-        if (i != 0xffffffffu && STP && STP->started) {
+        bool resumed = false, foreign = false;
+        if (i != 0xffffffffu && STP && STP->gen != kp.step_gen) {
+            // engine assertion: the state is not this process's -- nothing of it is read or written
+            foreign = true;
+            if (kp.r0) kp.r0[i] = 0;
+            if (kp.status) kp.status[i] = (uint8_t)MIMIC_ERR_ENGINE_STATE;
+            if (kp.steps) kp.steps[i] = 0;
+            if (kp.err_pc) kp.err_pc[i] = -1;
+        } else if (i != 0xffffffffu && STP && STP->started) {
             const StepState *S = STP;
 #pragma unroll
             for (int q = 0; q < NREGS; q++) REG(q) = S->r[q];
@@ -168,7 +175,7 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         // packet again without Load's side effects (the room bytes keep what it wrote), then its
         // registers and dynamic lane state come back and its slot runs next
         const bool resume_here = MODE == MODE_RESUME && i != 0xffffffffu && j == j0;
-        if (resumed) {
+        if (resumed || foreign) {
         } else if (i != 0xffffffffu && kp.ctx_kind == CTX_SKB) {   // LinuxContextSKBuff.Load (skb.h)
             uint64_t r1 = 0;
             const int ls = skb_load<MODE == MODE_RESUME>(kp, L, i, r1, resume_here);
@@ -451,7 +458,13 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mimic_xdp_kernel(const KParams *__restrict__ kpp) { xdp_body<MODE_BATCH>(kpp); }
 // the same body at the compiler's own budget (3 waves per SIMD, no spills): MIMIC_INTERP_WAVES=3
 extern "C" __global__ __launch_bounds__(256) void mimic_xdp_kernel_w3(const KParams *__restrict__ kpp) { xdp_body<MODE_BATCH>(kpp); }
-extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KParams *__restrict__ kpp) { xdp_body<MODE_STEP>(kpp); }
+// Process.Step / Run: launch parameters by value (no parameter slot, no copy ahead of the launch)
+extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KParams kp_arg) {
+    (void)kp_arg;
+    const KParams __attribute__((address_space(4))) *k4 =
+        (const KParams __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();
+    xdp_body<MODE_STEP>((const KParams *)k4);
+}
 // after a JIT kernel with deferred slow paths, with the same launch parameters (by value: read
 // in place from the kernarg segment, as the JIT kernels do)
 extern "C" __global__ __launch_bounds__(256) void mimic_xdp_resume_kernel(const KParams kp_arg) {
@@ -638,7 +651,7 @@ extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStrea
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
     static const bool w3 = [] { const char *e = getenv("MIMIC_INTERP_WAVES"); return e && e[0] == '3'; }();
-    if (kp->step) hipLaunchKernelGGL(mimic_xdp_step_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
+    if (kp->step) hipLaunchKernelGGL(mimic_xdp_step_kernel, dim3(blocks), dim3(256), 0, st, *kp);
     else if (w3) hipLaunchKernelGGL(mimic_xdp_kernel_w3, dim3(blocks), dim3(256), 0, st, d_kp);
     else hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -176,7 +176,7 @@ struct KParams {
     const int32_t *egress_arr;
     uint32_t headroom, tailroom;
     int32_t ingress, rxq, egress;
-    uint32_t pad1;
+    uint32_t step_gen;          // single-process stepping: the generation the process's StepState must carry
     const uint32_t *sched_start;   // EXPLICIT: CSR over local lanes [lanes+1]
     const uint32_t *sched_pkts;
     // results
@@ -255,7 +255,8 @@ struct DeferRec {
     uint32_t flag;        // == KParams::defer_epoch: suspended in that launch
 };
 
-// The state of one stepped process between launches (engine.cpp mimic_process_*): the
+// The state of one stepped process between launches (engine.cpp mimic_process_*; it lives in the
+// process's pinned, device-mapped host block, read and written in place by the stepping kernel): the
 // reference's Registers (PC, R0-R10), the current program, the step count, and the lane
 // state (stack validity, xdp_md overlay, frames, tail calls, translation cache) -- the stack,
 // frames and xdp_md overlay themselves stay in the process's own private memory.
@@ -268,6 +269,6 @@ struct StepState {
     uint32_t started;     // NewProcess + Load done
     uint32_t finished;    // exited (status OK) or terminated by a fatal error
     int32_t cpu;          // Process.cpuID (-1 until SetCPUID)
-    uint32_t pad;
+    uint32_t gen;         // the process's NewProcess number (KParams::step_gen of its launches)
     uint8_t lane[256];    // the kernel's Lane record (runtime.h), opaque to the host
 };

@@ -78,7 +78,7 @@ def spread_spec(progs: Sequence[Tuple[bytes, Sequence]], maps: Sequence[dict], v
     ``vcpus`` vCPUs: (pc, shapes, lds_rows) -- the (program, slot, map id) of every LD_IMM64 slot
     naming a per-CPU array's object, those maps' (id, E * S, S), and the LDS table's rows
     (min(ppb, V) when that many rows of the largest such row fit 32 KiB, else 0).  own: the owned
-    form's (spread_build_own: min(128, 32 KiB / row) rows, bit 31 set)."""
+    form's (spread_build_own: min(256, 32 KiB / row) rows, bit 31 set)."""
     by_name = {m["name"]: (i, m) for i, m in enumerate(maps)}
     pc, shapes = [], {}
     for pi, (raw, rel) in enumerate(progs):

@@ -41,7 +41,7 @@ def test_abi_version():
     hdr = int(re.search(r"#define MIMIC_ABI_VERSION (\d+)", open(HDR).read()).group(1))
     # 2: mimic_skb_batch grew `custom`, statuses 29/30, mimic_last_exec may return MIMIC_EXEC_SPREAD
     # 3: mimic_last_exec may return MIMIC_EXEC_SPREAD_OWN
-    assert hdr == _lib.ABI_VERSION == 3
+    assert hdr == _lib.ABI_VERSION == 4
 
 
 def test_status_numbering_matches_oracle():
