@@ -94,6 +94,32 @@ def main():
     dt = time.perf_counter() - t0
     out["process_run_xdp_cabi"] = {"us_per_call": round(dt / args.calls * 1e6, 1), "calls": args.calls,
                                    "what": "mimic_process_new + _set_cpu + _run + _free through ctypes, classifier, 64 B"}
+    # where a call's time goes: each C-ABI call timed alone (medians), next to a torch op + sync
+    parts = {"new": [], "set_cpu": [], "run": [], "free": []}
+    for k in range(args.calls):
+        h = C.c_void_p()
+        t0 = time.perf_counter()
+        lib.mimic_process_new(hv, prog_id, pk[k], len(pk[k]), c0.Headroom, c0.Tailroom, c0.IngessIfIndex,
+                              c0.RxQueueIndex, c0.EgressIfIndex, C.byref(h))
+        t1 = time.perf_counter()
+        lib.mimic_process_set_cpu(h, k % V)
+        t2 = time.perf_counter()
+        lib.mimic_process_run(h, 0, C.byref(regs))
+        t3 = time.perf_counter()
+        lib.mimic_process_free(h)
+        t4 = time.perf_counter()
+        for key, d in zip(parts, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            parts[key].append(d * 1e6)
+    import torch
+    x = torch.zeros(16, device="cuda:0")
+    lat = []
+    for _ in range(args.calls):
+        t0 = time.perf_counter()
+        x.add_(1)
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t0) * 1e6)
+    out["process_run_xdp_cabi_split_us"] = {k: round(float(np.median(v)), 1) for k, v in parts.items()}
+    out["process_run_xdp_cabi_split_us"]["torch_op_plus_sync"] = round(float(np.median(lat)), 1)
 
     # ---- ProcessPool, xdp_md jobs ------------------------------------------------------------------
     n = args.xdp_jobs
