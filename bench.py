@@ -66,12 +66,27 @@ def dist_env():
     return ws, rank, local
 
 
-def algorithmic_bytes(lens: np.ndarray, vcpus: int, maps, reads_packet: bool = True) -> int:
-    """per packet L + 8 (descriptor) + 8 (r0); per batch 2*V*E*S of per-CPU array
-    state, 2*E*(K+S) of hash-map state (K + V*S for a per-CPU hash), 2*E*S of plain arrays.
-    A program that never reads packet bytes (pass8) is charged only its 16 B per packet.
-    (The engine's actual descriptor is 12 B and it also writes a 1-B status; not counted.)"""
-    b = (int(lens.astype(np.int64).sum()) if reads_packet else 0) + 16 * len(lens)
+def reach_kind(cfg_name: str) -> str:
+    return {"flowtrack_insert": "flowtrack"}.get(cfg_name, cfg_name)
+
+
+def algorithmic_bytes(wl, vcpus: int) -> int:
+    """Bytes one launch must move, SURVEY.md 8(d) with the packet term made exact: per packet the
+    32-byte sectors holding the frame bytes the programs can read (workloads.packet_reach: the
+    headers they parse, with their bounds checks; never more than L) + 8 (descriptor) + 8 (r0);
+    sk_buff contexts also the 96 room bytes Load hands over zeroed and the sector the verdict
+    program's one-byte packet store writes; per batch 2*V*E*S of per-CPU array state, 2*E*(K+S) of
+    hash-map state (K + V*S for a per-CPU hash), 2*E*S of plain arrays.  (SURVEY's L per packet
+    charged the 1500-byte packets' payloads no program reads: cfg 3 came out at frac 1.25.)"""
+    from mimic_amd import workloads as W
+
+    reach = wl.reach if wl.reach is not None else W.packet_reach(reach_kind(wl.name), wl.buf, wl.off, wl.lens)
+    wl.reach = reach
+    maps = wl.maps
+    n = len(wl.lens)
+    b = int(W.read_sector_bytes(reach).sum()) + 16 * n
+    if wl.skb:
+        b += (W.SKB_HEADROOM + W.SKB_TAILROOM + W.SECTOR) * n
     for m in maps:
         if m["type"] in (1, 5):
             ncpu = vcpus if m["type"] == 5 else 1
@@ -116,6 +131,7 @@ class Workload:
             self.buf, self.off, self.lens = W.make_packets(n, self.cfg["sizes"], self.cfg["weights"], seed=seed)
             self.map_init = []
         self.ctx = 1 if self.skb else 0
+        self.reach = None   # per-packet read reach (algorithmic_bytes), computed once
 
     def kernel_src_hash(self, spread_vcpus: int = 0, own: bool = False) -> str:
         return kernel_src_hash_of(self.name, spread_vcpus, own)
@@ -552,12 +568,13 @@ def main(argv=None):
         total_pkts = n * ws * args.steps
         value = total_pkts / elapsed / 1e6
         avg_launch_s = region_ms / args.steps / 1e3   # per launch, gaps between launches included
-        alg = sum(algorithmic_bytes(batches[b][0].lens, vpg, wl.maps, wl.cfg.get("reads_packet", True))
-                  for b in timed) / len(timed)
+        alg_of = {b: algorithmic_bytes(batches[b][0], vpg) for b in set(timed)}
+        alg = sum(alg_of[b] for b in timed) / len(timed)
         achieved = alg / avg_launch_s
         kernel = "mimic_jit_kernel" if vm.LastExec() in ("jit", "spread", "spread_own") else "mimic_xdp_kernel"
         src_hash = wl.kernel_src_hash(vpg if vm.LastExec() in ("spread", "spread_own") else 0, vm.LastExec() == "spread_own")
         prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched)
+        prof_ns = (prof.get("kernel_stats") or {}).get("avg_ns") if prof else None
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",
             "value": round(value, 3),
@@ -582,8 +599,11 @@ def main(argv=None):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
                          "traffic": prof["bytes_per_launch"] if prof else None,
                          "traffic_over_algorithmic": round(prof["bytes_per_launch"] / alg, 3) if prof else None,
-                         # the same launch time against the bytes the counters measured (FETCH x 2 + WRITE)
-                         "frac_on_traffic": round(prof["bytes_per_launch"] / avg_launch_s / HBM_PEAK, 5) if prof else None,
+                         # the profile's measured bytes over the profile's own kernel time (one rocprofv3
+                         # session: traffic and time from the same runs, not from this line's)
+                         "frac_on_traffic": round(prof["bytes_per_launch"] / (prof_ns * 1e-9) / HBM_PEAK, 5)
+                                            if prof_ns else None,
+                         "profile_kernel_ms": round(prof_ns * 1e-6, 4) if prof_ns else None,
                          "valu_busy": prof.get("valu_busy") if prof else None,
                          "profile": prof["file"] if prof else None,
                          "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(avg_launch_s * 1e3, 4)},

@@ -909,3 +909,85 @@ def skb_flow_keys(buf, off, lens, every: int = 3, limit: int = 4096):
         keys.setdefault(k, None)
     sel = list(keys)[::every][:limit]
     return [(k, (int.from_bytes(k[:8], "little") * 0x9E3779B1 & (2**64 - 1)).to_bytes(8, "little")) for k in sel]
+
+
+# ---------------------------------------------------------------------------------------------
+# the bytes each workload's programs can read (bench.py's algorithmic-byte model)
+# ---------------------------------------------------------------------------------------------
+SECTOR = 32   # HBM read granularity: the smallest read request (TCC_EA0_RDREQ_32B, MI355X_MICROARCH.md)
+
+
+def _header_rows(buf, off, base: int, width: int, lo: int, hi: int) -> np.ndarray:
+    idx = off[lo:hi].astype(np.int64)[:, None] + base + np.arange(width, dtype=np.int64)[None, :]
+    np.minimum(idx, len(buf) - 1, out=idx)
+    return buf[idx]
+
+
+def _be16(rows, at):
+    return (rows[:, at].astype(np.int64) << 8) | rows[:, at + 1]
+
+
+def packet_reach(kind: str, buf, off, lens, chunk: int = 1 << 20) -> np.ndarray:
+    """Per packet: one past the furthest frame byte the workload's programs read, with every bounds
+    check they make (0 = no packet byte).  Restates the programs above:
+
+      classifier  L < 34: none; else ethertype [12,14) and, for IPv4, protocol / addresses to 34
+      parse5      ethertype, an 802.1Q tag, IPv4 [l3, l3+20) and the ports at l3 + 4*IHL, or IPv6
+                  [l3, l3+40) and its ports; each only when its bounds check passes
+      flowtrack   ethertype; IPv4 to 38, IPv6 to 58 when the frame is that long
+      skb         the header stack SKBuffFromBytes decodes (emulator_linux_sk_buff.go:108-265:
+                  Ethernet, IPv4 IHL / IPv6, TCP data offset, UDP / ICMP 8), which covers the
+                  chain's LD_ABS / LD_IND reads; other frames (the 5 % variants) min(L, 96)
+      pass8       none (reads xdp_md fields only)
+    """
+    lens = np.asarray(lens)
+    n = len(lens)
+    out = np.zeros(n, np.int64)
+    if kind == "pass8" or n == 0:
+        return out
+    base = SKB_HEADROOM if kind == "skb" else 0
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        L = lens[lo:hi].astype(np.int64)
+        r = _header_rows(buf, off, base, 96, lo, hi)
+        et = _be16(r, 12)
+        if kind == "classifier":
+            reach = np.where(L < 34, 0, np.where(et == 0x0800, 34, 14))
+        elif kind == "flowtrack":
+            reach = np.where(L < 14, 0, 14)
+            reach = np.where((et == 0x0800) & (L >= 38), 38, reach)
+            reach = np.where((et == 0x86DD) & (L >= 58), 58, reach)
+        elif kind == "parse5":
+            reach = np.where(L < 14, 0, 14)
+            vlan = (et == 0x8100) & (L >= 18)
+            reach = np.where(vlan, 18, reach)
+            l3 = np.where(vlan, 18, 14)
+            et2 = np.where(vlan, _be16(r, 16), et)
+            rows = np.arange(len(L))
+            ihl = (r[rows, np.minimum(l3, 95)] & 15).astype(np.int64)
+            v4 = (et2 == 0x0800) & (l3 + 20 <= L)
+            l4 = l3 + 4 * ihl
+            reach = np.where(v4, np.where(l4 + 4 <= L, np.maximum(l3 + 20, l4 + 4), l3 + 20), reach)
+            v6 = (et2 == 0x86DD) & (l3 + 40 <= L)
+            reach = np.where(v6, np.where(l3 + 44 <= L, l3 + 44, l3 + 40), reach)
+        elif kind == "skb":
+            rows = np.arange(len(L))
+            ihl = (r[:, 14] & 15).astype(np.int64)
+            v4 = (et == 0x0800) & ((r[:, 14] >> 4) == 4)
+            v6 = (et == 0x86DD)
+            l4 = np.where(v4, 14 + 4 * ihl, 54)
+            proto = np.where(v4, r[:, 23], r[:, 20]).astype(np.int64)
+            doff = (r[rows, np.minimum(l4 + 12, 95)] >> 4).astype(np.int64) * 4
+            # TCP: its data offset; UDP, ICMP, ICMPv6: 8; else the ports the chain's LD_IND reads
+            l4len = np.where(proto == 6, np.maximum(doff, 20), np.where(np.isin(proto, (17, 1, 58)), 8, 4))
+            common = (v4 | v6) & (l4 + l4len <= L) & (l4 + l4len <= 96)
+            reach = np.where(common, l4 + l4len, np.minimum(L, 96))
+        else:
+            raise ValueError(kind)
+        out[lo:hi] = np.minimum(reach, L)
+    return out
+
+
+def read_sector_bytes(reach: np.ndarray) -> np.ndarray:
+    """Bytes of the 32-byte sectors holding frame bytes [0, reach) (frames start sector-aligned)."""
+    return -(-np.asarray(reach, np.int64) // SECTOR) * SECTOR
