@@ -61,18 +61,24 @@ HDEV HT h_table(uint8_t *arena, const DMap &m) {
 // base and count in the batch's slot (generation mod 16); the others take their share at the offset
 // their add returned.  The batch's positions are contiguous and ordered by arrival -- a valid order
 // of pops, as if those waves had popped one after another -- and a lone wave gets exactly what a
-// direct add gives (FIFO slots of sequential runs unchanged).  A slot's ready word also counts the
-// joiners that have not read it yet (low 8 bits), and the opener of a later batch on the same
-// slot waits for that count to reach zero before it publishes: no slot is overwritten before every joiner read it, whatever the timing.
-// The waits are on joiners already past their join (they only read), so the protocol cannot deadlock.
+// direct add gives (FIFO slots of sequential runs unchanged).
+// Slot reuse (round 6): every batch publishes, joiners or not, and its ready word is
+// (generation + 1) << 8 | joiners yet to read.  The opener of generation g claims its slot with a
+// CAS from exactly "generation g - 16, no reader left" (0 for g < 16) to "g, being written" (low
+// byte 0xff), writes base / got and then stores "g, joiners"; each joiner waits for "g" with a
+// count below 0xff, reads, and decrements.  So a slot is never overwritten before every joiner of
+// its previous batch read it, and a late publication of g - 16 cannot overwrite g's.  Nothing waits
+// on a later generation, so the protocol cannot deadlock; a spin still gives up after
+// HCOMB_SPIN_LIMIT sleeps, marks HashCtl::comb_fault (the host reports the launch as failed at the
+// next sync) and returns no position, rather than hang.
 // (Per-wave mailboxes written in a loop by the opener, round 5's first fix, cost the cfg-4 kernel 8
-// more spilled VGPRs and its lookup-hit launch 0.126 -> 0.143 ms; this form 2 and 0.130 ms.)
+// more spilled VGPRs and its lookup-hit launch 0.126 -> 0.143 ms.)
 #define HCOMB_MAPS 4u
 #define HCOMB_SLOTS 16u
 struct HComb {
     unsigned long long word;
     uint32_t owner;                     // the map (HT::tag) this combiner serves in this block
-    uint32_t ready[HCOMB_SLOTS];        // (generation + 1) << 8 | joiners yet to read, once base / got are published
+    uint32_t ready[HCOMB_SLOTS];        // (generation + 1) << 8 | joiners yet to read (0xff: being written)
     uint32_t got[HCOMB_SLOTS];          // positions below tail (bit 31: tail == E, the ring untouched)
     unsigned long long base[HCOMB_SLOTS];
 };
@@ -83,6 +89,10 @@ HDEV void h_comb_init() {
     for (uint32_t q = threadIdx.x; q < sizeof(h_comb_) / 4; q += blockDim.x) w[q] = 0;
     __syncthreads();
 }
+#ifndef HCOMB_SPIN_LIMIT
+#define HCOMB_SPIN_LIMIT (1u << 22)
+#endif
+HDEV void h_comb_fault(HashCtl *c) { __hip_atomic_store(&c->comb_fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 // k (>= 1) positions for the calling wave (one lane): *base, *got (positions below tail), *ident
 HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, uint32_t *got, uint32_t *ident) {
     HComb &cb = h_comb_[(t.tag >> 4) & (HCOMB_MAPS - 1)];
@@ -96,8 +106,10 @@ HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, ui
     const unsigned long long old = __hip_atomic_fetch_add(&cb.word, (1ull << 32) + k, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t gen = (uint32_t)(old >> 40), off = (uint32_t)old, s = gen & (HCOMB_SLOTS - 1);
+    const uint32_t mine = ((gen & 0x7fffffu) + 1u) << 8;   // this batch's ready word, reader count 0
     uint64_t b0;
     uint32_t g0;
+    uint32_t spins = 0;
     if (((old >> 32) & 0xffu) == 0) {   // the batch's opener
 #ifndef MIMIC_HCOMB_SLEEP
 #define MIMIC_HCOMB_SLEEP 2
@@ -109,16 +121,38 @@ HDEV bool h_comb_reserve(const HT &t, HashCtl *c, uint32_t k, uint64_t *base, ui
         b0 = __hip_atomic_fetch_add(&c->head, (unsigned long long)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tl = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         g0 = (b0 >= tl ? 0u : (tl - b0 < total ? (uint32_t)(tl - b0) : total)) | (tl == t.E ? 0x80000000u : 0u);
-        if (joiners) {
-            while (__hip_atomic_load(&cb.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & 0xffu)
-                __builtin_amdgcn_s_sleep(1);   // the slot's batch of 16 generations ago is still being read
-            cb.base[s] = b0;
-            cb.got[s] = g0;
-            __hip_atomic_store(&cb.ready[s], (((gen & 0x7fffffu) + 1u) << 8) | joiners, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    } else {
-        while ((__hip_atomic_load(&cb.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 8) != (gen & 0x7fffffu) + 1u)
+        // the slot: published by the batch 16 generations earlier and read by all its joiners
+        const uint32_t prev = gen < HCOMB_SLOTS ? 0u : (((gen - HCOMB_SLOTS) & 0x7fffffu) + 1u) << 8;
+        for (;;) {
+            uint32_t e = prev;
+            if (__hip_atomic_compare_exchange_strong(&cb.ready[s], &e, mine | 0xffu, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+                break;
+            if (++spins > HCOMB_SPIN_LIMIT) {
+                h_comb_fault(c);
+                *base = 0;
+                *got = 0;
+                *ident = 0;
+                return true;
+            }
             __builtin_amdgcn_s_sleep(1);
+        }
+        cb.base[s] = b0;
+        cb.got[s] = g0;
+        __hip_atomic_store(&cb.ready[s], mine | joiners, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        for (;;) {
+            const uint32_t r = __hip_atomic_load(&cb.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((r & ~0xffu) == mine && (r & 0xffu) != 0xffu) break;
+            if (++spins > HCOMB_SPIN_LIMIT) {
+                h_comb_fault(c);
+                *base = 0;
+                *got = 0;
+                *ident = 0;
+                return true;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
         b0 = cb.base[s];
         g0 = cb.got[s];
         __hip_atomic_fetch_sub(&cb.ready[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);

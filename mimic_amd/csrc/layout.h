@@ -72,7 +72,8 @@ struct DMap {
 #define HT_USED_SHARDS 16
 struct HashCtl {
     unsigned long long head;   // next ring position to pop
-    uint32_t pad0[30];
+    uint32_t comb_fault;       // a block combiner gave up waiting (hashmap.h h_comb_reserve): the launch failed
+    uint32_t pad0[29];
     unsigned long long tail;   // next ring position to push
     int32_t avail;             // free slots not yet claimed (stale after a pop-only launch: normalised)
     uint32_t used0;            // buckets that are not EMPTY (live + tombstones + busy), minus the shards

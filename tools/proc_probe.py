@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Process.Run per call through the C ABI for a few programs (run under rocprofv3 --kernel-trace to
+split kernel time from host time): classifier (36 slots, packet + map), pass8 (8 slots, no memory)."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+
+def main():
+    import mimic_amd as M
+    from harness import Scenario, build_engine
+    from mimic_amd import _lib as L
+    from mimic_amd import workloads as W
+
+    out = {}
+    buf, off, lens = W.make_packets(4096, seed=3)
+    pk = [bytes(buf[int(o):int(o) + int(n)]) for o, n in zip(off, lens)]
+    for name in ("prog_pass8", "prog_classifier"):
+        p = getattr(W, name)()
+        sc = Scenario(vcpus=256, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+        vm, maps, pids = build_engine(sc)
+        lib, hv, regs = vm.lib, vm.h, L.ProcessRegs()
+        ts = {"new": [], "run": [], "free": []}
+        for k in range(400):
+            h = C.c_void_p()
+            t0 = time.perf_counter()
+            assert lib.mimic_process_new(hv, pids[0], pk[k], len(pk[k]), 0, 0, 1, 0, 0, C.byref(h)) == 0
+            t1 = time.perf_counter()
+            assert lib.mimic_process_run(h, 0, C.byref(regs)) == 0
+            t2 = time.perf_counter()
+            lib.mimic_process_free(h)
+            t3 = time.perf_counter()
+            if k >= 100:
+                for key, d in zip(ts, (t1 - t0, t2 - t1, t3 - t2)):
+                    ts[key].append(d * 1e6)
+        out[name] = {k: round(float(np.median(v)), 1) for k, v in ts.items()}
+        out[name]["steps"] = int(regs.steps)
+        vm.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
