@@ -181,6 +181,7 @@ struct mimic_vm {
     void *d_spread_part = nullptr;   // spread launches: the blocks' counter tables (mimic_spread_reduce_kernel)
     uint64_t spread_part_cap = 0;
     bool spread_used = false;
+    bool comb_used = false;   // a launch ran a kernel with the hash maps' block combiner (HashCtl::comb_fault)
     // host map operations staged for the device (flush_host): value / array writes, deduplicated
     // per arena offset (a later write to the same bytes replaces the earlier one)
     struct PendWrite {
@@ -1815,6 +1816,18 @@ static int priv_ensure(mimic_vm *vm, uint32_t q_per_lane, uint32_t lanes, hipStr
 // jit.cpp analyze_spread's base provenance keeps such program sets off spread kernels): its
 // results may not be the reference's, which is reported as an engine error (stream synchronized)
 static int spread_check(mimic_vm *vm) {
+    // a block combiner that gave up waiting (hashmap.h h_comb_reserve): its lanes got no position
+    if (vm->comb_used) {
+        for (const HostMap &m : vm->maps) {
+            if (!is_hash(m)) continue;
+            uint64_t rb, fo, co;
+            ht_offsets(m, &rb, &fo, &co);
+            uint32_t f = 0;
+            HIP_OK(vm, hipMemcpy(&f, vm->arena + m.ht_dev_off + co + offsetof(HashCtl, comb_fault), 4, hipMemcpyDeviceToHost));
+            if (f) return fail(vm, MIMIC_EDEVICE, "map '%s': a block combiner of freelist reservations gave up (engine fault)",
+                               m.name.c_str());
+        }
+    }
     if (!vm->spread_used || !vm->d_spread_bad) return 0;
     uint32_t f = 0;
     HIP_OK(vm, hipMemcpy(&f, vm->d_spread_bad, 4, hipMemcpyDeviceToHost));
@@ -2219,6 +2232,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.defer_any = vm->d_defer_any;
         kp.defer_epoch = vm->defer_epoch;
     }
+    if (jit && ji.hash_combine) vm->comb_used = true;
     if (jit && ji.karg) {  // launch parameters by value: the runtime copies them into the kernarg segment
         if (mimic_jit_launch(jfn, ji, &kp, nullptr, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));

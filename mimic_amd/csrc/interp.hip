@@ -50,6 +50,27 @@ static __device__ void step_save(const KParams &kp, const Lane &L, const uint64_
 }
 
 #define WAVES_PER_BLOCK 4
+
+// Process.Step / Run launch one lane: its instruction fetches, segment / map table reads and its
+// packet loads would each be a cold HBM round trip in sequence (the single-lane Run of a 36-slot
+// program measured ~30 us of kernel time).  The block's three idle waves touch one dword of every
+// 64-byte line of those tables and of the process's descriptor and packet memory first, so the
+// lane's fetches find them in L2.  (Volatile loads: nothing is done with the values.)
+static __device__ __noinline__ void step_warm(const KParams &kp, uint32_t t, uint32_t nt) {
+    const DProg last = kp.progs[kp.nprogs - 1];
+    const uint64_t spans[5][2] = {{(uint64_t)(uintptr_t)kp.insns, (uint64_t)(last.base + last.n) * sizeof(DInsn)},
+                                  {(uint64_t)(uintptr_t)kp.segs, (uint64_t)kp.nsegs * sizeof(Seg)},
+                                  {(uint64_t)(uintptr_t)kp.maps, (uint64_t)kp.nmaps * sizeof(DMap)},
+                                  {(uint64_t)(uintptr_t)kp.progs, (uint64_t)kp.nprogs * sizeof(DProg)},
+                                  {(uint64_t)(uintptr_t)kp.pkt_data, 512}};
+    uint32_t n = 0;
+    for (int k = 0; k < 5; k++) {
+        const uint64_t lines = (spans[k][1] + 63) / 64;
+        for (uint64_t q = t; q < lines && q < 4096; q += nt) n += *(const volatile uint32_t *)(spans[k][0] + q * 64);
+    }
+    if (t == 0) n += *(const volatile uint32_t *)kp.pkt_off + *(const volatile uint32_t *)kp.pkt_len;
+    (void)n;
+}
 #define NREGS 11
 #define KEY_DONE 0xffffffffu
 
@@ -84,6 +105,7 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         if (__ballot(DR != nullptr) == 0) return;
     }
     const bool lane_valid = g < kp.lanes && (MODE != MODE_RESUME || DR);
+    if (MODE == MODE_STEP && threadIdx.x >= 64) step_warm(kp, threadIdx.x - 64, blockDim.x - 64);
     Lane L;
     L.lane = g;
     L.cpu = STP ? STP->cpu : lane_cpu(kp, g);

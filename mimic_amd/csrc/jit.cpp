@@ -2336,6 +2336,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->karg = g.karg != 0;
         info->spread = g.spread_on;
         info->spread_own = g.spread_own;
+        info->hash_combine = g.hash_combine;
         info->spread_map = g.spread_map;
         info->spread_n = g.spread_n;
         info->spread_roww = g.spread_n ? g.spread_row / g.spread_n : 0;

@@ -21,6 +21,7 @@ struct JitInfo {
     bool skb_fast;       // sk_buff kernel that derives the records of common frames itself (sparse prep)
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
     bool spread_own;     // ... in its owned form: a block runs every packet of its vCPUs (SpreadReq::own)
+    bool hash_combine;   // pop-only inline inserts through the block combiner (hashmap.h h_comb_reserve)
     // spread kernels: the counted per-CPU array, counter width, counters per row, LDS table rows
     uint32_t spread_map, spread_n, spread_roww, spread_rows;
 };

@@ -444,3 +444,28 @@ def test_launches_and_host_ops_interleaved(gpu, host_ops):
         assert em.Values(0) == ovm.map_values(om, 0), rnd
     evm.close()
     ovm.close()
+
+
+def test_combiner_gives_up_with_a_status(gpu, monkeypatch):
+    """The block combiner's waits are bounded (hashmap.h h_comb_reserve, HCOMB_SPIN_LIMIT): built
+    with a limit of 0 (every wait gives up at once) and a long batching window (MIMIC_HCOMB_SLEEP,
+    so several waves of a block join each batch and wait for its publication), an inserting launch
+    ends -- no hang -- and the sync reports the engine fault instead of results.  The default build
+    of the same program then runs the batch exact per key."""
+    import mimic_amd as M
+
+    p = W.prog_flowtrack(max_entries=1 << 16)
+    sc = _sc(p, 4096)
+    n = 1 << 16
+    buf, off, lens = W.make_packets(n, **W.IMIX, seed=23)
+    cpu = W.schedule_cpu(n, 4096, "interleaved")
+    monkeypatch.setenv("MIMIC_JIT_DEFS", "HCOMB_SPIN_LIMIT=0,MIMIC_HCOMB_SLEEP=60")
+    vm, maps, pids = build_engine(sc)
+    batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+    with pytest.raises(M.MimicError, match="combiner"):
+        vm.RunXDPBatch(pids[0], batch)
+    vm.close()
+    monkeypatch.delenv("MIMIC_JIT_DEFS")
+    o = run_oracle(sc, buf, off, lens, cpu)
+    e = run_engine(sc, buf, off, lens, cpu, schedule=M.SCHED_INTERLEAVED)
+    assert_same(o, e, check_pkt=False, hash_exact=False, check_steps=False)
