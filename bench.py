@@ -321,6 +321,9 @@ def parse_args(argv=None):
                     help="distinct input batches the timed launches rotate over (default: enough that the "
                          f"working set exceeds {ROTATE_BYTES >> 20} MiB, so no batch is served from the "
                          "256 MiB Infinity Cache)")
+    ap.add_argument("--many", type=int, default=1,
+                    help="batches per launch (mimic_run_xdp_many, up to 8: one owned-spread launch runs K of the "
+                         "rotated batches back to back); --steps counts launches, ms_per_step stays per batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-resident", action="store_true", help="skip the PCIe-inclusive rate")
@@ -502,7 +505,19 @@ def main(argv=None):
 
     reset = [maps[m["name"]] for m in wl.maps] if cfg.get("reset_maps") else []
 
+    K = max(1, args.many)
+    if K > 1 and (wl.skb or reset or nb % K and nb > K):
+        sys.stderr.write("bench.py: --many needs an xdp_md config without map resets and a batch count K divides\n")
+        return 2
+
+    def launch_many(k):   # batches k*K .. k*K + K - 1 (mod nb) in one mimic_run_xdp_many call
+        sel = [batches[(k * K + q) % nb] for q in range(K)]
+        vm.RunXDPMany(pid, [b for _, b, _ in sel], [r for _, _, r in sel], stream=stream, sync=False)
+
     def launch(k):
+        if K > 1:
+            launch_many(k)
+            return
         w, batch, res = batches[k % nb]
         for m in reset:   # a fresh map per step: every flow of the batch is inserted again
             m.Reset(stream)
@@ -533,7 +548,7 @@ def main(argv=None):
     elapsed = t1 - t0
     region_ms = ev0.elapsed_time(ev1)
     st = np.concatenate([res.status[:n].cpu().numpy() for _, _, res in batches])
-    timed = [(args.warmup + k) % nb for k in range(args.steps)]
+    timed = [((args.warmup + k) * K + q) % nb for k in range(args.steps) for q in range(K)]
     if use_dist:
         elapsed = D.allreduce_max_f64(elapsed, cdev)
 
@@ -557,7 +572,10 @@ def main(argv=None):
     # batch after the readout above
     steps_of = []
     for b in range(nb):
-        launch(b)
+        if K > 1:   # one batch per launch here: LastSteps of exactly this batch
+            vm.RunXDPBatch(pid, batches[b][1], batches[b][2], stream=stream, sync=False)
+        else:
+            launch(b)
         torch.cuda.synchronize(dev)
         steps_of.append(vm.LastSteps())
     steps_timed = float(sum(steps_of[b] for b in timed))
@@ -565,9 +583,9 @@ def main(argv=None):
         steps_timed = float(D.allreduce_sum_u64([int(steps_timed)], cdev)[0])
 
     if rank == 0:
-        total_pkts = n * ws * args.steps
+        total_pkts = n * ws * args.steps * K
         value = total_pkts / elapsed / 1e6
-        avg_launch_s = region_ms / args.steps / 1e3   # per launch, gaps between launches included
+        avg_launch_s = region_ms / (args.steps * K) / 1e3   # per batch (a launch runs K), gaps included
         alg_of = {b: algorithmic_bytes(batches[b][0], vpg) for b in set(timed)}
         alg = sum(alg_of[b] for b in timed) / len(timed)
         achieved = alg / avg_launch_s
@@ -580,9 +598,10 @@ def main(argv=None):
             "value": round(value, 3),
             "unit": "Mpkts/s",
             "n_gpus": ws,
-            "steps": args.steps,
+            "steps": args.steps * K,   # batches (a step is one pass over one batch); launches below
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "launches": args.steps,
+            "ms_per_step": round(elapsed / (args.steps * K) * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -592,9 +611,9 @@ def main(argv=None):
                        "schedule": args.sched, "parallelism": f"dp{ws}", "batches_rotated": nb,
                        "working_set_bytes": sum(int(w.buf.nbytes) + 21 * n for w, _, _ in batches),
                        "program_slots": sum(len(p.raw) // 8 for p in wl.progs), "engine": vm.LastExec(),
-                       "kernel_src_hash": src_hash},
+                       "kernel_src_hash": src_hash, "batches_per_launch": K},
             "insns_per_s": round(steps_timed / elapsed, 1),
-            "mean_insns_per_packet": round(steps_timed / (n * ws * args.steps), 3),
+            "mean_insns_per_packet": round(steps_timed / (n * ws * args.steps * K), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
                          "traffic": prof["bytes_per_launch"] if prof else None,

@@ -218,6 +218,13 @@ int mimic_stack_addr(mimic_vm *vm, uint32_t *addr_out);
  * Enqueued on `hip_stream` (a hipStream_t, NULL = the vm's own stream); returns when enqueued. */
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch,
                   const mimic_xdp_results *results, void *hip_stream);
+/* k batches (DEVICE pointers as above), enqueued like mimic_run_xdp, as few launches as possible: up
+ * to 8 batches of the same size, schedule (not EXPLICIT) and scalar fields, with no per-packet arrays,
+ * run as ONE launch when the programs allow the owned spread kernel (mimic_set_spread); every vCPU
+ * then runs its packets of batch 0, then of batch 1, ... (processPool draining a backlog of batches,
+ * vm.go:548-573).  Otherwise one launch per batch.  Not in the reference API. */
+int mimic_run_xdp_many(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batches,
+                       const mimic_xdp_results *results, uint32_t k, void *hip_stream);
 /* One batch of sk_buff processes (LinuxContextSKBuff, context_sk_buff.go:20-119).  DEVICE
  * pointers as in mimic_xdp_batch.  Process i's packet memory is pkt_data[pkt_off[i] ..
  * pkt_off[i]+32+L+64) with the packet's L = pkt_len[i] bytes at +32 (SKBuffFromBytes'

@@ -1550,6 +1550,10 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
     const uint64_t *skb_prefix = nullptr, *skb_base = nullptr;
     const mimic_skb_custom *skb_custom = nullptr;   // its user-given sock / flow keys (device, one entry) or null
     uint32_t gen = 0;   // the generation its state carries (StepState::gen)
+    // its first launch: the NewProcess image (device-visible host address), its device block, bytes
+    const uint8_t *img = nullptr;
+    uint8_t *img_dst = nullptr;
+    uint32_t img_n = 0;
 };
 
 struct CtxRun {      // Run(ctx) of a batch: one context for every packet, or one per packet (host array)
@@ -1559,13 +1563,51 @@ struct CtxRun {      // Run(ctx) of a batch: one context for every packet, or on
     // array once; a sub-batch points into it): no per-launch upload
     const uint32_t *const *dev_pp = nullptr;
 };
+// mimic_run_xdp_many: the batches of one launch (b[0] is the one run_xdp_impl is given); `used` is
+// set when the launch ran all of them (an owned spread kernel), else it ran b[0] only
+struct ManyRun {
+    const mimic_xdp_batch *b;
+    const mimic_xdp_results *r;
+    uint32_t k;
+    bool used;
+};
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                         hipStream_t st_in, uint64_t shift, const SkbRun *skb = nullptr, const StepRun *step = nullptr,
-                        const CtxRun *cx = nullptr);
+                        const CtxRun *cx = nullptr, ManyRun *mr = nullptr);
 
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                   void *hip_stream) {
     return run_xdp_impl(vm, prog_id, b, res, (hipStream_t)hip_stream, 0);
+}
+
+// k batches of one program as few launches as possible: groups of up to MIMIC_MANY_MAX batches run as
+// ONE launch of the owned spread kernel when the programs and the batches allow it (every thread runs
+// its packets of each batch in turn: a vCPU's packets keep batch order, as processPool draining a
+// backlog of batches would), else one launch per batch.  Not in the reference API.
+int mimic_run_xdp_many(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res, uint32_t k,
+                       void *hip_stream) {
+    if (!vm || (k && (!b || !res))) return MIMIC_EINVAL;
+    hipStream_t st = (hipStream_t)hip_stream;
+    // batches that can share a launch: same size, schedule and scalar fields, no per-packet arrays
+    auto same = [&](const mimic_xdp_batch &x, const mimic_xdp_batch &y) {
+        return x.n == y.n && x.schedule == y.schedule && x.schedule != MIMIC_SCHED_EXPLICIT && !x.headroom && !y.headroom &&
+               !x.tailroom && !y.tailroom && !x.ingress_ifindex && !y.ingress_ifindex && !x.rx_queue_index &&
+               !y.rx_queue_index && !x.egress_ifindex && !y.egress_ifindex && x.headroom_all == y.headroom_all &&
+               x.tailroom_all == y.tailroom_all && x.ingress_all == y.ingress_all && x.rxq_all == y.rxq_all &&
+               x.egress_all == y.egress_all && x.step_budget == y.step_budget;
+    };
+    for (uint32_t a = 0; a < k;) {
+        uint32_t e = a + 1;
+        while (e < k && e - a < MIMIC_MANY_MAX && same(b[a], b[e])) e++;
+        ManyRun mr{b + a, res + a, e - a, false};
+        int rc = run_xdp_impl(vm, prog_id, b + a, res + a, st, 0, nullptr, nullptr, nullptr, e - a > 1 ? &mr : nullptr);
+        if (rc) return rc;
+        if (!mr.used)   // one launch per batch
+            for (uint32_t q = a + 1; q < e; q++)
+                if ((rc = run_xdp_impl(vm, prog_id, b + q, res + q, st, 0))) return rc;
+        a = e;
+    }
+    return 0;
 }
 
 int mimic_run_xdp_ctx(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
@@ -1850,7 +1892,7 @@ static std::vector<std::pair<uint32_t, uint32_t>> vc_slots_of(const mimic_vm *vm
 
 static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b, const mimic_xdp_results *res,
                         hipStream_t st_in, uint64_t first_index, const SkbRun *skb, const StepRun *step,
-                        const CtxRun *cx) {
+                        const CtxRun *cx, ManyRun *mr) {
     if (!vm || !b || !res) return MIMIC_EINVAL;
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (b->n > 0 && (!b->pkt_data || !b->pkt_off || !b->pkt_len)) return fail(vm, MIMIC_EINVAL, "missing packet arrays");
@@ -1925,6 +1967,12 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.budget = step ? step->budget : (b->step_budget ? b->step_budget : MIMIC_DEFAULT_BUDGET);
     kp.step = step ? step->state : nullptr;
     kp.step_gen = step ? step->gen : 0u;
+    if (step) {
+        kp.step_img = step->img;
+        kp.step_dst = step->img_dst;
+        kp.step_img_n = step->img_n;
+        kp.step_ins_n = (uint32_t)std::min<size_t>(vm->h_all.size(), 2048);   // 32 KiB of LDS
+    }
     kp.n = b->n;
     kp.sched = b->schedule;
     kp.pkt_data = b->pkt_data;
@@ -2233,6 +2281,15 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         kp.defer_epoch = vm->defer_epoch;
     }
     if (jit && ji.hash_combine) vm->comb_used = true;
+    if (mr) {   // every batch of a multi-batch launch in this one (the owned form only: jit.cpp)
+        mr->used = jit && own && !ji.defer && mr->k >= 1 && mr->k <= MIMIC_MANY_MAX;
+        if (mr->used) {
+            kp.many_n = mr->k;
+            for (uint32_t q = 0; q < mr->k; q++)
+                kp.many[q] = BatchRef{mr->b[q].pkt_data, mr->b[q].pkt_off, mr->b[q].pkt_len, mr->r[q].r0, mr->r[q].status,
+                                      mr->r[q].steps, mr->r[q].err_pc, 0};
+        }
+    }
     if (jit && ji.karg) {  // launch parameters by value: the runtime copies them into the kernarg segment
         if (mimic_jit_launch(jfn, ji, &kp, nullptr, st))
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
@@ -2333,6 +2390,8 @@ struct mimic_process {
     Blk mem;                          // the block above
     Blk priv;                         // private memory (stack, frames, ...): device only
     uint64_t last_seq = 0;            // vm->seq number of the last work enqueued that touches mem / priv
+    bool uploaded = false;            // the device block holds the NewProcess image (else only the host half)
+    size_t img_n = 0;                 // the image's bytes (the device block's [0, img_n))
 };
 
 // blocks of single processes, from the VM's cache (one hipMalloc / hipHostMalloc per size class ever)
@@ -2453,6 +2512,11 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     r.err_pc = (int32_t *)(p->hres_dev + (PH_EPC - PH_RES));
     StepRun sr{p->hs_dev, p->priv.dev, p->priv_bytes, budget};
     sr.gen = p->gen;
+    if (!p->uploaded) {   // the kernel copies the image in before the process's first step
+        sr.img = p->mem.hdev + PH_IMG;
+        sr.img_dst = p->mem.dev;
+        sr.img_n = (uint32_t)p->img_n;
+    }
     SkbRun skr{p->ifindex};
     if (p->skb) {
         sr.skb_rec = (SkbRec *)p->d_skbmem;
@@ -2464,6 +2528,7 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     proc_enq(p);
     const hipError_t e = proc_sync(vm);   // the one host sync of Run / Step
     if (rc) return rc;
+    p->uploaded = true;
     if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
     if (p->hres[PH_ST - PH_RES] == MIMIC_ERR_ENGINE_STATE || S->gen != p->gen)
         return fail(vm, MIMIC_EDEVICE, "process: the stepping launch found another process's state (engine assertion)");
@@ -2477,7 +2542,7 @@ extern "C" {
 // device with one asynchronous copy on vm->stream (run_mu held)
 static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t headroom,
                         uint32_t tailroom, int32_t ingress_ifindex, int32_t rx_queue_index, int32_t egress_ifindex,
-                        const mimic_skb_custom *custom, mimic_process **out) {
+                        const mimic_skb_custom *custom, bool upload, mimic_process **out) {
     hipSetDevice(vm->s.device);
     const uint64_t M = (uint64_t)headroom + len + tailroom;
     const size_t total = PD_PKT + (size_t)std::max<uint64_t>(M, 1);
@@ -2512,8 +2577,14 @@ static int process_make(mimic_vm *vm, uint32_t prog_id, const void *packet, uint
     if (custom) memcpy(img + PD_SKB + sizeof(SkbRec) + 24, custom, sizeof *custom);
     if (len) memcpy(img + PD_PKT + headroom, packet, len);
     memset(img + PD_PKT + headroom + len, 0, total - (PD_PKT + headroom + len));
-    const hipError_t e = hipMemcpyAsync(db, img, total, hipMemcpyHostToDevice, vm->stream);
-    proc_enq(p);
+    p->img_n = total;
+    // an xdp_md process's first launch copies the image itself (interp.hip MODE_STEP); an sk_buff
+    // process's Load runs now and needs it on the device
+    const hipError_t e = upload ? hipMemcpyAsync(db, img, total, hipMemcpyHostToDevice, vm->stream) : hipSuccess;
+    if (upload) {
+        proc_enq(p);
+        p->uploaded = true;
+    }
     if (e != hipSuccess) {
         process_release(p, proc_fence(vm, p->last_seq));
         delete p;
@@ -2531,7 +2602,7 @@ int mimic_process_new(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32
     if (prog_id >= vm->progs.size()) return fail(vm, MIMIC_EINVAL, "no program with id '%u' is loaded", prog_id);
     if (vm->skb_leaked) return fail(vm, MIMIC_ENOTSUP, "xdp_md processes after sk_buff batches are not supported");
     return process_make(vm, prog_id, packet, len, headroom, tailroom, ingress_ifindex, rx_queue_index, egress_ifindex,
-                        nullptr, out);
+                        nullptr, false, out);
 }
 
 int mimic_process_new_skb(mimic_vm *vm, uint32_t prog_id, const void *packet, uint32_t len, uint32_t ifindex,
@@ -2547,7 +2618,7 @@ int mimic_process_new_skb_ctx(mimic_vm *vm, uint32_t prog_id, const void *packet
     // the packet memory is SKB_HEADROOM + len + SKB_TAILROOM with the frame at +SKB_HEADROOM
     // (context_sk_buff.go:42-107), run by the interpreter's stepping kernel as a one-packet batch
     const bool cust = custom && custom->flags;
-    int rc = process_make(vm, prog_id, packet, len, SKB_HEADROOM, SKB_TAILROOM, 0, 0, 0, cust ? custom : nullptr, out);
+    int rc = process_make(vm, prog_id, packet, len, SKB_HEADROOM, SKB_TAILROOM, 0, 0, 0, cust ? custom : nullptr, true, out);
     if (rc) return rc;
     mimic_process *p = *out;
     p->skb = true;
@@ -2825,6 +2896,10 @@ int mimic_process_packet(mimic_process *p, void *buf, size_t cap) {
     if (cap < M) return fail(p->vm, MIMIC_EINVAL, "buffer too small");
     mimic_vm *vm = p->vm;
     std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
+    if (!p->uploaded) {   // never launched: the packet memory is the NewProcess image
+        memcpy(buf, p->mem.host + PH_IMG + PD_PKT, M);
+        return (int)M;
+    }
     hipSetDevice(vm->s.device);
     // on the process's stream: behind its NewProcess upload and its launches
     const hipError_t e = hipMemcpyAsync(buf, p->d_pkt, M, hipMemcpyDeviceToHost, vm->stream);

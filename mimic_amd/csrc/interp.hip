@@ -105,7 +105,22 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
         if (__ballot(DR != nullptr) == 0) return;
     }
     const bool lane_valid = g < kp.lanes && (MODE != MODE_RESUME || DR);
-    if (MODE == MODE_STEP && threadIdx.x >= 64) step_warm(kp, threadIdx.x - 64, blockDim.x - 64);
+    // Process.Step / Run: the first launch of a process copies its NewProcess image (pinned host
+    // memory) into its device block, 16 bytes per thread and round; the first step_ins_n slots go to
+    // LDS (one round trip for all, then LDS reads instead of a cold scalar fetch per instruction)
+    extern __shared__ DInsn step_ins_[];
+    if (MODE == MODE_STEP) {
+        if (kp.step_img) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const uint32_t nq = kp.step_img_n >> 4;
+            for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x)
+                ((u32x4 *)kp.step_dst)[q] = ((const u32x4 *)kp.step_img)[q];
+            for (uint32_t b = (nq << 4) + threadIdx.x; b < kp.step_img_n; b += blockDim.x) kp.step_dst[b] = kp.step_img[b];
+        }
+        for (uint32_t q = threadIdx.x; q < kp.step_ins_n; q += blockDim.x) step_ins_[q] = kp.insns[q];
+        __syncthreads();
+        if (threadIdx.x >= 64) step_warm(kp, threadIdx.x - 64, blockDim.x - 64);
+    }
     Lane L;
     L.lane = g;
     L.cpu = STP ? STP->cpu : lane_cpu(kp, g);
@@ -275,7 +290,7 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
             if (cand != KEY_DONE && (__ballot(key != cand) & live) == 0) kw = cand;  // converged
             else kw = wave_min(key);                                                 // min-PC
             kw = (uint32_t)__builtin_amdgcn_readfirstlane((int)kw);
-            const DInsn in = cget(kp.insns, kw);    // scalar loads
+            const DInsn in = MODE == MODE_STEP && kw < kp.step_ins_n ? step_ins_[kw] : cget(kp.insns, kw);    // scalar loads
             const uint64_t act = __ballot(key == kw);
             const uint64_t wbefore = wsteps++;
             if (key == kw) {
@@ -673,7 +688,7 @@ extern "C" int mimic_launch_xdp(const KParams *kp, const KParams *d_kp, hipStrea
     const uint32_t blocks = (kp->lanes + 255) / 256;
     if (blocks == 0) return 0;
     static const bool w3 = [] { const char *e = getenv("MIMIC_INTERP_WAVES"); return e && e[0] == '3'; }();
-    if (kp->step) hipLaunchKernelGGL(mimic_xdp_step_kernel, dim3(blocks), dim3(256), 0, st, *kp);
+    if (kp->step) hipLaunchKernelGGL(mimic_xdp_step_kernel, dim3(blocks), dim3(256), (size_t)kp->step_ins_n * sizeof(DInsn), st, *kp);
     else if (w3) hipLaunchKernelGGL(mimic_xdp_kernel_w3, dim3(blocks), dim3(256), 0, st, d_kp);
     else hipLaunchKernelGGL(mimic_xdp_kernel, dim3(blocks), dim3(256), 0, st, d_kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -567,6 +567,17 @@ class Gen {
         lpf_on = pf && xpf.on && lpf_knob && !xpf_knob && !spread_on && !stage && !vc_lds && !lds_stack_on && !defer_mode &&
                  !hash_combine && lpf_safe();
         if (!lpf_on && !xpf_knob) xpf.on = false;   // (the one-packet-ahead form only on request)
+        if (spread_own) {
+            // Multi-batch launches (mimic_run_xdp_many): every thread runs its packets of batch 0, then
+            // of batch 1, ... (all batches have the same n, so the same packet indices), the block's
+            // LDS counter table accumulating over all of them and flushed once; the last packet of a
+            // batch prefetches the next batch's first descriptor.  many_n = 0: the one batch in kp.
+            if (pf) E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
+            E.line("  const uint32_t nb_ = kp.many_n ? kp.many_n : 1u;");
+            E.line("  bool bpre_ = false;   // this batch's first descriptor came with the previous batch's last packet");
+            E.line("  for (uint32_t bt_ = 0; bt_ < nb_; bt_++) {");
+            E.line("  const BatchRef br_ = kp.many_n ? cget(kp.many, bt_) : BatchRef{kp.pkt_data, kp.pkt_off, kp.pkt_len, kp.r0, kp.status, kp.steps, kp.err_pc, 0};");
+        }
         if (lpf_on) {
             const uint32_t D = kLpfD, XW = xpf.words;
             E.line("  // lane prefetch: packets 0..%u of the lane, descriptors + P%u slot %u window (data + %u, %u words)", D - 1,
@@ -609,10 +620,12 @@ class Gen {
             E.line("  nidx2_ = nidx_ != NO_PKT ? pkt_next(kp, nidx_, 1u, ex_begin, ex_count) : NO_PKT;");
             E.line("  if (nidx2_ != NO_PKT) { noff2_ = *gp(kp.pkt_off + nidx2_); nlen2_ = *gp(kp.pkt_len + nidx2_); }");
         } else if (pf) {
-            E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
             if (spread_own)
-                E.line("  if (oi_ != NO_PKT) { noff_ = *gp(kp.pkt_off + oi_); nlen_ = *gp(kp.pkt_len + oi_); }");
-            else if (spread_on)
+                E.line("  if (!bpre_ && oi_ != NO_PKT) { noff_ = *gp(br_.pkt_off + oi_); nlen_ = *gp(br_.pkt_len + oi_); } bpre_ = false;");
+            else
+                E.line("  uint64_t noff_ = 0; uint32_t nlen_ = 0;");
+            if (spread_own) {
+            } else if (spread_on)
                 E.line("  { const uint32_t n_ = blo_ + threadIdx.x; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else
                 E.line("  { const uint32_t n_ = pkt_index(kp, g, 0u, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
@@ -656,7 +669,10 @@ class Gen {
         } else if (pf) {
             E.line("    const uint64_t poff_ = noff_; const uint32_t plen_ = nlen_;");
             if (nt) E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = ld_nt(kp.pkt_off + n_); nlen_ = ld_nt(kp.pkt_len + n_); } }");
-            else if (spread_own) E.line("    if (j + 1u < oQ_) { const uint32_t n_ = OWN_IDX(j + 1u); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
+            else if (spread_own) {
+                E.line("    if (j + 1u < oQ_) { const uint32_t n_ = OWN_IDX(j + 1u); if (n_ != NO_PKT) { noff_ = *gp(br_.pkt_off + n_); nlen_ = *gp(br_.pkt_len + n_); } }");
+                E.line("    else if (bt_ + 1u < nb_ && oi_ != NO_PKT) { const BatchRef nx_ = cget(kp.many, bt_ + 1u); noff_ = *gp(nx_.pkt_off + oi_); nlen_ = *gp(nx_.pkt_len + oi_); bpre_ = true; }");
+            }
             else if (spread_on) E.line("    { const uint32_t n_ = i + 256u; if (n_ < bhi_) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
             else E.line("    { const uint32_t n_ = pkt_next(kp, i, j + 1, ex_begin, ex_count); if (n_ != NO_PKT) { noff_ = *gp(kp.pkt_off + n_); nlen_ = *gp(kp.pkt_len + n_); } }");
         }
@@ -719,7 +735,10 @@ class Gen {
             E.line("    const uint32_t T = kq_.tailroom_arr ? ld_nt(kq_.tailroom_arr + i) : kq_.tailroom;");
             if (pf) {
                 E.line("    const uint32_t len = plen_;");
-                E.line("    L.pkt = kq_.pkt_data + poff_;");
+                E.line("    L.pkt = %s + poff_;", spread_own ? "br_.pkt_data" : "kq_.pkt_data");
+            } else if (spread_own) {
+                E.line("    const uint32_t len = *gp(br_.pkt_len + i);");
+                E.line("    L.pkt = br_.pkt_data + *gp(br_.pkt_off + i);");
             } else if (nt) {
                 E.line("    const uint32_t len = ld_nt(kq_.pkt_len + i);");
                 E.line("    L.pkt = kq_.pkt_data + ld_nt(kq_.pkt_off + i);");
@@ -793,22 +812,26 @@ class Gen {
         else
             E.line("    {");
         E.line("#ifndef MIMIC_MEAS_NORES");
-        if (nt || ntres) {
-            E.line("    if (kq_.r0) st_nt(kq_.r0 + i, r0);");
-            E.line("    if (kq_.status) st_nt(kq_.status + i, (uint8_t)st_);");
-        } else {
-            E.line("    if (kq_.r0) *gp(kq_.r0 + i) = r0;");
-            E.line("    if (kq_.status) *gp(kq_.status + i) = (uint8_t)st_;");
+        {   // the owned form's results go to the batch of this iteration (br_)
+            const char *rb = spread_own ? "br_" : "kq_";
+            if (nt || ntres) {
+                E.line("    if (%s.r0) st_nt(%s.r0 + i, r0);", rb, rb);
+                E.line("    if (%s.status) st_nt(%s.status + i, (uint8_t)st_);", rb, rb);
+            } else {
+                E.line("    if (%s.r0) *gp(%s.r0 + i) = r0;", rb, rb);
+                E.line("    if (%s.status) *gp(%s.status + i) = (uint8_t)st_;", rb, rb);
+            }
+            if (census) E.line("    if (%s.steps) st_nt(%s.steps + i, coldn_);   // census: slow-path calls, not steps", rb, rb);
+            else if (memtime) E.line("    if (%s.steps) st_nt(%s.steps + i, (uint32_t)__builtin_amdgcn_s_memrealtime());", rb, rb);
+            else E.line("    if (%s.steps) st_nt(%s.steps + i, steps);", rb, rb);
+            if (memtime) E.line("    if (%s.err_pc) st_nt(%s.err_pc + i, (int32_t)mt0_);", rb, rb);
+            else E.line("    if (%s.err_pc) st_nt(%s.err_pc + i, epc_);", rb, rb);
         }
-        if (census) E.line("    if (kq_.steps) st_nt(kq_.steps + i, coldn_);   // census: slow-path calls, not steps");
-        else if (memtime) E.line("    if (kq_.steps) st_nt(kq_.steps + i, (uint32_t)__builtin_amdgcn_s_memrealtime());");
-        else E.line("    if (kq_.steps) st_nt(kq_.steps + i, steps);");
-        if (memtime) E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, (int32_t)mt0_);");
-        else E.line("    if (kq_.err_pc) st_nt(kq_.err_pc + i, epc_);");
         E.line("#endif");
         E.line("    }");
         E.line("    lane_steps += steps;");
         E.line("  }");
+        if (spread_own) E.line("  }   // batches");
         if (vc_on) E.line("  VC_FLUSH();");
         if (spread_own) {
             // the block's rows into the map: plain read-modify-writes (the block owns these vCPUs)

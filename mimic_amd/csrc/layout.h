@@ -137,6 +137,20 @@ enum Sched : uint32_t { SCHED_CHUNKED = 0, SCHED_INTERLEAVED = 1, SCHED_EXPLICIT
 enum CtxKind : uint32_t { CTX_XDP = 0, CTX_SKB = 1 };
 struct SkbRec;
 
+// mimic_run_xdp_many: the k-th batch of a multi-batch launch (its packets and results; every
+// batch of the launch has the same n, schedule and scalar context fields)
+#define MIMIC_MANY_MAX 8u
+struct BatchRef {
+    uint8_t *pkt_data;
+    const uint64_t *pkt_off;
+    const uint32_t *pkt_len;
+    uint64_t *r0;
+    uint8_t *status;
+    uint32_t *steps;
+    int32_t *err_pc;
+    uint64_t pad;
+};
+
 struct KParams {
     // program / static memory
     const DInsn *insns;
@@ -236,6 +250,17 @@ struct KParams {
     uint32_t cancel_any;
     // owned spread launches (jit.cpp spread_own): packets per thread, a divisor of per_lane
     uint32_t own_q;
+    // multi-batch owned launches (mimic_run_xdp_many): many_n batches, run one after another by
+    // every thread (0: the one batch above)
+    uint32_t many_n;
+    struct BatchRef many[MIMIC_MANY_MAX];
+    // single-process stepping: the process's first launch copies its NewProcess image (pinned,
+    // device-mapped host memory) into its device block itself (no copy ahead of the launch), and
+    // the stepping kernel stages the first step_ins_n instruction slots in LDS (dynamic LDS)
+    const uint8_t *step_img;
+    uint8_t *step_dst;
+    uint32_t step_img_n;
+    uint32_t step_ins_n;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

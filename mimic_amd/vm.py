@@ -641,6 +641,28 @@ class VM:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
         return results
 
+    def RunXDPMany(self, prog_id: int, batches: Sequence["XDPBatch"], results: Optional[Sequence["XDPResults"]] = None,
+                   stream=None, sync: bool = True) -> List["XDPResults"]:
+        """Several device batches of one program (mimic_run_xdp_many): up to 8 of one shape run as ONE
+        launch when the programs allow the owned spread kernel, each vCPU running its packets of
+        batch 0, then batch 1, ... (a processPool draining a backlog, vm.go:548-573); else one launch
+        per batch.  Not in the reference API."""
+        if results is None:
+            results = [XDPResults.empty(b.n, b.pkt_data.device) for b in batches]
+        k = len(batches)
+        bs, rs = (L.XDPBatch * max(k, 1))(), (L.XDPResults * max(k, 1))()
+        for q, (bt, rt) in enumerate(zip(batches, results)):
+            bt._c()
+            rt._c()
+            bs[q], rs[q] = bt._cstruct_obj, rt._cstruct_obj
+        st = stream.cuda_stream if stream is not None else None
+        rc = self.lib.mimic_run_xdp_many(self.h, prog_id, bs, rs, k, st)
+        if rc:
+            _check(self.h, rc, "RunXDPMany")
+        if sync:
+            _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
+        return list(results)
+
     def RunSKBBatch(self, prog_id: int, batch: "SKBBatch", results: Optional["XDPResults"] = None,
                     stream=None, sync: bool = True, ctx: Optional["Context"] = None,
                     ctx_per_packet: Optional[Sequence[Optional["Context"]]] = None) -> "XDPResults":
