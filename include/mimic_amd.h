@@ -270,6 +270,12 @@ typedef struct {
     const int32_t *cpu;         /* HOST array for MIMIC_SCHED_EXPLICIT */
     uint64_t step_budget;       /* 0 = MIMIC default */
     const mimic_skb_custom *custom;   /* DEVICE array [n] of user-given sock / flow keys, or NULL (none) */
+    /* DEVICE word (optional) the engine keeps for this batch's packet memory: 1 once a launch left
+     * every head- and tailroom byte zero, 0 (the caller's initial value) when unknown.  A launch that
+     * finds 1 skips reading the 96 room bytes per packet (Load hands the program zeroed rooms,
+     * context_sk_buff.go:42-107); a program store into a room sets it back to 0.  Reset it to 0 after
+     * writing the packet memory by other means, and give each set of packets its own word. */
+    uint32_t *rooms_state;
 } mimic_skb_batch;
 
 /* Batch form of: for each packet i { p := vm.NewProcess(prog, &LinuxContextSKBuff{Packet: pkt_i,

@@ -65,7 +65,7 @@ class XDPBatch(C.Structure):
 class SKBBatch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("schedule", C.c_uint32), ("pkt_data", C.c_void_p),
                 ("pkt_off", C.c_void_p), ("pkt_len", C.c_void_p), ("ifindex", C.c_uint32), ("pad", C.c_int32),
-                ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("custom", C.c_void_p)]
+                ("cpu", C.c_void_p), ("step_budget", C.c_uint64), ("custom", C.c_void_p), ("rooms_state", C.c_void_p)]
 
 
 # mimic_skb_custom (include/mimic_amd.h): a user-given sock / flow keys of one sk_buff context

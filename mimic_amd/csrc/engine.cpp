@@ -48,7 +48,8 @@ extern "C" int mimic_launch_skb_gather(const uint8_t *const *mem, uint32_t n, ui
                                        mimic_skb_custom *cust, const uint8_t *has_cust, hipStream_t st);
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
-                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse, hipStream_t st);
+                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse,
+                                     uint32_t *rooms_state, hipStream_t st);
 
 namespace {
 
@@ -1539,6 +1540,7 @@ struct SkbRun {     // the sk_buff part of a batch (mimic_run_skb)
     // processes whose Load ran at NewProcess (mimic_process_run_many): their derived record words,
     // absolute leak addresses (+ flags) and a zero base, gathered -- no prep kernel for this batch
     const uint64_t *pre_drv = nullptr, *pre_prefix = nullptr, *pre_base = nullptr;
+    uint32_t *rooms_state = nullptr;   // the batch's rooms-clean word (mimic_skb_batch.rooms_state) or null
 };
 struct StepRun {    // a stepped single process (mimic_process_*): its state, private memory and budget
     StepState *state;
@@ -1642,7 +1644,8 @@ static int run_skb_impl(mimic_vm *vm, uint32_t prog_id, const mimic_skb_batch *s
     b.pkt_len = sb->pkt_len;
     b.cpu = sb->cpu;
     b.step_budget = sb->step_budget;
-    const SkbRun r{sb->ifindex, sb->custom};
+    SkbRun r{sb->ifindex, sb->custom};
+    r.rooms_state = sb->rooms_state;
     return run_xdp_impl(vm, prog_id, &b, res, (hipStream_t)hip_stream, 0, &r, nullptr, cx);
 }
 
@@ -1678,7 +1681,7 @@ struct SkbInto {
 };
 static int skb_ensure(mimic_vm *vm, uint32_t n, hipStream_t st);
 static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, const SkbInto *into = nullptr,
-                       bool records = true, bool sparse = false) {
+                       bool records = true, bool sparse = false, uint32_t *rooms_state = nullptr) {
     const uint32_t n = b->n;
     if (vm->skb_stream && vm->skb_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->skb_stream));
     // batches released on a stream the caller may have destroyed since: ordered through their event
@@ -1696,7 +1699,7 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     static const bool rooms_zero = getenv("MIMIC_SKB_ROOMS_ZERO") && getenv("MIMIC_SKB_ROOMS_ZERO")[0] == '1';
     if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
                               vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : rooms_zero ? 2u : 1u,
-                              (sparse && !into) ? 1u : 0u, st))
+                              (sparse && !into) ? 1u : 0u, into ? nullptr : rooms_state, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;
     vm->skb_stream = st;
@@ -2225,8 +2228,9 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
         // a JIT kernel that walks the headers itself needs the footprints only; one that derives the
         // common frames' records itself (skb_load_fast): exception records only
         const bool own_recs = jit && ji.skb_walk, sparse = jit && ji.skb_fast;
-        rc = skb_prepare(vm, b, st, nullptr, !own_recs, sparse);
+        rc = skb_prepare(vm, b, st, nullptr, !own_recs, sparse, skb->rooms_state);
         if (rc) return rc;
+        kp.skb_rooms_state = skb->rooms_state;
         kp.skb_rec_built = own_recs ? 0u : sparse ? 2u : 1u;
         kp.ctx_kind = CTX_SKB;
         kp.skb_ifindex = skb->ifindex;

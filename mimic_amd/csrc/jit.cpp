@@ -1823,6 +1823,7 @@ class Gen {
     // fast-path conditions and values for an access of n bytes at address ga_ (see hint())
     struct Fast {
         std::string cond, val, store;
+        std::string scond = "";   // the store's condition when it differs from the load's
     };
     std::vector<Fast> fast_forms(uint32_t base, uint32_t n, const std::string &v) {
         std::vector<Fast> f;
@@ -1842,13 +1843,18 @@ class Gen {
             break;  // sk_buff fields: see skb_ctx_fast()
         default: {
             const std::string o = "(uint32_t)(ga_ - " + std::string(pa()) + ")";
+            // sk_buff packets: the fast STORE covers the frame only -- a store into a head- or tailroom
+            // takes the generic path, which marks the batch's rooms-clean word (runtime.h
+            // skb_room_mark); the same test on the loads cost the cfg-5 chain 2 VGPRs, its second wave
             if (stage) {
                 const std::string wo = "(uint32_t)(ga_ - " + std::string(pa()) + " - " + std::to_string(wb()) + "u)";
                 f.push_back({"(uint64_t)" + wo + " + " + N + " <= W_", ord("win_load(pwin_, tl_, " + wo + ", " + N + ")", n), ""});
             }
-            f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M", ord(std::string(nt ? "ld_n_nt" : "ld_n") + "(L.pkt + " + o + ", " + N + ")", n),
+            f.push_back({"(uint64_t)" + o + " + " + N + " <= L.M",
+                         ord(std::string(nt ? "ld_n_nt" : "ld_n") + "(L.pkt + " + o + ", " + N + ")", n),
                          "{ PKT_ST(L.pkt + " + o + ", " + N + ", " + ord(v, n) + ");" +
-                             (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }"});
+                             (stage ? " win_store_rel(pwin_, tl_, W_, " + o + ", " + std::to_string(wb()) + "u, " + N + ", " + ord(v, n) + ");" : "") + " }",
+                         ctx == CTX_SKB ? "(uint64_t)(uint32_t)(" + o + " - SKB_HEADROOM) + " + N + " <= (L.rec->len & ~SKB_LOAD_FAILED)" : ""});
             // the lane's cached per-CPU row (analyze_vc): every access inside the row while the
             // cache is valid is served here, so memory and registers never disagree
             if (vc_on && vc_lds)
@@ -1948,14 +1954,14 @@ class Gen {
         E.line("    ga_ = %s;", addr(base, off).c_str());
         if (!deferred && elided.count({cur_prog, i})) {   // the write happens in the lookup's cold path
             const auto f = fast_forms(base, n, val);
-            E.line("    if (!(%s)) %s{ %s%s }", f.at(0).cond.c_str(), hint_knob ? "[[unlikely]] " : "", base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
+            E.line("    if (!(%s)) %s{ %s%s }", (f.at(0).scond.empty() ? f.at(0).cond : f.at(0).scond).c_str(), hint_knob ? "[[unlikely]] " : "", base == 10 && !spec_use.empty() ? "spv_ = 0u; " : "",
                    cold("cold_store(kp, sp_, ga_, " + std::to_string(n) + "u, " + val + ")", i).c_str());
             return;
         }
         std::string pre = "    ";
         for (auto &f : fast_forms(base, n, val)) {
             if (f.store.empty()) continue;
-            E.line("%sif (%s) { %s; }", pre.c_str(), f.cond.c_str(), f.store.c_str());
+            E.line("%sif (%s) { %s; }", pre.c_str(), (f.scond.empty() ? f.cond : f.scond).c_str(), f.store.c_str());
             pre = "    else ";
         }
         if (fast_paths && ctx == CTX_SKB && hint(base) == HINT_CTX) {

@@ -261,6 +261,9 @@ struct KParams {
     uint8_t *step_dst;
     uint32_t step_img_n;
     uint32_t step_ins_n;
+    // sk_buff batches: the batch's rooms-clean word (mimic_skb_batch.rooms_state) or null; a program
+    // store into a head- or tailroom sets it to 0
+    uint32_t *skb_rooms_state;
 };
 
 // A process a JIT lane suspended at a slow path (defer mode): the registers the slot and its

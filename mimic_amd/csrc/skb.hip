@@ -69,13 +69,17 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(uint8
                                                                           const uint32_t *__restrict__ pkt_len,
                                                                           uint32_t n, uint64_t *__restrict__ rec,
                                                                           uint32_t rec_q, uint64_t *__restrict__ prefix,
-                                                                          uint32_t rooms, uint32_t sparse) {
+                                                                          uint32_t rooms, uint32_t sparse,
+                                                                          const uint32_t *__restrict__ rooms_state) {
     __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
     __shared__ uint64_t wtot[PREP_T / 64];
     uint32_t *win = (uint32_t *)area;
     const uint32_t t = threadIdx.x, i0 = blockIdx.x * PREP_T, i = i0 + t;
     if (i0 >= n) return;   // whole block past the batch (uniform: the barriers below are safe)
     const bool live = i < n;
+    // the batch's rooms-clean word (mimic_skb_batch.rooms_state): 1 = an earlier launch left every
+    // room zero and no program store has touched one since -- nothing to read (rooms 3)
+    if (rooms == 1 && rooms_state && *rooms_state == 1u) rooms = 3;
     SkbRec r;
     uint64_t f = 0;   // the leak footprint
     uint64_t flags = 0;   // skb.h SKB_PFX_*
@@ -104,10 +108,10 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(uint8
         rooms = 0;
 #endif
         // (rooms 0 / 1: loaded whatever `rooms` says, one straight-line load sequence for the wait
-        // counter; rooms 2: not read, zeroed below)
+        // counter; rooms 2: not read, zeroed below; rooms 3: known zero, not read)
         const u32x4u *hr = (const u32x4u *)(pkt - SKB_HEADROOM), *tr = (const u32x4u *)(pkt + L);
         u32x4u rh0 = {0, 0, 0, 0}, rh1 = rh0, rt[SKB_TAILROOM / 16];
-        if (rooms != 2) {
+        if (rooms < 2) {
             rh0 = hr[0];
             rh1 = hr[1];
 #pragma unroll
@@ -214,7 +218,8 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(uint8
 // ordering wait held every block's tail: 77 -> 94 us per 1 M packets.)
 #define BLK_T 1024u
 extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint64_t *bs, uint32_t nb, uint64_t *state,
-                                                                          uint64_t init_base, uint32_t use_init) {
+                                                                          uint64_t init_base, uint32_t use_init,
+                                                                          uint32_t *rooms_state) {
     __shared__ uint64_t wtot[BLK_T / 64];
     const uint32_t t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
     const uint32_t per = (nb + BLK_T - 1) / BLK_T, lo = t * per;
@@ -239,6 +244,9 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
         bs[lo + k] = o;
         o += v;
     }
+    // every room of the batch is zero once the chain has run (it zeroes the ones prep flagged) unless
+    // a program stores into one, which sets the word back to 0; prep read it already (stream order)
+    if (t == 0 && rooms_state) *rooms_state = 1u;
     if (t == 0) {
         const uint64_t base = use_init ? init_base : state[0];
         state[1] = base;
@@ -250,9 +258,9 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
                                    uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state, hipStream_t st) {
     hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
-                       rec, rec_q, prefix, 1u, 0u);
+                       rec, rec_q, prefix, 1u, 0u, (const uint32_t *)nullptr);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
-                       0ull, 0u);
+                       0ull, 0u, (uint32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -260,12 +268,13 @@ extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_
 // does not take only (SKB_PFX_EXC), every packet's flags in its prefix word
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
-                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse, hipStream_t st) {
+                                     uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse,
+                                     uint32_t *rooms_state, hipStream_t st) {
     if (n)
         hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
-                           rec, rec_q, prefix, rooms, sparse);
+                           rec, rec_q, prefix, rooms, sparse, (const uint32_t *)rooms_state);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
-                       init_base, use_init);
+                       init_base, use_init, rooms == 1 ? rooms_state : (uint32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

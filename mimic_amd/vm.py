@@ -1114,9 +1114,21 @@ class SKBBatch:
             b.cpu = None
         b.step_budget = self.step_budget
         b.custom = self.custom.data_ptr() if self.custom is not None else None
+        if getattr(self, "rooms_state", None) is None:
+            import torch
+
+            # the engine's rooms-clean word for this batch's packets (mimic_skb_batch.rooms_state)
+            self.rooms_state = torch.zeros(1, dtype=torch.int32, device=self.pkt_data.device)
+        b.rooms_state = self.rooms_state.data_ptr()
         self._cstruct_obj = b
         self._cstruct = C.byref(b)
         return self._cstruct
+
+    def PacketsWritten(self) -> None:
+        """The packet memory was written by other means than the engine's runs: the next run reads
+        every room again (mimic_skb_batch.rooms_state)."""
+        if getattr(self, "rooms_state", None) is not None:
+            self.rooms_state.zero_()
 
     @classmethod
     def layout(cls, lengths: Sequence[int], align: int = 64):

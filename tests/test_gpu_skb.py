@@ -7,7 +7,7 @@ import pytest
 
 import kat_skb
 from fuzz_skb import random_skb_program
-from harness import (Scenario, assert_same, assert_same_sequence, kernel_of, run_engine_skb, run_oracle_skb,
+from harness import (Scenario, assert_same, assert_same_sequence, build_engine, kernel_of, run_engine_skb, run_oracle_skb,
                      run_sequence_engine, run_sequence_oracle)
 from mimic_amd import workloads as W
 
@@ -227,3 +227,39 @@ def test_process_with_user_sock_and_flow_keys(gpu, name):
             assert p.Registers.R0 == ex["r0"], (name, k, hex(p.Registers.R0))
         p.Cleanup()
     vm.close()
+
+
+@pytest.mark.parametrize("exec_mode", ["jit", "interp"])
+def test_rooms_clean_word(gpu, exec_mode):
+    """mimic_skb_batch.rooms_state: one batch launched three times.  A program that reads a headroom
+    and a tailroom byte (R0 = tail << 8 | head) and then writes them must see zero rooms every time
+    (Load hands over zeroed rooms, context_sk_buff.go:42-107): its room stores set the word back to
+    0, so the next launch's prep reads the rooms and the chain zeroes them.  A program that never
+    touches a room leaves the word at 1 (the next prep reads no room) and stays exact."""
+    import mimic_amd as M
+    from mimic_amd import asm as A
+
+    S = A.SKB
+    rooms_rw, _ = A.assemble([
+        A.ldx(4, 2, 1, S["data"]), A.ldx(4, 3, 1, S["len"]), A.mov64_reg(4, 2), A.alu64("add", 4, 3, reg=True),
+        A.ldx(1, 5, 2, -1), A.ldx(1, 6, 4, 3),                  # headroom byte, tailroom byte
+        A.mov64_reg(0, 6), A.alu64("lsh", 0, 8), A.alu64("or", 0, 5, reg=True),
+        A.alu64("add", 5, 1), A.stx(1, 2, -1, 5), A.alu64("add", 6, 2), A.stx(1, 4, 3, 6),
+        A.exit_()])
+    quiet, _ = A.assemble([A.ldx(4, 2, 1, S["data"]), A.ldx(1, 0, 2, 0), A.exit_()])
+    buf, off, lens = W.make_skb_packets(3000, sizes=(60, 300, 1500), weights=(2, 1, 1), seed=41)
+    for name, raw, touches in (("rooms_rw", rooms_rw, True), ("quiet", quiet, False)):
+        sc = Scenario(vcpus=8, progs=[(name, raw, [])])
+        cpu = W.schedule_cpu(len(lens), 8, "chunked")
+        o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=1)
+        assert (o["status"] == 0).all() and (o["r0"] == 0).all() if touches else True
+        vm, maps, pids = build_engine(sc, ctx=1, exec_mode=exec_mode)
+        batch = M.SKBBatch.from_numpy(buf, off, lens, device="cuda:0", ifindex=1, schedule=M.SCHED_EXPLICIT, cpu=cpu)
+        for k in range(3):
+            e = vm.RunSKBBatch(pids[0], batch).numpy(len(lens))
+            for f in ("r0", "status", "steps"):
+                assert np.array_equal(np.asarray(o[f]).astype(np.int64), np.asarray(e[f]).astype(np.int64)), (name, k, f)
+            assert int(batch.rooms_state.item()) == (0 if touches else 1), (name, k)
+            vm.SKBRelease()
+        assert np.array_equal(o["pkt"], batch.pkt_data.cpu().numpy()), name
+        vm.close()

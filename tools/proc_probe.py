@@ -22,8 +22,15 @@ def main():
     out = {}
     buf, off, lens = W.make_packets(4096, seed=3)
     pk = [bytes(buf[int(o):int(o) + int(n)]) for o, n in zip(off, lens)]
-    for name in ("prog_pass8", "prog_classifier"):
-        p = getattr(W, name)()
+    from mimic_amd import asm as A
+
+    def loop_prog(n):   # n iterations of a 3-slot loop: the per-step cost once the code is warm
+        raw, rel = A.assemble([A.mov64_imm(1, n), A.mov64_imm(0, 0), "l", A.alu64("add", 0, 1, reg=True),
+                               A.alu64("add", 1, -1), A.jmp("jne", 1, 0, "l"), A.exit_()])
+        return W.Program(f"loop{n}", raw, rel, [])
+
+    for name in ("prog_pass8", "prog_classifier", "loop100", "loop2000"):
+        p = getattr(W, name)() if name.startswith("prog_") else loop_prog(int(name[4:]))
         sc = Scenario(vcpus=256, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
         vm, maps, pids = build_engine(sc)
         lib, hv, regs = vm.lib, vm.h, L.ProcessRegs()
