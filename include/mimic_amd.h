@@ -197,6 +197,14 @@ int mimic_map_read_values_range(mimic_vm *vm, uint32_t map_id, int32_t cpu_begin
                                 size_t cap);
 /* Sum over vCPUs [cpu_begin, cpu_end) of a per-CPU map's u64 values -> out[E] (device reduction). */
 int mimic_map_sum_u64(mimic_vm *vm, uint32_t map_id, int32_t cpu_begin, int32_t cpu_end, uint64_t *out, size_t cap);
+/* One hash table for two VMs (not in the reference API: its LinuxHashMap is shared by every process
+ * of a processPool, emulator_linux_map_hash.go:21-255; here by engines that each run a shard of the
+ * packets).  vm's map `map_id` uses owner's map `owner_map_id` -- same spec, same device -- as its
+ * memory: every insert, E2BIG, lookup and host operation of either VM sees the other's.  Call after
+ * both VMs created all their maps; the programs of both must not delete (every launch on the table
+ * is pop-only); the owner must outlive the other VM.  Host operations on a shared table wait for
+ * the whole device first. */
+int mimic_map_share(mimic_vm *vm, uint32_t map_id, mimic_vm *owner, uint32_t owner_map_id);
 /* MemoryController.GetEntryByObject(map).Addr */
 int mimic_map_addr(mimic_vm *vm, uint32_t map_id, uint32_t *addr_out);
 

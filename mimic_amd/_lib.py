@@ -141,6 +141,7 @@ EXPORTS = {
     "mimic_run_xdp": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPBatch), C.POINTER(XDPResults), C.c_void_p]),
     "mimic_run_xdp_many": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(XDPBatch), C.POINTER(XDPResults), C.c_uint32,
                                      C.c_void_p]),
+    "mimic_map_share": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     "mimic_run_skb": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(SKBBatch), C.POINTER(XDPResults), C.c_void_p]),
     "mimic_skb_release": (C.c_int, [C.c_void_p]),
     "mimic_jit_source_for_ctx": (C.c_long, [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_int32,

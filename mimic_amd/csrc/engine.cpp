@@ -79,6 +79,18 @@ struct HashMirror {
     uint32_t faults = 0;
 };
 
+// mimic_map_share: the VMs whose hash map of one spec is ONE table in the memory of the first
+// (the owner); each member's offsets point into it from its own arena
+struct ShareGroup {
+    struct Member {
+        void *vm;              // mimic_vm *
+        uint32_t map;
+        uint8_t *arena;        // that VM's arena when it joined (an arena that moves would strand the offsets)
+    };
+    std::vector<Member> members;
+    bool owner_gone = false;   // the owner VM was destroyed: the table's memory is gone
+};
+
 struct HostMap {
     std::string name;
     uint32_t type, family, key_size, value_size, max_entries, datasec;
@@ -95,6 +107,7 @@ struct HostMap {
     mutable bool may_tomb = false;
     mutable bool pop_dirty = false;   // a pop-only launch left head / avail to normalise (hashmap.h)
     std::shared_ptr<HashMirror> mir;  // hash families: the host image of the index
+    mutable std::shared_ptr<ShareGroup> share;   // mimic_map_share: one table with other VMs' maps
 };
 
 // can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
@@ -710,6 +723,18 @@ void mimic_vm_destroy(mimic_vm *vm) {
     if (!vm) return;
     hipSetDevice(vm->s.device);
     if (vm->stream) hipStreamSynchronize(vm->stream);
+    for (auto &m : vm->maps) {   // leave the shared tables (an owner takes its table's memory along)
+        if (!m.share) continue;
+        auto &mem = m.share->members;
+        if (!mem.empty() && mem[0].vm == vm) m.share->owner_gone = true;
+        for (size_t k = 0; k < mem.size(); k++)
+            if (mem[k].vm == vm) {
+                if (k == 0) hipDeviceSynchronize();   // the members' launches on the owner's table end first
+                mem.erase(mem.begin() + (long)k);
+                break;
+            }
+        m.share.reset();
+    }
     vm->blk.drain([](Blk &b) {
         hipFree(b.dev);
         if (b.host) hipHostFree(b.host);
@@ -1140,6 +1165,52 @@ static int flush_host(mimic_vm *vm) {
     return 0;
 }
 
+// ---- shared tables (mimic_map_share) ----------------------------------------------------------
+// every member's host image of a shared table is stale (a launch or host write of any member)
+static void share_stale(const HostMap &m) {
+    if (!m.share) return;
+    for (auto &mb : m.share->members) {
+        const HostMap &x = ((mimic_vm *)mb.vm)->maps[mb.map];
+        if (x.mir) x.mir->valid = false;
+    }
+}
+// a shared table can be used by this VM: its owner alive, no member's arena moved, no member's
+// programs delete (every launch on it is pop-only: hashmap.h h_insert_nolock)
+static int share_check(mimic_vm *vm, const HostMap &m) {
+    if (!m.share) return 0;
+    if (m.share->owner_gone) return fail(vm, MIMIC_ENOTSUP, "map '%s': the VM that owns the shared table was destroyed", m.name.c_str());
+    for (auto &mb : m.share->members) {
+        const mimic_vm *o = (const mimic_vm *)mb.vm;
+        if (o->arena != mb.arena)
+            return fail(vm, MIMIC_ENOTSUP, "map '%s': a VM sharing it created maps after the share (its arena moved)", m.name.c_str());
+        if (o->prog_deletes)
+            return fail(vm, MIMIC_ENOTSUP, "map '%s': shared tables take programs that never delete (map_delete_elem)", m.name.c_str());
+    }
+    return 0;
+}
+// before a host operation on a shared table: every member's staged writes and launches have
+// reached the device (a device-wide wait: the other VMs run on their own streams), and this VM's
+// image is fetched again
+static int share_pre(mimic_vm *vm, const HostMap &m) {
+    if (!m.share) return 0;
+    int rc = share_check(vm, m);
+    if (rc) return rc;
+    for (auto &mb : m.share->members) {
+        mimic_vm *o = (mimic_vm *)mb.vm;
+        if (o != vm && o->host_dirty && (rc = flush_host(o))) return fail(vm, rc, "shared map: %s", o->err.c_str());
+    }
+    HIP_OK(vm, hipDeviceSynchronize());
+    if (m.mir) m.mir->valid = false;
+    return 0;
+}
+// after a host write on a shared table: on the device at once, the members' images stale
+static int share_post(mimic_vm *vm, const HostMap &m, int rc) {
+    if (!m.share || rc < 0) return rc;
+    const int fr = flush_host(vm);
+    share_stale(m);
+    return fr ? fr : rc;
+}
+
 // the sequential hash algorithm on the image (hashmap.h h_find / h_probe_held / h_place_held /
 // h_fl_pop / h_fl_push with one thread): slot of the key or -1; *pos = its bucket, *freep = the
 // first reusable bucket on its probe path
@@ -1247,8 +1318,8 @@ int mimic_map_update(mimic_vm *vm, uint32_t id, const void *key, const void *val
     if (is_hash(m)) {
         if (m.family == FAM_HASH) cpu = 0;  // LinuxHashMap ignores cpuid
         else if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
-        if ((rc = mirror_ensure(vm, m))) return rc;
-        return mh_update(vm, m, key, value, cpu);
+        if ((rc = share_pre(vm, m)) || (rc = mirror_ensure(vm, m))) return rc;
+        return share_post(vm, m, mh_update(vm, m, key, value, cpu));
     }
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     if (m.key_size != 4) return fail(vm, MIMIC_EINVAL, "invalid key length, must be 4 bytes for array maps");
@@ -1288,7 +1359,7 @@ int mimic_map_lookup(mimic_vm *vm, uint32_t id, const void *key, int32_t cpu, ui
             if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
             b += (uint32_t)cpu * m.addr_period;
         }
-        if ((rc = mirror_ensure(vm, m))) return rc;
+        if ((rc = share_pre(vm, m)) || (rc = mirror_ensure(vm, m))) return rc;
         const KeyBytes ks{(const uint8_t *)key, m.key_size};
         uint32_t pos = 0, freep;
         const int32_t slot = mh_probe(vm, m, ks, h_hash(ks, m.key_size), &pos, &freep);
@@ -1311,14 +1382,15 @@ int mimic_map_delete(mimic_vm *vm, uint32_t id, const void *key) {
     if (rc) return rc;
     const HostMap &m = vm->maps[id];
     if (!is_hash(m)) return fail(vm, MIMIC_EINVAL, "can't delete from given LinuxMap");
-    if ((rc = mirror_ensure(vm, m))) return rc;
-    return mh_delete(vm, m, key);
+    if ((rc = share_pre(vm, m)) || (rc = mirror_ensure(vm, m))) return rc;
+    return share_post(vm, m, mh_delete(vm, m, key));
 }
 
 // live (key, slot) pairs of a hash map in table order
 static int hash_entries(mimic_vm *vm, const HostMap &m, uint8_t *keys, int32_t *slots, size_t cap_entries,
                         uint32_t *n_out) {
-    int rc = mirror_ensure(vm, m);
+    int rc = share_pre(vm, m);
+    if (!rc) rc = mirror_ensure(vm, m);
     if (!rc) rc = mirror_pages(vm, m, false, 0, (uint64_t)m.ht_cap * m.rec_q * 8);   // every record
     if (rc) return rc;
     const std::vector<uint64_t> &rec = m.mir->rec;
@@ -1370,9 +1442,45 @@ int mimic_map_read_values(mimic_vm *vm, uint32_t id, int32_t cpu, void *out, siz
     if ((rc = array_cpu(vm, m, cpu, &base))) return rc;
     uint64_t n = (uint64_t)m.max_entries * m.value_size;
     if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
-    if ((rc = flush_host(vm)) || (rc = settle(vm))) return rc;
+    if ((rc = share_pre(vm, m)) || (rc = flush_host(vm)) || (rc = settle(vm))) return rc;
     HIP_OK(vm, hipMemcpy(out, vm->arena + base, n, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+// mimic_map_share: vm's map `id` becomes the owner VM's map `owner_id` -- ONE table for both (the
+// reference's LinuxHashMap shared by every process of a pool, emulator_linux_map_hash.go:21-255):
+// every insert, E2BIG and lookup of either VM's launches and host operations sees the other's.
+int mimic_map_share(mimic_vm *vm, uint32_t id, mimic_vm *owner, uint32_t owner_id) {
+    if (!vm || !owner || vm == owner) return MIMIC_EINVAL;
+    int rc = map_check(vm, id);
+    if (rc) return rc;
+    if (owner_id >= owner->maps.size()) return fail(vm, MIMIC_ENOENT, "owner has no map %u", owner_id);
+    HostMap &m = vm->maps[id];
+    const HostMap &o = owner->maps[owner_id];
+    if (vm->s.device != owner->s.device)
+        return fail(vm, MIMIC_ENOTSUP, "shared tables live on one device (peer tables over xGMI are not built)");
+    if (!is_hash(m) || m.family != o.family || m.key_size != o.key_size || m.value_size != o.value_size ||
+        m.max_entries != o.max_entries || m.ncpu != o.ncpu || m.dev_stride != o.dev_stride || m.ht_cap != o.ht_cap ||
+        m.rec_q != o.rec_q || m.nlocks != o.nlocks || m.fl_cap != o.fl_cap)
+        return fail(vm, MIMIC_EINVAL, "map '%s': only a hash map of the same spec can share a table", m.name.c_str());
+    if (m.share) return fail(vm, MIMIC_EINVAL, "map '%s' already shares a table", m.name.c_str());
+    if ((rc = flush_host(vm)) || (rc = flush_host(owner)) || (rc = settle(vm)) || (rc = settle(owner))) return rc;
+    if (!o.share) {
+        o.share = std::make_shared<ShareGroup>();
+        o.share->members.push_back({owner, owner_id, owner->arena});
+    }
+    // this map's offsets now lead from this VM's arena into the owner's table (64-bit wraparound)
+    const uint64_t a = (uint64_t)(uintptr_t)vm->arena, b = (uint64_t)(uintptr_t)owner->arena;
+    m.dev_off = b + o.dev_off - a;
+    m.keys_dev_off = b + o.keys_dev_off - a;
+    m.ht_dev_off = b + o.ht_dev_off - a;
+    m.share = o.share;
+    m.share->members.push_back({vm, id, vm->arena});
+    m.pop_dirty = o.pop_dirty;
+    m.may_tomb = o.may_tomb;
+    share_stale(m);
+    vm->tables_dirty = true;   // the device map table carries the new offsets
+    return share_check(vm, m);
 }
 
 int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
@@ -1381,7 +1489,7 @@ int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
     const HostMap &m = vm->maps[id];
     if (m.type == 3) return fail(vm, MIMIC_ENOTSUP, "program arrays are not reset");   // ebpf.ProgramArray
     hipSetDevice(vm->s.device);
-    if ((rc = skb_settle(vm)) || (rc = flush_host(vm))) return rc;
+    if ((rc = share_pre(vm, m)) || (rc = skb_settle(vm)) || (rc = flush_host(vm))) return rc;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : vm->stream;
     if (vm->last_stream && vm->last_stream != st) HIP_OK(vm, hipStreamSynchronize(vm->last_stream));
     if (is_hash(m)) {   // one kernel: values, keys, index (interp.hip mimic_hash_reset_kernel)
@@ -1389,6 +1497,7 @@ int mimic_map_reset(mimic_vm *vm, uint32_t id, void *hip_stream) {
         const DMap dm = to_dmap(m);
         if (mimic_launch_hash_reset(vm->arena, &dm, st))
             return fail(vm, MIMIC_EDEVICE, "reset: %s", hipGetErrorString(hipGetLastError()));
+        share_stale(m);
         mirror_fresh(m);   // the image of the table the reset leaves
     } else {
         HIP_OK(vm, hipMemsetAsync(vm->arena + m.dev_off, 0, (size_t)m.dev_stride * m.ncpu, st));
@@ -1412,7 +1521,7 @@ int mimic_map_read_values_range(mimic_vm *vm, uint32_t id, int32_t cpu_begin, in
     const uint64_t row = (uint64_t)m.max_entries * m.value_size, n = row * (c1 - c0);
     if (cap < n) return fail(vm, MIMIC_EINVAL, "buffer too small");
     if (n == 0) return 0;
-    if ((rc = flush_host(vm)) || (rc = settle(vm))) return rc;
+    if ((rc = share_pre(vm, m)) || (rc = flush_host(vm)) || (rc = settle(vm))) return rc;
     if (m.dev_stride == row || c1 - c0 == 1)
         HIP_OK(vm, hipMemcpy(out, vm->arena + m.dev_off + (uint64_t)c0 * m.dev_stride, n, hipMemcpyDeviceToHost));
     else
@@ -1434,7 +1543,7 @@ int mimic_map_sum_u64(mimic_vm *vm, uint32_t id, int32_t cpu_begin, int32_t cpu_
         c1 = (uint32_t)cpu_end;
     }
     if (m.max_entries == 0) return 0;
-    if ((rc = flush_host(vm))) return rc;
+    if ((rc = share_pre(vm, m)) || (rc = flush_host(vm))) return rc;
     uint64_t *d = nullptr;
     HIP_OK(vm, hipMalloc(&d, m.max_entries * sizeof(uint64_t)));
     hipStream_t st = vm->last_stream ? vm->last_stream : vm->stream;
@@ -2251,6 +2360,14 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.hash_ro = (vm->prog_deletes || vm->prog_updates) ? 0u : 1u;
     for (auto &m : vm->maps) {
         if (!is_hash(m)) continue;
+        if (m.share) {   // one table with other VMs' maps: their staged host writes first
+            if ((rc = share_check(vm, m))) return rc;
+            for (auto &mb : m.share->members) {
+                mimic_vm *o = (mimic_vm *)mb.vm;
+                if (o != vm && o->host_dirty && (rc = flush_host(o))) return fail(vm, rc, "shared map: %s", o->err.c_str());
+            }
+            share_stale(m);   // this launch may write the table: every member's image
+        }
         const DMap dm = to_dmap(m);
         if (vm->prog_deletes && m.pop_dirty) {
             if (mimic_launch_hash_normalize(vm->arena, &dm, st))

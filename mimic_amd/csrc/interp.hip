@@ -284,14 +284,22 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
                 const uint32_t cz = ctx_done(kp, i);
                 if (cz) TERM(MIMIC_ERR_CANCELED - 1 + (int)cz, (int32_t)(key - pbase));
             }
-            const uint64_t live = __ballot(key != KEY_DONE);
-            if (live == 0) break;
             uint32_t kw;
-            if (cand != KEY_DONE && (__ballot(key != cand) & live) == 0) kw = cand;  // converged
-            else kw = wave_min(key);                                                 // min-PC
-            kw = (uint32_t)__builtin_amdgcn_readfirstlane((int)kw);
+            uint64_t act;
+            if (MODE == MODE_STEP) {
+                // one process, on lane 0 of wave 0: no min-PC scheduling (the other lanes are done)
+                kw = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+                if (kw == KEY_DONE) break;
+                act = 1;
+            } else {
+                const uint64_t live = __ballot(key != KEY_DONE);
+                if (live == 0) break;
+                if (cand != KEY_DONE && (__ballot(key != cand) & live) == 0) kw = cand;  // converged
+                else kw = wave_min(key);                                                 // min-PC
+                kw = (uint32_t)__builtin_amdgcn_readfirstlane((int)kw);
+                act = __ballot(key == kw);
+            }
             const DInsn in = MODE == MODE_STEP && kw < kp.step_ins_n ? step_ins_[kw] : cget(kp.insns, kw);    // scalar loads
-            const uint64_t act = __ballot(key == kw);
             const uint64_t wbefore = wsteps++;
             if (key == kw) {
                 const uint32_t pc = kw - pbase;     // PC of this instruction

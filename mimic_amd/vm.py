@@ -190,6 +190,13 @@ class LinuxMap:
         _check(vm.h, vm.lib.mimic_map_read_values(vm.h, self.id, cpuid, buf, max(n, 1)), "read values")
         return buf.raw[:n]
 
+    def Share(self, owner: "LinuxMap") -> None:
+        """This map (of another VM) becomes ONE table with `owner` (mimic_map_share): inserts, E2BIG,
+        lookups and host operations of either VM see the other's.  Not in the reference API."""
+        vm, ovm = self._vm, owner._vm
+        _check(vm.h, vm.lib.mimic_map_share(vm.h, self.id, ovm.h, owner.id), "share")
+        self._share_owner = owner   # the owner's VM must outlive this one
+
     def Reset(self, stream=None) -> None:
         """Not in the reference API: back to a freshly created map at the same addresses (zeroed
         values, hash maps empty with the freelist 0..E-1), queued on `stream` (mimic_map_reset)."""

@@ -1,0 +1,158 @@
+"""One hash table shared by two engines (mimic_map_share, LinuxMap.Share): north_star's cfg 4 "shared
+hash map (emulator_linux_map_hash.go) in HBM" -- the reference's LinuxHashMap is ONE table for every
+process of a pool, and a full table answers E2BIG (:174-181, R0 = 7 in the helper,
+emulator_linux_helpers.go:549).  Two VMs, each running a shard of the vCPUs, insert into the same
+device table.
+
+* sequential: shard A (vCPU 0) then shard B (vCPU 1), the two shards' flows together past E --
+  every packet's R0 / status / steps, every key's slot and value equal ONE oracle VM running A's
+  packets then B's on one table (the E2BIG packets included);
+* concurrent: both shards' launches in flight at once on two streams -- per key exact when the union
+  fits, and exactly E keys when it does not (which packets are refused depends on the interleaving,
+  as in the reference's pool);
+* host operations through either VM see the other's inserts."""
+import numpy as np
+import pytest
+
+from harness import Scenario, build_engine, build_oracle, kernel_of
+from mimic_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+PASS, DROP = 2, 1
+
+
+def _sc(E, V):
+    p = W.prog_flowtrack(max_entries=E)
+    return Scenario(vcpus=V, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+
+
+def jit_kernels():
+    return [kernel_of(_sc(4096, 2)), kernel_of(_sc(32768, 128)), kernel_of(_sc(4096, 128))]
+
+
+def _pair(sc, va, vb):
+    a = build_engine(sc, shard=(0, va))
+    b = build_engine(sc, shard=(va, vb))
+    b[1]["flows"].Share(a[1]["flows"])
+    return a, b
+
+
+def _batch(M, buf, off, lens, cpu):
+    return M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_EXPLICIT, cpu=cpu)
+
+
+def _oracle(sc, shards):
+    ovm, omids, opids = build_oracle(sc)
+    outs = [ovm.run_xdp_batch(opids[0], buf.copy(), off, lens, cpu, write_back=False) for buf, off, lens, cpu in shards]
+    m = omids["flows"]
+    vals = ovm.map_values(m, 0)
+    table = {bytes(k): (s, vals[s * 8:(s + 1) * 8]) for k, s in ovm.map_entries(m)}
+    ovm.close()
+    return outs, table
+
+
+def _table(fm):
+    vals = fm.Values(0)
+    return {bytes(k): (s, vals[s * 8:(s + 1) * 8]) for k, s in fm.Entries()}
+
+
+def test_two_shards_one_table_sequential_exact(gpu):
+    import mimic_amd as M
+
+    E = 4096
+    sc = _sc(E, 2)
+    sa = W.make_packets(6000, **W.IMIX, seed=W.SEED + 1)
+    sb = W.make_packets(6000, **W.IMIX, seed=W.SEED + 2)
+    shards = [sa + (np.zeros(6000, np.int32),), sb + (np.ones(6000, np.int32),)]
+    keys = {bytes(k) for s in (sa, sb) for k in W.flow_keys_np(*s)}
+    assert len(keys) > E + 1000   # the union overflows the table
+    outs, want = _oracle(sc, shards)
+    (va, ma, pa), (vb, mb, pb) = _pair(sc, 1, 1)
+    got = []
+    for (vm, pid), (buf, off, lens, cpu) in zip(((va, pa[0]), (vb, pb[0])), shards):
+        got.append(vm.RunXDPBatch(pid, _batch(M, buf, off, lens, cpu)).numpy(len(lens)))
+    for k, (o, e) in enumerate(zip(outs, got)):
+        for f in ("r0", "status", "steps", "err_pc"):
+            a, b = np.asarray(o[f]).astype(np.int64), np.asarray(e[f]).astype(np.int64)
+            bad = np.nonzero(a != b)[0]
+            assert len(bad) == 0, f"shard {k} {f} differs at {bad[:6]}"
+    assert (np.asarray(outs[1]["r0"]) == DROP).sum() > 500   # shard B met the full table: E2BIG
+    assert _table(ma["flows"]) == want
+    assert _table(mb["flows"]) == want   # the same table through the other VM
+    vb.close()
+    va.close()
+
+
+def _concurrent(E, n, seeds):
+    import torch
+
+    import mimic_amd as M
+
+    V = 64
+    sc = _sc(E, 2 * V)
+    sa = W.make_packets(n, **W.IMIX, seed=seeds[0])
+    sb = W.make_packets(n, **W.IMIX, seed=seeds[1])
+    ca = W.schedule_cpu(n, V, "interleaved").astype(np.int32)
+    cb = (W.schedule_cpu(n, V, "interleaved") + V).astype(np.int32)
+    (va, ma, pa), (vb, mb, pb) = _pair(sc, V, V)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    ra = va.RunXDPBatch(pa[0], _batch(M, *sa, ca), stream=s1, sync=False)
+    rb = vb.RunXDPBatch(pb[0], _batch(M, *sb, cb), stream=s2, sync=False)
+    torch.cuda.synchronize()
+    return sc, (sa, ca, ra.numpy(n)), (sb, cb, rb.numpy(n)), (va, ma), (vb, mb)
+
+
+def test_two_shards_concurrent_union_fits(gpu):
+    sc, (sa, ca, ea), (sb, cb, eb), (va, ma), (vb, mb) = _concurrent(32768, 20000, (W.SEED + 3, W.SEED + 4))
+    outs, want = _oracle(sc, [sa + (ca,), sb + (cb,)])
+    for o, e in ((outs[0], ea), (outs[1], eb)):
+        assert np.array_equal(np.asarray(o["r0"]).astype(np.int64), np.asarray(e["r0"]).astype(np.int64))
+        assert (np.asarray(e["status"]) == 0).all()
+    got = _table(ma["flows"])
+    assert {k: v[1] for k, v in got.items()} == {k: v[1] for k, v in want.items()}   # per key (slots: arrival order)
+    assert sorted(s for s, _ in got.values()) == list(range(len(want)))   # the first m freelist slots, each once
+    vb.close()
+    va.close()
+
+
+def test_two_shards_concurrent_overflow_fills_exactly_e(gpu):
+    E = 4096
+    sc, (sa, ca, ea), (sb, cb, eb), (va, ma), (vb, mb) = _concurrent(E, 20000, (W.SEED + 5, W.SEED + 6))
+    got = _table(ma["flows"])
+    assert len(got) == E and sorted(s for s, _ in got.values()) == list(range(E))
+    allk = {}
+    for (buf, off, lens), e in ((sa, ea), (sb, eb)):
+        kk, idx = W.flow_keys_np(buf, off, lens, with_index=True)   # packets that reach the map call
+        r0 = np.asarray(e["r0"])[idx]
+        for k, r in zip((bytes(x) for x in kk), r0):
+            allk[k] = allk.get(k, False) or r == PASS
+            if r == PASS:
+                assert k in got   # a packet that saw its flow tracked finds it in the table
+    assert set(got) <= set(allk)
+    for k, (_, v) in got.items():   # the program's value: key[0:8] * 0x01000193 ^ key[8:16] (prog_flowtrack)
+        lo, hi = int.from_bytes(k[:8], "little"), int.from_bytes(k[8:], "little")
+        assert int.from_bytes(v, "little") == ((lo * 0x01000193) & (2 ** 64 - 1)) ^ hi
+    vb.close()
+    va.close()
+
+
+def test_host_operations_through_either_vm(gpu):
+    import mimic_amd as M
+
+    sc = _sc(4096, 2)
+    (va, ma, pa), (vb, mb, pb) = _pair(sc, 1, 1)
+    fa, fb = ma["flows"], mb["flows"]
+    k1, k2 = bytes(range(16)), bytes(range(16, 32))
+    assert fb.Update(k1, (7).to_bytes(8, "little")) == 0   # through the sharer ...
+    assert fa.Lookup(k1) != 0 and fa.Lookup(k1) == fb.Lookup(k1)   # ... seen by the owner, same address
+    assert fa.Update(k2, (9).to_bytes(8, "little")) == 0
+    assert sorted(fb.Entries()) == sorted(fa.Entries()) == [(k1, 0), (k2, 1)]
+    buf, off, lens = W.make_packets(300, **W.IMIX, seed=W.SEED + 9)
+    va.RunXDPBatch(pa[0], _batch(M, buf, off, lens, np.zeros(300, np.int32)))
+    n_after = len(fa.Entries())
+    assert len(fb.Entries()) == n_after > 2   # the owner's launch, seen through the sharer
+    fb.Delete(k1)
+    assert fa.Lookup(k1) == 0
+    vb.close()
+    va.close()
