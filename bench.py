@@ -261,7 +261,7 @@ def default_batches(cfg_name: str, n: int) -> int:
 
 
 def read_profile(cfg_name: str, kernel: str, src_hash: str, n: int, vcpus: int, batches: int = 1,
-                 sched: str = "interleaved"):
+                 sched: str = "interleaved", per_launch: int = 1):
     """The committed rocprofv3 summary of exactly this kernel (source hash) on this workload."""
     import glob
 
@@ -273,7 +273,7 @@ def read_profile(cfg_name: str, kernel: str, src_hash: str, n: int, vcpus: int, 
             continue
         if (d.get("config") == cfg_name and d.get("kernel") == kernel and d.get("kernel_src_hash") == src_hash
                 and d.get("packets") == n and d.get("vcpus") == vcpus and d.get("batches", 1) == batches
-                and d.get("schedule", "interleaved") == sched):
+                and d.get("schedule", "interleaved") == sched and d.get("batches_per_launch", 1) == per_launch):
             best = dict(d, file=os.path.relpath(f, ROOT))
     return best
 
@@ -591,8 +591,10 @@ def main(argv=None):
         achieved = alg / avg_launch_s
         kernel = "mimic_jit_kernel" if vm.LastExec() in ("jit", "spread", "spread_own") else "mimic_xdp_kernel"
         src_hash = wl.kernel_src_hash(vpg if vm.LastExec() in ("spread", "spread_own") else 0, vm.LastExec() == "spread_own")
-        prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched)
-        prof_ns = (prof.get("kernel_stats") or {}).get("avg_ns") if prof else None
+        prof = read_profile(args.config, kernel, src_hash, n, vpg, nb, args.sched, K)
+        # a profiled launch ran K batches: its bytes and time per batch, like alg and avg_launch_s
+        prof_ns = (prof.get("kernel_stats") or {}).get("avg_ns") / K if prof and (prof.get("kernel_stats") or {}).get("avg_ns") else None
+        prof_bytes = prof["bytes_per_launch"] / K if prof and prof.get("bytes_per_launch") else None
         out = {
             "metric": "Mpkts/s (device-resident, one XDP program over 64-1500B batches)",
             "value": round(value, 3),
@@ -616,12 +618,12 @@ def main(argv=None):
             "mean_insns_per_packet": round(steps_timed / (n * ws * args.steps * K), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
-                         "traffic": prof["bytes_per_launch"] if prof else None,
-                         "traffic_over_algorithmic": round(prof["bytes_per_launch"] / alg, 3) if prof else None,
+                         "traffic": prof_bytes,
+                         "traffic_over_algorithmic": round(prof_bytes / alg, 3) if prof_bytes else None,
                          # the profile's measured bytes over the profile's own kernel time (one rocprofv3
                          # session: traffic and time from the same runs, not from this line's)
-                         "frac_on_traffic": round(prof["bytes_per_launch"] / (prof_ns * 1e-9) / HBM_PEAK, 5)
-                                            if prof_ns else None,
+                         "frac_on_traffic": round(prof_bytes / (prof_ns * 1e-9) / HBM_PEAK, 5)
+                                            if prof_ns and prof_bytes else None,
                          "profile_kernel_ms": round(prof_ns * 1e-6, 4) if prof_ns else None,
                          "valu_busy": prof.get("valu_busy") if prof else None,
                          "profile": prof["file"] if prof else None,

@@ -582,11 +582,12 @@ DEV int mem_load(const KParams &kp, const Lane &L, const Ref &R, uint32_t n, uin
     else v = ld_n(R.ptr + R.off, n);
     return 0;
 }
-// a store into an sk_buff packet's head- or tailroom (packet-memory offset o, n bytes): the batch's
-// rooms-clean word goes back to 0, so the next launch's prep reads the rooms again (skb.hip)
-DEV void skb_room_mark(const KParams &kp, const Lane &L, uint32_t o, uint32_t n) {
-    if (kp.skb_rooms_state && (o < SKB_HEADROOM || (uint64_t)o + n > (uint64_t)L.M - SKB_TAILROOM))
-        __hip_atomic_store(kp.skb_rooms_state, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// a store into an sk_buff's packet memory outside the JIT's frame-only fast store (jit.cpp: those stay
+// inside the frame): the batch's rooms-clean word goes back to 0, so the next launch's prep reads the
+// rooms again (skb.hip). Every such store marks, not only the head- / tailroom ones: the room test
+// here cost the batch interpreter 14 spilled VGPRs (tests/test_interp_regs.py)
+DEV void skb_room_mark(const KParams &kp) {
+    if (kp.skb_rooms_state) __hip_atomic_store(kp.skb_rooms_state, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 DEV int mem_store(const KParams &kp, Lane &L, const Ref &R, uint32_t n, uint64_t v) {
     if (R.rk == RK_UNRES) return MIMIC_ERR_MEM_UNRESOLVED;
@@ -598,7 +599,7 @@ DEV int mem_store(const KParams &kp, Lane &L, const Ref &R, uint32_t n, uint64_t
     else if (R.rk == RK_XDP) xdp_store(kp, L, R.off, n, v);
     else if (R.rk == RK_BEPKT) {
         st_n(R.ptr + R.off, n, bswap_n(v, n));
-        skb_room_mark(kp, L, R.off, n);
+        skb_room_mark(kp);
     } else st_n(R.ptr + R.off, n, v);
     return 0;
 }

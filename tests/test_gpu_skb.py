@@ -235,7 +235,9 @@ def test_rooms_clean_word(gpu, exec_mode):
     and a tailroom byte (R0 = tail << 8 | head) and then writes them must see zero rooms every time
     (Load hands over zeroed rooms, context_sk_buff.go:42-107): its room stores set the word back to
     0, so the next launch's prep reads the rooms and the chain zeroes them.  A program that never
-    touches a room leaves the word at 1 (the next prep reads no room) and stays exact."""
+    touches a room leaves the word at 1 (the next prep reads no room) and stays exact.  A program that
+    stores into the frame only keeps the word at 1 on the JIT (its frame-only fast store) and sets it
+    to 0 on the interpreter (whose every packet store marks, runtime.h skb_room_mark): both exact."""
     import mimic_amd as M
     from mimic_amd import asm as A
 
@@ -247,12 +249,15 @@ def test_rooms_clean_word(gpu, exec_mode):
         A.alu64("add", 5, 1), A.stx(1, 2, -1, 5), A.alu64("add", 6, 2), A.stx(1, 4, 3, 6),
         A.exit_()])
     quiet, _ = A.assemble([A.ldx(4, 2, 1, S["data"]), A.ldx(1, 0, 2, 0), A.exit_()])
+    frame_w, _ = A.assemble([A.ldx(4, 2, 1, S["data"]), A.mov64_imm(3, 0x5A), A.stx(1, 2, 0, 3),
+                             A.mov64_imm(0, 7), A.exit_()])   # the frame's first byte := 0x5A
     buf, off, lens = W.make_skb_packets(3000, sizes=(60, 300, 1500), weights=(2, 1, 1), seed=41)
-    for name, raw, touches in (("rooms_rw", rooms_rw, True), ("quiet", quiet, False)):
+    for name, raw, touches in (("rooms_rw", rooms_rw, True), ("quiet", quiet, False),
+                               ("frame_w", frame_w, exec_mode == "interp")):
         sc = Scenario(vcpus=8, progs=[(name, raw, [])])
         cpu = W.schedule_cpu(len(lens), 8, "chunked")
         o = run_oracle_skb(sc, buf, off, lens, cpu, ifindex=1)
-        assert (o["status"] == 0).all() and (o["r0"] == 0).all() if touches else True
+        assert (o["status"] == 0).all() and (o["r0"] == 0).all() if name == "rooms_rw" else True
         vm, maps, pids = build_engine(sc, ctx=1, exec_mode=exec_mode)
         batch = M.SKBBatch.from_numpy(buf, off, lens, device="cuda:0", ifindex=1, schedule=M.SCHED_EXPLICIT, cpu=cpu)
         for k in range(3):

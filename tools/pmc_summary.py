@@ -103,6 +103,7 @@ def main():
                                                          "its trailing per-batch step-count launches are left out)")
     ap.add_argument("--batches", type=int, default=0, help="batches the bench rotated over (0: its default)")
     ap.add_argument("--sched", default="interleaved")
+    ap.add_argument("--per-launch", type=int, default=1, help="batches one launch ran (bench.py --many K)")
     ap.add_argument("--name", default="", help="the pass directories' suffix (default: the config)")
     ap.add_argument("--spread", action="store_true", help="the run used the spread kernel (its source hash)")
     ap.add_argument("--own", action="store_true", help="... in its owned form (engine 'spread_own')")
@@ -123,7 +124,7 @@ def main():
            "kernel_src_hash": bench.kernel_src_hash_of(c, vcpus if (a.spread or a.own) else 0, a.own),
            "spread": a.spread or a.own, "spread_own": a.own,
            "packets": n, "vcpus": vcpus, "batches": a.batches or bench.default_batches(c, n),
-           "schedule": a.sched, "kernel_stats": ks}
+           "schedule": a.sched, "batches_per_launch": a.per_launch, "kernel_stats": ks}
     if fetch is not None and write is not None:
         out["fetch_size_kib_per_launch"] = fetch
         out["write_size_kib_per_launch"] = write
