@@ -180,6 +180,16 @@ struct mimic_vm {
     JitInfo jit_info[2]{};
     hipFunction_t jit_fn_cx[2] = {nullptr, nullptr};   // the same with the Run(ctx) check (launches given contexts)
     JitInfo jit_info_cx[2]{};
+    // Process.Run tiering (process_advance): a fresh xdp_md process runs on the interpreter's
+    // stepping kernel until the VM has made proc_jit_after Runs, then on the program set's
+    // single-process JIT form (jit.cpp Gen::proc) -- a compiled program instead of ~0.7 us of
+    // interpretation per step.  MIMIC_PROC_JIT=N at VM creation (default 32; 0 at once, -1
+    // never).  proc_jit: 0 not built, 1 built and usable, -1 not usable for this program set
+    int64_t proc_jit_after = 32;
+    uint64_t proc_runs = 0;
+    int proc_jit = 0;
+    hipFunction_t jit_fn_proc = nullptr;
+    JitInfo jit_info_proc{};
     // the spread kernel (jit.cpp analyze_spread, xdp_md only): 0 not built yet, 1 built, -1 the
     // program set does not allow it; spread_bad is the device word a spread launch marks when a
     // generic access reached per-CPU memory (spread_used: some launch could have marked it)
@@ -575,6 +585,8 @@ static int upload_tables(mimic_vm *vm) {
     }
     vm->jit_fn[0] = vm->jit_fn[1] = nullptr;
     vm->jit_fn_cx[0] = vm->jit_fn_cx[1] = nullptr;
+    vm->jit_fn_proc = nullptr;
+    vm->proc_jit = 0;
     vm->jit_fn_spread = nullptr;
     vm->spread_state = 0;
     vm->jit_fn_spread_own = nullptr;
@@ -707,6 +719,7 @@ int mimic_vm_create(const mimic_vm_settings *settings, mimic_vm **out) {
         const char *e = getenv("MIMIC_EXEC");
         vm->exec_mode = (e && !strcmp(e, "interp")) ? MIMIC_EXEC_INTERP : MIMIC_EXEC_JIT;
     }
+    if (const char *pj = getenv("MIMIC_PROC_JIT")) vm->proc_jit_after = *pj ? atoll(pj) : 32;
     if (vm->exec_mode != MIMIC_EXEC_INTERP && vm->exec_mode != MIMIC_EXEC_JIT) {
         delete vm;
         return MIMIC_EINVAL;
@@ -1665,6 +1678,10 @@ struct StepRun {    // a stepped single process (mimic_process_*): its state, pr
     const uint8_t *img = nullptr;
     uint8_t *img_dst = nullptr;
     uint32_t img_n = 0;
+    // Process.Run of a fresh xdp_md process on the single-process JIT form (vm->jit_fn_proc) on
+    // vCPU `cpu` (this engine's): a one-lane batch whose exit writes the state
+    bool jit = false;
+    int32_t cpu = 0;
 };
 
 struct CtxRun {      // Run(ctx) of a batch: one context for every packet, or one per packet (host array)
@@ -2027,6 +2044,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     if (rc) return rc;
     hipStream_t st = st_in ? st_in : vm->stream;
     const uint32_t cpu_lanes = step ? 1u : (uint32_t)vm->s.vcpu_count;
+    const bool proc_jit = step && step->jit;
     // EXPLICIT batches may hold processes whose CPU ID is unset (-1) or V: two extra lanes
     bool extra = false;
     if (!step && b->schedule == MIMIC_SCHED_EXPLICIT && b->cpu)
@@ -2068,7 +2086,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     kp.chunk_shift = shift;
     kp.max_tail_calls = (uint32_t)std::max(0, vm->s.max_tail_calls);
     kp.total_vcpus = (uint32_t)vm->s.vcpus;
-    kp.vcpu_begin = (uint32_t)vm->s.vcpu_begin;
+    kp.vcpu_begin = proc_jit ? (uint32_t)step->cpu : (uint32_t)vm->s.vcpu_begin;   // (lane 0 = the process's vCPU)
     kp.lanes = lanes;
     kp.cpu_lanes = cpu_lanes;
     kp.priv_lanes = step ? 1u : vm->priv_lanes;
@@ -2187,8 +2205,10 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     default:
         return fail(vm, MIMIC_EINVAL, "unknown schedule %u", b->schedule);
     }
-    bool jit = vm->exec_mode == MIMIC_EXEC_JIT && !step;   // stepping runs on the interpreter
-    if (jit && !vm->jit_fn[ctx]) {
+    // stepping runs on the interpreter; a Run the engine chose for the single-process JIT form
+    // (process_advance) on that form
+    bool jit = vm->exec_mode == MIMIC_EXEC_JIT && (!step || proc_jit);
+    if (jit && !proc_jit && !vm->jit_fn[ctx]) {
         std::string log;
         const std::vector<std::pair<uint32_t, uint32_t>> vc = vc_slots_of(vm);
         if (mimic_jit_compile(vm->s.device, mimic_jit_source(vm->h_dp, vm->h_all, ctx, &vm->jit_info[ctx], &vc),
@@ -2211,7 +2231,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             }
         }
     }
-    if (jit) {  // a loop-free kernel has no budget checks: tiny budgets run on the interpreter
+    if (jit && !proc_jit) {  // a loop-free kernel has no budget checks: tiny budgets run on the interpreter
         const uint64_t bound = mimic_jit_step_bound(vm->jit_info[ctx], kp.max_tail_calls);
         if (bound && kp.budget < bound) jit = false;
     }
@@ -2220,7 +2240,7 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
     // per lane, e.g. V = runtime.NumCPU(), vm.go:64).  MIMIC_SPREAD=0: never; =1: whenever the
     // program set allows it; default: when n >= 8 V.
     bool spread = false, own = false;
-    if (jit && !skb && b->n > 0 && (b->schedule == MIMIC_SCHED_CHUNKED || b->schedule == MIMIC_SCHED_INTERLEAVED)) {
+    if (jit && !step && !skb && b->n > 0 && (b->schedule == MIMIC_SCHED_CHUNKED || b->schedule == MIMIC_SCHED_INTERLEAVED)) {
         const char *sv = getenv("MIMIC_SPREAD");
         const int knob = vm->spread_mode >= 0 ? vm->spread_mode : sv && *sv ? atoi(sv) : -1;
         // the owned form, for batches of 2..256 packets per vCPU (Q packets per thread, below): by
@@ -2269,8 +2289,11 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
                 return fail(vm, MIMIC_EDEVICE, "JIT build failed: %s", log.c_str());
         }
     }
-    const JitInfo &ji = own ? vm->jit_info_spread_own : spread ? vm->jit_info_spread : cxk ? vm->jit_info_cx[ctx] : vm->jit_info[ctx];
-    hipFunction_t jfn = own ? vm->jit_fn_spread_own : spread ? vm->jit_fn_spread : cxk ? vm->jit_fn_cx[ctx] : vm->jit_fn[ctx];
+    const JitInfo &ji = proc_jit ? vm->jit_info_proc : own ? vm->jit_info_spread_own : spread ? vm->jit_info_spread
+                        : cxk ? vm->jit_info_cx[ctx] : vm->jit_info[ctx];
+    hipFunction_t jfn = proc_jit ? vm->jit_fn_proc : own ? vm->jit_fn_spread_own : spread ? vm->jit_fn_spread
+                        : cxk ? vm->jit_fn_cx[ctx] : vm->jit_fn[ctx];
+    if (proc_jit && (!jfn || !ji.proc_ok || !ji.karg)) return fail(vm, MIMIC_EDEVICE, "process: no single-process JIT kernel (engine)");
     uint32_t run_lanes = lanes;
     if (spread) {
         // owned: 256 / P vCPU lanes per block
@@ -2590,7 +2613,36 @@ static void process_regs(const mimic_process *p, mimic_process_regs *out) {
 // The kernel restores the state from the pinned host half and saves it there (interp.hip MODE_STEP);
 // nothing else of the process is in flight then (every operation on it ends with a sync, and its
 // NewProcess upload precedes this launch on the same stream).
-static int process_advance(mimic_process *p, uint64_t budget) {
+// Process.Run tiering (mimic_vm::proc_jit_after): the program set's single-process JIT form, built
+// once per program set; false when it is not usable (then Runs stay on the interpreter)
+static bool proc_jit_ready(mimic_vm *vm) {
+    if (vm->proc_jit == 0) {
+        vm->proc_jit = -1;
+        const std::vector<std::pair<uint32_t, uint32_t>> vc = vc_slots_of(vm);
+        std::string log;
+        JitInfo ji{};
+        hipFunction_t fn = nullptr;
+        const std::string src = mimic_jit_source(vm->h_dp, vm->h_all, CTX_XDP, &ji, &vc, false, nullptr, false, true);
+        if (ji.proc_ok && ji.karg && !mimic_jit_compile(vm->s.device, src, &fn, &log)) {
+            vm->jit_fn_proc = fn;
+            vm->jit_info_proc = ji;
+            vm->proc_jit = 1;
+        }
+    }
+    return vm->proc_jit > 0;
+}
+// a Run (not a Step) of a process that has not started, on one of this engine's vCPUs, with a
+// budget the loop-free form cannot exceed, once the VM has made enough Runs
+static bool proc_jit_use(mimic_process *p, uint64_t budget) {
+    mimic_vm *vm = p->vm;
+    if (vm->exec_mode != MIMIC_EXEC_JIT || vm->proc_jit_after < 0 || p->skb || p->h.started) return false;
+    if (p->cpu < vm->s.vcpu_begin || p->cpu >= vm->s.vcpu_begin + vm->s.vcpu_count) return false;
+    if (vm->proc_runs++ < (uint64_t)vm->proc_jit_after || !proc_jit_ready(vm)) return false;
+    const uint64_t bound = mimic_jit_step_bound(vm->jit_info_proc, (uint32_t)std::max(0, vm->s.max_tail_calls));
+    return bound && bound <= budget;
+}
+
+static int process_advance(mimic_process *p, uint64_t budget, bool run = false) {
     mimic_vm *vm = p->vm;
     std::lock_guard<std::recursive_mutex> lk(vm->run_mu);
     hipSetDevice(vm->s.device);
@@ -2633,7 +2685,19 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     r.err_pc = (int32_t *)(p->hres_dev + (PH_EPC - PH_RES));
     StepRun sr{p->hs_dev, p->priv.dev, p->priv_bytes, budget};
     sr.gen = p->gen;
-    if (!p->uploaded) {   // the kernel copies the image in before the process's first step
+    if (run && !upload_tables(vm) && proc_jit_use(p, budget)) {   // (the tables the form is built from first)
+        // the compiled program on lane 0 = the process's vCPU; a process whose image is still only
+        // in the pinned half runs on it there (its packet bytes read and written over the bus, no
+        // upload copy ahead of the launch: mimic_process_packet reads that half while !uploaded)
+        sr.jit = true;
+        sr.cpu = p->cpu;
+        if (!p->uploaded) {
+            uint8_t *img = p->mem.hdev + PH_IMG;
+            b.pkt_data = img + PD_PKT;
+            b.pkt_off = (const uint64_t *)img;
+            b.pkt_len = (const uint32_t *)(img + PD_LEN);
+        }
+    } else if (!p->uploaded) {   // the kernel copies the image in before the process's first step
         sr.img = p->mem.hdev + PH_IMG;
         sr.img_dst = p->mem.dev;
         sr.img_n = (uint32_t)p->img_n;
@@ -2649,7 +2713,7 @@ static int process_advance(mimic_process *p, uint64_t budget) {
     proc_enq(p);
     const hipError_t e = proc_sync(vm);   // the one host sync of Run / Step
     if (rc) return rc;
-    p->uploaded = true;
+    if (!sr.jit) p->uploaded = true;
     if (e != hipSuccess) return fail(vm, MIMIC_EDEVICE, "process: %s", hipGetErrorString(e));
     if (p->hres[PH_ST - PH_RES] == MIMIC_ERR_ENGINE_STATE || S->gen != p->gen)
         return fail(vm, MIMIC_EDEVICE, "process: the stepping launch found another process's state (engine assertion)");
@@ -2804,7 +2868,7 @@ int mimic_process_step(mimic_process *p, uint32_t n, mimic_process_regs *out) {
 int mimic_process_run(mimic_process *p, uint64_t budget, mimic_process_regs *out) {
     if (!p) return MIMIC_EINVAL;
     if (p->h.finished) return mimic_process_step(p, 0, out);
-    const int rc = process_advance(p, (uint64_t)p->h.steps + (budget ? budget : MIMIC_DEFAULT_BUDGET));
+    const int rc = process_advance(p, (uint64_t)p->h.steps + (budget ? budget : MIMIC_DEFAULT_BUDGET), true);
     if (rc) return rc;
     process_regs(p, out);
     return 0;
@@ -3106,7 +3170,11 @@ long mimic_jit_source_for_ctx(const void *const *progs, const uint32_t *n_slots,
 
 long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint32_t n_progs, int32_t ctx_kind,
                          const uint32_t *vc_slots, uint32_t n_vc, char *buf, size_t cap) {
+    // (ctx_kind | 0x100: the single-process form of an xdp_md set, what Process.Run tiers up to)
+    const bool proc = (ctx_kind & 0x100) != 0;
+    ctx_kind &= 0xff;
     if (ctx_kind != MIMIC_CTX_XDP && ctx_kind != MIMIC_CTX_SKB) return MIMIC_EINVAL;
+    if (proc && ctx_kind != MIMIC_CTX_XDP) return MIMIC_EINVAL;
     std::vector<HostProg> hp(n_progs);
     for (uint32_t p = 0; p < n_progs; p++) {
         std::string err;
@@ -3121,7 +3189,7 @@ long mimic_jit_source_vc(const void *const *progs, const uint32_t *n_slots, uint
         if (p >= dp.size() || s >= dp[p].n) return MIMIC_EINVAL;
         vc.push_back({dp[p].base + s, rb});
     }
-    const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr, &vc);
+    const std::string src = mimic_jit_source(dp, all, (uint32_t)ctx_kind, nullptr, &vc, false, nullptr, false, proc);
     if (buf && cap > src.size()) memcpy(buf, src.c_str(), src.size() + 1);
     return (long)src.size();
 }

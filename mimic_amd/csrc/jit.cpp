@@ -251,6 +251,11 @@ class Gen {
     bool vc_on = false;
     const SpreadReq *spread_req = nullptr;   // the VM's per-CPU arrays: spread mode is possible (analyze_spread)
     bool ctx_check = false;   // the kernel reads each packet's Run(ctx) context before its first step
+    // The single-process form (Process.Run of one process, engine.cpp process_advance): every exit
+    // stores r0..r10, the PC (the exit instruction's on a clean exit, as Step leaves it), the
+    // program and the steps into KParams::step.  No fused counter increments: their register is
+    // dead for the rest of the program, not after it (Run leaves every register readable).
+    bool proc = false;
     bool spread_on = false;
     bool spread_own = false;   // the owned form (SpreadReq::own): every packet of a block's vCPUs in the block
     uint32_t spread_map = 0, spread_n = 0, spread_row = 0;   // the counted map, counter width, E * S
@@ -322,8 +327,9 @@ class Gen {
             }
         if (careful_copies) sites *= 2;
         cold_sites = sites;
-        cold_inline = cold_mode == 2 || (cold_mode == 0 && sites <= kColdInlineSites);
-        defer_mode = !cold_inline && (cold_mode == 3 || cold_mode == 0) && !census && !stage && fast_paths;
+        // (the single-process form calls its slow paths: one lane, and hipRTC time is its tier-up cost)
+        cold_inline = !proc && (cold_mode == 2 || (cold_mode == 0 && sites <= kColdInlineSites));
+        defer_mode = !cold_inline && (cold_mode == 3 || cold_mode == 0) && !census && !stage && fast_paths && !proc;
         if (fast_paths) analyze_live();
         analyze_vc();
         if (forward)
@@ -406,7 +412,12 @@ class Gen {
             E.line("#define spread_add(k_) __hip_atomic_fetch_add((GAS spread_t *)(L.t_ptr + (uint32_t)(ga_ - L.t_lo)), (spread_t)(k_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)");
             E.line("#endif");
         }
-        E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
+        if (proc) {   // PGID_: the program whose code the TERM is in (program() redefines it)
+            E.line("#define PGID_ kp.entry_prog");
+            E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); pg_ = PGID_; goto L_term; } while (0)");
+        } else {
+            E.line("#define TERM(s_, pc_) do { st_ = (int)(s_); epc_ = (int32_t)(pc_); goto L_term; } while (0)");
+        }
         // Around a cold call the lane state and the argument / result registers go through the
         // Spill record (runtime.h); only what a cold path can change comes back.
         E.line("#define SPILL() do { sp_.L = L; sp_.r[0] = r0; sp_.r[1] = r1; sp_.r[2] = r2; sp_.r[3] = r3; sp_.r[4] = r4; "
@@ -435,7 +446,7 @@ class Gen {
         // per SIMD -- 262 144 lanes then run in one round on the 1 024 SIMDs.  cfg 4 (169 VGPRs,
         // 2 waves): 0.172 -> 0.137 ms per launch; cfg 2 and 3 fit 4 waves anyway.  Large kernels
         // (cfg 5) keep the compiler's choice: forcing 2 waves there spills 264 VGPRs (1.2 vs 0.7 ms).
-        const int wv = waves > 0 ? waves : (cold_inline ? 4 : 0);
+        const int wv = proc ? 0 : waves > 0 ? waves : (cold_inline ? 4 : 0);
         const std::string param = karg ? "const KParams kp_arg_" : "const KParams *__restrict__ kpp";
         if (wv > 0)
             E.line("%s", (std::string("extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(") +
@@ -767,6 +778,7 @@ class Gen {
         if (!spec_use.empty()) E.line("    spv_ = 1;");
         E.line("    int st_ = 0;");
         E.line("    int32_t epc_ = -1;");
+        if (proc) E.line("    uint32_t pg_ = kp.entry_prog;");
         if (ctx == CTX_SKB) E.line("    if (ls_) TERM(ls_, -1);");
         // Run(ctx): a context already done when the process would take its first step ends it
         // there (vm.go:344-349); a launch without contexts skips this on a uniform scalar test
@@ -829,6 +841,12 @@ class Gen {
         }
         E.line("#endif");
         E.line("    }");
+        if (proc) {   // Process.Run: the whole state (interp.hip step_save), the process done
+            E.line("    if (kq_.step) { StepState *S_ = kq_.step;");
+            E.line("      S_->r[0] = r0; S_->r[1] = r1; S_->r[2] = r2; S_->r[3] = r3; S_->r[4] = r4; S_->r[5] = r5;");
+            E.line("      S_->r[6] = r6; S_->r[7] = r7; S_->r[8] = r8; S_->r[9] = r9; S_->r[10] = r10;");
+            E.line("      S_->pc = epc_; S_->prog = pg_; S_->steps = steps; S_->status = st_; S_->started = 1u; S_->finished = 1u; }");
+        }
         E.line("    lane_steps += steps;");
         E.line("  }");
         if (spread_own) E.line("  }   // batches");
@@ -1576,6 +1594,7 @@ class Gen {
         if (p.n == 0) return;
         ctx_hints(p);
         cur_prog = p.id;
+        if (proc) E.line("#undef PGID_\n#define PGID_ %uu", p.id);
         std::vector<uint32_t> L = leaders(p);
         for (int careful = 0; careful < (careful_copies ? 2 : 1); careful++) {
             for (size_t b = 0; b < L.size(); b++) {
@@ -2028,7 +2047,7 @@ class Gen {
             break;
         case H_EXIT:  // inst.go:277-296
             if (!any_local) {
-                E.line("    TERM(MIMIC_OK, -1);");
+                E.line("    TERM(MIMIC_OK, %d);", proc ? (int)i : -1);   // Step leaves PC on the exit
                 break;
             }
             E.line("    if (L.nframes > 0) {");
@@ -2049,7 +2068,7 @@ class Gen {
             E.line("      default: TERM(MIMIC_ERR_ENGINE_HELPER, %u);", i);
             E.line("      }");
             E.line("    }");
-            E.line("    TERM(MIMIC_OK, -1);");
+            E.line("    TERM(MIMIC_OK, %d);", proc ? (int)i : -1);
             break;
         case H_CALL_LOCAL:  // BPF-to-BPF, inst.go:244-258
             E.line("    if (L.nframes >= MIMIC_MAX_FRAMES) TERM(MIMIC_ERR_CALL_DEPTH, %u);", i);
@@ -2143,7 +2162,11 @@ class Gen {
                     for (auto &q : P)
                         if (q.n) E.line("        case %u: goto P%u_0;", q.id, q.id);
                 }
-                E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);   // empty or unknown program
+                if (proc)   // the interpreter's process is in the (empty) program it tail-called
+                    E.line("        default: st_ = MIMIC_ERR_PC_OOB; epc_ = %d; pg_ = (uint32_t)(%s) < kp.nprogs ? (uint32_t)(%s) : PGID_; goto L_term;",
+                           (int)i, var, var);
+                else
+                    E.line("        default: TERM(MIMIC_ERR_PC_OOB, %u);", i);   // empty or unknown program
                 E.line("        }");
             };
             if (j >= 0) {
@@ -2340,7 +2363,7 @@ std::map<CacheKey, hipFunction_t> g_cache;
 
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
                              JitInfo *info, const std::vector<std::pair<uint32_t, uint32_t>> *vc_slots, bool no_early_loads,
-                             const SpreadReq *spread, bool ctx_check) {
+                             const SpreadReq *spread, bool ctx_check, bool proc) {
     std::vector<ProgView> v;
     for (size_t p = 0; p < progs.size(); p++) v.push_back(ProgView{(uint32_t)p, progs[p].n, progs[p].base, all.data() + progs[p].base});
     Gen g(v, ctx_kind);
@@ -2352,6 +2375,8 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
     // (MIMIC_JIT_CTXCHECK=1: the context variant from every entry point -- CPU compile tests)
     static const bool ctx_env = getenv("MIMIC_JIT_CTXCHECK") && getenv("MIMIC_JIT_CTXCHECK")[0] == '1';
     g.ctx_check = ctx_check || ctx_env;
+    g.proc = proc;
+    if (proc) g.inc_knob = false;
     std::string src = g.source();
     if (info) {
         info->checks_budget = g.careful_copies;
@@ -2366,6 +2391,8 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->spread = g.spread_on;
         info->spread_own = g.spread_own;
         info->hash_combine = g.hash_combine;
+        info->proc = proc;
+        info->proc_ok = proc && ctx_kind == CTX_XDP && !g.careful_copies && !g.defer_mode && !g.spread_on && !g.census;
         info->spread_map = g.spread_map;
         info->spread_n = g.spread_n;
         info->spread_roww = g.spread_n ? g.spread_row / g.spread_n : 0;

@@ -22,6 +22,10 @@ struct JitInfo {
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
     bool spread_own;     // ... in its owned form: a block runs every packet of its vCPUs (SpreadReq::own)
     bool hash_combine;   // pop-only inline inserts through the block combiner (hashmap.h h_comb_reserve)
+    // the single-process form (Process.Run, engine.cpp process_advance): every exit stores the
+    // process's registers, PC, program and steps into KParams::step; proc_ok = usable for it
+    // (loop-free, no BPF-to-BPF calls, no deferred slow paths, the exit's program known)
+    bool proc, proc_ok;
     // spread kernels: the counted per-CPU array, counter width, counters per row, LDS table rows
     uint32_t spread_map, spread_n, spread_roww, spread_rows;
 };
@@ -37,6 +41,7 @@ struct SpreadReq {
 };
 // ctx_kind: CtxKind of the batches the kernel runs
 // ctx_check: the variant for launches given Run(ctx) contexts (KParams::cancel_any)
+// proc: the single-process form for Process.Run (JitInfo::proc)
 // vc_slots: (kernel-wide index, E * S) of the LD_IMM64 slots whose constant is the object of a
 // per-CPU array whose row the lane value cache may hold: E * S a multiple of 8, at most
 // MIMIC_VC_MAX_ROW bytes (rows up to 32 bytes in registers, longer ones in LDS)
@@ -44,7 +49,7 @@ struct SpreadReq {
 std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<DInsn> &all, uint32_t ctx_kind,
                              JitInfo *info, const std::vector<std::pair<uint32_t, uint32_t>> *vc_slots = nullptr,
                              bool no_early_loads = false,
-                             const SpreadReq *spread = nullptr, bool ctx_check = false);
+                             const SpreadReq *spread = nullptr, bool ctx_check = false, bool proc = false);
 // 0 when the kernel checks the budget itself; else the most steps one packet can take -- a
 // batch with a smaller budget must run on the interpreter
 uint64_t mimic_jit_step_bound(const JitInfo &info, uint32_t max_tail_calls);

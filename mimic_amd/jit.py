@@ -30,21 +30,24 @@ def _progs_args(raws: Sequence[bytes]):
     return bufs, arr, ns
 
 
-def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int, int]] = (), spread=None) -> str:
+def kernel_source(raws: Sequence[bytes], ctx: int = CTX_XDP, vc: Sequence[Tuple[int, int, int]] = (), spread=None,
+                  proc: bool = False) -> str:
     """vc: (program index, slot, E * S) of the LD_IMM64 slots that name a per-CPU array whose
     per-vCPU row is at most 128 bytes, a multiple of 8 -- what a VM with those maps generates (see
-    ``vc_slots``).  spread: a ``spread_spec`` -- the VM's spread kernel instead (xdp_md)."""
+    ``vc_slots``).  spread: a ``spread_spec`` -- the VM's spread kernel instead (xdp_md).  proc: the
+    single-process form Process.Run tiers up to (MIMIC_PROC_JIT, xdp_md)."""
     if spread is not None:
         return spread_source(raws, *spread)[0]
     lib = _lib.load()
     keep, arr, ns = _progs_args(raws)
     flat = [v for t in vc for v in t]
     vca = (C.c_uint32 * max(len(flat), 1))(*flat)
-    n = lib.mimic_jit_source_vc(arr, ns, len(raws), ctx, vca, len(vc), None, 0)
+    kind = ctx | (0x100 if proc else 0)
+    n = lib.mimic_jit_source_vc(arr, ns, len(raws), kind, vca, len(vc), None, 0)
     if n < 0:
         raise ValueError(f"cannot decode programs ({n})")
     buf = C.create_string_buffer(n + 1)
-    lib.mimic_jit_source_vc(arr, ns, len(raws), ctx, vca, len(vc), buf, n + 1)
+    lib.mimic_jit_source_vc(arr, ns, len(raws), kind, vca, len(vc), buf, n + 1)
     return buf.value.decode()
 
 

@@ -646,6 +646,8 @@ class VM:
             _check(self.h, rc, "RunXDPBatch")
         if sync:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
+        else:   # the launch reads the batch until it ends: the results keep it (and the contexts) alive
+            results._inflight = (batch, _keep)
         return results
 
     def RunXDPMany(self, prog_id: int, batches: Sequence["XDPBatch"], results: Optional[Sequence["XDPResults"]] = None,
@@ -668,6 +670,9 @@ class VM:
             _check(self.h, rc, "RunXDPMany")
         if sync:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
+        else:
+            for bt, rt in zip(batches, results):
+                rt._inflight = bt
         return list(results)
 
     def RunSKBBatch(self, prog_id: int, batch: "SKBBatch", results: Optional["XDPResults"] = None,
@@ -686,6 +691,8 @@ class VM:
             _check(self.h, rc, "RunSKBBatch")
         if sync:
             _check(self.h, self.lib.mimic_sync(self.h, st), "sync")
+        else:
+            results._inflight = (batch, _keep)
         return results
 
     def CleanupProcesses(self, procs: Sequence["Process"]) -> None:

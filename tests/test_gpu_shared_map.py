@@ -28,7 +28,7 @@ def _sc(E, V):
 
 
 def jit_kernels():
-    return [kernel_of(_sc(4096, 2)), kernel_of(_sc(32768, 128)), kernel_of(_sc(4096, 128))]
+    return [kernel_of(_sc(4096, 2)), kernel_of(_sc(65536, 128)), kernel_of(_sc(4096, 128))]
 
 
 def _pair(sc, va, vb):
@@ -97,14 +97,18 @@ def _concurrent(E, n, seeds):
     cb = (W.schedule_cpu(n, V, "interleaved") + V).astype(np.int32)
     (va, ma, pa), (vb, mb, pb) = _pair(sc, V, V)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    ra = va.RunXDPBatch(pa[0], _batch(M, *sa, ca), stream=s1, sync=False)
-    rb = vb.RunXDPBatch(pb[0], _batch(M, *sb, cb), stream=s2, sync=False)
+    ba, bb = _batch(M, *sa, ca), _batch(M, *sb, cb)   # (alive until both launches end)
+    torch.cuda.synchronize()
+    ra = va.RunXDPBatch(pa[0], ba, stream=s1, sync=False)
+    rb = vb.RunXDPBatch(pb[0], bb, stream=s2, sync=False)
     torch.cuda.synchronize()
     return sc, (sa, ca, ra.numpy(n)), (sb, cb, rb.numpy(n)), (va, ma), (vb, mb)
 
 
 def test_two_shards_concurrent_union_fits(gpu):
-    sc, (sa, ca, ea), (sb, cb, eb), (va, ma), (vb, mb) = _concurrent(32768, 20000, (W.SEED + 3, W.SEED + 4))
+    E = 65536
+    sc, (sa, ca, ea), (sb, cb, eb), (va, ma), (vb, mb) = _concurrent(E, 20000, (W.SEED + 3, W.SEED + 4))
+    assert len({bytes(k) for s in (sa, sb) for k in W.flow_keys_np(*s)}) <= E   # the union fits (33 448 keys)
     outs, want = _oracle(sc, [sa + (ca,), sb + (cb,)])
     for o, e in ((outs[0], ea), (outs[1], eb)):
         assert np.array_equal(np.asarray(o["r0"]).astype(np.int64), np.asarray(e["r0"]).astype(np.int64))

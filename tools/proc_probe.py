@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Process.Run per call through the C ABI for a few programs (run under rocprofv3 --kernel-trace to
-split kernel time from host time): classifier (36 slots, packet + map), pass8 (8 slots, no memory)."""
+split kernel time from host time): classifier (36 slots, packet + map), pass8 (8 slots, no memory),
+loops (the interpreter's per-step cost).  Each on the stepping interpreter (MIMIC_PROC_JIT=-1) and
+on the single-process JIT form (MIMIC_PROC_JIT=0; loop programs stay on the interpreter)."""
 import ctypes as C
 import json
 import os
@@ -29,16 +31,22 @@ def main():
                                A.alu64("add", 1, -1), A.jmp("jne", 1, 0, "l"), A.exit_()])
         return W.Program(f"loop{n}", raw, rel, [])
 
-    for name in ("prog_pass8", "prog_classifier", "loop100", "loop2000"):
+    for name, mode in [(n, m) for n in ("prog_pass8", "prog_classifier", "prog_flowtrack", "loop100", "loop2000")
+                       for m in ("interp", "jit")]:
+        if name.startswith("loop") and mode == "jit":
+            continue
         p = getattr(W, name)() if name.startswith("prog_") else loop_prog(int(name[4:]))
         sc = Scenario(vcpus=256, maps=p.maps, progs=[(p.name, p.raw, p.relocs)])
+        os.environ["MIMIC_PROC_JIT"] = "-1" if mode == "interp" else "0"
         vm, maps, pids = build_engine(sc)
+        os.environ.pop("MIMIC_PROC_JIT")
         lib, hv, regs = vm.lib, vm.h, L.ProcessRegs()
         ts = {"new": [], "run": [], "free": []}
         for k in range(400):
             h = C.c_void_p()
             t0 = time.perf_counter()
             assert lib.mimic_process_new(hv, pids[0], pk[k], len(pk[k]), 0, 0, 1, 0, 0, C.byref(h)) == 0
+            assert lib.mimic_process_set_cpu(h, k % 256) == 0
             t1 = time.perf_counter()
             assert lib.mimic_process_run(h, 0, C.byref(regs)) == 0
             t2 = time.perf_counter()
@@ -47,8 +55,10 @@ def main():
             if k >= 100:
                 for key, d in zip(ts, (t1 - t0, t2 - t1, t3 - t2)):
                     ts[key].append(d * 1e6)
-        out[name] = {k: round(float(np.median(v)), 1) for k, v in ts.items()}
-        out[name]["steps"] = int(regs.steps)
+        key = f"{name}_{mode}"
+        out[key] = {k: round(float(np.median(v)), 1) for k, v in ts.items()}
+        out[key]["steps"] = int(regs.steps)
+        out[key]["exec"] = vm.LastExec()
         vm.close()
     print(json.dumps(out))
 
