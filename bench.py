@@ -36,7 +36,10 @@ HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table
 CONFIGS = {
     "pass8": dict(prog="prog_pass8", packets=1 << 20, sizes=(64,), weights=(1,), reads_packet=False,
                   workload="cfg1-shape: 8-insn XDP_PASS over 1M x 64B xdp_md (reads ctx fields, no packet bytes)"),
-    "classifier": dict(prog="prog_classifier", packets=1 << 20, sizes=(64,), weights=(1,),
+    # many: batches per launch by default (mimic_run_xdp_many: a processPool draining its backlog,
+    # vm.go:548-573; every batch's packets all run, ms_per_step stays per 1M-packet batch); --many 1
+    # is the one-batch-per-launch line
+    "classifier": dict(prog="prog_classifier", packets=1 << 20, sizes=(64,), weights=(1,), many=5,
                        workload="cfg2: 1M x 64B xdp_md, 36-slot parse+hash DROP/PASS classifier, "
                                 "per-CPU array E=4 S=8"),
     "parse5": dict(prog="prog_parse5", packets=1 << 24, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 18,
@@ -321,9 +324,10 @@ def parse_args(argv=None):
                     help="distinct input batches the timed launches rotate over (default: enough that the "
                          f"working set exceeds {ROTATE_BYTES >> 20} MiB, so no batch is served from the "
                          "256 MiB Infinity Cache)")
-    ap.add_argument("--many", type=int, default=1,
+    ap.add_argument("--many", type=int, default=0,
                     help="batches per launch (mimic_run_xdp_many, up to 8: one owned-spread launch runs K of the "
-                         "rotated batches back to back); --steps counts launches, ms_per_step stays per batch")
+                         "rotated batches back to back); --steps counts launches, ms_per_step stays per batch "
+                         "(0: the config's default, 5 for the classifier, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-resident", action="store_true", help="skip the PCIe-inclusive rate")
@@ -505,7 +509,7 @@ def main(argv=None):
 
     reset = [maps[m["name"]] for m in wl.maps] if cfg.get("reset_maps") else []
 
-    K = max(1, args.many)
+    K = max(1, args.many or min(cfg.get("many", 1), nb))   # (the default never repeats a batch in a launch)
     if K > 1 and (wl.skb or reset or nb % K and nb > K):
         sys.stderr.write("bench.py: --many needs an xdp_md config without map resets and a batch count K divides\n")
         return 2

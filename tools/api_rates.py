@@ -56,7 +56,7 @@ def main():
         pr.Cleanup()
         return r0
 
-    for k in range(20):
+    for k in range(64):   # past the Run tier-up (MIMIC_PROC_JIT, 32 Runs) and its one hipRTC build
         one_xdp(k)
     t0 = time.perf_counter()
     for k in range(args.calls):
@@ -120,6 +120,23 @@ def main():
         lat.append((time.perf_counter() - t0) * 1e6)
     out["process_run_xdp_cabi_split_us"] = {k: round(float(np.median(v)), 1) for k, v in parts.items()}
     out["process_run_xdp_cabi_split_us"]["torch_op_plus_sync"] = round(float(np.median(lat)), 1)
+    out["process_run_xdp_cabi_split_us"]["run_exec"] = vm.LastExec()
+    # the same C-ABI calls on a VM that never tiers up (every Run on the stepping interpreter)
+    os.environ["MIMIC_PROC_JIT"] = "-1"
+    vmi, _, pidsi = build_engine(sc)
+    del os.environ["MIMIC_PROC_JIT"]
+    hvi = vmi.h
+    runs = []
+    for k in range(args.calls):
+        h = C.c_void_p()
+        lib.mimic_process_new(hvi, pidsi[0], pk[k], len(pk[k]), 0, 0, c0.IngessIfIndex, 0, 0, C.byref(h))
+        lib.mimic_process_set_cpu(h, k % V)
+        t0 = time.perf_counter()
+        lib.mimic_process_run(h, 0, C.byref(regs))
+        runs.append((time.perf_counter() - t0) * 1e6)
+        lib.mimic_process_free(h)
+    out["process_run_xdp_cabi_split_us"]["run_interp"] = round(float(np.median(runs[32:])), 1)
+    vmi.close()
 
     # ---- ProcessPool, xdp_md jobs ------------------------------------------------------------------
     n = args.xdp_jobs

@@ -12,12 +12,12 @@ TAG=$T bash tools/run_driver.sh || exit 1
 for c in classifier parse5 flowtrack flowtrack_insert skb pass8; do
   $B --config $c > $D/bench_$c.json 2> $D/bench_$c.err || { tail -20 $D/bench_$c.err; exit 1; }
 done
-$B --config classifier --many 5 > $D/bench_classifier_many5.json 2> $D/bench_classifier_many5.err || exit 1
+$B --config classifier --many 1 > $D/bench_classifier_many1.json 2> $D/bench_classifier_many1.err || exit 1   # one batch per launch
 fi
 if [ "${PART:-2}" = 2 ]; then
 mkdir -p $D
-$B --config classifier --vcpus 256 > $D/bench_classifier_v256.json 2> $D/bench_classifier_v256.err || exit 1
-$B --config classifier --sched chunked > $D/bench_classifier_chunked.json 2> $D/bench_classifier_chunked.err || exit 1
+$B --config classifier --many 1 --vcpus 256 > $D/bench_classifier_v256.json 2> $D/bench_classifier_v256.err || exit 1
+$B --config classifier --many 1 --sched chunked > $D/bench_classifier_chunked.json 2> $D/bench_classifier_chunked.err || exit 1
 $B --config classifier --steps 20 > $D/bench_classifier_20steps.json 2> $D/bench_classifier_20steps.err || exit 1
 $B --config flowtrack --rccl > $D/bench_flowtrack_rccl.json 2> $D/bench_flowtrack_rccl.err || exit 1
 for c in classifier flowtrack; do   # the N-rank path at N = 2, both engines on GPU 0, gloo collectives
