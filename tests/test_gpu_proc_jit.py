@@ -148,3 +148,50 @@ def test_tier_up_after_n_runs(gpu):
     assert got == ["interp"] * 3 + ["jit"] * 3
     assert _run(vm, pids[0], pkt, cpu=-1)["exec"] == "interp"   # no CPU ID: the interpreter
     vm.close()
+
+
+def test_processes_from_many_threads(gpu):
+    """processPool's pattern: NewProcess / SetCPUID / Run / Step / Cleanup from several
+    threads on one VM at once -- the engine serialises them per VM and recycles process blocks
+    behind fences.  Every process's R0 equals the oracle's for its packet, and the per-CPU counters
+    equal the oracle's (sums: the interleaving of the threads does not change them)."""
+    import threading
+
+    from harness import build_oracle
+
+    sc = _wl("prog_classifier")
+    n, T = 1200, 4
+    buf, off, lens = W.make_packets(n, **W.IMIX, seed=W.SEED + 29)
+    pk = [bytes(buf[int(o):int(o) + int(m)]) for o, m in zip(off, lens)]
+    cpus = [k % 64 for k in range(n)]
+    ovm, omids, opids = build_oracle(sc)
+    want = ovm.run_xdp_batch(opids[0], buf.copy(), off, lens, np.array(cpus, np.int32), ingress=np.ones(n, np.int32),
+                             write_back=False)
+    wmap = [ovm.map_values(omids[sc.maps[0]["name"]], c) for c in range(64)]
+    ovm.close()
+    vm, maps, pids = _engine(sc, 8)
+    got = [None] * n
+    errs = []
+
+    def work(t):
+        try:
+            for k in range(t, n, T):
+                p = vm.NewProcess(pids[0], M.LinuxContextXDP(Packet=pk[k], IngessIfIndex=1))
+                p.SetCPUID(cpus[k])
+                if k % 7 == 0:   # a few stepped first: those stay on the interpreter
+                    p.Step()
+                p.Run()
+                got[k] = p.Registers.R0
+                p.Cleanup()
+        except Exception as e:   # noqa: BLE001 (reported below)
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:3]
+    assert got == [int(v) for v in np.asarray(want["r0"])]
+    assert [bytes(maps[sc.maps[0]["name"]].Values(c)) for c in range(64)] == [bytes(v) for v in wmap]
+    vm.close()
