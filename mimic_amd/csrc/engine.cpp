@@ -40,6 +40,7 @@ extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st);
 extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t force, hipStream_t st);
 extern "C" int mimic_launch_hash_reset(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st);
+extern "C" int mimic_launch_hash_compact(uint8_t *arena, const DMap *m, hipStream_t st);
 extern "C" int mimic_launch_spread_reduce(const void *part, uint32_t nblocks, uint32_t lanes, uint32_t roww, uint32_t n,
                                           uint8_t *dst, uint64_t stride, hipStream_t st);
 extern "C" int mimic_launch_sum_u64(const uint8_t *base, uint64_t stride, uint32_t nvals, uint32_t cpus, uint64_t *out,
@@ -108,6 +109,7 @@ struct HostMap {
     mutable bool pop_dirty = false;   // a pop-only launch left head / avail to normalise (hashmap.h)
     std::shared_ptr<HashMirror> mir;  // hash families: the host image of the index
     mutable std::shared_ptr<ShareGroup> share;   // mimic_map_share: one table with other VMs' maps
+    mutable bool chunk = false;   // the VM's chunk map (layout.h HT_F_CHUNK), picked at the table upload
 };
 
 // can the JIT's lane value cache hold a vCPU's row of this map (jit.cpp analyze_vc)?
@@ -537,6 +539,7 @@ static DMap to_dmap(const HostMap &m) {
     d.rec_q = m.rec_q;
     d.nlocks = m.nlocks;
     d.fl_cap = m.fl_cap;
+    d.hflags = m.chunk ? HT_F_CHUNK : 0u;
     return d;
 }
 
@@ -595,6 +598,14 @@ static int upload_tables(mimic_vm *vm) {
     std::vector<DProg> dp = vm->h_dp;
     all.push_back(DInsn{0, 0, 0});  // keep the array non-empty
     std::vector<DMap> dm;
+    // the chunk map (hashmap.h MIMIC_HASH_CHUNK): the first hash map not shared with another VM whose
+    // compaction fits one kernel's LDS -- one per VM, so a block never waits for positions of one map
+    // while it holds a chunk of another
+    bool picked = false;
+    for (auto &m : vm->maps) {
+        m.chunk = !picked && m.family == FAM_HASH && !m.share && m.max_entries >= 1 && m.max_entries <= HT_CHUNK_MAXE;
+        picked |= m.chunk;
+    }
     for (auto &m : vm->maps) dm.push_back(to_dmap(m));
     if (dm.empty()) dm.push_back(DMap{});
     if (dp.empty()) dp.push_back(DProg{});
@@ -915,9 +926,11 @@ int mimic_map_create(mimic_vm *vm, const mimic_map_spec *spec, uint32_t *map_id)
         const uint64_t rec_bytes = (uint64_t)m.ht_cap * m.rec_q * 8;
         const uint64_t lock_off = 2 * rec_bytes, fl_off = lock_off + (uint64_t)m.nlocks * 4,
                        ctl_off = (fl_off + (uint64_t)m.fl_cap * 4 + 127) & ~127ull;   // hashmap.h h_ctl
-        if (!rc) rc = arena_reserve(vm, ctl_off + sizeof(HashCtl), &m.ht_dev_off);
+        // (+ the chunked reservations' slot bits, slot buckets and handed-back remainders)
+        if (!rc) rc = arena_reserve(vm, ctl_off + sizeof(HashCtl) + ht_ext_bytes(spec->max_entries), &m.ht_dev_off);
         if (rc) return rc;
         HIP_OK(vm, hipMemset(vm->arena + m.ht_dev_off, 0xff, rec_bytes));
+        HIP_OK(vm, hipMemset(vm->arena + m.ht_dev_off + ctl_off + sizeof(HashCtl), 0, ht_ext_bytes(spec->max_entries)));
         std::vector<int32_t> fl(m.fl_cap, -1);
         for (uint32_t i = 0; i < spec->max_entries; i++) fl[i] = (int32_t)i;  // freelist <- 0..E-1 (:61-64)
         HIP_OK(vm, hipMemcpy(vm->arena + m.ht_dev_off + fl_off, fl.data(), fl.size() * 4, hipMemcpyHostToDevice));
@@ -1493,6 +1506,7 @@ int mimic_map_share(mimic_vm *vm, uint32_t id, mimic_vm *owner, uint32_t owner_i
     m.may_tomb = o.may_tomb;
     share_stale(m);
     vm->tables_dirty = true;   // the device map table carries the new offsets
+    owner->tables_dirty = true;   // (and the owner's map is no longer its chunk map)
     return share_check(vm, m);
 }
 
@@ -1995,7 +2009,7 @@ static int spread_check(mimic_vm *vm) {
             ht_offsets(m, &rb, &fo, &co);
             uint32_t f = 0;
             HIP_OK(vm, hipMemcpy(&f, vm->arena + m.ht_dev_off + co + offsetof(HashCtl, comb_fault), 4, hipMemcpyDeviceToHost));
-            if (f) return fail(vm, MIMIC_EDEVICE, "map '%s': a block combiner of freelist reservations gave up (engine fault)",
+            if (f) return fail(vm, MIMIC_EDEVICE, "map '%s': a block combiner or chunk refill of freelist reservations gave up (engine fault)",
                                m.name.c_str());
         }
     }
@@ -2453,6 +2467,14 @@ static int run_xdp_impl(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *b
             return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
         HIP_OK(vm, hipEventRecord(vm->kp_ev[slot], st));   // the slot is free again once this passes
         vm->kp_used[slot] = true;
+    }
+    if (jit && ji.hash_chunk) {   // the chunk map's holes filled (interp.hip mimic_hash_compact_kernel)
+        for (const HostMap &m : vm->maps) {
+            if (!m.chunk) continue;
+            const DMap dm = to_dmap(m);
+            if (mimic_launch_hash_compact(vm->arena, &dm, st))
+                return fail(vm, MIMIC_EDEVICE, "launch: %s", hipGetErrorString(hipGetLastError()));
+        }
     }
     if (jit && kp.spread_part) {   // a spread launch's block counter tables into the map
         const DMap dm = to_dmap(vm->maps[ji.spread_map]);

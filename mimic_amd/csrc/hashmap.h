@@ -42,10 +42,11 @@ struct HT {
     uint8_t *base;
     uint32_t cap, rec_q, K, nlocks, fl_cap, E;
     uint32_t tag;   // nonzero per map: which block combiner (below) is this map's
+    uint32_t flags; // DMap::hflags (HT_F_CHUNK)
 };
 HDEV HT h_table(uint8_t *arena, const DMap &m) {
     return HT{arena + m.ht_dev_off, m.ht_cap, m.rec_q, m.key_size, m.nlocks, m.fl_cap, m.max_entries,
-              (uint32_t)(m.ht_dev_off >> 3) | 1u};
+              (uint32_t)(m.ht_dev_off >> 3) | 1u, m.hflags};
 }
 
 #ifdef MIMIC_HASH_COMBINE
@@ -172,6 +173,11 @@ HDEV int32_t *h_ring(const HT &t) { return (int32_t *)(h_locks(t) + t.nlocks); }
 HDEV HashCtl *h_ctl(const HT &t) {   // 128-byte aligned after the ring (engine.cpp: ctl_off)
     return (HashCtl *)(((uintptr_t)(h_ring(t) + t.fl_cap) + 127) & ~(uintptr_t)127);
 }
+// after HashCtl (layout.h ht_ext_bytes): slot bits, slot -> bucket, the blocks' handed-back remainders
+HDEV uint64_t h_e32(const HT &t) { return ((uint64_t)t.E + 1023) & ~1023ull; }
+HDEV uint32_t *h_bits(const HT &t) { return (uint32_t *)((uint8_t *)h_ctl(t) + sizeof(HashCtl)); }
+HDEV uint32_t *h_s2b(const HT &t) { return h_bits(t) + h_e32(t) / 32; }
+HDEV unsigned long long *h_left(const HT &t) { return (unsigned long long *)(h_s2b(t) + h_e32(t)); }
 HDEV uint32_t *h_used_shard(HashCtl *c) {   // the calling wave's shard of the `used` count
     const uint32_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (HT_USED_SHARDS - 1);
     return &c->used_sh[32 * w];
@@ -181,6 +187,204 @@ HDEV uint32_t h_used_total(const HashCtl *c) {
     for (uint32_t s = 0; s < HT_USED_SHARDS; s++) u += c->used_sh[32 * s];
     return u;
 }
+
+#ifdef MIMIC_HASH_CHUNK
+// Chunked reservations (round 6).  The VM's chunk map (HT_F_CHUNK, one per VM)
+// in a pop-only JIT launch whose ring is still the identity (tail == E: nothing was ever pushed,
+// so ring position p holds slot p): a block takes freelist positions from `head` in chunks of up to
+// MIMIC_HCHUNK with one agent-scope add (cfg 4 made ~60 K same-address adds per launch, one per
+// inserting wave-round: they serialise at the memory side), and its waves take from the chunk with
+// LDS atomics.  A remainder a block leaves is a hole below head; mimic_hash_compact_kernel, launched
+// after every such launch, moves the entries above the holes into them, so after the launch the used
+// slots are again exactly [0, m) -- ring positions 0..m-1 popped, as m sequential pops leave them.
+// (Which key got which slot inside one concurrent launch already depends on arrival order.)
+//
+// E2BIG stays exact.  An insert is refused only when every position is live: once head has reached
+// tail a block ("scarce") takes positions from the remainders finished blocks handed back (left[],
+// h_chunk_fini), and refuses only after proving live == E from the live counts (the positions below
+// this launch's first reservation, found in the ring, plus what every block gave to inserts: blocks
+// add their LDS count to live_sh when they go scarce and when they finish).  Otherwise its lanes
+// wait (no bucket held) for running blocks to finish and hand their remainders back.  A block never
+// waits while it holds positions (its chunk is empty when it is scarce), and a non-scarce block never
+// waits on another block, so the wait ends; it is bounded anyway (HCHUNK_SPIN_LIMIT rounds, then
+// comb_fault: the sync reports an engine error).  Chunk sizes shrink as the table fills (the
+// remaining positions / (2 * blocks)), so holes stay below half of what is left and a table that
+// does not fill never goes scarce.
+#ifndef MIMIC_HCHUNK
+#define MIMIC_HCHUNK 32u
+#endif
+#ifndef HCHUNK_SPIN_LIMIT
+#define HCHUNK_SPIN_LIMIT (1u << 16)
+#endif
+struct HBlk {
+    unsigned long long cw;   // the block's chunk: end << 32 | next (ring positions = slots)
+    uint32_t lock;           // a wave is refilling cw
+    uint32_t mode;           // 0 not known yet, 1 chunks (ring identity), 2 the combiner path (hashmap.h above)
+    uint32_t scarce;         // head reached tail: positions only from handed-back remainders
+    uint32_t rem1;           // 1 + positions left after the last refill (chunk size hint; 0: none yet)
+    uint32_t h0;             // 1 + live positions below this launch's reservations (0: not read yet)
+    uint32_t live;           // positions this block gave to inserts, not yet added to live_sh
+    uint32_t act, exited;    // waves of the block that run / have reached h_chunk_fini
+    uint32_t spins;          // scarce rounds that found nothing
+    HashCtl *ctl;            // the chunk map's counters and remainders (h_chunk_fini)
+    unsigned long long *left;
+};
+static __shared__ HBlk h_blk_;
+#define HB_LD(p) __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define HB_ST(p, v) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+// thread 0, before the prologue's barrier (h_comb_init): waves whose first lane is below lim run
+HDEV void h_chunk_init(uint32_t lim) {
+    if (threadIdx.x) return;
+    HBlk &B = h_blk_;
+    B.cw = 0;
+    B.lock = B.mode = B.scarce = B.rem1 = B.h0 = B.live = B.exited = B.spins = 0;
+    B.ctl = nullptr;
+    B.left = nullptr;
+    uint32_t a = 0;
+    for (uint32_t w = 0; w * 64 < blockDim.x; w++) a += (uint64_t)blockIdx.x * blockDim.x + w * 64 < lim ? 1u : 0u;
+    B.act = a;
+}
+// is the map's ring the identity this launch (tail == E; pop-only launches never push)?
+HDEV bool h_chunk_on(const HT &t, HashCtl *c) {
+    if (!(t.flags & HT_F_CHUNK)) return false;
+    HBlk &B = h_blk_;
+    uint32_t md = HB_LD(&B.mode);
+    if (!md) {
+        md = __hip_atomic_load(&c->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == t.E ? 1u : 2u;
+        HB_ST(&B.mode, md);
+    }
+    return md == 1u;
+}
+// ring[0, h0) are -1 (popped before this launch, all live: nothing was pushed) and ring[h0, E) hold
+// their own index (chunk launches do not write the ring): the first index that is not -1
+HDEV uint32_t h_ring_h0(const HT &t) {
+    const int32_t *ring = h_ring(t);
+    uint32_t lo = 0, hi = t.E;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (__hip_atomic_load(ring + mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// One lane of a wave whose k lanes need positions, when the block's chunk is empty: refill it (from
+// head; when scarce from a handed-back remainder).  1 = every position is live (E2BIG), 0 = the
+// chunk has positions now, or none can be had yet (another wave holds the refill lock, or running
+// blocks still hold the rest: try again next round).
+static __device__ __attribute__((noinline)) uint32_t h_chunk_fill(const HT &t, HashCtl *c, uint32_t k) {
+    HBlk &B = h_blk_;
+    uint32_t z = 0;
+    if (!__hip_atomic_compare_exchange_strong(&B.lock, &z, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        return 0;
+    uint32_t full = 0;
+    const unsigned long long w = HB_LD(&B.cw);
+    if ((uint32_t)w >= (uint32_t)(w >> 32)) {   // still empty
+        B.ctl = c;
+        B.left = h_left(t);
+        bool got = false;
+        if (!HB_LD(&B.scarce)) {
+            const uint32_t hint = B.rem1 ? B.rem1 - 1u : t.E;
+            uint32_t g = blockIdx.x < HT_LEFT_CAP ? hint / (2u * gridDim.x) : 0u;   // no left[] slot: exact
+            g = g > MIMIC_HCHUNK ? MIMIC_HCHUNK : g;
+            g = g < k ? k : g;
+            const unsigned long long p = __hip_atomic_fetch_add(&c->head, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (p < t.E) {
+                const uint32_t n = t.E - p < g ? (uint32_t)(t.E - p) : g;
+                __hip_atomic_fetch_max(&c->cminv, 0xffffffffu - (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                B.rem1 = (uint32_t)(t.E - p) - n + 1u;
+                HB_ST(&B.cw, ((p + n) << 32) | p);
+                got = true;
+            } else {
+                HB_ST(&B.scarce, 1u);
+            }
+        }
+        if (!got) {   // scarce: the block's count first, then is every position live?
+            const uint32_t lv = __hip_atomic_exchange(&B.live, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lv) __hip_atomic_fetch_add(&c->live_sh[32 * (blockIdx.x & (HT_USED_SHARDS - 1))], lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_load(&c->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                full = 1;
+            } else {
+                if (!B.h0) B.h0 = h_ring_h0(t) + 1u;
+                uint64_t live = B.h0 - 1u;
+                for (uint32_t s = 0; s < HT_USED_SHARDS; s++)
+                    live += __hip_atomic_load(&c->live_sh[32 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (live >= t.E) {
+                    full = 1;
+                    __hip_atomic_store(&c->full, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {   // a remainder a finished block handed back
+                    unsigned long long *L = B.left;
+                    uint32_t nl = __hip_atomic_load(&c->nleft, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    nl = nl < HT_LEFT_CAP ? nl : HT_LEFT_CAP;
+                    for (uint32_t j0 = 0; j0 < nl && !got; j0 += 16) {   // 16 loads in flight at a time
+                      unsigned long long ev[16];
+#pragma unroll
+                      for (uint32_t q = 0; q < 16; q++)
+                          ev[q] = j0 + q < nl ? __hip_atomic_load(L + j0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                      for (uint32_t q = 0; q < 16 && !got; q++) {
+                        const uint32_t j = j0 + q;
+                        unsigned long long e = ev[q];
+                        while ((uint32_t)e < (uint32_t)(e >> 32)) {
+                            const uint32_t nx = (uint32_t)e, en = (uint32_t)(e >> 32), n = en - nx < k ? en - nx : k;
+                            if (__hip_atomic_compare_exchange_strong(L + j, &e, ((unsigned long long)en << 32) | (nx + n),
+                                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                                HB_ST(&B.cw, ((unsigned long long)(nx + n) << 32) | nx);
+                                got = true;
+                                break;
+                            }
+                        }
+                      }
+                    }
+                    if (!got && ++B.spins > HCHUNK_SPIN_LIMIT) {   // a broken protocol: stop loudly, not hang
+                        __hip_atomic_store(&c->comb_fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        full = 1;
+                    }
+                }
+            }
+        }
+    }
+    __hip_atomic_store(&B.lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return full;
+}
+// up to k positions from the block's chunk (LDS): *base, returns how many (the lanes given them insert)
+HDEV uint32_t h_chunk_grab(uint32_t k, uint64_t *base) {
+    HBlk &B = h_blk_;
+    unsigned long long w = HB_LD(&B.cw);
+    for (;;) {
+        const uint32_t nx = (uint32_t)w, en = (uint32_t)(w >> 32);
+        if (nx >= en) return 0;
+        const uint32_t n = en - nx < k ? en - nx : k;
+        if (__hip_atomic_compare_exchange_strong(&B.cw, &w, ((unsigned long long)en << 32) | (nx + n), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            if (HB_LD(&B.scarce))
+                __hip_atomic_fetch_add(&B.ctl->live_sh[32 * (blockIdx.x & (HT_USED_SHARDS - 1))], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                __hip_atomic_fetch_add(&B.live, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            *base = nx;
+            return n;
+        }
+    }
+}
+HDEV bool h_chunk_empty() {
+    const unsigned long long w = HB_LD(&h_blk_.cw);
+    return (uint32_t)w >= (uint32_t)(w >> 32);
+}
+// every running wave at the kernel's end (its active lanes): the last of the block adds the block's
+// count to live_sh and hands its chunk's remainder back (left[block], then nleft with release)
+HDEV void h_chunk_fini() {
+    HBlk &B = h_blk_;
+    if (__lane_id() != (uint32_t)__builtin_ctzll(__ballot(1))) return;
+    const uint32_t o = __hip_atomic_fetch_add(&B.exited, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (o + 1u != B.act || !B.ctl) return;
+    HashCtl *c = B.ctl;
+    const uint32_t lv = __hip_atomic_exchange(&B.live, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lv) __hip_atomic_fetch_add(&c->live_sh[32 * (blockIdx.x & (HT_USED_SHARDS - 1))], lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long w = HB_LD(&B.cw);
+    if ((uint32_t)w < (uint32_t)(w >> 32) && blockIdx.x < HT_LEFT_CAP) {
+        __hip_atomic_store(B.left + blockIdx.x, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(&c->nleft, blockIdx.x + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+#endif
 
 // key hash over the zero-padded little-endian key words (any good 64-bit mix; the reference's
 // sha256 only names Go-map buckets, which no program can observe)
@@ -460,6 +664,11 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
     bool done = false;
     int32_t idx = -1;
     *inserted = false;
+#ifdef MIMIC_HASH_CHUNK
+    const bool chunk = h_chunk_on(t, c);   // positions from the block's chunk (h_chunk_take above)
+#else
+    const bool chunk = false;
+#endif
     for (;;) {
         const uint64_t pend = __ballot(!done);
         if (!pend) break;
@@ -494,6 +703,22 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
                 }
             }
         }
+#ifdef MIMIC_HASH_CHUNK
+        if (chunk) {   // an empty chunk is refilled before any bucket is claimed (no claim is held while waiting)
+            const uint64_t candm = __ballot(!done && !blocked && cand != HT_EMPTY);
+            uint32_t v = 0;   // 1: every position is live (E2BIG); 2: none to be had this round
+            if (candm) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(candm);
+                if (me == f && h_chunk_empty()) v = h_chunk_fill(t, c, (uint32_t)__builtin_popcountll(candm)) ? 1u : h_chunk_empty() ? 2u : 0u;
+                v = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)f);
+            }
+            if (v == 1u && !done && !blocked && cand != HT_EMPTY) {
+                idx = -1;
+                done = true;
+            }
+            if (v) cand = HT_EMPTY;
+        }
+#endif
         const bool mine = !done && !blocked && cand != HT_EMPTY &&
                           h_cas(h_rec(t, cand), cw, ((uint64_t)tag << 32) | HT_BUSY);
         if (mine) {   // the key words go out now: their completion overlaps the reservation's round trip
@@ -509,6 +734,12 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
             uint64_t base = 0;
             uint32_t ident = 0;
             if (me == first) {
+#ifdef MIMIC_HASH_CHUNK
+              if (chunk) {
+                  got = h_chunk_grab(k, &base);
+                  ident = 1;
+              } else
+#endif
 #ifdef MIMIC_HASH_COMBINE
               if (!h_comb_reserve(t, c, k, &base, &got, &ident))
 #endif
@@ -542,7 +773,7 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
             if (mine && rank < got) {   // positions below tail were written before this launch
                 int32_t *f = h_ring(t) + ((base + rank) & (t.fl_cap - 1));
                 slot = ident ? (int32_t)(base + rank) : __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!chunk) __hip_atomic_store(f, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (chunks: the compaction)
             }
         }
         bool empty_used = false;
@@ -554,13 +785,23 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
                 empty_used = (uint32_t)cw == HT_EMPTY;
                 idx = slot;
                 *inserted = true;
+#ifdef MIMIC_HASH_CHUNK
+                if (chunk) {   // for mimic_hash_compact_kernel: the slot is used, and which bucket holds it
+                    __hip_atomic_fetch_or(h_bits(t) + ((uint32_t)slot >> 5), 1u << (slot & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    h_s2b(t)[slot] = cand;
+                }
+#endif
+                done = true;
             } else {
                 // the freelist is spent: E2BIG, the bucket as it was (the key words it holds now are
-                // never compared: only a live record's are)
+                // never compared: only a live record's are).  Chunks: the block's chunk ran dry between
+                // the refill and the claim -- the bucket back, the lane tries again next round.
                 h_st(r, cw);
-                idx = -1;
+                if (!chunk) {
+                    idx = -1;
+                    done = true;
+                }
             }
-            done = true;
         }
         const uint64_t um = __ballot(empty_used);
         if (um && me == (uint32_t)__builtin_ctzll(um))

@@ -623,6 +623,135 @@ extern "C" __global__ void mimic_hash_normalize_kernel(uint8_t *arena, DMap m) {
     c->avail = (int32_t)(tl - hd);
 }
 
+// After a launch whose chunk map took its freelist positions in per-block chunks (hashmap.h
+// MIMIC_HASH_CHUNK): the holes the blocks' chunk remainders left below head are filled with the
+// entries above them, so that the used slots are [0, m) again and ring positions [0, m) popped --
+// the state m sequential pops leave (emulator_linux_map_hash.go:179-186).  The launch's inserts set
+// bits (h_bits) in [lo, hi), lo = the lowest position a block reserved, hi = min(head, E); below lo
+// every slot is live.  m = lo + inserts; movers = used slots >= m, holes = free slots in [lo, m); the
+// r-th mover (slot order) goes to the r-th hole: key and value bytes copied, the source zeroed (a
+// slot never popped holds zeros -- nothing was ever pushed, the ring is the identity), the state
+// word of its bucket (h_s2b) rewritten.  Every block turns the bit words (<= 8192: E <= 2^18) into
+// LDS prefix counts and moves its share of the movers; the last block to finish clears the bits and
+// the handed-back remainders, pops ring positions [lo, m) and resets the counters.  A launch that
+// reserved no chunk returns at once.
+#define HC_MAXW (HT_CHUNK_MAXE / 32u)
+struct HcWords {   // the bit words of [lo, hi): below lo counted as used, from hi on as free
+    const uint32_t *bits;
+    uint32_t w0, lo, hi;
+    __device__ uint32_t operator()(uint32_t i) const {
+        uint32_t x = __hip_atomic_load(bits + w0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t b0 = (w0 + i) << 5;
+        if (b0 < lo) x |= (1u << (lo - b0)) - 1u;   // (only word 0: lo - b0 in 1..31)
+        if (b0 + 32u > hi) x &= hi > b0 ? (1u << (hi - b0)) - 1u : 0u;
+        return x;
+    }
+};
+static __device__ uint32_t hc_select(uint32_t x, uint32_t n) {   // bit index of x's n-th set bit
+    for (uint32_t q = 0; q < n; q++) x &= x - 1u;
+    return (uint32_t)__builtin_ctz(x);
+}
+static __device__ void hc_move(const HT &t, uint8_t *arena, const DMap &m, uint32_t s, uint32_t d) {
+    const uint32_t p = __hip_atomic_load(h_s2b(t) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint8_t *kb = arena + m.keys_dev_off, *vb = arena + m.dev_off;
+    for (uint32_t b = 0; b < m.key_size; b++) {
+        kb[(size_t)d * m.key_size + b] = kb[(size_t)s * m.key_size + b];
+        kb[(size_t)s * m.key_size + b] = 0;
+    }
+    for (uint32_t b = 0; b < m.value_size; b++) {
+        vb[(size_t)d * m.value_size + b] = vb[(size_t)s * m.value_size + b];
+        vb[(size_t)s * m.value_size + b] = 0;
+    }
+    uint64_t *r = h_rec(t, p);
+    h_st(r, (h_ld(r) & ~0xffffffffull) | d);
+}
+extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint8_t *arena, DMap m) {
+    const HT t = h_table(arena, m);
+    HashCtl *c = h_ctl(t);
+    const uint32_t cminv = c->cminv, fullf = c->full;
+    if (!cminv && !fullf) return;
+    __shared__ uint32_t pf[HC_MAXW];   // set bits in words [0, i)
+    __shared__ uint32_t wsum[4], total_, last_;
+    const uint32_t E = t.E;
+    const unsigned long long hd = c->head;
+    const uint32_t hi = hd < E ? (uint32_t)hd : E;
+    uint32_t lo = cminv ? 0xffffffffu - cminv : hi;
+    lo = lo < hi ? lo : hi;
+    const HcWords W{h_bits(t), lo >> 5, lo, hi};
+    const uint32_t nw = ((hi + 31u) >> 5) - W.w0;
+    // exclusive prefix counts: thread t sums words [t * per, +per), the threads' sums are scanned
+    const uint32_t per = (nw + 255u) / 256u, beg = threadIdx.x * per;
+    uint32_t own = 0;
+    for (uint32_t i = beg; i < beg + per && i < nw; i++) own += (uint32_t)__builtin_popcount(W(i));
+    uint32_t inc = own;   // inclusive scan over the wave
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (__lane_id() >= o) inc += y;
+    }
+    if (__lane_id() == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t before = inc - own;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += wsum[w];
+    if (threadIdx.x == 255) total_ = before + own;
+    for (uint32_t i = beg; i < beg + per && i < nw; i++) {
+        pf[i] = before;
+        before += (uint32_t)__builtin_popcount(W(i));
+    }
+    __syncthreads();
+    const uint32_t T = total_, mm = (W.w0 << 5) + T;   // m: used slots after the move = [0, m)
+    const uint32_t mw = (mm >> 5) - W.w0, mb = mm & 31u;
+    const uint32_t Sm = (mw < nw ? pf[mw] : T) + (mw < nw && mb ? (uint32_t)__builtin_popcount(W(mw) & ((1u << mb) - 1u)) : 0u);
+    const uint32_t H = T - Sm;   // movers = holes
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < H; r += gridDim.x * 256u) {
+        // the mover: the (Sm + r)-th used slot; the hole: the r-th free slot (zeros before word i: 32 i - pf[i])
+        const uint32_t j = Sm + r;
+        uint32_t a = 0, b = nw;   // last word with pf <= j
+        while (b - a > 1) {
+            const uint32_t h = (a + b) >> 1;
+            if (pf[h] <= j) a = h; else b = h;
+        }
+        const uint32_t s = ((W.w0 + a) << 5) + hc_select(W(a), j - pf[a]);
+        a = 0;
+        b = nw;
+        while (b - a > 1) {
+            const uint32_t h = (a + b) >> 1;
+            if (32u * h - pf[h] <= r) a = h; else b = h;
+        }
+        const uint32_t d = ((W.w0 + a) << 5) + hc_select(~W(a), r - (32u * a - pf[a]));
+        hc_move(t, arena, m, s, d);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last_ = __hip_atomic_fetch_add(&c->cdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!last_) return;
+    __threadfence();
+    uint32_t *bits = h_bits(t);
+    for (uint32_t i = threadIdx.x; i < nw; i += 256u) bits[W.w0 + i] = 0;
+    int32_t *ring = h_ring(t);
+    for (uint32_t p = lo + threadIdx.x; p < mm; p += 256u) ring[p] = -1;
+    unsigned long long *left = h_left(t);
+    const uint32_t nl = c->nleft < HT_LEFT_CAP ? c->nleft : HT_LEFT_CAP;
+    for (uint32_t j = threadIdx.x; j < nl; j += 256u) left[j] = 0;
+    if (threadIdx.x < HT_USED_SHARDS) c->live_sh[32 * threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        c->head = mm;
+        c->avail = (int32_t)(E - mm);
+        c->cminv = 0;
+        c->full = 0;
+        c->cdone = 0;
+        c->nleft = 0;
+    }
+}
+
+extern "C" int mimic_launch_hash_compact(uint8_t *arena, const DMap *m, hipStream_t st) {
+    const uint32_t blocks = std::min<uint32_t>(64u, std::max<uint32_t>(1u, m->max_entries / 4096u));
+    hipLaunchKernelGGL(mimic_hash_compact_kernel, dim3(blocks), dim3(256), 0, st, arena, *m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int mimic_launch_hash_normalize(uint8_t *arena, const DMap *m, hipStream_t st) {
     hipLaunchKernelGGL(mimic_hash_normalize_kernel, dim3(1), dim3(64), 0, st, arena, *m);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -655,13 +784,17 @@ extern "C" __global__ void mimic_hash_reset_kernel(uint8_t *arena, DMap m) {
     fill_bytes(arena + m.keys_dev_off, (size_t)m.max_entries * m.key_size, 0, g, stride);
     int32_t *ring = h_ring(t);
     for (size_t i = g; i < t.fl_cap; i += stride) ring[i] = i < m.max_entries ? (int32_t)i : -1;
+    // chunked reservations' slot bits and handed-back remainders (hashmap.h h_bits / h_left)
+    fill_bytes((uint8_t *)h_bits(t), h_e32(t) / 8, 0, g, stride);
+    fill_bytes((uint8_t *)h_left(t), (size_t)HT_LEFT_CAP * 8, 0, g, stride);
     if (g == 0) {
         HashCtl *c = h_ctl(t);
         c->head = 0;
         c->tail = m.max_entries;
         c->avail = (int32_t)m.max_entries;
         c->used0 = 0;
-        for (uint32_t sh = 0; sh < HT_USED_SHARDS; sh++) c->used_sh[32 * sh] = 0;
+        for (uint32_t sh = 0; sh < HT_USED_SHARDS; sh++) c->used_sh[32 * sh] = c->live_sh[32 * sh] = 0;
+        c->cminv = c->full = c->cdone = c->nleft = 0;
     }
 }
 

@@ -116,6 +116,8 @@ class Gen {
         ntres = !(nr && nr[0] == '0');
         const char *cbv = getenv("MIMIC_JIT_COMBINE");
         combine_knob = !(cbv && cbv[0] == '0');
+        const char *hcv = getenv("MIMIC_JIT_HCHUNK");   // 0: no chunked reservations; N: chunks of up to N positions
+        if (hcv) hchunk_knob = atoi(hcv);
         const char *dnr = getenv("MIMIC_JIT_DEFER_NOREGS");
         defer_noregs = dnr ? atoi(dnr) : 0;
         const char *sf = getenv("MIMIC_JIT_SKBFIELD");   // 0: sk_buff fields through the generic convertAccess
@@ -228,6 +230,8 @@ class Gen {
     int defer_noregs = 0;   // MIMIC_JIT_DEFER_NOREGS=1: deferral sites store no registers, 2: low halves (register census only)
     bool combine_knob = true;  // MIMIC_JIT_COMBINE=0: every wave reserves freelist positions with its own add
     bool hash_combine = false;
+    int hchunk_knob = 32;       // MIMIC_JIT_HCHUNK (hashmap.h MIMIC_HCHUNK; 0: off)
+    bool hash_chunk = false;    // the chunk map's positions come in per-block chunks (hashmap.h h_chunk_fill)
     bool ntres = true;         // MIMIC_JIT_NTRES=0: r0 / status stores not non-temporal (measured 1-3 % slower)
     bool forward = true;       // MIMIC_JIT_FWD=0: helper-1 keys always reread from the stack
     int waves = 0;             // MIMIC_JIT_WAVES=W: amdgpu_waves_per_eu(W) on the kernel
@@ -396,6 +400,10 @@ class Gen {
             // reservations (hashmap.h h_comb_reserve); zeroed in the prologue
             hash_combine = combine_knob && writes && !deletes && cold_inline && fast_paths;
             if (hash_combine) E.line("#define MIMIC_HASH_COMBINE 1");
+            // ... and the VM's chunk map takes them in per-block chunks (batch kernels only: every
+            // launch of one is followed by mimic_hash_compact_kernel, engine.cpp)
+            hash_chunk = hash_combine && !proc && hchunk_knob > 0;
+            if (hash_chunk) E.line("#define MIMIC_HASH_CHUNK 1\n#define MIMIC_HCHUNK %uu", (uint32_t)hchunk_knob);
         }
         E.line("#include \"runtime.h\"");
         if (spread_on) {
@@ -466,6 +474,7 @@ class Gen {
         }
         E.line("  const KParams &kp = *kpp;");
         E.line("  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;");
+        if (hash_chunk) E.line("  h_chunk_init(%s);   // (its waves: those the early return below keeps)", spread_on ? "0xffffffffu" : "kp.lanes");
         if (hash_combine) E.line("  h_comb_init();   // before any thread of the block can leave");
         if (!spread_on) E.line("  if (g >= kp.lanes) return;");
         if (stage && fast_paths) {
@@ -892,6 +901,7 @@ class Gen {
             E.line("#endif");
         }
         E.line("  if (kp.lane_steps) st_nt(kp.lane_steps + g, lane_steps);");
+        if (hash_chunk) E.line("  h_chunk_fini();   // the block's last wave hands its chunk's remainder back");
         E.line("}");
         if (census) {   // diagnostics: each slow-path call adds 1 to its kind's 4-bit field of coldn_
             static const char *kinds[] = {"cold_load(", "cold_store(", "cold_lookup(", "cold_update(", "cold_delete(",
@@ -2391,6 +2401,7 @@ std::string mimic_jit_source(const std::vector<DProg> &progs, const std::vector<
         info->spread = g.spread_on;
         info->spread_own = g.spread_own;
         info->hash_combine = g.hash_combine;
+        info->hash_chunk = g.hash_chunk;
         info->proc = proc;
         info->proc_ok = proc && ctx_kind == CTX_XDP && !g.careful_copies && !g.defer_mode && !g.spread_on && !g.census;
         info->spread_map = g.spread_map;

@@ -22,6 +22,7 @@ struct JitInfo {
     bool spread;         // a spread kernel (a vCPU's packets on many lanes; jit.cpp analyze_spread)
     bool spread_own;     // ... in its owned form: a block runs every packet of its vCPUs (SpreadReq::own)
     bool hash_combine;   // pop-only inline inserts through the block combiner (hashmap.h h_comb_reserve)
+    bool hash_chunk;     // ... and per-block chunks for the chunk map: mimic_hash_compact_kernel after each launch
     // the single-process form (Process.Run, engine.cpp process_advance): every exit stores the
     // process's registers, PC, program and steps into KParams::step; proc_ok = usable for it
     // (loop-free, no BPF-to-BPF calls, no deferred slow paths, the exit's program known)

@@ -460,6 +460,7 @@ def test_combiner_gives_up_with_a_status(gpu, monkeypatch):
     buf, off, lens = W.make_packets(n, **W.IMIX, seed=23)
     cpu = W.schedule_cpu(n, 4096, "interleaved")
     monkeypatch.setenv("MIMIC_JIT_DEFS", "HCOMB_SPIN_LIMIT=0,MIMIC_HCOMB_SLEEP=60")
+    monkeypatch.setenv("MIMIC_JIT_HCHUNK", "0")   # the combiner, not the chunked reservations
     vm, maps, pids = build_engine(sc)
     batch = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
     with pytest.raises(M.MimicError, match="combiner"):
@@ -469,3 +470,80 @@ def test_combiner_gives_up_with_a_status(gpu, monkeypatch):
     o = run_oracle(sc, buf, off, lens, cpu)
     e = run_engine(sc, buf, off, lens, cpu, schedule=M.SCHED_INTERLEAVED)
     assert_same(o, e, check_pkt=False, hash_exact=False, check_steps=False)
+
+
+def _distinct_keys(buf, off, lens) -> int:
+    k = W.flow_keys_np(buf, off, lens)
+    return len(np.unique(np.ascontiguousarray(k).view(np.dtype((np.void, 16)))))
+
+
+@pytest.mark.parametrize("V,E", [(4096, 32768), (65536, 32768), (262144, 1 << 17)])
+def test_chunked_launch_leaves_the_used_slots_dense(gpu, V, E):
+    """Chunked reservations (hashmap.h MIMIC_HASH_CHUNK: blocks take freelist positions in chunks,
+    interp.hip mimic_hash_compact_kernel fills the holes their remainders leave): after a concurrent
+    inserting launch the used slots are exactly [0, m), as after m sequential pops
+    (emulator_linux_map_hash.go:179-186); verdicts and every key's value are the oracle's; a second
+    launch over new flows (table partly full) keeps both; and the next insert from the host takes
+    slot m (the freelist's head), as it does on the oracle."""
+    import mimic_amd as M
+
+    p = W.prog_flowtrack(max_entries=E)
+    sc = _sc(p, V)
+    ovm, omids, opids = build_oracle(sc)
+    vm, maps, pids = build_engine(sc)
+    fm, om = maps["flows"], omids["flows"]
+    for rnd in range(2):
+        n = 60000 if V < 65536 else 400000
+        buf, off, lens = W.make_packets(n, **W.IMIX, seed=300 + rnd)
+        cpu = W.schedule_cpu(n, V, "interleaved")
+        o = ovm.run_xdp_batch(opids[0], buf.copy(), off, lens, cpu, write_back=False)
+        b = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+        e = vm.RunXDPBatch(pids[0], b).numpy(n)
+        for k in ("r0", "status"):
+            assert np.array_equal(np.asarray(o[k]).astype(np.int64), np.asarray(e[k]).astype(np.int64)), (rnd, k)
+        ents = fm.Entries()
+        assert sorted(s for _, s in ents) == list(range(len(ents))), rnd
+        oe = ovm.map_entries(om)
+        assert sorted(k for k, _ in ents) == sorted(k for k, _ in oe), rnd
+        ov, ev = ovm.map_values(om, 0), fm.Values(0)
+        want = {k: ov[s * 8:(s + 1) * 8] for k, s in oe}
+        assert {k: ev[s * 8:(s + 1) * 8] for k, s in ents} == want, rnd
+        # slots nobody holds read zero (a slot never popped; a moved entry's old slot was cleared)
+        assert ev[len(ents) * 8:] == bytes(len(ev) - len(ents) * 8), rnd
+    m = len(fm.Entries())
+    newk = b"\xfd" * 16
+    assert fm.Update(newk, b"\x03" * 8) == ovm.map_update(om, newk, b"\x03" * 8, 0, 0) == 0
+    assert dict(fm.Entries())[newk] == m == dict(ovm.map_entries(om))[newk]
+    vm.close()
+    ovm.close()
+
+
+@pytest.mark.parametrize("short", [0, 1, 37])
+def test_chunked_launch_fills_a_table_exactly(gpu, short):
+    """MaxEntries = the batch's distinct flows - short.  short = 0: every flow must get a slot (no
+    E2BIG), although blocks still hold chunk remainders when head reaches tail -- the last inserts take
+    the remainders finished blocks handed back (hashmap.h h_chunk_fill, scarce).  short > 0: exactly E
+    flows get slots 0..E-1, the refused packets are exactly those of the `short` flows left out (every
+    packet of a flow gets the same verdict), and E2BIG is answered only once every slot is live."""
+    import mimic_amd as M
+
+    V, n = 16384, 200000
+    buf, off, lens = W.make_packets(n, **W.IMIX, seed=77)
+    D = _distinct_keys(buf, off, lens)
+    E = D - short
+    p = W.prog_flowtrack(max_entries=E)
+    sc = _sc(p, V)
+    vm, maps, pids = build_engine(sc)
+    b = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+    e = vm.RunXDPBatch(pids[0], b).numpy(n)
+    ents = maps["flows"].Entries()
+    assert len(ents) == E and sorted(s for _, s in ents) == list(range(E))
+    assert (np.asarray(e["status"]) == 0).all()
+    keys, rows = W.flow_keys_np(buf, off, lens, with_index=True)
+    kb = [bytes(k) for k in np.ascontiguousarray(keys).view(np.uint8).reshape(-1, 16)]
+    inside = set(k for k, _ in ents)
+    r0 = np.asarray(e["r0"]).astype(np.int64)
+    refused = set(kb[j] for j in range(len(kb)) if r0[rows[j]] == 1)
+    assert len(refused) == short and not (refused & inside)
+    assert all(r0[rows[j]] == 1 for j in range(len(kb)) if kb[j] in refused)
+    vm.close()

@@ -173,9 +173,10 @@ def test_cfg4_kernel_register_budget():
     slow paths (jit.cpp), so the 262 144 lanes run in one round.  That spills about 40 VGPRs of
     its slow paths to scratch and measured faster anyway: 0.137 vs 0.172 ms per launch at its
     natural 169 VGPRs / 2 waves.  Its LDS stack window is there too, and the block
-    combiner of its freelist reservations (hashmap.h h_comb_reserve: 4 x 272 bytes)."""
+    combiner of its freelist reservations (hashmap.h h_comb_reserve: 4 x 272 bytes) and the block's
+    chunk of positions (h_chunk_fill: 64 bytes)."""
     r = _resources([W.prog_flowtrack().raw])
-    assert r["vgpr_total"] <= 128 and r["waves_per_simd"] >= 4 and r["lds"] == 16 * 256 * 8 + 4 * 272, r
+    assert r["vgpr_total"] <= 128 and r["waves_per_simd"] >= 4 and r["lds"] == 16 * 256 * 8 + 4 * 272 + 64, r
     assert r["vgpr_spill"] <= 64, r
 
 
