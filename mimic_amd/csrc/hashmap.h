@@ -173,10 +173,11 @@ HDEV int32_t *h_ring(const HT &t) { return (int32_t *)(h_locks(t) + t.nlocks); }
 HDEV HashCtl *h_ctl(const HT &t) {   // 128-byte aligned after the ring (engine.cpp: ctl_off)
     return (HashCtl *)(((uintptr_t)(h_ring(t) + t.fl_cap) + 127) & ~(uintptr_t)127);
 }
-// after HashCtl (layout.h ht_ext_bytes): slot bits, slot -> bucket, the blocks' handed-back remainders
+// after HashCtl (layout.h ht_ext_bytes): a used byte per slot, slot -> bucket, the blocks' handed-back
+// remainders
 HDEV uint64_t h_e32(const HT &t) { return ((uint64_t)t.E + 1023) & ~1023ull; }
-HDEV uint32_t *h_bits(const HT &t) { return (uint32_t *)((uint8_t *)h_ctl(t) + sizeof(HashCtl)); }
-HDEV uint32_t *h_s2b(const HT &t) { return h_bits(t) + h_e32(t) / 32; }
+HDEV uint8_t *h_used8(const HT &t) { return (uint8_t *)h_ctl(t) + sizeof(HashCtl); }
+HDEV uint32_t *h_s2b(const HT &t) { return (uint32_t *)(h_used8(t) + h_e32(t)); }
 HDEV unsigned long long *h_left(const HT &t) { return (unsigned long long *)(h_s2b(t) + h_e32(t)); }
 HDEV uint32_t *h_used_shard(HashCtl *c) {   // the calling wave's shard of the `used` count
     const uint32_t w = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (HT_USED_SHARDS - 1);
@@ -665,7 +666,7 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
     int32_t idx = -1;
     *inserted = false;
 #ifdef MIMIC_HASH_CHUNK
-    const bool chunk = h_chunk_on(t, c);   // positions from the block's chunk (h_chunk_take above)
+    const bool chunk = h_chunk_on(t, c);   // positions from the block's chunk (h_chunk_fill above)
 #else
     const bool chunk = false;
 #endif
@@ -787,7 +788,7 @@ HDEV int32_t h_insert_nolock(const HT &t, const KS &ks, uint64_t h, bool *insert
                 *inserted = true;
 #ifdef MIMIC_HASH_CHUNK
                 if (chunk) {   // for mimic_hash_compact_kernel: the slot is used, and which bucket holds it
-                    __hip_atomic_fetch_or(h_bits(t) + ((uint32_t)slot >> 5), 1u << (slot & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    h_used8(t)[slot] = 1;   // (plain stores: one lane per slot; a bit map's atomic ORs cost more)
                     h_s2b(t)[slot] = cand;
                 }
 #endif

@@ -627,7 +627,7 @@ extern "C" __global__ void mimic_hash_normalize_kernel(uint8_t *arena, DMap m) {
 // MIMIC_HASH_CHUNK): the holes the blocks' chunk remainders left below head are filled with the
 // entries above them, so that the used slots are [0, m) again and ring positions [0, m) popped --
 // the state m sequential pops leave (emulator_linux_map_hash.go:179-186).  The launch's inserts set
-// bits (h_bits) in [lo, hi), lo = the lowest position a block reserved, hi = min(head, E); below lo
+// used bytes (h_used8) in [lo, hi), lo = the lowest position a block reserved, hi = min(head, E); below lo
 // every slot is live.  m = lo + inserts; movers = used slots >= m, holes = free slots in [lo, m); the
 // r-th mover (slot order) goes to the r-th hole: key and value bytes copied, the source zeroed (a
 // slot never popped holds zeros -- nothing was ever pushed, the ring is the identity), the state
@@ -636,53 +636,79 @@ extern "C" __global__ void mimic_hash_normalize_kernel(uint8_t *arena, DMap m) {
 // the handed-back remainders, pops ring positions [lo, m) and resets the counters.  A launch that
 // reserved no chunk returns at once.
 #define HC_MAXW (HT_CHUNK_MAXE / 32u)
-struct HcWords {   // the bit words of [lo, hi): below lo counted as used, from hi on as free
-    const uint32_t *bits;
-    uint32_t w0, lo, hi;
-    __device__ uint32_t operator()(uint32_t i) const {
-        uint32_t x = __hip_atomic_load(bits + w0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t b0 = (w0 + i) << 5;
-        if (b0 < lo) x |= (1u << (lo - b0)) - 1u;   // (only word 0: lo - b0 in 1..31)
-        if (b0 + 32u > hi) x &= hi > b0 ? (1u << (hi - b0)) - 1u : 0u;
-        return x;
-    }
-};
 static __device__ uint32_t hc_select(uint32_t x, uint32_t n) {   // bit index of x's n-th set bit
     for (uint32_t q = 0; q < n; q++) x &= x - 1u;
     return (uint32_t)__builtin_ctz(x);
 }
-static __device__ void hc_move(const HT &t, uint8_t *arena, const DMap &m, uint32_t s, uint32_t d) {
-    const uint32_t p = __hip_atomic_load(h_s2b(t) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint8_t *kb = arena + m.keys_dev_off, *vb = arena + m.dev_off;
-    for (uint32_t b = 0; b < m.key_size; b++) {
-        kb[(size_t)d * m.key_size + b] = kb[(size_t)s * m.key_size + b];
-        kb[(size_t)s * m.key_size + b] = 0;
+// n bytes from slot s to slot d of a backing with stride n, the source zeroed: 8-, 4- or 1-byte units
+static __device__ void hc_copy(uint8_t *base, uint32_t n, uint32_t s, uint32_t d) {
+    uint8_t *src = base + (size_t)s * n, *dst = base + (size_t)d * n;
+    if (!(((uintptr_t)base | n) & 7u)) {
+        for (uint32_t b = 0; b < n; b += 8) {
+            *(uint64_t *)(dst + b) = *(const uint64_t *)(src + b);
+            *(uint64_t *)(src + b) = 0;
+        }
+    } else if (!(((uintptr_t)base | n) & 3u)) {
+        for (uint32_t b = 0; b < n; b += 4) {
+            *(uint32_t *)(dst + b) = *(const uint32_t *)(src + b);
+            *(uint32_t *)(src + b) = 0;
+        }
+    } else {
+        for (uint32_t b = 0; b < n; b++) {
+            dst[b] = src[b];
+            src[b] = 0;
+        }
     }
-    for (uint32_t b = 0; b < m.value_size; b++) {
-        vb[(size_t)d * m.value_size + b] = vb[(size_t)s * m.value_size + b];
-        vb[(size_t)s * m.value_size + b] = 0;
-    }
-    uint64_t *r = h_rec(t, p);
-    h_st(r, (h_ld(r) & ~0xffffffffull) | d);
 }
-extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint8_t *arena, DMap m) {
+extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint8_t *arena, DMap m, uint32_t meas) {
     const HT t = h_table(arena, m);
     HashCtl *c = h_ctl(t);
     const uint32_t cminv = c->cminv, fullf = c->full;
     if (!cminv && !fullf) return;
-    __shared__ uint32_t pf[HC_MAXW];   // set bits in words [0, i)
+    __shared__ uint32_t wd[HC_MAXW], pf[HC_MAXW];   // the bit words of [lo, hi); set bits in words [0, i)
     __shared__ uint32_t wsum[4], total_, last_;
     const uint32_t E = t.E;
     const unsigned long long hd = c->head;
     const uint32_t hi = hd < E ? (uint32_t)hd : E;
     uint32_t lo = cminv ? 0xffffffffu - cminv : hi;
     lo = lo < hi ? lo : hi;
-    const HcWords W{h_bits(t), lo >> 5, lo, hi};
-    const uint32_t nw = ((hi + 31u) >> 5) - W.w0;
+    const uint32_t w0 = lo >> 5, nw = ((hi + 31u) >> 5) - w0;
+    const uint8_t *used = h_used8(t);
+    // the used bytes as bit words (plain loads: the launch that wrote them has ended), below lo
+    // counted as used, from hi on as free.  Every load of the thread first (indices clamped, no
+    // branch between them: one wait), then the packing (a loop of load-then-use waited per word)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    constexpr uint32_t PW = HC_MAXW / 256u;   // words per thread
+    u32x4 v[2 * PW];
+#pragma unroll
+    for (uint32_t k = 0; k < PW; k++) {
+        const uint32_t i = threadIdx.x + 256u * k, ic = i < nw ? i : 0u;
+        const u32x4 *q = (const u32x4 *)(used + ((size_t)(w0 + ic) << 5));
+        v[2 * k] = q[0];
+        v[2 * k + 1] = q[1];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PW; k++) {
+        const uint32_t i = threadIdx.x + 256u * k;
+        if (i >= nw) break;
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const u32x4 u = v[2 * k + h];
+            const uint32_t d[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (uint32_t c = 0; c < 16; c++) x |= ((d[c >> 2] >> (8 * (c & 3))) & 1u) << (16 * h + c);
+        }
+        const uint32_t b0 = (w0 + i) << 5;
+        if (b0 < lo) x |= (1u << (lo - b0)) - 1u;   // (word 0 only: lo - b0 in 1..31)
+        if (b0 + 32u > hi) x &= hi > b0 ? (1u << (hi - b0)) - 1u : 0u;
+        wd[i] = x;
+    }
+    __syncthreads();
     // exclusive prefix counts: thread t sums words [t * per, +per), the threads' sums are scanned
     const uint32_t per = (nw + 255u) / 256u, beg = threadIdx.x * per;
     uint32_t own = 0;
-    for (uint32_t i = beg; i < beg + per && i < nw; i++) own += (uint32_t)__builtin_popcount(W(i));
+    for (uint32_t i = beg; i < beg + per && i < nw; i++) own += (uint32_t)__builtin_popcount(wd[i]);
     uint32_t inc = own;   // inclusive scan over the wave
     for (uint32_t o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(inc, o, 64);
@@ -695,46 +721,54 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     if (threadIdx.x == 255) total_ = before + own;
     for (uint32_t i = beg; i < beg + per && i < nw; i++) {
         pf[i] = before;
-        before += (uint32_t)__builtin_popcount(W(i));
+        before += (uint32_t)__builtin_popcount(wd[i]);
     }
     __syncthreads();
-    const uint32_t T = total_, mm = (W.w0 << 5) + T;   // m: used slots after the move = [0, m)
-    const uint32_t mw = (mm >> 5) - W.w0, mb = mm & 31u;
-    const uint32_t Sm = (mw < nw ? pf[mw] : T) + (mw < nw && mb ? (uint32_t)__builtin_popcount(W(mw) & ((1u << mb) - 1u)) : 0u);
+    const uint32_t T = total_, mm = (w0 << 5) + T;   // m: the used slots after the moves are [0, m)
+    const uint32_t mw = (mm >> 5) - w0, mb = mm & 31u;
+    const uint32_t Sm = (mw < nw ? pf[mw] : T) + (mw < nw && mb ? (uint32_t)__builtin_popcount(wd[mw] & ((1u << mb) - 1u)) : 0u);
     const uint32_t H = T - Sm;   // movers = holes
-    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < H; r += gridDim.x * 256u) {
+    uint8_t *kb = arena + m.keys_dev_off, *vb = arena + m.dev_off;
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < ((meas & 1u) ? 0u : H); r += gridDim.x * 256u) {
         // the mover: the (Sm + r)-th used slot; the hole: the r-th free slot (zeros before word i: 32 i - pf[i])
         const uint32_t j = Sm + r;
-        uint32_t a = 0, b = nw;   // last word with pf <= j
+        uint32_t a = 0, b = nw;   // the last word with pf <= j
         while (b - a > 1) {
             const uint32_t h = (a + b) >> 1;
             if (pf[h] <= j) a = h; else b = h;
         }
-        const uint32_t s = ((W.w0 + a) << 5) + hc_select(W(a), j - pf[a]);
+        const uint32_t sl = ((w0 + a) << 5) + hc_select(wd[a], j - pf[a]);
         a = 0;
         b = nw;
         while (b - a > 1) {
             const uint32_t h = (a + b) >> 1;
             if (32u * h - pf[h] <= r) a = h; else b = h;
         }
-        const uint32_t d = ((W.w0 + a) << 5) + hc_select(~W(a), r - (32u * a - pf[a]));
-        hc_move(t, arena, m, s, d);
+        const uint32_t d = ((w0 + a) << 5) + hc_select(~wd[a], r - (32u * a - pf[a]));
+        const uint32_t p = h_s2b(t)[sl];   // the mover's bucket
+        hc_copy(kb, m.key_size, sl, d);
+        hc_copy(vb, m.value_size, sl, d);
+        *(uint32_t *)h_rec(t, p) = d;   // the state half of the bucket's first word (the tag stays)
     }
+    // ring positions [lo, m) popped (every block a share: nothing in this kernel reads the ring)
+    int32_t *ring = h_ring(t);
+    for (uint32_t q = lo + blockIdx.x * 256u + threadIdx.x; q < ((meas & 2u) ? lo : mm); q += gridDim.x * 256u) ring[q] = -1;
+    // The last block to get here clears what every block has read (their reads are complete: each
+    // block used the values before counting itself).  No fence: nothing written here is read back in
+    // this kernel, and the kernel's end publishes it (a release fence per block -- an L2 write-back
+    // on gfx950 -- cost 10 of this kernel's 19 us)
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last_ = __hip_atomic_fetch_add(&c->cdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
-    }
+    if (threadIdx.x == 0)
+        last_ = __hip_atomic_fetch_add(&c->cdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
     __syncthreads();
     if (!last_) return;
-    __threadfence();
-    uint32_t *bits = h_bits(t);
-    for (uint32_t i = threadIdx.x; i < nw; i += 256u) bits[W.w0 + i] = 0;
-    int32_t *ring = h_ring(t);
-    for (uint32_t p = lo + threadIdx.x; p < mm; p += 256u) ring[p] = -1;
+    typedef uint32_t u32x4z __attribute__((ext_vector_type(4)));
+    u32x4z *uz = (u32x4z *)(h_used8(t) + ((size_t)w0 << 5));
+    const u32x4z z4 = {0, 0, 0, 0};
+    for (uint32_t i = threadIdx.x; i < 2 * nw; i += 256u) uz[i] = z4;
     unsigned long long *left = h_left(t);
     const uint32_t nl = c->nleft < HT_LEFT_CAP ? c->nleft : HT_LEFT_CAP;
-    for (uint32_t j = threadIdx.x; j < nl; j += 256u) left[j] = 0;
+    for (uint32_t q = threadIdx.x; q < nl; q += 256u) left[q] = 0;
     if (threadIdx.x < HT_USED_SHARDS) c->live_sh[32 * threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         c->head = mm;
@@ -747,8 +781,13 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
 }
 
 extern "C" int mimic_launch_hash_compact(uint8_t *arena, const DMap *m, hipStream_t st) {
-    const uint32_t blocks = std::min<uint32_t>(64u, std::max<uint32_t>(1u, m->max_entries / 4096u));
-    hipLaunchKernelGGL(mimic_hash_compact_kernel, dim3(blocks), dim3(256), 0, st, arena, *m);
+    // every block scans all bit words (<= 4096), then takes a share of the movers: about a mover per
+    // thread (MIMIC_COMPACT_BLOCKS=n: n blocks, measurement)
+    static const uint32_t forced = [] { const char *e = getenv("MIMIC_COMPACT_BLOCKS"); return e ? (uint32_t)atoi(e) : 0u; }();
+    const uint32_t blocks = forced ? forced : std::min<uint32_t>(256u, std::max<uint32_t>(1u, m->max_entries / 1024u));
+    // MIMIC_COMPACT_MEAS (measurement only, results wrong): 1 no moves, 2 no ring writes
+    static const uint32_t meas = [] { const char *e = getenv("MIMIC_COMPACT_MEAS"); return e ? (uint32_t)atoi(e) : 0u; }();
+    hipLaunchKernelGGL(mimic_hash_compact_kernel, dim3(blocks), dim3(256), 0, st, arena, *m, meas);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -784,8 +823,8 @@ extern "C" __global__ void mimic_hash_reset_kernel(uint8_t *arena, DMap m) {
     fill_bytes(arena + m.keys_dev_off, (size_t)m.max_entries * m.key_size, 0, g, stride);
     int32_t *ring = h_ring(t);
     for (size_t i = g; i < t.fl_cap; i += stride) ring[i] = i < m.max_entries ? (int32_t)i : -1;
-    // chunked reservations' slot bits and handed-back remainders (hashmap.h h_bits / h_left)
-    fill_bytes((uint8_t *)h_bits(t), h_e32(t) / 8, 0, g, stride);
+    // chunked reservations' used bytes and handed-back remainders (hashmap.h h_used8 / h_left)
+    fill_bytes(h_used8(t), h_e32(t), 0, g, stride);
     fill_bytes((uint8_t *)h_left(t), (size_t)HT_LEFT_CAP * 8, 0, g, stride);
     if (g == 0) {
         HashCtl *c = h_ctl(t);

@@ -71,10 +71,10 @@ struct DMap {
     uint32_t hflags;         // HT_F_*: set per launch table upload (engine.cpp tables_upload)
 };
 // the VM's one hash map whose pop-only JIT launches reserve freelist positions in per-block chunks
-// (hashmap.h h_chunk_take; engine.cpp picks it: a FAM_HASH map not shared with another VM,
+// (hashmap.h h_chunk_fill; engine.cpp picks it: a FAM_HASH map not shared with another VM,
 // E <= HT_CHUNK_MAXE); each such launch is followed by mimic_hash_compact_kernel
 #define HT_F_CHUNK 1u
-#define HT_CHUNK_MAXE (1u << 18)
+#define HT_CHUNK_MAXE (1u << 17)   // (the compaction kernel keeps the bit words and their prefix counts in LDS)
 #define HT_LEFT_CAP 16384u   // blocks of one launch that can hand a chunk remainder back (h_chunk_fini)
 
 // freelist ring + table counters of one hash map (device, agent-scope atomics).  head is on a
@@ -90,7 +90,7 @@ struct HashCtl {
     uint32_t used0;            // buckets that are not EMPTY (live + tombstones + busy), minus the shards
     uint32_t pad1[28];
     uint32_t used_sh[HT_USED_SHARDS * 32];   // shard s at [32 s]
-    // chunked reservations (hashmap.h h_chunk_take, interp.hip mimic_hash_compact_kernel); all zero
+    // chunked reservations (hashmap.h h_chunk_fill, interp.hip mimic_hash_compact_kernel); all zero
     // outside a chunk launch and its compaction
     uint32_t cminv;            // 0xffffffff - the lowest position a chunk refill took this launch (0: none)
     uint32_t full;             // a chunk launch proved every position live (E2BIG from then on)
@@ -99,11 +99,11 @@ struct HashCtl {
     uint32_t pad2[28];
     uint32_t live_sh[HT_USED_SHARDS * 32];   // positions chunk launches gave to inserts, shard s at [32 s]
 };
-// after HashCtl (hashmap.h h_bits / h_s2b / h_left): a bit per slot (inserted by the chunk launch),
+// after HashCtl (hashmap.h h_used8 / h_s2b / h_left): a byte per slot (inserted by the chunk launch),
 // the bucket of each such slot, the blocks' handed-back chunk remainders (end << 32 | next)
 HHD_LAYOUT uint64_t ht_ext_bytes(uint32_t E) {
     const uint64_t e32 = ((uint64_t)E + 1023) & ~1023ull;   // slots rounded to whole 128-byte lines of bits
-    return e32 / 8 + e32 * 4 + (uint64_t)HT_LEFT_CAP * 8;
+    return e32 + e32 * 4 + (uint64_t)HT_LEFT_CAP * 8;
 }
 #define HT_EMPTY 0xffffffffu
 #define HT_TOMB 0xfffffffeu

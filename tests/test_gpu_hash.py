@@ -477,24 +477,27 @@ def _distinct_keys(buf, off, lens) -> int:
     return len(np.unique(np.ascontiguousarray(k).view(np.dtype((np.void, 16)))))
 
 
-@pytest.mark.parametrize("V,E", [(4096, 32768), (65536, 32768), (262144, 1 << 17)])
-def test_chunked_launch_leaves_the_used_slots_dense(gpu, V, E):
+@pytest.mark.parametrize("V,n", [(4096, 60000), (65536, 60000), (262144, 400000)])
+def test_chunked_launch_leaves_the_used_slots_dense(gpu, V, n):
     """Chunked reservations (hashmap.h MIMIC_HASH_CHUNK: blocks take freelist positions in chunks,
     interp.hip mimic_hash_compact_kernel fills the holes their remainders leave): after a concurrent
     inserting launch the used slots are exactly [0, m), as after m sequential pops
     (emulator_linux_map_hash.go:179-186); verdicts and every key's value are the oracle's; a second
     launch over new flows (table partly full) keeps both; and the next insert from the host takes
-    slot m (the freelist's head), as it does on the oracle."""
+    slot m (the freelist's head), as it does on the oracle.  MaxEntries = the two batches' flows +
+    500: no flow is refused (which flows would be is order-dependent), and the second launch ends
+    with the table nearly full, where blocks go scarce and take other blocks' remainders."""
     import mimic_amd as M
 
+    batches = [W.make_packets(n, **W.IMIX, seed=300 + rnd) for rnd in range(2)]
+    E = W.distinct_keys(*[W.flow_keys_np(*bt) for bt in batches]) + 500
     p = W.prog_flowtrack(max_entries=E)
     sc = _sc(p, V)
     ovm, omids, opids = build_oracle(sc)
     vm, maps, pids = build_engine(sc)
     fm, om = maps["flows"], omids["flows"]
     for rnd in range(2):
-        n = 60000 if V < 65536 else 400000
-        buf, off, lens = W.make_packets(n, **W.IMIX, seed=300 + rnd)
+        buf, off, lens = batches[rnd]
         cpu = W.schedule_cpu(n, V, "interleaved")
         o = ovm.run_xdp_batch(opids[0], buf.copy(), off, lens, cpu, write_back=False)
         b = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
