@@ -660,13 +660,14 @@ static __device__ void hc_copy(uint8_t *base, uint32_t n, uint32_t s, uint32_t d
         }
     }
 }
-extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint8_t *arena, DMap m, uint32_t meas) {
+#define HC_T 1024u   // threads per block
+extern "C" __global__ __launch_bounds__(HC_T) void mimic_hash_compact_kernel(uint8_t *arena, DMap m, uint32_t meas) {
     const HT t = h_table(arena, m);
     HashCtl *c = h_ctl(t);
     const uint32_t cminv = c->cminv, fullf = c->full;
     if (!cminv && !fullf) return;
     __shared__ uint32_t wd[HC_MAXW], pf[HC_MAXW];   // the bit words of [lo, hi); set bits in words [0, i)
-    __shared__ uint32_t wsum[4], total_, last_;
+    __shared__ uint32_t wsum[HC_T / 64], total_, last_;
     const uint32_t E = t.E;
     const unsigned long long hd = c->head;
     const uint32_t hi = hd < E ? (uint32_t)hd : E;
@@ -678,18 +679,18 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     // counted as used, from hi on as free.  Every load of the thread first (indices clamped, no
     // branch between them: one wait), then the packing (a loop of load-then-use waited per word)
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    constexpr uint32_t PW = HC_MAXW / 256u;   // words per thread
+    constexpr uint32_t PW = HC_MAXW / HC_T;   // words per thread (4: eight 16-byte loads in flight)
     u32x4 v[2 * PW];
 #pragma unroll
     for (uint32_t k = 0; k < PW; k++) {
-        const uint32_t i = threadIdx.x + 256u * k, ic = i < nw ? i : 0u;
+        const uint32_t i = threadIdx.x + HC_T * k, ic = i < nw ? i : 0u;
         const u32x4 *q = (const u32x4 *)(used + ((size_t)(w0 + ic) << 5));
         v[2 * k] = q[0];
         v[2 * k + 1] = q[1];
     }
 #pragma unroll
     for (uint32_t k = 0; k < PW; k++) {
-        const uint32_t i = threadIdx.x + 256u * k;
+        const uint32_t i = threadIdx.x + HC_T * k;
         if (i >= nw) break;
         uint32_t x = 0;
 #pragma unroll
@@ -706,7 +707,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     }
     __syncthreads();
     // exclusive prefix counts: thread t sums words [t * per, +per), the threads' sums are scanned
-    const uint32_t per = (nw + 255u) / 256u, beg = threadIdx.x * per;
+    const uint32_t per = (nw + HC_T - 1u) / HC_T, beg = threadIdx.x * per;
     uint32_t own = 0;
     for (uint32_t i = beg; i < beg + per && i < nw; i++) own += (uint32_t)__builtin_popcount(wd[i]);
     uint32_t inc = own;   // inclusive scan over the wave
@@ -718,7 +719,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     __syncthreads();
     uint32_t before = inc - own;
     for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += wsum[w];
-    if (threadIdx.x == 255) total_ = before + own;
+    if (threadIdx.x == HC_T - 1u) total_ = before + own;
     for (uint32_t i = beg; i < beg + per && i < nw; i++) {
         pf[i] = before;
         before += (uint32_t)__builtin_popcount(wd[i]);
@@ -729,7 +730,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     const uint32_t Sm = (mw < nw ? pf[mw] : T) + (mw < nw && mb ? (uint32_t)__builtin_popcount(wd[mw] & ((1u << mb) - 1u)) : 0u);
     const uint32_t H = T - Sm;   // movers = holes
     uint8_t *kb = arena + m.keys_dev_off, *vb = arena + m.dev_off;
-    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < ((meas & 1u) ? 0u : H); r += gridDim.x * 256u) {
+    for (uint32_t r = blockIdx.x * HC_T + threadIdx.x; r < ((meas & 1u) ? 0u : H); r += gridDim.x * HC_T) {
         // the mover: the (Sm + r)-th used slot; the hole: the r-th free slot (zeros before word i: 32 i - pf[i])
         const uint32_t j = Sm + r;
         uint32_t a = 0, b = nw;   // the last word with pf <= j
@@ -752,7 +753,7 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     }
     // ring positions [lo, m) popped (every block a share: nothing in this kernel reads the ring)
     int32_t *ring = h_ring(t);
-    for (uint32_t q = lo + blockIdx.x * 256u + threadIdx.x; q < ((meas & 2u) ? lo : mm); q += gridDim.x * 256u) ring[q] = -1;
+    for (uint32_t q = lo + blockIdx.x * HC_T + threadIdx.x; q < ((meas & 2u) ? lo : mm); q += gridDim.x * HC_T) ring[q] = -1;
     // The last block to get here clears what every block has read (their reads are complete: each
     // block used the values before counting itself).  No fence: nothing written here is read back in
     // this kernel, and the kernel's end publishes it (a release fence per block -- an L2 write-back
@@ -765,10 +766,10 @@ extern "C" __global__ __launch_bounds__(256) void mimic_hash_compact_kernel(uint
     typedef uint32_t u32x4z __attribute__((ext_vector_type(4)));
     u32x4z *uz = (u32x4z *)(h_used8(t) + ((size_t)w0 << 5));
     const u32x4z z4 = {0, 0, 0, 0};
-    for (uint32_t i = threadIdx.x; i < 2 * nw; i += 256u) uz[i] = z4;
+    for (uint32_t i = threadIdx.x; i < 2 * nw; i += HC_T) uz[i] = z4;
     unsigned long long *left = h_left(t);
     const uint32_t nl = c->nleft < HT_LEFT_CAP ? c->nleft : HT_LEFT_CAP;
-    for (uint32_t q = threadIdx.x; q < nl; q += 256u) left[q] = 0;
+    for (uint32_t q = threadIdx.x; q < nl; q += HC_T) left[q] = 0;
     if (threadIdx.x < HT_USED_SHARDS) c->live_sh[32 * threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         c->head = mm;
@@ -784,10 +785,10 @@ extern "C" int mimic_launch_hash_compact(uint8_t *arena, const DMap *m, hipStrea
     // every block scans all bit words (<= 4096), then takes a share of the movers: about a mover per
     // thread (MIMIC_COMPACT_BLOCKS=n: n blocks, measurement)
     static const uint32_t forced = [] { const char *e = getenv("MIMIC_COMPACT_BLOCKS"); return e ? (uint32_t)atoi(e) : 0u; }();
-    const uint32_t blocks = forced ? forced : std::min<uint32_t>(256u, std::max<uint32_t>(1u, m->max_entries / 1024u));
+    const uint32_t blocks = forced ? forced : std::min<uint32_t>(64u, std::max<uint32_t>(1u, m->max_entries / 4096u));
     // MIMIC_COMPACT_MEAS (measurement only, results wrong): 1 no moves, 2 no ring writes
     static const uint32_t meas = [] { const char *e = getenv("MIMIC_COMPACT_MEAS"); return e ? (uint32_t)atoi(e) : 0u; }();
-    hipLaunchKernelGGL(mimic_hash_compact_kernel, dim3(blocks), dim3(256), 0, st, arena, *m, meas);
+    hipLaunchKernelGGL(mimic_hash_compact_kernel, dim3(blocks), dim3(HC_T), 0, st, arena, *m, meas);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
