@@ -81,7 +81,7 @@ static __device__ __noinline__ void step_warm(const KParams &kp, uint32_t t, uin
 // SIMD).
 enum { MODE_BATCH = 0, MODE_STEP = 1, MODE_RESUME = 2 };
 template <int MODE>
-static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp) {
+static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp, uint32_t goff = 0) {
     const KParams &kp = *kpp;  // device copy (engine.cpp kp_slot) or the kernarg segment: fields load where used
     StepState *const STP = MODE == MODE_STEP ? kp.step : nullptr;
     // eBPF registers r0..r10 of every lane live in LDS, [wave][reg][lane] (8-byte words): a
@@ -91,7 +91,7 @@ static __device__ __forceinline__ void xdp_body(const KParams *__restrict__ kpp)
     uint64_t *const RB = &sreg[threadIdx.x >> 6][0][threadIdx.x & 63];
 #define REG(r) RB[(r) * 64]
 
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t g = goff + blockIdx.x * blockDim.x + threadIdx.x;
     // resume: only the lanes the JIT kernel deferred in this launch (defer_finish, runtime.h) run,
     // from iteration j0 on; a wave without one returns at once
     const DeferRec *DR = nullptr;
@@ -512,11 +512,16 @@ extern "C" __global__ __launch_bounds__(256) void mimic_xdp_step_kernel(const KP
 }
 // after a JIT kernel with deferred slow paths, with the same launch parameters (by value: read
 // in place from the kernarg segment, as the JIT kernels do)
+// (a small grid striding over the lanes: a launch that deferred nothing -- the usual case, checked
+// first by every wave -- then costs a few waves instead of one per 64 lanes; cfg 5: 4.3 us)
+#define RESUME_BLOCKS 64u
 extern "C" __global__ __launch_bounds__(256) void mimic_xdp_resume_kernel(const KParams kp_arg) {
     (void)kp_arg;
     const KParams __attribute__((address_space(4))) *k4 =
         (const KParams __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();
-    xdp_body<MODE_RESUME>((const KParams *)k4);
+    const KParams *kp = (const KParams *)k4;
+    const uint32_t lanes = kp->lanes, stride = gridDim.x * blockDim.x;
+    for (uint32_t off = 0; off < lanes; off += stride) xdp_body<MODE_RESUME>(kp, off);
 }
 
 // Sum of a per-CPU u64 array over cpus: out[k] = sum_c base[c*stride + 8k] (the "sum over CPUs"
@@ -860,7 +865,7 @@ extern "C" int mimic_launch_hash_rebuild(uint8_t *arena, const DMap *m, uint32_t
 }
 
 extern "C" int mimic_launch_xdp_resume(const KParams *kp, hipStream_t st) {
-    const uint32_t blocks = (kp->lanes + 255) / 256;
+    const uint32_t blocks = std::min<uint32_t>((kp->lanes + 255) / 256, RESUME_BLOCKS);
     if (blocks == 0) return 0;
     hipLaunchKernelGGL(mimic_xdp_resume_kernel, dim3(blocks), dim3(256), 0, st, *kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -223,8 +223,28 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
     __shared__ uint64_t wtot[BLK_T / 64];
     const uint32_t t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
     const uint32_t per = (nb + BLK_T - 1) / BLK_T, lo = t * per;
+    // the cursor first: its round trip overlaps the sums'
+    const uint64_t base0 = t == 0 && !use_init ? state[0] : 0ull;
+    // up to BLK_PER sums per thread (batches of up to 2 M packets) loaded at once, no branch between
+    // the loads (indices clamped, values masked): one wait, and the write-back reuses them
+    constexpr uint32_t BLK_PER = 8;
+    uint64_t v[BLK_PER];
     uint64_t s = 0;
-    for (uint32_t k = 0; k < per && lo + k < nb; k++) s += bs[lo + k];
+    const bool held = nb > 0 && per <= BLK_PER;   // (nb = 0: an empty batch, nothing to read)
+    if (held) {
+#pragma unroll
+        for (uint32_t k = 0; k < BLK_PER; k++) {
+            const uint32_t i = lo + k < nb ? lo + k : nb - 1u;
+            v[k] = bs[i];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < BLK_PER; k++) {
+            v[k] = k < per && lo + k < nb ? v[k] : 0ull;
+            s += v[k];
+        }
+    } else {
+        for (uint32_t k = 0; k < per && lo + k < nb; k++) s += bs[lo + k];
+    }
     uint64_t x = s;
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -239,16 +259,25 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
         o += k < wv ? wtot[k] : 0ull;
         all += wtot[k];
     }
-    for (uint32_t k = 0; k < per && lo + k < nb; k++) {
-        const uint64_t v = bs[lo + k];
-        bs[lo + k] = o;
-        o += v;
+    if (held) {
+#pragma unroll
+        for (uint32_t k = 0; k < BLK_PER; k++)
+            if (k < per && lo + k < nb) {
+                bs[lo + k] = o;
+                o += v[k];
+            }
+    } else {
+        for (uint32_t k = 0; k < per && lo + k < nb; k++) {
+            const uint64_t w = bs[lo + k];
+            bs[lo + k] = o;
+            o += w;
+        }
     }
     // every room of the batch is zero once the chain has run (it zeroes the ones prep flagged) unless
     // a program stores into one, which sets the word back to 0; prep read it already (stream order)
     if (t == 0 && rooms_state) *rooms_state = 1u;
     if (t == 0) {
-        const uint64_t base = use_init ? init_base : state[0];
+        const uint64_t base = use_init ? init_base : base0;
         state[1] = base;
         state[0] = base + all;
     }
