@@ -328,6 +328,9 @@ def parse_args(argv=None):
                     help="batches per launch (mimic_run_xdp_many, up to 8: one owned-spread launch runs K of the "
                          "rotated batches back to back); --steps counts launches, ms_per_step stays per batch "
                          "(0: the config's default, 5 for the classifier, else 1)")
+    ap.add_argument("--digest", action="store_true",
+                    help="add sha256 digests of every rank's per-packet R0 (batch 0, after the timed region) and "
+                         "of the merged hash map's (key, value) records to the line (tests/test_gpu_bench_dist.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-resident", action="store_true", help="skip the PCIe-inclusive rate")
@@ -571,6 +574,14 @@ def main(argv=None):
         b0, cnt = D.shard(vpg, rank)
         local_sum = maps[pcm[0]["name"]].SumU64(b0, b0 + cnt)
         counters = D.allreduce_sum_u64(local_sum, cdev) if use_dist else local_sum
+    digests = None
+    if args.digest:   # per-packet and per-key evidence for the N-rank tests (nothing timed)
+        import hashlib
+
+        h = hashlib.sha256(batches[0][2].r0[:n].cpu().numpy().astype(np.uint64).tobytes()).digest()
+        digests = {"r0": [d.hex() for d in (D.allgather_records(h, 32, cdev) if use_dist else [h])]}
+        if hm and not wl.skb:
+            digests["hash"] = hashlib.sha256(b"".join(k + v for k, v in sorted(merged.items()))).hexdigest()
 
     # eBPF instructions per batch (exact per-lane step counts): one more untimed launch of each
     # batch after the readout above
@@ -636,6 +647,8 @@ def main(argv=None):
             "counters_sum": counters,
             "hash_keys": hash_keys,
         }
+        if digests:
+            out["digests"] = digests
         if use_dist:
             out["collectives"] = f"{'gloo' if gloo else 'rccl'}, world size {ws}"
         if args.one_device and ws > 1:

@@ -30,7 +30,8 @@ def jit_kernels():
 
 def _bench2(cfg):
     cmd = [sys.executable, "-u", "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--one-device", "--config", cfg,
-           "--steps", str(STEPS), "--warmup", str(WARMUP), "--batches", "1", "--no-host-resident", "--no-cpu-baseline"]
+           "--steps", str(STEPS), "--warmup", str(WARMUP), "--batches", "1", "--no-host-resident", "--no-cpu-baseline",
+           "--digest"]
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -41,10 +42,17 @@ def _bench2(cfg):
     return json.loads(lines[0])
 
 
+def _sha(b: bytes) -> str:
+    import hashlib
+
+    return hashlib.sha256(b).hexdigest()
+
+
 def test_two_rank_classifier_counters_equal_one_oracle(gpu):
     """cfg 2 at bench size per rank (1M packets, 262 144 vCPUs each): the all-reduced per-CPU
     verdict counters = the verdict counts of one oracle run over both ranks' packets, times the
-    launches before the readout."""
+    launches before the readout; every packet's R0 on each rank = the oracle's (digests gathered to
+    rank 0)."""
     import bench
     import oracle
     from mimic_amd import workloads as W
@@ -62,6 +70,7 @@ def test_two_rank_classifier_counters_equal_one_oracle(gpu):
         o = vm.run_xdp_batch(pid, wl.buf, wl.off, wl.lens, W.schedule_cpu(len(wl.lens), 64, "interleaved"),
                              write_back=False)
         want += np.bincount(o["r0"].astype(np.int64), minlength=4)[:4]
+        assert d["digests"]["r0"][r] == _sha(np.asarray(o["r0"]).astype(np.uint64).tobytes()), r
         vm.close()
     assert d["counters_sum"] == [int(x) * (WARMUP + STEPS) for x in want]
     assert d["mean_insns_per_packet"] > 20
@@ -69,7 +78,9 @@ def test_two_rank_classifier_counters_equal_one_oracle(gpu):
 
 def test_two_rank_flowtrack_replicas_merge_to_one_oracle_table(gpu):
     """cfg 4 at bench size per rank (2M packets of ONE 4M-packet batch, E = 131 072): the merged
-    replicas hold exactly the keys one oracle table holds after both shards."""
+    replicas hold exactly the keys and values one oracle table holds after both shards, and every
+    packet's R0 on each rank (the last launch: all lookups) is the oracle's for that packet (no flow is
+    refused: the union fits E)."""
     import bench
     import oracle
     from mimic_amd import workloads as W
@@ -83,9 +94,14 @@ def test_two_rank_flowtrack_replicas_merge_to_one_oracle_table(gpu):
     pid = vm.prog_load(p.name, p.raw, [(s, mid) for s, _ in p.relocs])
     for r in range(2):
         wl = bench.Workload("flowtrack", 1 << 21, W.SEED + r, r, 2)
-        vm.run_xdp_batch(pid, wl.buf, wl.off, wl.lens, W.schedule_cpu(len(wl.lens), 64, "interleaved"),
-                         write_back=False)
-    want = len(vm.map_entries(mid))
+        o = vm.run_xdp_batch(pid, wl.buf, wl.off, wl.lens, W.schedule_cpu(len(wl.lens), 64, "interleaved"),
+                             write_back=False)
+        assert d["digests"]["r0"][r] == _sha(np.asarray(o["r0"]).astype(np.uint64).tobytes()), r
+    ents = vm.map_entries(mid)
+    ov = vm.map_values(mid, 0)
+    want = len(ents)
+    table = sorted((k, ov[s * 8:(s + 1) * 8]) for k, s in ents)
     vm.close()
     assert 120000 < want <= m["max_entries"]
     assert d["hash_keys"] == want
+    assert d["digests"]["hash"] == _sha(b"".join(k + v for k, v in table))
