@@ -223,7 +223,11 @@ int mimic_stack_addr(mimic_vm *vm, uint32_t *addr_out);
 
 /* Batch form of: for each packet i { p := vm.NewProcess(prog, &LinuxContextXDP{...});
  * p.SetCPUID(cpu(i)); p.Run(ctx); r0[i] = p.Registers.R0; p.Cleanup() }  (vm.go:198-374).
- * Enqueued on `hip_stream` (a hipStream_t, NULL = the vm's own stream); returns when enqueued. */
+ * Enqueued on `hip_stream` (a hipStream_t, NULL = the vm's own stream); returns when enqueued.
+ * Hash inserts of concurrent vCPUs take freelist slots in arrival order (the reference's pool is
+ * no different); after the batch the used slots of a hash map are [0, m), as m sequential pops leave
+ * them (a compaction kernel follows a launch that reserved positions in chunks, on the same stream),
+ * and E2BIG is answered exactly when every slot is live. */
 int mimic_run_xdp(mimic_vm *vm, uint32_t prog_id, const mimic_xdp_batch *batch,
                   const mimic_xdp_results *results, void *hip_stream);
 /* k batches (DEVICE pointers as above), enqueued like mimic_run_xdp, as few launches as possible: up
