@@ -50,7 +50,7 @@ extern "C" int mimic_launch_skb_gather(const uint8_t *const *mem, uint32_t n, ui
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
                                      uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse,
-                                     uint32_t *rooms_state, uint64_t *lb, uint32_t ep, hipStream_t st);
+                                     uint32_t *rooms_state, hipStream_t st);
 
 namespace {
 
@@ -257,9 +257,6 @@ struct mimic_vm {
     uint64_t *d_skb_drv = nullptr;   // the prep kernel's derived record words, SKB_DERIVED_Q per packet
     uint64_t *d_skb_prefix = nullptr, *d_skb_state = nullptr;
     size_t skb_cap = 0;
-    // the prep kernel's look-back words (skb.hip: one per block, epoch-tagged) and the epoch
-    uint64_t *d_skb_lb = nullptr;
-    uint32_t skb_lb_cap = 0, skb_lb_ep = 0;
     // mimic_process_run_many: the gathered descriptors, records, prefixes, custom entries and results
     // of the processes of one launch (one allocation, grown as needed)
     uint8_t *d_many = nullptr;
@@ -797,7 +794,6 @@ void mimic_vm_destroy(mimic_vm *vm) {
     hipFree(vm->d_skb_rec);
     hipFree(vm->d_skb_drv);
     hipFree(vm->d_skb_prefix);
-    hipFree(vm->d_skb_lb);
     hipFree(vm->d_many);
     hipFree(vm->d_skb_state);
     if (vm->s_h2d) hipStreamDestroy(vm->s_h2d);
@@ -1841,33 +1837,9 @@ static int skb_prepare(mimic_vm *vm, const mimic_xdp_batch *b, hipStream_t st, c
     static const bool rooms_chain = getenv("MIMIC_SKB_ROOMS_CHAIN") && getenv("MIMIC_SKB_ROOMS_CHAIN")[0] == '1';
     // MIMIC_SKB_ROOMS_ZERO=1: the prep zeroes every loaded packet's rooms without reading them
     static const bool rooms_zero = getenv("MIMIC_SKB_ROOMS_ZERO") && getenv("MIMIC_SKB_ROOMS_ZERO")[0] == '1';
-    // a batch's block offsets by look-back in the prep kernel (skb.hip; MIMIC_SKB_LOOKBACK=0: the
-    // one-workgroup blocks kernel after it, round 5): one word per block, tagged with an epoch that
-    // changes every launch; the words are cleared when the 24-bit epoch wraps
-    static const bool lb_on = !(getenv("MIMIC_SKB_LOOKBACK") && getenv("MIMIC_SKB_LOOKBACK")[0] == '0');
-    uint64_t *lb = nullptr;
-    uint32_t ep = 0;
-    if (lb_on && !into && n) {
-        const uint32_t nb = (n + (1u << SKB_PREP_LOG2) - 1) >> SKB_PREP_LOG2;
-        if (nb > vm->skb_lb_cap) {
-            HIP_OK(vm, hipStreamSynchronize(st));
-            hipFree(vm->d_skb_lb);
-            vm->d_skb_lb = nullptr;
-            HIP_OK(vm, hipMalloc(&vm->d_skb_lb, (size_t)nb * 8));
-            HIP_OK(vm, hipMemset(vm->d_skb_lb, 0, (size_t)nb * 8));
-            vm->skb_lb_cap = nb;
-            vm->skb_lb_ep = 0;
-        }
-        if (++vm->skb_lb_ep >= (1u << 24)) {
-            HIP_OK(vm, hipMemsetAsync(vm->d_skb_lb, 0, (size_t)vm->skb_lb_cap * 8, st));
-            vm->skb_lb_ep = 1;
-        }
-        lb = vm->d_skb_lb;
-        ep = vm->skb_lb_ep;
-    }
     if (mimic_launch_skb_prep(b->pkt_data, b->pkt_off, b->pkt_len, n, out, out_q, into ? into->prefix : vm->d_skb_prefix,
                               vm->d_skb_state, init, vm->skb_leaked ? 0u : 1u, (rooms_chain && !into) ? 0u : rooms_zero ? 2u : 1u,
-                              (sparse && !into) ? 1u : 0u, into ? nullptr : rooms_state, lb, ep, st))
+                              (sparse && !into) ? 1u : 0u, into ? nullptr : rooms_state, st))
         return fail(vm, MIMIC_EDEVICE, "sk_buff prep: %s", hipGetErrorString(hipGetLastError()));
     if (n) vm->skb_leaked = true;
     vm->skb_stream = st;

@@ -70,10 +70,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(uint8
                                                                           uint32_t n, uint64_t *__restrict__ rec,
                                                                           uint32_t rec_q, uint64_t *__restrict__ prefix,
                                                                           uint32_t rooms, uint32_t sparse,
-                                                                          const uint32_t *__restrict__ rooms_state,
-                                                                          uint64_t *__restrict__ lb, uint32_t ep,
-                                                                          uint64_t *__restrict__ state, uint64_t init_base,
-                                                                          uint32_t use_init, uint32_t *rooms_set) {
+                                                                          const uint32_t *__restrict__ rooms_state) {
     __shared__ uint64_t area[(PREP_W / 8) * PREP_T];   // the windows first, then the records
     __shared__ uint64_t wtot[PREP_T / 64];
     uint32_t *win = (uint32_t *)area;
@@ -211,42 +208,7 @@ extern "C" __global__ __launch_bounds__(PREP_T) void mimic_skb_prep_kernel(uint8
     uint64_t bsum;
     const uint64_t ex = prep_exscan(f, wtot, &bsum);
     if (live) prefix[i] = ex | flags;
-    if (t != 0) return;
-    if (!lb) {
-        prefix[n + blockIdx.x] = bsum;
-        return;
-    }
-    // lb: the blocks' offsets by decoupled look-back, no mimic_skb_blocks_kernel (a launch of ~5 us).
-    // Block b publishes its sum (flag A), adds its predecessors' words walking back until one carries
-    // an inclusive prefix (flag P), then publishes its own inclusive prefix.  A word is epoch << 40 |
-    // flag << 38 | value (38 bits): one 64-bit atomic, so no fence orders a flag with its value, and
-    // words of earlier launches (another epoch) read as "not yet".  A block waits only on blocks of
-    // lower index, which the dispatcher started before it.
-    const uint32_t b = blockIdx.x;
-    const uint64_t E = (uint64_t)ep << 40, VM38 = (1ull << 38) - 1;
-    uint64_t excl = 0;
-    if (b) {
-        __hip_atomic_store(lb + b, E | (1ull << 38) | bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t j = b - 1;;) {
-            const uint64_t w = __hip_atomic_load(lb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(w >> 40) != ep) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += w & VM38;
-            if (((w >> 38) & 3u) == 2u) break;
-            j--;
-        }
-    }
-    __hip_atomic_store(lb + b, E | (2ull << 38) | ((excl + bsum) & VM38), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prefix[n + b] = excl;
-    if (b == gridDim.x - 1u) {   // the last block: the batch's leak base and the cursor past it (as the blocks kernel)
-        const uint64_t base = use_init ? init_base : state[0];
-        state[1] = base;
-        state[0] = base + excl + bsum;
-        // every block read the rooms word at its start: each published before this block could finish
-        if (rooms_set) *rooms_set = 1u;
-    }
+    if (t == 0) prefix[n + blockIdx.x] = bsum;
 }
 
 // The blocks' offsets in the batch (exclusive scan of the nb block sums at bs, in place; one
@@ -325,8 +287,7 @@ extern "C" __global__ __launch_bounds__(BLK_T) void mimic_skb_blocks_kernel(uint
 extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len, uint32_t n,
                                    uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state, hipStream_t st) {
     hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
-                       rec, rec_q, prefix, 1u, 0u, (const uint32_t *)nullptr, (uint64_t *)nullptr, 0u, (uint64_t *)nullptr, 0ull,
-                       0u, (uint32_t *)nullptr);
+                       rec, rec_q, prefix, 1u, 0u, (const uint32_t *)nullptr);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        0ull, 0u, (uint32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -337,17 +298,10 @@ extern "C" int mimic_skb_prep_only(const uint8_t *pkt_data, const uint64_t *pkt_
 extern "C" int mimic_launch_skb_prep(const uint8_t *pkt_data, const uint64_t *pkt_off, const uint32_t *pkt_len,
                                      uint32_t n, uint64_t *rec, uint32_t rec_q, uint64_t *prefix, uint64_t *state,
                                      uint64_t init_base, uint32_t use_init, uint32_t rooms, uint32_t sparse,
-                                     uint32_t *rooms_state, uint64_t *lb, uint32_t ep, hipStream_t st) {
-    if (n && lb) {   // the blocks' offsets by look-back inside the prep kernel (no blocks kernel)
-        hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
-                           rec, rec_q, prefix, rooms, sparse, (const uint32_t *)rooms_state, lb, ep, state, init_base, use_init,
-                           rooms == 1 ? rooms_state : (uint32_t *)nullptr);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
+                                     uint32_t *rooms_state, hipStream_t st) {
     if (n)
         hipLaunchKernelGGL(mimic_skb_prep_kernel, dim3((n + PREP_T - 1) / PREP_T), dim3(PREP_T), 0, st, (uint8_t *)pkt_data, pkt_off, pkt_len, n,
-                           rec, rec_q, prefix, rooms, sparse, (const uint32_t *)rooms_state, (uint64_t *)nullptr, 0u,
-                           (uint64_t *)nullptr, 0ull, 0u, (uint32_t *)nullptr);
+                           rec, rec_q, prefix, rooms, sparse, (const uint32_t *)rooms_state);
     hipLaunchKernelGGL(mimic_skb_blocks_kernel, dim3(1), dim3(BLK_T), 0, st, prefix + n, (n + PREP_T - 1) / PREP_T, state,
                        init_base, use_init, rooms == 1 ? rooms_state : (uint32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
