@@ -678,7 +678,7 @@ extern "C" __global__ __launch_bounds__(HC_T) void mimic_hash_compact_kernel(uin
     const uint32_t hi = hd < E ? (uint32_t)hd : E;
     uint32_t lo = cminv ? 0xffffffffu - cminv : hi;
     lo = lo < hi ? lo : hi;
-    const uint32_t w0 = lo >> 5, nw = ((hi + 31u) >> 5) - w0;
+    const uint32_t w0 = lo >> 5, nw = (meas & 8u) ? 0u : ((hi + 31u) >> 5) - w0;
     const uint8_t *used = h_used8(t);
     // the used bytes as bit words (plain loads: the launch that wrote them has ended), below lo
     // counted as used, from hi on as free.  Every load of the thread first (indices clamped, no
@@ -771,7 +771,7 @@ extern "C" __global__ __launch_bounds__(HC_T) void mimic_hash_compact_kernel(uin
     typedef uint32_t u32x4z __attribute__((ext_vector_type(4)));
     u32x4z *uz = (u32x4z *)(h_used8(t) + ((size_t)w0 << 5));
     const u32x4z z4 = {0, 0, 0, 0};
-    for (uint32_t i = threadIdx.x; i < 2 * nw; i += HC_T) uz[i] = z4;
+    for (uint32_t i = threadIdx.x; i < ((meas & 4u) ? 0u : 2 * nw); i += HC_T) uz[i] = z4;
     unsigned long long *left = h_left(t);
     const uint32_t nl = c->nleft < HT_LEFT_CAP ? c->nleft : HT_LEFT_CAP;
     for (uint32_t q = threadIdx.x; q < nl; q += HC_T) left[q] = 0;
@@ -791,7 +791,8 @@ extern "C" int mimic_launch_hash_compact(uint8_t *arena, const DMap *m, hipStrea
     // thread (MIMIC_COMPACT_BLOCKS=n: n blocks, measurement)
     static const uint32_t forced = [] { const char *e = getenv("MIMIC_COMPACT_BLOCKS"); return e ? (uint32_t)atoi(e) : 0u; }();
     const uint32_t blocks = forced ? forced : std::min<uint32_t>(64u, std::max<uint32_t>(1u, m->max_entries / 4096u));
-    // MIMIC_COMPACT_MEAS (measurement only, results wrong): 1 no moves, 2 no ring writes
+    // MIMIC_COMPACT_MEAS (measurement only, results wrong): 1 no moves, 2 no ring writes, 4 no clearing
+    // of the used bytes, 8 no scan (nothing found)
     static const uint32_t meas = [] { const char *e = getenv("MIMIC_COMPACT_MEAS"); return e ? (uint32_t)atoi(e) : 0u; }();
     hipLaunchKernelGGL(mimic_hash_compact_kernel, dim3(blocks), dim3(HC_T), 0, st, arena, *m, meas);
     return hipGetLastError() == hipSuccess ? 0 : -1;
