@@ -39,7 +39,7 @@ CONFIGS = {
     # many: batches per launch by default (mimic_run_xdp_many: a processPool draining its backlog,
     # vm.go:548-573; every batch's packets all run, ms_per_step stays per 1M-packet batch); --many 1
     # is the one-batch-per-launch line
-    "classifier": dict(prog="prog_classifier", packets=1 << 20, sizes=(64,), weights=(1,), many=5,
+    "classifier": dict(prog="prog_classifier", packets=1 << 20, sizes=(64,), weights=(1,), many=8,
                        workload="cfg2: 1M x 64B xdp_md, 36-slot parse+hash DROP/PASS classifier, "
                                 "per-CPU array E=4 S=8"),
     "parse5": dict(prog="prog_parse5", packets=1 << 24, sizes=(64, 576, 1500), weights=(7, 4, 1), vcpus=1 << 18,
@@ -425,7 +425,9 @@ def make_batches(wl, args, n, rank, dev, sched):
     import mimic_amd as M
     from mimic_amd import workloads as W
 
-    nb = args.batches or default_batches(args.config, n)
+    # (a config that runs several batches per launch rotates over at least that many: no batch twice
+    # in one launch)
+    nb = args.batches or max(default_batches(args.config, n), 1 if args.many else CONFIGS[args.config].get("many", 1))
     ws = dist_env()[0]
     out = []
     for b in range(nb):

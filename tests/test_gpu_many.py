@@ -61,6 +61,22 @@ def test_five_rotated_batches_one_launch(gpu, sched):
     _run(sc, batches, sched, "spread_own")
 
 
+@pytest.mark.parametrize("sched", ["interleaved", "chunked"])
+def test_eight_rotated_batches_one_launch(gpu, sched):
+    """The bench's default: 8 batches (MIMIC_MANY_MAX) in one owned launch, cfg 2's shape scaled down."""
+    sc = _sc(W.prog_classifier(), 4096)
+    batches = [W.make_packets(16384, seed=W.SEED + 17 * k) for k in range(8)]
+    _run(sc, batches, sched, "spread_own")
+
+
+def test_eight_batches_at_bench_size(gpu):
+    """cfg 2 at bench size, as the default bench line runs it: 8 batches of 1 048 576 x 64 B at
+    V = 262 144 in one launch, every packet and every counter row exact."""
+    sc = _sc(W.prog_classifier(), 1 << 18)
+    batches = [W.make_packets(1 << 20, seed=W.SEED + k) for k in range(8)]
+    _run(sc, batches, "interleaved", "spread_own")
+
+
 def test_ragged_batches_and_more_than_eight(gpu):
     """10 batches (two launches: 8 + 2) of 3 001 packets at V = 1 000 (3-4 packets per vCPU)."""
     sc = _sc(W.prog_classifier(), 1000)
