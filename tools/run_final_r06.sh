@@ -13,6 +13,7 @@ for c in classifier parse5 flowtrack flowtrack_insert skb pass8; do
   $B --config $c > $D/bench_$c.json 2> $D/bench_$c.err || { tail -20 $D/bench_$c.err; exit 1; }
 done
 $B --config classifier --many 1 > $D/bench_classifier_many1.json 2> $D/bench_classifier_many1.err || exit 1   # one batch per launch
+$B --config classifier --many 5 --batches 5 > $D/bench_classifier_many5.json 2> $D/bench_classifier_many5.err || exit 1   # round 6's first default
 fi
 if [ "${PART:-2}" = 2 ]; then
 mkdir -p $D
