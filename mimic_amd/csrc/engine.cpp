@@ -746,7 +746,9 @@ int mimic_vm_create(const mimic_vm_settings *settings, mimic_vm **out) {
 void mimic_vm_destroy(mimic_vm *vm) {
     if (!vm) return;
     hipSetDevice(vm->s.device);
-    if (vm->stream) hipStreamSynchronize(vm->stream);
+    // everything this VM enqueued, on any stream (its own, side streams, callers' streams), ends
+    // before its memory -- device blocks, pinned process state, the arena -- is released
+    hipDeviceSynchronize();
     for (auto &m : vm->maps) {   // leave the shared tables (an owner takes its table's memory along)
         if (!m.share) continue;
         auto &mem = m.share->members;

@@ -41,6 +41,20 @@ def _session_kernels(session):
     return kernels
 
 
+@pytest.fixture(autouse=True)
+def _gpu_settle(request):
+    """After every GPU test the device is synchronised: an error its asynchronous work left (a
+    faulting kernel, a copy into freed memory) is reported at that test's teardown, not at the next
+    test's first HIP call."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 @pytest.fixture(scope="session")
 def gpu(request):
     """The GPU session: first compiles the session's JIT kernels in parallel worker processes
