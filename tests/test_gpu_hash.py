@@ -521,6 +521,34 @@ def test_chunked_launch_leaves_the_used_slots_dense(gpu, V, n):
     ovm.close()
 
 
+@pytest.mark.parametrize("hchunk", ["1", "8", "64"])
+def test_chunk_sizes_leave_the_used_slots_dense(gpu, hchunk, monkeypatch):
+    """Chunks of at most 1 (every refill exact: no holes), 8 and 64 positions (MIMIC_JIT_HCHUNK, a
+    generation knob): the same launch leaves used slots [0, m), verdicts and values the oracle's."""
+    import mimic_amd as M
+
+    monkeypatch.setenv("MIMIC_JIT_HCHUNK", hchunk)
+    V, n = 65536, 200000
+    buf, off, lens = W.make_packets(n, **W.IMIX, seed=91)
+    E = _distinct_keys(buf, off, lens) + 200
+    p = W.prog_flowtrack(max_entries=E)
+    sc = _sc(p, V)
+    ovm, omids, opids = build_oracle(sc)
+    o = ovm.run_xdp_batch(opids[0], buf.copy(), off, lens, W.schedule_cpu(n, V, "interleaved"), write_back=False)
+    vm, maps, pids = build_engine(sc)
+    b = M.XDPBatch.from_numpy(buf, off, lens, device="cuda:0", schedule=M.SCHED_INTERLEAVED)
+    e = vm.RunXDPBatch(pids[0], b).numpy(n)
+    for k in ("r0", "status"):
+        assert np.array_equal(np.asarray(o[k]).astype(np.int64), np.asarray(e[k]).astype(np.int64)), k
+    ents = maps["flows"].Entries()
+    assert sorted(s for _, s in ents) == list(range(len(ents)))
+    oe = ovm.map_entries(omids["flows"])
+    ov, ev = ovm.map_values(omids["flows"], 0), maps["flows"].Values(0)
+    assert {k: ev[s * 8:(s + 1) * 8] for k, s in ents} == {k: ov[s * 8:(s + 1) * 8] for k, s in oe}
+    vm.close()
+    ovm.close()
+
+
 @pytest.mark.parametrize("short", [0, 1, 37])
 def test_chunked_launch_fills_a_table_exactly(gpu, short):
     """MaxEntries = the batch's distinct flows - short.  short = 0: every flow must get a slot (no
