@@ -403,9 +403,21 @@ HHD uint64_t h_hash(const KS &ks, uint32_t K) {
     return h;
 }
 
+// Keys of up to 32 bytes: every word loaded before any is compared (one memory round trip; a
+// load-compare-exit loop waited for each word in turn: two round trips per probe of a 16-byte key)
 template <class KS>
 HDEV bool h_key_eq(const uint64_t *r, const KS &ks, uint32_t K) {
     const uint32_t nq = (K + 7) >> 3;
+    if (nq <= 4) {
+        uint64_t w[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) w[q] = q < nq ? h_ld(r + 1 + q) : 0ull;
+        bool eq = true;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+            if (q < nq) eq &= w[q] == ks.word(q);
+        return eq;
+    }
     for (uint32_t q = 0; q < nq; q++)
         if (h_ld(r + 1 + q) != ks.word(q)) return false;
     return true;
