@@ -403,11 +403,14 @@ HHD uint64_t h_hash(const KS &ks, uint32_t K) {
     return h;
 }
 
-// Keys of up to 32 bytes: every word loaded before any is compared (one memory round trip; a
-// load-compare-exit loop waited for each word in turn: two round trips per probe of a 16-byte key)
+// JIT kernels (MIMIC_CTX_FIXED), keys of up to 32 bytes: every word loaded before any is compared
+// (one memory round trip; a load-compare-exit loop waited for each word in turn: two round trips per
+// probe of a 16-byte key; cfg-4 lookup-hit step 0.136 -> 0.133 ms).  The batch interpreter keeps the
+// loop: the four words cost it 46 more spilled VGPRs.
 template <class KS>
 HDEV bool h_key_eq(const uint64_t *r, const KS &ks, uint32_t K) {
     const uint32_t nq = (K + 7) >> 3;
+#ifdef MIMIC_CTX_FIXED
     if (nq <= 4) {
         uint64_t w[4];
 #pragma unroll
@@ -418,6 +421,7 @@ HDEV bool h_key_eq(const uint64_t *r, const KS &ks, uint32_t K) {
             if (q < nq) eq &= w[q] == ks.word(q);
         return eq;
     }
+#endif
     for (uint32_t q = 0; q < nq; q++)
         if (h_ld(r + 1 + q) != ks.word(q)) return false;
     return true;
